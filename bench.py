@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Benchmark: RQ-VAE training throughput on MI355X (BASELINE.json metric, configs[1]).
+
+Workload (one "step"): a full RQ-VAE train step at the MovieLens-32M config
+(configs/rqvae_ml32m.gin: input 768 -> [512, 256, 128] -> D=64, K=256 codewords, L=3 levels,
+ROTATION_TRICK, beta 0.25, AdamW lr 1e-4 wd 0.01), synthetic unit-norm 768-d items resident in
+HBM, per-GPU batch 65,536 items (throughput shape; the config's B=64 latency is reported
+beside it): encoder MLP -> fused HIP L-level quantize -> decoder MLP -> losses -> backward
+(HIP quantize VJP) -> RCCL gradient all-reduce (N>1) -> AdamW.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline] [--no-extras]
+
+N>1 is launched by torch.distributed.run (one process per GPU); every rank processes its own
+disjoint 65,536-item shard ("weak" scaling) and rank 0 prints ONE JSON line.
+
+roofline: the fused quantize forward kernel (rq_quantize_fwd), algorithmic FLOPs
+2*K*D*L per item divided by its mean device time, measured with HIP events on
+the launching stream inside the timed region; peak = fp32 MFMA 157.3 TFLOP/s (gfx950 has no
+xf32). cpu_baseline: the pinned numpy oracle of the same train step (oracle/rqvae.py) on a
+bounded sample, timed on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rq-vae-recommender_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-in MFMA = vector peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+CFG = dict(input_dim=768, hidden=[512, 256, 128], D=64, K=256, L=3, lr=1e-4, wd=0.01, beta=0.25)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="items per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def make_items(n, dim, gen, device):
+    x = torch.randn(n, dim, generator=gen, device=device)
+    return x / x.norm(dim=1, keepdim=True)
+
+
+def build_model(device, seed=0):
+    from modules.quantize import QuantizeForwardMode
+    from modules.rqvae import RqVae
+    torch.manual_seed(seed)
+    m = RqVae(input_dim=CFG["input_dim"], embed_dim=CFG["D"], hidden_dims=CFG["hidden"], codebook_size=CFG["K"],
+              codebook_kmeans_init=False, codebook_mode=QuantizeForwardMode.ROTATION_TRICK, n_layers=CFG["L"],
+              commitment_weight=CFG["beta"], n_cat_features=0).to(device)
+    # k-means-init-like codebooks: level l = K residual rows of disjoint random items
+    g = torch.Generator(device=device).manual_seed(seed + 1)
+    with torch.no_grad():
+        res = m.encode(make_items(CFG["K"] * CFG["L"], CFG["input_dim"], g, device))
+        for l, layer in enumerate(m.layers):
+            cb = res[l * CFG["K"]:(l + 1) * CFG["K"]].clone()
+            layer.embedding.weight.copy_(cb)
+    return m
+
+
+def time_region(fn, steps, warmup, sync_all):
+    for _ in range(warmup):
+        fn()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync_all()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(budget_s, B=2048):
+    """Oracle (numpy) RqVae train step, same shapes, bounded sample of ~budget_s seconds."""
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits, threadpool_info = None, None
+    from oracle import rqvae as R
+    import gen_inputs as gi  # tests/golden (seeded synthetic inputs)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+    try:
+        D, K, L, inp, hid = CFG["D"], CFG["K"], CFG["L"], CFG["input_dim"], CFG["hidden"]
+        st = {f"encoder.mlp.{2 * j}.weight": w for j, w in enumerate(gi.mlp_weights([inp] + hid + [D], 5))}
+        st.update({f"decoder.mlp.{2 * j}.weight": w for j, w in enumerate(gi.mlp_weights([D] + hid[::-1] + [inp], 6))})
+        enc_items = gi.items(K * L, inp, 7)
+        res0, _ = R.mlp_fwd(enc_items, [st[f"encoder.mlp.{2 * j}.weight"] for j in range(len(hid) + 1)], False)
+        for l in range(L):
+            st[f"layers.{l}.embedding.weight"] = res0[l * K:(l + 1) * K].copy()
+        orc = R.RqVaeOracle(st, L)
+        x = gi.items(B, inp, 8)
+        orc.train_step(x, CFG["lr"], CFG["wd"])          # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            orc.train_step(x, CFG["lr"], CFG["wd"])
+            n += 1
+            if time.perf_counter() - t0 >= budget_s or n >= 200:
+                break
+        dt = time.perf_counter() - t0
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+    return dict(value=round(n * B / dt, 1), unit="items/s", cores=threads, kind="port",
+                sample=f"{n} numpy-oracle RqVae train steps (fwd+bwd+AdamW) at B={B}, ML-32M dims, "
+                       f"{dt:.1f} s on {threads} host threads")
+
+
+def main():
+    args = parse()
+    from rqvae_hip import dp, ops
+    from data.schemas import SeqBatch
+    rk, ws, lr = dp.init_from_env()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs an MI355X (no GPU visible)")
+    device = torch.device("cuda", lr)
+    torch.cuda.set_device(device)
+    B = args.batch
+
+    model = build_model(device)
+    buckets = dp.GradBuckets(model.parameters())
+    buckets.broadcast_params()
+    try:
+        opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"], fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"], foreach=True)
+    gen = torch.Generator(device=device).manual_seed(1000 + rk)
+    pool = [make_items(B, CFG["input_dim"], gen, device) for _ in range(4)]   # resident in HBM
+    it = [0]
+
+    def step():
+        xb = pool[it[0] % len(pool)]
+        it[0] += 1
+        buckets.zero_grad()
+        out = model(SeqBatch(None, None, None, xb, None, None), gumbel_t=0.2)
+        out.loss.backward()
+        buckets.synchronize()
+        opt.step()
+        return out
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+    ops.TIMER.reset()
+    ops.TIMER.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    ops.TIMER.enabled = False
+    if ws > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    q_ms, q_n = ops.TIMER.mean_ms("rq_quantize_fwd")
+    loss = float(last.loss)
+
+    extras = {}
+    if not args.no_extras and rk == 0:
+        extras = measure_extras(model, device, pool[0])
+
+    if rk != 0:
+        if ws > 1:
+            dist.barrier()
+        return
+    flops_per_item = 2 * CFG["K"] * CFG["D"] * CFG["L"]
+    achieved = flops_per_item * B / (q_ms * 1e-3) / 1e12
+    line = {
+        "metric": "decoder-train tokens/sec + RQ-VAE items/sec at 1/2/4/8 MI355X; achieved HBM %",
+        "value": round(ws * B * args.steps / elapsed, 1),
+        "unit": "items/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded unit-norm 768-d items resident in HBM; random-init MLPs, k-means-like codebooks)",
+        "config": {"workload": "RQ-VAE MovieLens-32M train step (configs[1]): 768->[512,256,128]->D64, K256, L3, "
+                               "ROTATION_TRICK, AdamW", "global_batch": ws * B, "per_gpu_batch": B,
+                   "parallelism": f"dp{ws}"},
+        "roofline": {"kernel": "rq_quantize_fwd", "bound": "mfma", "achieved": round(achieved, 3),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": None, "launch_ms": round(q_ms, 4), "launches": q_n,
+                     "flops_per_launch": flops_per_item * B},
+        "loss_last": round(loss, 5),
+    }
+    line.update(extras)
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.barrier()
+
+
+def measure_extras(model, device, x):
+    """Secondary rows of BASELINE C2 on rank 0 (outside the timed region)."""
+    from rqvae_hip import ops
+    from data.schemas import SeqBatch
+    out = {}
+    sync = torch.cuda.synchronize
+    # quantize-only fwd+bwd (items quantized / s)
+    with torch.no_grad():
+        res0 = model.encode(x)
+    cbs = torch.stack([l.embedding.weight.detach() for l in model.layers]).requires_grad_(True)
+    r0 = res0.clone().requires_grad_(True)
+
+    def qstep():
+        emb, res, ids, ql, es = ops.rq_quantize(r0, cbs, ops.MODE_ROTATION, 0.25)
+        (es.sum() + ql.sum()).backward()
+    dt = time_region(qstep, 10, 3, sync)
+    out["quantize_fwd_bwd_items_per_s"] = round(10 * x.shape[0] / dt, 1)
+    # eval tokenization (encoder + eval quantize)
+    model.eval()
+
+    def tok():
+        with torch.no_grad():
+            model.get_semantic_ids(x)
+    dt = time_region(tok, 10, 3, sync)
+    out["eval_tokenize_items_per_s"] = round(10 * x.shape[0] / dt, 1)
+    model.train()
+    # config batch B=64 step latency (eager)
+    xs = x[:64].contiguous()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True)
+
+    def small():
+        opt.zero_grad(set_to_none=False)
+        o = model(SeqBatch(None, None, None, xs, None, None), gumbel_t=0.2)
+        o.loss.backward()
+        opt.step()
+    dt = time_region(small, 20, 5, sync)
+    out["b64_step_ms"] = round(dt / 20 * 1e3, 3)
+    return out
+
+
+if __name__ == "__main__":
+    main()

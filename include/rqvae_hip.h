@@ -1,0 +1,105 @@
+/* rqvae_hip.h — C ABI of the MI355X (gfx950) RQ-VAE training hot path.
+ *
+ * Library: rq-vae-recommender_amd/rqvae_hip/librqvae_hip.so (built by `make -C
+ * rq-vae-recommender_amd/csrc`). Plain pointers and sizes only; no framework types.
+ *
+ * Conventions (every entry point):
+ *   - All data pointers are DEVICE pointers owned by the caller; kernels never allocate/free.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream). Calls are asynchronous,
+ *     stream-ordered, never synchronise the host, and are safe to capture in a hipGraph.
+ *   - Return 0 on success, a hipError_t (> 0) on a launch/runtime failure, or a negative
+ *     argument-check code (-22); rq_last_error() returns the message (thread-local).
+ *   - Stateless and re-entrant (autograd may call backward from another host thread).
+ *
+ * The reference (AdamLTy/RQ-VAE-Recommender) has no FFI of its own: its hot path is Python
+ * over ATen + one Triton kernel. Each entry point below names the reference function whose
+ * semantics it implements; INTEGRATION.md shows the ctypes binding used by the drop-in
+ * nn.Module / autograd.Function surface.
+ */
+#ifndef RQVAE_HIP_H_
+#define RQVAE_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Library identification / errors. */
+int rq_abi_version(void);
+const char* rq_last_error(void);
+
+/* Quantize modes (modules/quantize.py:16-20 QuantizeForwardMode; 0 = eval path :148-150). */
+#define RQ_MODE_EVAL 0
+#define RQ_MODE_STE 2
+#define RQ_MODE_ROTATION 3
+
+/* out[r] = sum_d rows[r][d]^2 for r < n — the (codebook.T**2).sum(0) term of the L2 distance
+ * (modules/quantize.py:110). rows: (n, D) fp32. */
+int rq_codebook_sqnorm(const float* rows, int64_t n, int64_t D, float* out, void* stream);
+
+/* Fused L-level residual quantization forward = RqVae.get_semantic_ids' level loop
+ * (modules/rqvae.py:114-138) over Quantize.forward (modules/quantize.py:99-156, L2 distance,
+ * out_proj = Identity) with QuantizeLoss (modules/loss.py:34-42).
+ *   x (B,D) fp32 encoder output; codebooks (L,K,D); cb_sqnorm (L,K) from rq_codebook_sqnorm.
+ *   mode RQ_MODE_ROTATION / RQ_MODE_STE (training) or RQ_MODE_EVAL; beta = commitment weight.
+ * Outputs: ids (B,L) int64; emb_out (L,B,D); residuals (L,B,D) with residuals[0] = x;
+ *   qloss (B,) = sum_l loss_l; emb_sum (B,D) = sum_l emb_out_l, or NULL.
+ * Requires D a power of two in [8, 1024], 1 <= K <= 2^20, 1 <= L <= 64. Ids are the lowest
+ * index among equal minimum distances (torch.min semantics, quantize.py:121). */
+int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
+                    int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
+                    float* emb_sum, void* stream);
+
+/* Backward of rq_quantize_fwd (the autograd graph of modules/quantize.py:99-156 chained by
+ * modules/rqvae.py:129): grads of emb_out (g_emb, (L,B,D) or NULL), of sum_l emb_out
+ * (g_emb_sum, (B,D) or NULL), of residuals (g_res, (L,B,D) or NULL) and of qloss (g_qloss,
+ * (B,) or NULL). Writes grad_x (B,D) and grad_codebooks (L,K,D) (every element written).
+ * The codebook gradient is reduced in ascending row order per codeword (stable counting
+ * sort + segmented sum): bitwise deterministic. K <= 4096.
+ * workspace: device scratch of at least rq_quantize_bwd_workspace(B,D,K,L) bytes. */
+size_t rq_quantize_bwd_workspace(int64_t B, int64_t D, int64_t K, int64_t L);
+int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* codebooks, int64_t B, int64_t D, int64_t K,
+                    int64_t L, int mode, float beta, const float* g_emb, const float* g_emb_sum, const float* g_res,
+                    const float* g_qloss, float* grad_x, float* grad_codebooks, void* workspace, size_t ws_bytes,
+                    void* stream);
+
+/* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
+ * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
+ * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */
+size_t rq_unique_workspace(int64_t B);
+int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
+                    size_t ws_bytes, void* stream);
+
+/* Jagged (NJT) conversion — ops/triton/jagged.py. dtype: 0 fp32, 1 bf16, 2 fp16.
+ * jagged_offsets: offsets (B+1) int64 = [0, cumsum(clamp(lengths, 0, N))]   (jagged.py:30-33)
+ * jagged_from_padded: values[offsets[b]+t] = x[b,t] (+1-1 rounding when add_one_sub_one, as
+ *   `target + 1 - 1` at jagged.py:65), x (B,N,D) contiguous            (jagged.py:11-66,92-125)
+ * jagged_to_padded: x = zeros(B,N,D); x[b,t] = values[offsets[b]+t] for t < len_b (jagged.py:69-77)
+ * B <= 65535 per call. */
+int jagged_offsets(const int64_t* lengths, int64_t B, int64_t N, int64_t* offsets, void* stream);
+int jagged_from_padded(const void* x, int64_t B, int64_t N, int64_t D, const int64_t* offsets, void* values, int dtype,
+                       int add_one_sub_one, void* stream);
+int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int64_t N, int64_t D, void* x, int dtype,
+                     void* stream);
+
+/* Varlen multi-head attention on packed rows = F.scaled_dot_product_attention on NJT q/k/v
+ * (modules/transformer/attention.py:113-124), dropout 0, is_causal top-left.
+ *   q[t][h][d] at q + t*sq + h*hd + d (likewise k, v, out, dout, dq, dk, dv with their strides);
+ *   cu_q, cu_k (B+1) int64 offsets; max_q / max_k >= the longest segment (grid bound);
+ *   lse (H, Tq) fp32 log-sum-exp per query (written by fwd, read by bwd). hd in {32, 64, 128}.
+ * Backward is deterministic (no atomics): dk/dv per key block, dq per query block. */
+int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                    const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream);
+int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
+                    int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
+                    const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
+                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RQVAE_HIP_H_ */

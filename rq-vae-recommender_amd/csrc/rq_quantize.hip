@@ -1,0 +1,599 @@
+// Residual quantization for the RQ-VAE hot path — fused L-level forward, its VJP, and the
+// deterministic codebook-gradient reduction. gfx950 / wave64 / fp32 MFMA.
+//
+// Reference semantics (AdamLTy/RQ-VAE-Recommender):
+//   modules/quantize.py:99-156  Quantize.forward (L2 dist :108-112, argmin :121,
+//                               STE :130-132, rotation trick :133-142 with :34-45, eval :148-150)
+//   modules/loss.py:34-42       QuantizeLoss (per-row, beta = commitment_weight)
+//   modules/rqvae.py:114-138    get_semantic_ids: res_{l+1} = res_l - emb_out_l over L levels
+//
+// Layout in HBM (row-major, fp32):
+//   x          (B, D)      encoder output = level-0 residual
+//   codebooks  (L, K, D)   one nn.Embedding weight per level (out_proj = Identity)
+//   cb_sqnorm  (L, K)      |c|^2 per codeword (rq_codebook_sqnorm)
+//   ids        (B, L)      int64 semantic ids
+//   emb_out    (L, B, D)   per-level quantized output (returned to Python as a (B,D,L) view)
+//   residuals  (L, B, D)   res_l fed to level l (residuals[0] = x)
+//   qloss      (B,)        sum over levels of the per-row VQ loss
+//   emb_sum    (B, D)      sum_l emb_out_l (decoder input), optional
+//
+// Forward kernel: one workgroup = 4 waves = TB=128 items. Per level: the distance GEMM
+// C_l (K x D) . X^T (D x 128) runs on v_mfma_f32_32x32x2_f32 (exact fp32 fma chain, no xf32
+// on gfx950) with codewords on the MFMA row axis and items on the lane axis, so each lane
+// owns one item's distances and the argmin is a register scan (+1 lane swap) — no cross-lane
+// reduction per codeword. Codebook chunks (NB=128 codewords x BK) and item chunks are staged
+// through LDS with conflict-free padded rows read by ds_read_b128. The row epilogue
+// (gather, rotation trick, VQ loss, residual update) runs LPI lanes per item, all levels
+// chained inside the launch so the residual never round-trips through a separate kernel.
+#include "common.h"
+
+#include <math.h>
+
+namespace rqhip {
+
+constexpr int kTB = 128;   // items per workgroup (4 waves x 32)
+constexpr int kNB = 128;   // codewords per LDS chunk (4 MFMA row tiles)
+
+enum Mode { kEval = 0, kGumbel = 1, kSte = 2, kRotation = 3 };
+
+// ---------------------------------------------------------------------------------------
+// |c|^2 per codeword: one wave per row.
+__global__ void __launch_bounds__(256) rq_sqnorm_kernel(const float* __restrict__ rows, int64_t n, int D,
+                                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const float* p = rows + r * D;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += p[d] * p[d];
+  s = group_sum<64>(s);
+  if (lane == 0) out[r] = s;
+}
+
+// Rotation-trick constants for one item held by an aligned group of LPI lanes (EPL elems each).
+template <int LPI, int EPL>
+struct RowRot {
+  float u[EPL], q[EPL], w[EPL];
+  float lam;
+  __device__ __forceinline__ void build(const float (&x)[EPL], const float (&e)[EPL], float xn, float en) {
+    // u = x/(|x|+1e-8), q = e/(|e|+1e-8), w = normalize(u+q, eps 1e-6)   (quantize.py:34-39,135-138)
+    const float xd = xn + 1e-8f, ed = en + 1e-8f;
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      u[k] = x[k] / xd;
+      q[k] = e[k] / ed;
+      const float s = u[k] + q[k];
+      w[k] = s;
+      s2 += s * s;
+    }
+    s2 = group_sum<LPI>(s2);
+    const float sn = fmaxf(sqrtf(s2), 1e-6f);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) w[k] = w[k] / sn;
+    lam = en / (xn + 1e-6f);   // (|emb| / (|x| + 1e-6)).detach()   (quantize.py:140-142)
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// Fused L-level forward.
+template <int BK, int LPI, int EPL>
+__global__ void __launch_bounds__(256, 2)
+rq_fwd_kernel(const float* __restrict__ x, int B, int D, const float* __restrict__ cbs,
+              const float* __restrict__ csq, int K, int L, int mode, float beta,
+              int64_t* __restrict__ ids, float* __restrict__ emb_out, float* __restrict__ res,
+              float* __restrict__ qloss, float* __restrict__ emb_sum) {
+  constexpr int LDA = BK + 4;             // padded LDS row (16-B aligned, ds_read_b128 conflict-free)
+  constexpr int G = 64 / LPI;             // items processed concurrently per wave in the epilogue
+  __shared__ __attribute__((aligned(16))) float smem[(kNB + kTB) * LDA + kNB + 3 * kTB];
+  float* A_s = smem;                       // codeword chunk  [kNB][LDA]
+  float* X_s = A_s + kNB * LDA;            // item chunk      [kTB][LDA]
+  float* cs_s = X_s + kTB * LDA;           // |c|^2 chunk     [kNB]
+  float* xsq_s = cs_s + kNB;               // |res_l|^2       [kTB]
+  float* ql_s = xsq_s + kTB;               // running qloss   [kTB]
+  int* id_s = reinterpret_cast<int*>(ql_s + kTB);  //        [kTB]
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
+  const int row0 = blockIdx.x * kTB;
+  const int64_t BD = (int64_t)B * D;
+  const int sub = lane % LPI, grp = lane / LPI;
+
+  // Prologue: residuals[0] = x, |x|^2, qloss accumulator.
+  for (int it = 0; it < 32 / G; ++it) {
+    const int jl = wave * 32 + it * G + grp;
+    const int b = row0 + jl;
+    const bool valid = b < B;
+    const int64_t o = (int64_t)(valid ? b : B - 1) * D + sub * EPL;
+    float xv[EPL];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + o + k);
+      xv[k] = v.x; xv[k + 1] = v.y; xv[k + 2] = v.z; xv[k + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) s += xv[k] * xv[k];
+    s = group_sum<LPI>(s);
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<float4*>(res + o + k) = make_float4(xv[k], xv[k + 1], xv[k + 2], xv[k + 3]);
+    }
+    if (sub == 0) { xsq_s[jl] = s; ql_s[jl] = 0.f; }
+  }
+
+  for (int l = 0; l < L; ++l) {
+    const float* src = res + (int64_t)l * BD;
+    const float* cb = cbs + (int64_t)l * K * D;
+    const float* cq = csq + (int64_t)l * K;
+    float best_d = INFINITY;
+    int best_i = 0;
+    __syncthreads();   // residual rows of level l written by every wave of the block
+    const float xs = xsq_s[wave * 32 + (lane & 31)];
+
+    for (int n0 = 0; n0 < K; n0 += kNB) {
+      floatx16 acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+      for (int k0 = 0; k0 < D; k0 += BK) {
+        __syncthreads();   // previous chunk fully consumed
+        constexpr int F4 = BK / 4;   // float4 per staged row
+        for (int f = tid; f < kNB * F4; f += 256) {
+          const int r = f / F4, c = (f % F4) * 4;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (n0 + r < K) v = *reinterpret_cast<const float4*>(cb + (int64_t)(n0 + r) * D + k0 + c);
+          *reinterpret_cast<float4*>(A_s + r * LDA + c) = v;
+        }
+        for (int f = tid; f < kTB * F4; f += 256) {
+          const int r = f / F4, c = (f % F4) * 4;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (row0 + r < B) v = *reinterpret_cast<const float4*>(src + (int64_t)(row0 + r) * D + k0 + c);
+          *reinterpret_cast<float4*>(X_s + r * LDA + c) = v;
+        }
+        if (k0 == 0 && tid < kNB) cs_s[tid] = (n0 + tid < K) ? cq[n0 + tid] : 0.f;
+        __syncthreads();
+
+        // Lane half h supplies logical k=h of every MFMA; physical k = h*BK/2 + step, the
+        // same permutation for both operands, so sum_k A[i][k] B[k][j] is unchanged.
+        const float* bp = X_s + (wave * 32 + (lane & 31)) * LDA + h * (BK / 2);
+        const float* ap = A_s + (lane & 31) * LDA + h * (BK / 2);
+#pragma unroll
+        for (int s4 = 0; s4 < BK / 2; s4 += 4) {
+          const float4 bv = *reinterpret_cast<const float4*>(bp + s4);
+          float4 av[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) av[t] = *reinterpret_cast<const float4*>(ap + t * 32 * LDA + s4);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t].x, bv.x, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t].y, bv.y, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t].z, bv.z, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t].w, bv.w, acc[t], 0, 0, 0);
+          }
+        }
+      }
+      // dist = (|x|^2 + |c|^2) - 2 x.c  (quantize.py:108-112); C/D map: row i = codeword,
+      // col = lane&31 = item. Lowest index wins ties (torch min, quantize.py:121).
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int il = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int i = n0 + il;
+          const float d = (xs + cs_s[il]) - 2.f * acc[t][r];
+          if (i < K && (d < best_d || (d == best_d && i < best_i))) { best_d = d; best_i = i; }
+        }
+      }
+    }
+    {
+      const float od = __shfl_xor(best_d, 32, 64);
+      const int oi = __shfl_xor(best_i, 32, 64);
+      if (od < best_d || (od == best_d && oi < best_i)) { best_d = od; best_i = oi; }
+      if (h == 0) id_s[wave * 32 + lane] = best_i;
+    }
+    __syncthreads();
+
+    // Row epilogue: gather codeword, emb_out per mode, VQ loss, next residual.
+    float* eo = emb_out + (int64_t)l * BD;
+    float* rn = res + (int64_t)(l + 1) * BD;
+    for (int it = 0; it < 32 / G; ++it) {
+      const int jl = wave * 32 + it * G + grp;
+      const int b = row0 + jl;
+      const bool valid = b < B;
+      const int64_t o = (int64_t)(valid ? b : B - 1) * D + sub * EPL;
+      const int id = id_s[jl];
+      const float* cr = cb + (int64_t)id * D + sub * EPL;
+      float xv[EPL], ev[EPL], out[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(src + o + k);
+        const float4 c = *reinterpret_cast<const float4*>(cr + k);
+        xv[k] = a.x; xv[k + 1] = a.y; xv[k + 2] = a.z; xv[k + 3] = a.w;
+        ev[k] = c.x; ev[k + 1] = c.y; ev[k + 2] = c.z; ev[k + 3] = c.w;
+      }
+      float dl = 0.f;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) { const float t = xv[k] - ev[k]; dl += t * t; }
+      dl = group_sum<LPI>(dl);
+      if (mode == kRotation) {
+        float x2 = 0.f, e2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) { x2 += xv[k] * xv[k]; e2 += ev[k] * ev[k]; }
+        x2 = group_sum<LPI>(x2);
+        e2 = group_sum<LPI>(e2);
+        RowRot<LPI, EPL> rr;
+        rr.build(xv, ev, sqrtf(x2), sqrtf(e2));
+        float ew = 0.f, eu = 0.f;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) { ew += xv[k] * rr.w[k]; eu += xv[k] * rr.u[k]; }
+        ew = group_sum<LPI>(ew);
+        eu = group_sum<LPI>(eu);
+        // out = e - 2 (e.w) w + 2 (e.u) q, then * lam   (quantize.py:41-45, :140-142)
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) out[k] = ((xv[k] - 2.f * (ew * rr.w[k])) + 2.f * (eu * rr.q[k])) * rr.lam;
+      } else if (mode == kSte) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) out[k] = xv[k] + (ev[k] - xv[k]);   // x + (emb - x).detach()
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) out[k] = ev[k];
+      }
+      float r2 = 0.f;
+      float nr[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) { nr[k] = xv[k] - out[k]; r2 += nr[k] * nr[k]; }
+      r2 = group_sum<LPI>(r2);
+      if (valid) {
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4) {
+          *reinterpret_cast<float4*>(eo + o + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+          if (l + 1 < L)
+            *reinterpret_cast<float4*>(rn + o + k) = make_float4(nr[k], nr[k + 1], nr[k + 2], nr[k + 3]);
+        }
+        if (emb_sum != nullptr && l == L - 1) {
+          // sum over the level axis in level order: ((e0 + e1) + e2) ...
+#pragma unroll
+          for (int k = 0; k < EPL; k += 4) {
+            float4 s = *reinterpret_cast<const float4*>(emb_out + o + k);
+            for (int m = 1; m < L; ++m) {
+              const float4 v = (m == l) ? make_float4(out[k], out[k + 1], out[k + 2], out[k + 3])
+                                        : *reinterpret_cast<const float4*>(emb_out + (int64_t)m * BD + o + k);
+              s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+            if (L == 1) s = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+            *reinterpret_cast<float4*>(emb_sum + o + k) = s;
+          }
+        }
+        if (sub == 0) {
+          ids[(int64_t)b * L + l] = id;
+          const float lq = dl + beta * dl;   // emb_loss + beta * query_loss (equal values fwd)
+          const float acc_l = ql_s[jl] + lq;
+          ql_s[jl] = acc_l;
+          xsq_s[jl] = r2;
+          if (l == L - 1) qloss[b] = acc_l;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Backward, per item: walk the levels last -> first.
+//   g_out_l = g_emb_l + g_emb_sum - g_{res_{l+1}}
+//   rotation: g_x = lam*g - 2 ((lam*g).w) w + 2 ((lam*g).q) u   (autograd order of :41-45,140)
+//   ste:      g_x = g_out_l ;  eval: g_x = 0, codeword row gets g_out_l
+//   VQ loss:  g_x += 2 beta gl (x - e) ; codeword += 2 gl (e - x)
+//   g_{res_l} = g_{res_{l+1}} + g_x (+ g_res_l)
+// Codeword contributions go to `contrib` (L,B,D); rq_cb_segsum reduces them per codeword.
+template <int LPI, int EPL>
+__global__ void __launch_bounds__(256)
+rq_bwd_rows_kernel(const float* __restrict__ res, const int64_t* __restrict__ ids, const float* __restrict__ cbs,
+                   int B, int D, int K, int L, int mode, float beta, const float* __restrict__ g_emb,
+                   const float* __restrict__ g_emb_sum, const float* __restrict__ g_res,
+                   const float* __restrict__ g_qloss, float* __restrict__ grad_x, float* __restrict__ contrib) {
+  constexpr int G = 64 / LPI;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPI, grp = lane / LPI;
+  const int b = (blockIdx.x * 4 + wave) * G + grp;
+  const bool valid = b < B;
+  const int bb = valid ? b : B - 1;
+  const int64_t BD = (int64_t)B * D;
+  const int64_t o = (int64_t)bb * D + sub * EPL;
+  const float gl = g_qloss ? g_qloss[bb] : 0.f;
+  float gn[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) gn[k] = 0.f;
+  for (int l = L - 1; l >= 0; --l) {
+    int id = (int)ids[(int64_t)bb * L + l];
+    const float* cr = cbs + ((int64_t)l * K + id) * D + sub * EPL;
+    float xv[EPL], ev[EPL], go[EPL], gx[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(res + (int64_t)l * BD + o + k);
+      const float4 c = *reinterpret_cast<const float4*>(cr + k);
+      xv[k] = a.x; xv[k + 1] = a.y; xv[k + 2] = a.z; xv[k + 3] = a.w;
+      ev[k] = c.x; ev[k + 1] = c.y; ev[k + 2] = c.z; ev[k + 3] = c.w;
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) go[k] = 0.f;
+    if (g_emb_sum) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) go[k] += g_emb_sum[o + k];
+    }
+    if (g_emb) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) go[k] += g_emb[(int64_t)l * BD + o + k];
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) go[k] -= gn[k];
+
+    if (mode == kRotation) {
+      float x2 = 0.f, e2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) { x2 += xv[k] * xv[k]; e2 += ev[k] * ev[k]; }
+      x2 = group_sum<LPI>(x2);
+      e2 = group_sum<LPI>(e2);
+      RowRot<LPI, EPL> rr;
+      rr.build(xv, ev, sqrtf(x2), sqrtf(e2));
+      float gw = 0.f, gq = 0.f, gs[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) { gs[k] = go[k] * rr.lam; gw += gs[k] * rr.w[k]; gq += gs[k] * rr.q[k]; }
+      gw = group_sum<LPI>(gw);
+      gq = group_sum<LPI>(gq);
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) gx[k] = (gs[k] - 2.f * (gw * rr.w[k])) + 2.f * (gq * rr.u[k]);
+    } else if (mode == kSte) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) gx[k] = go[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) gx[k] = 0.f;
+    }
+    float cc[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      gx[k] += (2.f * beta * gl) * (xv[k] - ev[k]);
+      cc[k] = (2.f * gl) * (ev[k] - xv[k]);
+      if (mode == kEval) cc[k] += go[k];
+      gn[k] = gn[k] + gx[k];
+      if (g_res) gn[k] += g_res[(int64_t)l * BD + o + k];
+    }
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<float4*>(contrib + (int64_t)l * BD + o + k) = make_float4(cc[k], cc[k + 1], cc[k + 2], cc[k + 3]);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4)
+      *reinterpret_cast<float4*>(grad_x + o + k) = make_float4(gn[k], gn[k + 1], gn[k + 2], gn[k + 3]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Stable counting sort of ids per level (keys < K <= 4096): per-block histograms, a
+// key-major exclusive scan, then an in-order scatter (ballot ranks) — deterministic order
+// (ascending row index within each key).
+constexpr int kSortRows = 256;   // rows per sort block
+
+__global__ void __launch_bounds__(256) sort_hist_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
+                                                         int nblk, int* __restrict__ hist) {
+  extern __shared__ int cnt[];
+  const int l = blockIdx.y, blk = blockIdx.x;
+  for (int k = threadIdx.x; k < K; k += 256) cnt[k] = 0;
+  __syncthreads();
+  const int r = blk * kSortRows + threadIdx.x;
+  if (r < B) atomicAdd(&cnt[(int)ids[(int64_t)r * L + l]], 1);
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += 256) hist[((int64_t)l * K + k) * nblk + blk] = cnt[k];
+}
+
+// Exclusive scan of hist[l] (K*nblk ints) in place; key_off[l][k] = first slot of key k.
+__global__ void __launch_bounds__(1024) sort_scan_kernel(int* __restrict__ hist, int K, int nblk, int B,
+                                                          int* __restrict__ key_off) {
+  __shared__ int part[1024];
+  const int l = blockIdx.x, t = threadIdx.x;
+  const int64_t n = (int64_t)K * nblk;
+  int* h = hist + (int64_t)l * n;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t a = t * per, e = a + per < n ? a + per : n;
+  int s = 0;
+  for (int64_t i = a; i < e; ++i) s += h[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan of the partials
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (int64_t i = a; i < e; ++i) { const int c = h[i]; h[i] = run; run += c; }
+  __syncthreads();
+  for (int k = t; k < K; k += 1024) key_off[(int64_t)l * (K + 1) + k] = h[(int64_t)k * nblk];
+  if (t == 0) key_off[(int64_t)l * (K + 1) + K] = B;
+}
+
+__global__ void __launch_bounds__(64) sort_scatter_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
+                                                          int nblk, const int* __restrict__ hist,
+                                                          int* __restrict__ perm) {
+  extern __shared__ int base[];
+  const int l = blockIdx.y, blk = blockIdx.x, lane = threadIdx.x;
+  for (int k = lane; k < K; k += 64) base[k] = hist[((int64_t)l * K + k) * nblk + blk];
+  __syncthreads();
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int c = 0; c < kSortRows; c += 64) {
+    const int r = blk * kSortRows + c + lane;
+    const bool v = r < B;
+    const int key = v ? (int)ids[(int64_t)r * L + l] : -1;
+    unsigned long long rem = __ballot(v);
+    while (rem) {
+      const int leader = __builtin_ctzll(rem);
+      const int k = __shfl(key, leader, 64);
+      const unsigned long long m = __ballot(v && key == k) & rem;
+      if (v && key == k) perm[(int64_t)l * B + base[k] + __popcll(m & lt)] = r;
+      __syncthreads();   // single wave: orders the LDS read above before the update below
+      if (lane == leader) base[k] += __popcll(m);
+      __syncthreads();
+      rem &= ~m;
+    }
+  }
+}
+
+// grad_cb[l][k] = sum over rows with id k (ascending row order) of contrib[l][row].
+__global__ void __launch_bounds__(64) rq_cb_segsum_kernel(const float* __restrict__ contrib, const int* __restrict__ perm,
+                                                          const int* __restrict__ key_off, int B, int D, int K,
+                                                          float* __restrict__ grad_cb) {
+  const int k = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
+  const int a = key_off[(int64_t)l * (K + 1) + k], e = key_off[(int64_t)l * (K + 1) + k + 1];
+  const int* p = perm + (int64_t)l * B;
+  const float* cbase = contrib + (int64_t)l * B * D;
+  float* out = grad_cb + ((int64_t)l * K + k) * D;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    if (d >= D) break;
+    float acc = 0.f;
+    int i = a;
+    for (; i + 4 <= e; i += 4) {
+      const float v0 = cbase[(int64_t)p[i] * D + d], v1 = cbase[(int64_t)p[i + 1] * D + d];
+      const float v2 = cbase[(int64_t)p[i + 2] * D + d], v3 = cbase[(int64_t)p[i + 3] * D + d];
+      acc += v0; acc += v1; acc += v2; acc += v3;
+    }
+    for (; i < e; ++i) acc += cbase[(int64_t)p[i] * D + d];
+    out[d] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+static bool row_split(int D, int& lpi, int& epl) {
+  if (D < 8 || D > 1024 || (D & (D - 1)) != 0) return false;
+  lpi = D / 4 < 64 ? D / 4 : 64;
+  epl = D / lpi;
+  return true;
+}
+
+template <int BK, int LPI, int EPL>
+static void launch_fwd(dim3 g, hipStream_t s, const float* x, int B, int D, const float* cbs, const float* csq, int K,
+                       int L, int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
+  hipLaunchKernelGGL((rq_fwd_kernel<BK, LPI, EPL>), g, dim3(256), 0, s, x, B, D, cbs, csq, K, L, mode, beta, ids, eo,
+                     res, ql, es);
+}
+
+template <int LPI, int EPL>
+static void launch_bwd(int B, hipStream_t s, const float* res, const int64_t* ids, const float* cbs, int D, int K,
+                       int L, int mode, float beta, const float* ge, const float* ges, const float* gr, const float* gq,
+                       float* gx, float* contrib) {
+  constexpr int G = 64 / LPI;
+  dim3 g((B + 4 * G - 1) / (4 * G));
+  hipLaunchKernelGGL((rq_bwd_rows_kernel<LPI, EPL>), g, dim3(256), 0, s, res, ids, cbs, B, D, K, L, mode, beta, ge, ges,
+                     gr, gq, gx, contrib);
+}
+
+}  // namespace rqhip
+
+using namespace rqhip;
+
+extern "C" {
+
+int rq_codebook_sqnorm(const float* rows, int64_t n, int64_t D, float* out, void* stream) {
+  RQ_CHECK_ARG(rows && out && n >= 0 && D > 0, "rq_codebook_sqnorm: bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rq_sqnorm_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, rows, n,
+                     (int)D, out);
+  RQ_LAUNCH_CHECK("rq_codebook_sqnorm");
+  return 0;
+}
+
+int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
+                    int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
+                    float* emb_sum, void* stream) {
+  int lpi, epl;
+  RQ_CHECK_ARG(x && codebooks && cb_sqnorm && ids && emb_out && residuals && qloss, "rq_quantize_fwd: null pointer");
+  RQ_CHECK_ARG(row_split((int)D, lpi, epl), "rq_quantize_fwd: D=%lld must be a power of two in [8, 1024]", (long long)D);
+  RQ_CHECK_ARG(K >= 1 && K <= (1 << 20) && L >= 1 && L <= 64, "rq_quantize_fwd: bad K=%lld / L=%lld", (long long)K,
+               (long long)L);
+  RQ_CHECK_ARG(B >= 0 && B < (1ll << 31) && B * D < (1ll << 40), "rq_quantize_fwd: bad B=%lld", (long long)B);
+  RQ_CHECK_ARG(mode == kEval || mode == kSte || mode == kRotation, "rq_quantize_fwd: mode %d has no fused kernel", mode);
+  if (B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g((unsigned)((B + kTB - 1) / kTB));
+  const int b = (int)B, d = (int)D, k = (int)K, l = (int)L;
+  switch (D) {
+#define RQ_FWD_CASE(DD, BK, LPI, EPL) \
+  case DD: launch_fwd<BK, LPI, EPL>(g, s, x, b, d, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;
+    RQ_FWD_CASE(8, 8, 2, 4)
+    RQ_FWD_CASE(16, 16, 4, 4)
+    RQ_FWD_CASE(32, 32, 8, 4)
+    RQ_FWD_CASE(64, 64, 16, 4)
+    RQ_FWD_CASE(128, 64, 32, 4)
+    RQ_FWD_CASE(256, 64, 64, 4)
+    RQ_FWD_CASE(512, 64, 64, 8)
+    RQ_FWD_CASE(1024, 64, 64, 16)
+#undef RQ_FWD_CASE
+    default: RQ_CHECK_ARG(false, "rq_quantize_fwd: unsupported D");
+  }
+  RQ_LAUNCH_CHECK("rq_quantize_fwd");
+  return 0;
+}
+
+size_t rq_quantize_bwd_workspace(int64_t B, int64_t D, int64_t K, int64_t L) {
+  const int64_t nblk = (B + kSortRows - 1) / kSortRows;
+  size_t bytes = 0;
+  bytes += (size_t)(L * B * D) * sizeof(float);          // contrib
+  bytes += (size_t)(L * K * nblk) * sizeof(int);         // hist / scanned positions
+  bytes += (size_t)(L * (K + 1)) * sizeof(int);          // key offsets
+  bytes += (size_t)(L * B) * sizeof(int);                // perm
+  return bytes + 256;
+}
+
+int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* codebooks, int64_t B, int64_t D, int64_t K,
+                    int64_t L, int mode, float beta, const float* g_emb, const float* g_emb_sum, const float* g_res,
+                    const float* g_qloss, float* grad_x, float* grad_codebooks, void* workspace, size_t ws_bytes,
+                    void* stream) {
+  int lpi, epl;
+  RQ_CHECK_ARG(residuals && ids && codebooks && grad_x && grad_codebooks, "rq_quantize_bwd: null pointer");
+  RQ_CHECK_ARG(row_split((int)D, lpi, epl), "rq_quantize_bwd: D=%lld must be a power of two in [8, 1024]", (long long)D);
+  RQ_CHECK_ARG(K >= 1 && K <= 4096 && L >= 1 && L <= 64, "rq_quantize_bwd: bad K/L");
+  RQ_CHECK_ARG(mode == kEval || mode == kSte || mode == kRotation, "rq_quantize_bwd: bad mode %d", mode);
+  RQ_CHECK_ARG(B >= 0 && B < (1ll << 31), "rq_quantize_bwd: bad B");
+  RQ_CHECK_ARG(workspace && ws_bytes >= rq_quantize_bwd_workspace(B, D, K, L), "rq_quantize_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int b = (int)B, d = (int)D, k = (int)K, l = (int)L;
+  const int nblk = (b + kSortRows - 1) / kSortRows;
+  char* w = (char*)workspace;
+  float* contrib = (float*)w; w += (size_t)(L * B * D) * sizeof(float);
+  int* hist = (int*)w;        w += (size_t)(L * K * nblk) * sizeof(int);
+  int* key_off = (int*)w;     w += (size_t)(L * (K + 1)) * sizeof(int);
+  int* perm = (int*)w;
+  if (B == 0) {
+    RQ_HIP(hipMemsetAsync(grad_codebooks, 0, (size_t)(L * K * D) * sizeof(float), s));
+    return 0;
+  }
+  switch (D) {
+#define RQ_BWD_CASE(DD, LPI, EPL) \
+  case DD: launch_bwd<LPI, EPL>(b, s, residuals, ids, codebooks, d, k, l, mode, beta, g_emb, g_emb_sum, g_res, g_qloss, grad_x, contrib); break;
+    RQ_BWD_CASE(8, 2, 4)
+    RQ_BWD_CASE(16, 4, 4)
+    RQ_BWD_CASE(32, 8, 4)
+    RQ_BWD_CASE(64, 16, 4)
+    RQ_BWD_CASE(128, 32, 4)
+    RQ_BWD_CASE(256, 64, 4)
+    RQ_BWD_CASE(512, 64, 8)
+    RQ_BWD_CASE(1024, 64, 16)
+#undef RQ_BWD_CASE
+    default: RQ_CHECK_ARG(false, "rq_quantize_bwd: unsupported D");
+  }
+  RQ_LAUNCH_CHECK("rq_bwd_rows");
+  hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, l), dim3(256), k * sizeof(int), s, ids, b, l, k, nblk, hist);
+  hipLaunchKernelGGL(sort_scan_kernel, dim3(l), dim3(1024), 0, s, hist, k, nblk, b, key_off);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, l), dim3(64), k * sizeof(int), s, ids, b, l, k, nblk, hist, perm);
+  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, l), dim3(64), 0, s, contrib, perm, key_off, b, d, k, grad_codebooks);
+  RQ_LAUNCH_CHECK("rq_codebook_grad");
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+"""Lloyd k-means for the lazy codebook init — reference semantics: init/kmeans.py:8-74.
+
+Same contract: ``kmeans_init_(weight, x)`` overwrites the (K, D) weight with centroids of x;
+``Kmeans(k, max_iters=None, stop_threshold=1e-10).run(x) -> KmeansOutput(centroids, assignment)``;
+init = rows ``np.random.choice(B, k, replace=False)`` (global numpy RNG, as the reference);
+empty clusters take a random row (torch.randint); stop when the largest centroid move is below
+``stop_threshold`` or after ``max_iters``.
+
+MI355X path: the assignment step reuses the fused quantize kernel in eval mode (MFMA fp32
+distance + argmin, O(B·K) memory) instead of materialising the B x K x D difference tensor
+(20000 x 256 x 64 fp32 = 1.3 GB per Lloyd iteration in the reference); the centroid update is a
+segmented mean (index_add_ + bincount) instead of a Python loop over K clusters.
+Argmin ties resolve to the lowest index in both; distances use |x|^2 + |c|^2 - 2 x.c instead of
+sum((x - c)^2), so assignments can differ only on fp32 near-ties.
+"""
+from typing import NamedTuple
+
+import numpy as np
+import torch
+
+from rqvae_hip import ops as hip_ops
+
+
+def kmeans_init_(tensor: torch.Tensor, x: torch.Tensor):
+    assert tensor.dim() == 2
+    assert x.dim() == 2
+    with torch.no_grad():
+        k, _ = tensor.shape
+        out = Kmeans(k=k).run(x)
+        tensor.data.copy_(out.centroids)
+
+
+class KmeansOutput(NamedTuple):
+    centroids: torch.Tensor
+    assignment: torch.Tensor
+
+
+class Kmeans:
+    def __init__(self, k: int, max_iters: int = None, stop_threshold: float = 1e-10) -> None:
+        self.k = k
+        self.iters = max_iters
+        self.stop_threshold = stop_threshold
+        self.centroids = None
+        self.assignment = None
+
+    def _init_centroids(self, x: torch.Tensor) -> None:
+        init_idx = np.random.choice(x.shape[0], self.k, replace=False)
+        self.centroids = x[torch.as_tensor(init_idx, device=x.device)].clone()
+        self.assignment = None
+
+    def _assign(self, x: torch.Tensor) -> torch.Tensor:
+        _, _, ids, _, _ = hip_ops.rq_quantize(x, self.centroids.unsqueeze(0), hip_ops.MODE_EVAL, 0.0)
+        return ids[:, 0]
+
+    def _update_centroids(self, x: torch.Tensor) -> None:
+        idx = self._assign(x)
+        sums = torch.zeros_like(self.centroids).index_add_(0, idx, x)
+        counts = torch.bincount(idx, minlength=self.k)
+        new = sums / counts.clamp_min(1).unsqueeze(1).to(x.dtype)
+        empty = torch.nonzero(counts == 0).flatten().tolist()
+        for c in empty:   # rare; same rule as the reference (random row)
+            new[c] = x[torch.randint(0, x.shape[0], (1,), device=x.device)].squeeze(0)
+        self.centroids = new
+        self.assignment = idx
+
+    def run(self, x: torch.Tensor) -> KmeansOutput:
+        if x.shape[0] == 0:
+            raise ValueError("Can not choose random element from x, x is empty")
+        x = x.detach().float().contiguous()
+        self._init_centroids(x)
+        i = 0
+        while self.iters is None or i < self.iters:
+            old = self.centroids.clone()
+            self._update_centroids(x)
+            if torch.norm(self.centroids - old, dim=1).max() < self.stop_threshold:
+                break
+            i += 1
+        return KmeansOutput(centroids=self.centroids, assignment=self.assignment)

@@ -1,0 +1,47 @@
+"""Token embedders — reference semantics: modules/embedding/id_embedder.py:14-53.
+
+SemIdEmbedder: one table of sem_ids_dim*K + 1 rows; token (type t, id s) -> row t*K + s;
+padded positions (seq_mask False) -> the padding row (index sem_ids_dim*K, padding_idx).
+UserIdEmbedder: user_id mod num_buckets -> row of a num_buckets table.
+"""
+from typing import NamedTuple
+
+import torch
+from torch import nn
+from torch import Tensor
+
+
+class SemIdEmbeddingBatch(NamedTuple):
+    seq: Tensor
+    fut: Tensor
+
+
+class SemIdEmbedder(nn.Module):
+    def __init__(self, num_embeddings, sem_ids_dim, embeddings_dim) -> None:
+        super().__init__()
+        self.sem_ids_dim = sem_ids_dim
+        self.num_embeddings = num_embeddings
+        self.padding_idx = sem_ids_dim * num_embeddings
+        self.emb = nn.Embedding(num_embeddings=self.padding_idx + 1, embedding_dim=embeddings_dim,
+                                padding_idx=self.padding_idx)
+
+    def _rows(self, type_ids, sem_ids):
+        return type_ids * self.num_embeddings + sem_ids
+
+    def forward(self, batch) -> SemIdEmbeddingBatch:
+        rows = torch.where(batch.seq_mask, self._rows(batch.token_type_ids, batch.sem_ids),
+                           torch.full_like(batch.sem_ids, self.padding_idx))
+        fut = None
+        if batch.sem_ids_fut is not None:
+            fut = self.emb(self._rows(batch.token_type_ids_fut, batch.sem_ids_fut))
+        return SemIdEmbeddingBatch(seq=self.emb(rows), fut=fut)
+
+
+class UserIdEmbedder(nn.Module):
+    def __init__(self, num_buckets, embedding_dim) -> None:
+        super().__init__()
+        self.num_buckets = num_buckets
+        self.emb = nn.Embedding(num_buckets, embedding_dim)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.emb(torch.remainder(x, self.num_buckets))

@@ -1,0 +1,160 @@
+"""Generative-retrieval encoder-decoder — drop-in for reference modules/model.py
+(ModelOutput :30-33, GenerationOutput :36-38, EncoderDecoderRetrievalModel :41-282; same
+constructor, parameter names, forward/generation contract).
+
+Forward (training) path, jagged mode (the only working mode in the reference, SURVEY A-9):
+  user token + (wpe + sem-ID embeddings) -> padded (B, 1+N, E) context, bos + (fut sem-ID +
+  tte) -> (B, L+2, E) future; both converted to NJTs by the HIP gather kernel (ops.jagged);
+  RMSNorm -> Dropout(0.5) -> in_proj{_context}; TransformerEncoderDecoder on NJT values with the
+  HIP varlen attention kernels; out_proj -> logits (B*(L+1), K) -> CE(ignore_index=-1) summed
+  over the L+1 positions and averaged over B; loss_d = per-position mean.
+The module-level Dropout(p=0.5) is hard-coded as in the reference (:67).
+"""
+from typing import NamedTuple
+
+import torch
+from torch import nn
+from torch import Tensor
+from torch.nn import functional as F
+
+from data.schemas import TokenizedSeqBatch
+from modules.embedding.id_embedder import SemIdEmbedder, UserIdEmbedder
+from modules.normalize import RMSNorm
+from modules.transformer.model import TransformerEncoderDecoder
+from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
+from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged_tensor
+
+
+class ModelOutput(NamedTuple):
+    loss: Tensor
+    logits: Tensor
+    loss_d: Tensor
+
+
+class GenerationOutput(NamedTuple):
+    sem_ids: Tensor
+    log_probas: Tensor
+
+
+class EncoderDecoderRetrievalModel(nn.Module):
+    def __init__(self, embedding_dim, attn_dim, dropout, num_heads, n_layers, num_embeddings, sem_id_dim,
+                 inference_verifier_fn, max_pos=2048, jagged_mode: bool = True) -> None:
+        super().__init__()
+        if not jagged_mode:
+            raise NotImplementedError("jagged_mode=False is broken in the reference (SURVEY A-9); "
+                                      "only the jagged path is provided")
+        self.jagged_mode = jagged_mode
+        self.num_embeddings = num_embeddings
+        self.sem_id_dim = sem_id_dim
+        self.attn_dim = attn_dim
+        self.inference_verifier_fn = inference_verifier_fn
+        self.enable_generation = False
+
+        self.bos_emb = nn.Parameter(torch.rand(embedding_dim))
+        self.norm = RMSNorm(embedding_dim)
+        self.norm_cxt = RMSNorm(embedding_dim)
+        self.do = nn.Dropout(p=0.5)
+        self.sem_id_embedder = SemIdEmbedder(num_embeddings=num_embeddings, sem_ids_dim=sem_id_dim,
+                                             embeddings_dim=embedding_dim)
+        self.user_id_embedder = UserIdEmbedder(2000, embedding_dim)
+        self.wpe = nn.Embedding(num_embeddings=max_pos, embedding_dim=embedding_dim)
+        self.tte = nn.Embedding(num_embeddings=sem_id_dim, embedding_dim=embedding_dim)
+        self.tte_fut = nn.Embedding(num_embeddings=sem_id_dim, embedding_dim=embedding_dim)  # unused (reference)
+        self.transformer = TransformerEncoderDecoder(d_in=attn_dim, d_out=attn_dim, dropout=dropout,
+                                                     num_heads=num_heads, encoder_layers=n_layers // 2,
+                                                     decoder_layers=n_layers // 2)
+        self.in_proj = nn.Linear(embedding_dim, attn_dim, bias=False)
+        self.in_proj_context = nn.Linear(embedding_dim, attn_dim, bias=False)
+        self.out_proj = nn.Linear(attn_dim, num_embeddings, bias=False)
+
+    def _predict(self, batch: TokenizedSeqBatch):
+        user_emb = self.user_id_embedder(batch.user_ids)                  # (B, 1, E)
+        sem = self.sem_id_embedder(batch)
+        seq_emb, fut_emb = sem.seq, sem.fut                               # (B, N, E), (B, L+1, E)
+        B, N, _ = seq_emb.shape
+        pos = self.wpe(torch.arange(N, device=seq_emb.device)).unsqueeze(0)
+        ctx = torch.cat([user_emb, pos + seq_emb], dim=1)                 # (B, 1+N, E)
+        fut = self.bos_emb.repeat(B, 1, 1)
+        if fut_emb is not None:
+            fut = torch.cat([fut, fut_emb + self.tte(batch.token_type_ids_fut)], dim=1)
+        ctx_lengths = batch.seq_mask.sum(axis=1) + 1
+        ctx_nt = padded_to_jagged_tensor(ctx.contiguous(), lengths=ctx_lengths, max_len=ctx.shape[1])
+        fut_lengths = torch.full((B,), fut.shape[1], device=fut.device, dtype=torch.int64)
+        fut_nt = padded_to_jagged_tensor(fut.contiguous(), lengths=fut_lengths, max_len=fut.shape[1])
+        transformer_context = self.in_proj_context(self.do(self.norm(ctx_nt)))
+        transformer_input = self.in_proj(self.do(self.norm_cxt(fut_nt)))
+        return self.transformer(x=transformer_input, context=transformer_context, padding_mask=batch.seq_mask,
+                                jagged=True)
+
+    def forward(self, batch: TokenizedSeqBatch) -> ModelOutput:
+        B = batch.seq_mask.shape[0]
+        trnsf_out = self._predict(batch)
+        if self.training or not self.enable_generation:
+            predict_out = self.out_proj(trnsf_out)
+            # sem_ids_fut is fixed length, so the jagged values reshape to (B, L+2, K)
+            logits = jagged_to_flattened_tensor(predict_out).view(B, -1, self.num_embeddings)[:, :-1, :].flatten(end_dim=1)
+            target = batch.sem_ids_fut.flatten(end_dim=1)
+            unred_loss = F.cross_entropy(logits, target, reduction="none", ignore_index=-1).view(B, -1)
+            loss = unred_loss.sum(axis=1).mean()
+            if not self.training:
+                self.transformer.cached_enc_output = None
+            return ModelOutput(loss=loss, logits=logits, loss_d=unred_loss.mean(axis=0))
+        last = jagged_to_flattened_tensor(trnsf_out.contiguous()).view(B, -1, self.attn_dim)[:, -1, :]
+        return ModelOutput(loss=None, logits=self.out_proj(last), loss_d=None)
+
+    @eval_mode
+    @reset_encoder_cache
+    @torch.no_grad()
+    def generate_next_sem_id(self, batch: TokenizedSeqBatch, temperature: int = 1, top_k: bool = True) -> GenerationOutput:
+        """Beam-style decoding of the next item's L+1 sem-ID tokens (reference :149-245): per step
+        sample 200 candidates per beam from softmax(logits / T), drop prefixes the verifier
+        rejects (-10000), keep the top 32 cumulative log-probabilities. The encoder output is
+        computed once and repeated per beam with the HIP jagged kernels (jagged -> padded,
+        repeat_interleave, padded -> jagged), as the reference does with torch ops."""
+        assert self.enable_generation, "Model generation is not enabled"
+        B = batch.sem_ids.shape[0]
+        generated, log_probas = None, 0
+        k = 32 if top_k else 1
+        n_cand = 200 if top_k else 1
+        cur = TokenizedSeqBatch(user_ids=batch.user_ids, sem_ids=batch.sem_ids, sem_ids_fut=None,
+                                seq_mask=batch.seq_mask, token_type_ids=batch.token_type_ids, token_type_ids_fut=None)
+        for i in range(self.sem_id_dim):
+            logits = self.forward(cur).logits
+            probas = F.softmax(logits / temperature, dim=-1)
+            samples_b = torch.multinomial(probas, num_samples=n_cand)
+            if generated is None:
+                valid = self.inference_verifier_fn(samples_b.unsqueeze(-1))
+            else:
+                prefix = torch.cat([generated.flatten(0, 1).unsqueeze(1).repeat_interleave(n_cand, axis=1),
+                                    samples_b.unsqueeze(-1)], axis=-1)
+                valid = self.inference_verifier_fn(prefix).reshape(B, -1)
+            sampled_lp = torch.log(torch.gather(probas, 1, samples_b)).reshape(B, -1)
+            samples = samples_b.reshape(B, -1)
+            sorted_lp, sorted_idx = (-10000 * (~valid) + sampled_lp +
+                                     maybe_repeat_interleave(log_probas, n_cand, dim=1)).sort(-1, descending=True)
+            top_lp, top_idx = sorted_lp[:, :k], sorted_idx[:, :k]
+            top_samples = torch.gather(samples, 1, top_idx)
+            if generated is not None:
+                parent = torch.gather(generated, 1, (top_idx // n_cand).unsqueeze(2).expand(-1, -1, i))
+                top_samples = torch.cat([parent, top_samples.unsqueeze(-1)], axis=-1)
+                nxt = top_samples.flatten(end_dim=1)
+                cur = TokenizedSeqBatch(user_ids=cur.user_ids, sem_ids=cur.sem_ids, sem_ids_fut=nxt,
+                                        token_type_ids_fut=torch.arange(nxt.shape[1], device=nxt.device).repeat(nxt.shape[0], 1),
+                                        seq_mask=cur.seq_mask, token_type_ids=cur.token_type_ids)
+                generated = top_samples.detach().clone()
+                log_probas = top_lp.detach().clone()
+            else:
+                nxt = top_samples.reshape(-1, 1)
+                enc = self.transformer.cached_enc_output
+                n_ctx = cur.sem_ids.shape[1] + 1
+                padded = jagged_to_padded_tensor(enc, n_ctx).repeat_interleave(k, dim=0)
+                lengths = enc.offsets().diff().repeat_interleave(k)
+                self.transformer.cached_enc_output = padded_to_jagged_tensor(padded.contiguous(), lengths, max_len=n_ctx)
+                cur = TokenizedSeqBatch(user_ids=cur.user_ids.repeat_interleave(k, dim=0),
+                                        sem_ids=cur.sem_ids.repeat_interleave(k, dim=0), sem_ids_fut=nxt,
+                                        token_type_ids_fut=torch.zeros_like(nxt),
+                                        seq_mask=cur.seq_mask.repeat_interleave(k, dim=0),
+                                        token_type_ids=cur.token_type_ids.repeat_interleave(k, dim=0))
+                generated = top_samples.unsqueeze(-1)
+                log_probas = top_lp.detach().clone()
+        return GenerationOutput(sem_ids=generated.squeeze(), log_probas=log_probas.squeeze())

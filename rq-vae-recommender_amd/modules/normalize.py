@@ -1,0 +1,40 @@
+"""Normalisation layers — reference semantics: modules/normalize.py:7-32.
+
+* ``l2norm``: divide by max(||x||_2, eps) along ``dim`` (eps 1e-12), i.e. F.normalize.
+* ``RMSNorm``: y = w * x / sqrt(mean(x^2, -1) + eps), evaluated in fp32 and cast back to the
+  input dtype before the weight multiply. Works on dense tensors and on jagged NJTs (it only
+  touches the last, dense axis).
+"""
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+__all__ = ["l2norm", "L2NormalizationLayer", "RMSNorm"]
+
+
+def l2norm(x, dim=-1, eps=1e-12):
+    return F.normalize(x, p=2, dim=dim, eps=eps)
+
+
+class L2NormalizationLayer(nn.Module):
+    def __init__(self, dim=-1, eps=1e-12) -> None:
+        super().__init__()
+        self.dim, self.eps = dim, eps
+
+    def forward(self, x):
+        return l2norm(x, self.dim, self.eps)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-6) -> None:
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def _norm(self, x):
+        inv_rms = torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + self.eps)
+        return x * inv_rms
+
+    def forward(self, x):
+        y = self._norm(x.float()).type_as(x)
+        return y * self.weight

@@ -1,0 +1,151 @@
+"""RQ-VAE — drop-in for reference modules/rqvae.py (RqVaeOutput :22-26, RqVaeComputedLosses
+:29-34, RqVae :37-165; same constructor, methods, outputs and state-dict keys
+``encoder.mlp.*``, ``decoder.mlp.*``, ``layers.{l}.embedding.weight``).
+
+Hot path: ``get_semantic_ids`` runs all L levels in ONE fused HIP launch
+(rqvae_hip.ops.rq_quantize: MFMA fp32 cdist -> argmin -> rotation trick / STE / eval -> VQ loss
+-> residual update, chained on-chip) and its VJP with a deterministic codebook gradient.
+``p_unique_ids`` uses a hash-count kernel (O(B L)) instead of the reference's O(B^2 L) mask.
+The reference wraps forward in torch.compile(mode="reduce-overhead"); this build instead
+exposes a whole-step hipGraph capture (rqvae_hip.graph) and never invokes inductor.
+"""
+from typing import List, NamedTuple
+
+import torch
+from torch import nn
+from torch import Tensor
+
+from data.schemas import SeqBatch
+from modules.encoder import MLP
+from modules.loss import CategoricalReconstuctionLoss, ReconstructionLoss
+from modules.normalize import l2norm
+from modules.quantize import Quantize, QuantizeDistance, QuantizeForwardMode, fused_mode
+from rqvae_hip import ops as hip_ops
+
+
+class RqVaeOutput(NamedTuple):
+    embeddings: Tensor      # (B, D, L)
+    residuals: Tensor       # (B, D, L)
+    sem_ids: Tensor         # (B, L) int64
+    quantize_loss: Tensor   # (B,)
+
+
+class RqVaeComputedLosses(NamedTuple):
+    loss: Tensor
+    reconstruction_loss: Tensor
+    rqvae_loss: Tensor
+    embs_norm: Tensor       # (B, L)
+    p_unique_ids: Tensor    # 0-d float
+
+
+class RqVae(nn.Module):
+    def __init__(
+        self,
+        input_dim: int,
+        embed_dim: int,
+        hidden_dims: List[int],
+        codebook_size: int,
+        codebook_kmeans_init: bool = True,
+        codebook_normalize: bool = False,
+        codebook_sim_vq: bool = False,
+        codebook_mode: QuantizeForwardMode = QuantizeForwardMode.GUMBEL_SOFTMAX,
+        n_layers: int = 3,
+        commitment_weight: float = 0.25,
+        n_cat_features: int = 18,
+    ) -> None:
+        # plain kwargs (the reference pickles `self` via locals(); SURVEY A-13)
+        self._config = dict(input_dim=input_dim, embed_dim=embed_dim, hidden_dims=list(hidden_dims),
+                            codebook_size=codebook_size, codebook_kmeans_init=codebook_kmeans_init,
+                            codebook_normalize=codebook_normalize, codebook_sim_vq=codebook_sim_vq,
+                            codebook_mode=codebook_mode, n_layers=n_layers, commitment_weight=commitment_weight,
+                            n_cat_features=n_cat_features)
+        super().__init__()
+        self.input_dim = input_dim
+        self.embed_dim = embed_dim
+        self.hidden_dims = hidden_dims
+        self.n_layers = n_layers
+        self.codebook_size = codebook_size
+        self.commitment_weight = commitment_weight
+        self.n_cat_feats = n_cat_features
+        self.layers = nn.ModuleList([
+            Quantize(embed_dim=embed_dim, n_embed=codebook_size, forward_mode=codebook_mode,
+                     do_kmeans_init=codebook_kmeans_init, codebook_normalize=(i == 0 and codebook_normalize),
+                     sim_vq=codebook_sim_vq, commitment_weight=commitment_weight)
+            for i in range(n_layers)
+        ])
+        self.encoder = MLP(input_dim=input_dim, hidden_dims=hidden_dims, out_dim=embed_dim,
+                           normalize=codebook_normalize)
+        self.decoder = MLP(input_dim=embed_dim, hidden_dims=list(hidden_dims)[::-1], out_dim=input_dim,
+                           normalize=True)
+        self.reconstruction_loss = (CategoricalReconstuctionLoss(n_cat_features) if n_cat_features != 0
+                                    else ReconstructionLoss())
+
+    @property
+    def config(self) -> dict:
+        return self._config
+
+    @property
+    def device(self) -> torch.device:
+        return next(self.encoder.parameters()).device
+
+    def load_pretrained(self, path: str) -> None:
+        """Load a checkpoint {"iter", "model", ...}. Only tensor payloads are accepted
+        (weights_only=True): reference checkpoints that pickle the module object itself must be
+        re-saved as a plain state dict first."""
+        state = torch.load(path, map_location=self.device, weights_only=True)
+        self.load_state_dict(state["model"])
+        print(f"---Loaded RQVAE Iter {state['iter']}---")
+
+    def encode(self, x: Tensor) -> Tensor:
+        return self.encoder(x)
+
+    def decode(self, x: Tensor) -> Tensor:
+        return self.decoder(x)
+
+    # ----------------------------------------------------------------- semantic ids
+    def _fused_kernel_mode(self):
+        modes = {fused_mode(layer.forward_mode, self.training) for layer in self.layers}
+        if len(modes) != 1 or None in modes:
+            return None
+        if any(layer.distance_mode != QuantizeDistance.L2 or layer.needs_init() for layer in self.layers):
+            return None
+        return modes.pop()
+
+    def quantize_levels(self, res0: Tensor, gumbel_t: float):
+        """All levels -> (emb (L,B,D), res (L,B,D), ids (B,L), qloss (B,), emb_sum (B,D))."""
+        mode = self._fused_kernel_mode()
+        if mode is not None:
+            codebooks = torch.stack([layer.codebook() for layer in self.layers])
+            return hip_ops.rq_quantize(res0, codebooks, mode, self.commitment_weight)
+        # generic per-level path (k-means init pending, gumbel / cosine layers)
+        res, qloss = res0, 0
+        embs, ress, ids = [], [], []
+        for layer in self.layers:
+            ress.append(res)
+            q = layer(res, temperature=gumbel_t)
+            qloss = qloss + q.loss
+            res = res - q.embeddings
+            embs.append(q.embeddings)
+            ids.append(q.ids)
+        emb = torch.stack(embs)
+        return emb, torch.stack(ress), torch.stack(ids, 1), qloss, emb.sum(0)
+
+    def get_semantic_ids(self, x: Tensor, gumbel_t: float = 0.001) -> RqVaeOutput:
+        emb, res, ids, qloss, _ = self.quantize_levels(self.encode(x), gumbel_t)
+        return RqVaeOutput(embeddings=emb.permute(1, 2, 0), residuals=res.permute(1, 2, 0), sem_ids=ids,
+                           quantize_loss=qloss)
+
+    def forward(self, batch: SeqBatch, gumbel_t: float) -> RqVaeComputedLosses:
+        x = batch.x
+        emb, _, ids, qloss, emb_sum = self.quantize_levels(self.encode(x), gumbel_t)
+        x_hat = self.decode(emb_sum)
+        n = self.n_cat_feats
+        if n > 0:   # the reference's cat is a no-op for n == 0 (SURVEY A-10)
+            x_hat = torch.cat([l2norm(x_hat[..., :-n]), x_hat[..., -n:]], axis=-1)
+        reconstruction = self.reconstruction_loss(x_hat, x)
+        loss = (reconstruction + qloss).mean()
+        with torch.no_grad():
+            embs_norm = emb.norm(dim=-1).T
+            p_unique_ids = hip_ops.unique_count(ids, self.codebook_size).to(torch.float32) / ids.shape[0]
+        return RqVaeComputedLosses(loss=loss, reconstruction_loss=reconstruction.mean(), rqvae_loss=qloss.mean(),
+                                   embs_norm=embs_norm, p_unique_ids=p_unique_ids)

@@ -1,0 +1,97 @@
+"""Jagged multi-head attention — drop-in for reference modules/transformer/attention.py.
+
+Kept: ``AttentionInput``, ``Attend(d_out, num_heads, head_dim, dropout)`` with
+``jagged_forward(qu, ke, va, is_causal)`` (:113-124) and ``MultiHeadAttention(d_in, d_out,
+num_heads, cross_attn=False, dropout=0.0, qkv_bias=False, enable_kv_cache=False)`` with
+``forward(x, x_kv=None, padding_mask=None, is_causal=True, jagged=False, use_cache=False)``
+(:147-233), module names ``qkv`` / ``q`` / ``kv`` / ``proj`` and the reference's assertions
+and exceptions (KV cache unsupported :161; dense attention raises :228-229).
+
+MI355X path: NJT q/k/v values (row-strided views of the fused projection output, consumed in
+place) go to the HIP varlen attention kernels (rqvae_hip.ops.varlen_attention: fp32 MFMA,
+online softmax, deterministic two-pass backward). Attention dropout is always 0, as in the
+reference (Attend is built with dropout=False).
+"""
+from typing import Optional, Union
+
+import torch
+from torch import nn
+from torch import Tensor
+
+from rqvae_hip import ops as hip_ops
+
+AttentionInput = Union[Tensor, "torch.nested.Tensor"]
+
+
+def _max_seqlen(nt) -> int:
+    m = getattr(nt, "_maybe_max_seqlen", None)
+    if m is None:
+        m = nt._get_max_seqlen()
+    return int(m)
+
+
+def _wrap_like(values: Tensor, like):
+    """NJT over `values` sharing `like`'s offsets (hence its ragged dimension)."""
+    kw = {}
+    for name, key in (("_maybe_min_seqlen", "min_seqlen"), ("_maybe_max_seqlen", "max_seqlen")):
+        v = getattr(like, name, None)
+        if v is not None:
+            kw[key] = int(v)
+    return torch.nested.nested_tensor_from_jagged(values, like.offsets(), **kw)
+
+
+class Attend(nn.Module):
+    def __init__(self, d_out, num_heads, head_dim, dropout):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = head_dim
+        self.d_out = d_out
+        self.dropout = dropout
+
+    def jagged_forward(self, qu, ke, va, is_causal: bool):
+        """softmax(q k^T / sqrt(head_dim)) v per sequence; NJT (B, j, H*hd) in and out."""
+        assert not (self.training and self.dropout), "attention dropout is not supported (reference forces 0)"
+        out = hip_ops.varlen_attention(qu.values(), ke.values(), va.values(), qu.offsets(), ke.offsets(),
+                                       self.num_heads, bool(is_causal), _max_seqlen(qu), _max_seqlen(ke))
+        return _wrap_like(out, qu)
+
+    def forward(self, qkv: Tensor, is_causal: bool = False) -> Tensor:
+        raise Exception("Unjagged attention currently not supported.")
+
+
+class MultiHeadAttention(nn.Module):
+    def __init__(self, d_in, d_out, num_heads, cross_attn=False, dropout=0.0, qkv_bias=False,
+                 enable_kv_cache=False) -> None:
+        super().__init__()
+        assert d_out % num_heads == 0, "embed_dim is indivisible by num_heads"
+        assert not enable_kv_cache, "KV Cache currently not supported"
+        self.cross_attn = cross_attn
+        self.num_heads = num_heads
+        self.head_dim = d_out // num_heads
+        self.d_out = d_out
+        self.enable_kv_cache = enable_kv_cache
+        if cross_attn:
+            self.q = nn.Linear(d_in, d_out, bias=qkv_bias)
+            self.kv = nn.Linear(d_in, 2 * d_out, bias=qkv_bias)
+        else:
+            self.qkv = nn.Linear(d_in, 3 * d_out, bias=qkv_bias)
+        self.proj = nn.Linear(d_out, d_out, bias=False)
+        self.attend = Attend(self.d_out, self.num_heads, self.head_dim, dropout=False)
+        self._kv_cache = None
+
+    @property
+    def kv_cache(self):
+        return self._kv_cache
+
+    def forward(self, x: AttentionInput, x_kv: Optional[AttentionInput] = None, padding_mask: Optional[Tensor] = None,
+                is_causal: Optional[bool] = True, jagged: bool = False, use_cache: bool = False) -> AttentionInput:
+        assert not self.cross_attn or x_kv is not None, "Found null x_kv in cross attn. layer"
+        if not jagged:
+            raise Exception("Unjagged attention currently not supported.")
+        if self.cross_attn:
+            queries = self.q(x)
+            keys, values = self.kv(x_kv).chunk(2, dim=-1)
+        else:
+            queries, keys, values = self.qkv(x).chunk(3, dim=-1)
+        context_vec = self.attend.jagged_forward(queries, keys, values, is_causal=is_causal)
+        return self.proj(context_vec)

@@ -1,0 +1,219 @@
+"""Torch-facing ops over the HIP C ABI: autograd Functions for the RQ-VAE hot path.
+
+  rq_quantize(x, codebooks, mode, beta)      fused L-level residual quantization (fwd + VJP)
+  unique_count(ids, K)                       #distinct semantic-ID tuples (device scalar)
+  padded_to_jagged_values(x, lengths, N)     jagged gather (+1-1 rounding) + offsets (fwd + VJP)
+  varlen_attention(q, k, v, cu_q, cu_k, ...) jagged SDPA (fwd + deterministic VJP)
+
+All kernels run on torch's current HIP stream; tensors must be on the GPU (no CPU path).
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_handle, require_gpu
+
+MODE_EVAL, MODE_GUMBEL, MODE_STE, MODE_ROTATION = 0, 1, 2, 3
+
+
+class KernelTimer:
+    """Opt-in measurement hook: when ``ops.TIMER.enabled`` is set, HIP events are recorded on the
+    launching stream around each named C-ABI call, so a benchmark can report per-kernel device
+    time for the exact launches inside its timed region (no extra synchronisation)."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events = {}
+
+    def around(self, name, fn, *args):
+        if not self.enabled:
+            return fn(*args)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn(*args)
+        b.record()
+        self.events.setdefault(name, []).append((a, b))
+
+    def reset(self):
+        self.events = {}
+
+    def mean_ms(self, name):
+        ev = self.events.get(name, [])
+        return sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev)), len(ev)
+
+
+TIMER = KernelTimer()
+_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
+# ------------------------------------------------------------------------------- quantize
+class RqQuantizeFunction(torch.autograd.Function):
+    """Fused RqVae level loop (modules/rqvae.py:114-138 over modules/quantize.py:99-156).
+
+    forward(x (B,D), codebooks (L,K,D)) -> emb_out (L,B,D), residuals (L,B,D), ids (B,L),
+    qloss (B,), emb_sum (B,D).
+    """
+
+    @staticmethod
+    def forward(ctx, x, codebooks, mode: int, beta: float):
+        require_gpu(x, codebooks, what="rq_quantize")
+        assert x.dim() == 2 and codebooks.dim() == 3 and x.shape[1] == codebooks.shape[2]
+        assert x.dtype == torch.float32 and codebooks.dtype == torch.float32, "fp32 path (reference default)"
+        x = x.contiguous()
+        cbs = codebooks.contiguous()
+        B, D = x.shape
+        L, K, _ = cbs.shape
+        dev = x.device
+        csq = torch.empty((L, K), device=dev, dtype=torch.float32)
+        ids = torch.empty((B, L), device=dev, dtype=torch.int64)
+        emb = torch.empty((L, B, D), device=dev, dtype=torch.float32)
+        res = torch.empty((L, B, D), device=dev, dtype=torch.float32)
+        ql = torch.empty((B,), device=dev, dtype=torch.float32)
+        es = torch.empty((B, D), device=dev, dtype=torch.float32)
+        s = stream_handle(dev)
+        call("rq_codebook_sqnorm", ptr(cbs), L * K, D, ptr(csq), s)
+        TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L, int(mode),
+                     float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), s)
+        ctx.save_for_backward(res, ids, cbs)
+        ctx.mode, ctx.beta = int(mode), float(beta)
+        ctx.mark_non_differentiable(ids)
+        return emb, res, ids, ql, es
+
+    @staticmethod
+    def backward(ctx, g_emb, g_res, g_ids, g_ql, g_es):
+        res, ids, cbs = ctx.saved_tensors
+        L, B, D = res.shape
+        K = cbs.shape[1]
+        dev = res.device
+        gx = torch.empty((B, D), device=dev, dtype=torch.float32)
+        gcb = torch.empty_like(cbs)
+        nbytes = _lib.load().rq_quantize_bwd_workspace(B, D, K, L)
+        ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
+        TIMER.around("rq_quantize_bwd", call, "rq_quantize_bwd", ptr(res), ptr(ids), ptr(cbs), B, D, K, L, ctx.mode,
+                     ctx.beta, ptr(_c(g_emb)), ptr(_c(g_es)), ptr(_c(g_res)), ptr(_c(g_ql)), ptr(gx), ptr(gcb), ptr(ws),
+                     nbytes, stream_handle(dev))
+        return gx, gcb, None, None
+
+
+def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25):
+    return RqQuantizeFunction.apply(x, codebooks, mode, beta)
+
+
+def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
+    """Number of distinct rows of ids (B, L) as a device int64 scalar (modules/rqvae.py:152-157)."""
+    require_gpu(ids, what="unique_count")
+    ids = ids.contiguous().to(torch.int64)
+    B, L = ids.shape
+    out = torch.empty((), device=ids.device, dtype=torch.int64)
+    nbytes = _lib.load().rq_unique_workspace(B)
+    ws = torch.empty((nbytes,), device=ids.device, dtype=torch.uint8)
+    call("rq_unique_count", ptr(ids), B, L, int(K), ptr(out), ptr(ws), nbytes, stream_handle(ids.device))
+    return out
+
+
+# --------------------------------------------------------------------------------- jagged
+def jagged_offsets(lengths: torch.Tensor, N: int) -> torch.Tensor:
+    require_gpu(lengths, what="jagged_offsets")
+    lengths = lengths.contiguous().to(torch.int64)
+    B = lengths.shape[0]
+    off = torch.empty((B + 1,), device=lengths.device, dtype=torch.int64)
+    call("jagged_offsets", ptr(lengths), B, int(N), ptr(off), stream_handle(lengths.device))
+    return off
+
+
+class PaddedToJaggedValues(torch.autograd.Function):
+    """values (T, D) of the NJT built by ops/triton/jagged.py:11-66; backward = :69-77."""
+
+    @staticmethod
+    def forward(ctx, x, offsets, total: int, add_one_sub_one: bool):
+        require_gpu(x, offsets, what="padded_to_jagged")
+        assert x.dim() == 3 and x.is_contiguous()
+        B, N, D = x.shape
+        vals = torch.empty((total, D), device=x.device, dtype=x.dtype)
+        call("jagged_from_padded", ptr(x), B, N, D, ptr(offsets), ptr(vals), _DTYPES[x.dtype], int(add_one_sub_one),
+             stream_handle(x.device))
+        ctx.save_for_backward(offsets)
+        ctx.shape = (B, N, D)
+        return vals
+
+    @staticmethod
+    def backward(ctx, g_vals):
+        (offsets,) = ctx.saved_tensors
+        B, N, D = ctx.shape
+        g_vals = g_vals.contiguous()
+        gx = torch.empty((B, N, D), device=g_vals.device, dtype=g_vals.dtype)
+        call("jagged_to_padded", ptr(g_vals), ptr(offsets), B, N, D, ptr(gx), _DTYPES[g_vals.dtype],
+             stream_handle(g_vals.device))
+        return gx, None, None, None
+
+
+class JaggedToPaddedValues(torch.autograd.Function):
+    """Inverse conversion (padded (B,N,D) with zero fill) — used for the encoder-cache repeat in
+    generation (modules/model.py:222-228) and as the backward of the gather."""
+
+    @staticmethod
+    def forward(ctx, vals, offsets, N: int):
+        require_gpu(vals, offsets, what="jagged_to_padded")
+        vals = vals.contiguous()
+        B = offsets.shape[0] - 1
+        D = vals.shape[1]
+        x = torch.empty((B, N, D), device=vals.device, dtype=vals.dtype)
+        call("jagged_to_padded", ptr(vals), ptr(offsets), B, N, D, ptr(x), _DTYPES[vals.dtype],
+             stream_handle(vals.device))
+        ctx.save_for_backward(offsets)
+        ctx.total = vals.shape[0]
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        (offsets,) = ctx.saved_tensors
+        return PaddedToJaggedValues.apply(gx.contiguous(), offsets, ctx.total, False), None, None
+
+
+# ------------------------------------------------------------------------------ attention
+class VarlenAttentionFunction(torch.autograd.Function):
+    """softmax(q k^T * scale [causal]) v per segment; q/k/v are (T, H*hd) row views (any row stride)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, cu_q, cu_k, num_heads: int, causal: bool, max_q: int, max_k: int, scale: float):
+        require_gpu(q, k, v, cu_q, cu_k, what="varlen_attention")
+        for t in (q, k, v):
+            assert t.dim() == 2 and t.stride(1) == 1 and t.dtype == torch.float32
+        Tq, A = q.shape
+        hd = A // num_heads
+        B = cu_q.shape[0] - 1
+        out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
+        lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
+        call("varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
+             B, num_heads, hd, int(max_q), int(max_k), int(causal), float(scale), ptr(out), out.stride(0), ptr(lse), Tq,
+             stream_handle(q.device))
+        ctx.save_for_backward(q, k, v, out, lse, cu_q, cu_k)
+        ctx.cfg = (num_heads, bool(causal), int(max_q), int(max_k), float(scale))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse, cu_q, cu_k = ctx.saved_tensors
+        H, causal, max_q, max_k, scale = ctx.cfg
+        dout = dout.contiguous()
+        Tq, A = q.shape
+        B = cu_q.shape[0] - 1
+        dq = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
+        dk = torch.empty((k.shape[0], A), device=q.device, dtype=torch.float32)
+        dv = torch.empty((v.shape[0], A), device=q.device, dtype=torch.float32)
+        call("varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+             out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
+             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0),
+             stream_handle(q.device))
+        return dq, dk, dv, None, None, None, None, None, None, None
+
+
+def varlen_attention(q, k, v, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[1] // num_heads)
+    return VarlenAttentionFunction.apply(q, k, v, cu_q, cu_k, num_heads, causal, max_q, max_k, scale)

@@ -1,0 +1,145 @@
+"""Parity of the HIP jagged conversion and varlen attention (and the decoder model built on them)
+with the reference's golden vectors and the pinned oracle.
+
+Jagged values / offsets / grads: bit-exact (byte-moving kernels; `+1-1` rounding reproduced).
+Attention: fp32 MFMA vs float64 oracle, |err| <= 2e-5 + 2e-4 |ref| (fwd) and 1e-4 + 1e-3 |ref| (bwd).
+Decoder model (reference fixture, dropout 0): loss rel 1e-5, logits atol 1e-4, grads rtol 2e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+import gen_inputs as gi
+from oracle import attention as A
+from oracle import jagged as J
+
+pytestmark = pytest.mark.gpu
+
+
+def test_jagged_vs_reference(golden, device):
+    from ops.jagged import padded_to_jagged_tensor, jagged_to_flattened_tensor
+    z = golden("jagged")
+    for case in ("ragged", "full", "ctx"):
+        x = torch.from_numpy(z[f"{case}_x"]).to(device).requires_grad_(True)
+        lengths = torch.from_numpy(z[f"{case}_lengths"]).to(device)
+        nt = padded_to_jagged_tensor(x, lengths, x.shape[1])
+        vals = jagged_to_flattened_tensor(nt)
+        assert np.array_equal(nt.offsets().cpu().numpy(), z[f"{case}_offsets"])
+        assert np.array_equal(vals.detach().cpu().numpy().view(np.uint32), z[f"{case}_values"].view(np.uint32))
+        (vals * torch.from_numpy(z[f"{case}_gv"]).to(device)).sum().backward()
+        assert np.array_equal(x.grad.cpu().numpy(), z[f"{case}_grad_x"])
+
+
+@pytest.mark.parametrize("B,N,D,dtype", [(256, 81, 128, torch.float32), (64, 801, 128, torch.float32),
+                                         (3, 7, 6, torch.float32), (37, 20, 128, torch.bfloat16),
+                                         (5, 1, 8, torch.float32)])
+def test_jagged_roundtrip_sizes(device, B, N, D, dtype):
+    """padded -> jagged -> padded reproduces x on valid rows and zeros elsewhere (incl. empty rows)."""
+    from rqvae_hip import ops
+    g = gi.rng(B * N + D)
+    lengths = torch.from_numpy(g.integers(0, N + 1, size=B)).to(device)
+    x = torch.from_numpy(g.standard_normal((B, N, D), dtype=np.float32)).to(device=device, dtype=dtype)
+    off = ops.jagged_offsets(lengths, N)
+    total = int(off[-1])
+    vals = ops.PaddedToJaggedValues.apply(x, off, total, False)
+    back = ops.JaggedToPaddedValues.apply(vals, off, N)
+    mask = torch.arange(N, device=device)[None, :] < lengths[:, None]
+    assert torch.equal(back[mask], x[mask])
+    assert torch.count_nonzero(back[~mask]) == 0
+    v_np, o_np = J.padded_to_jagged(x.float().cpu().numpy(), lengths.cpu().numpy())
+    if dtype == torch.float32:
+        p1 = ops.PaddedToJaggedValues.apply(x, off, total, True)
+        assert np.array_equal(p1.cpu().numpy().view(np.uint32), v_np.view(np.uint32))
+    assert np.array_equal(off.cpu().numpy(), o_np)
+
+
+def _varlen_case(g, B, max_q, max_k, H, hd, same):
+    lq = g.integers(1, max_q + 1, size=B)
+    lk = lq.copy() if same else g.integers(1, max_k + 1, size=B)
+    cq = np.concatenate([[0], np.cumsum(lq)]).astype(np.int64)
+    ck = np.concatenate([[0], np.cumsum(lk)]).astype(np.int64)
+    q = g.standard_normal((cq[-1], H, hd), dtype=np.float32)
+    k = g.standard_normal((ck[-1], H, hd), dtype=np.float32)
+    v = g.standard_normal((ck[-1], H, hd), dtype=np.float32)
+    do = g.standard_normal((cq[-1], H, hd), dtype=np.float32)
+    return q, k, v, do, cq, ck
+
+
+@pytest.mark.parametrize("B,max_q,max_k,H,hd,causal,same", [
+    (7, 81, 81, 8, 64, False, True),     # encoder self-attention (DA)
+    (9, 5, 5, 8, 64, True, True),        # decoder causal self-attention (DA)
+    (6, 5, 81, 8, 64, False, False),     # cross-attention (DA)
+    (3, 300, 300, 6, 64, False, True),   # long context (DM-like)
+    (4, 70, 70, 4, 32, True, True),
+    (2, 40, 90, 2, 128, False, False),
+])
+def test_varlen_attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
+    from rqvae_hip import ops
+    g = gi.rng(B * 131 + max_q + hd)
+    q, k, v, do, cq, ck = _varlen_case(g, B, max_q, max_k, H, hd, same)
+    A_ = H * hd
+    # strided inputs like the fused qkv projection output: (T, 3A) buffer
+    qkv = np.concatenate([q.reshape(-1, A_), np.zeros_like(q.reshape(-1, A_)), np.zeros_like(q.reshape(-1, A_))], 1)
+    qb = torch.from_numpy(qkv).to(device)[:, :A_].requires_grad_(True)
+    kt = torch.from_numpy(k.reshape(-1, A_)).to(device).requires_grad_(True)
+    vt = torch.from_numpy(v.reshape(-1, A_)).to(device).requires_grad_(True)
+    cqt, ckt = torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device)
+    out = ops.varlen_attention(qb, kt, vt, cqt, ckt, H, causal, int(np.diff(cq).max()), int(np.diff(ck).max()))
+    out.backward(torch.from_numpy(do.reshape(-1, A_)).to(device))
+    ref, _ = A.attn_fwd(q, k, v, cq, ck, causal)
+    dq, dk, dv = A.attn_bwd(q, k, v, do, cq, ck, causal)
+    def chk(a, b, atol, rtol, what):
+        a = a.detach().cpu().double().numpy().reshape(b.shape)
+        err = np.abs(a - b) - (atol + rtol * np.abs(b))
+        assert err.max() <= 0, f"{what}: max abs err {np.abs(a - b).max():.3e}"
+    chk(out, ref, 2e-5, 2e-4, "out")
+    chk(qb.grad, dq, 1e-4, 1e-3, "dq")
+    chk(kt.grad, dk, 1e-4, 1e-3, "dk")
+    chk(vt.grad, dv, 1e-4, 1e-3, "dv")
+
+
+def test_varlen_attention_deterministic(device):
+    from rqvae_hip import ops
+    g = gi.rng(11)
+    q, k, v, do, cq, ck = _varlen_case(g, 16, 81, 81, 8, 64, True)
+    outs = []
+    for _ in range(2):
+        qt, kt, vt = (torch.from_numpy(a.reshape(a.shape[0], -1)).to(device).requires_grad_(True) for a in (q, k, v))
+        o = ops.varlen_attention(qt, kt, vt, torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device), 8, False, 81, 81)
+        o.backward(torch.from_numpy(do.reshape(do.shape[0], -1)).to(device))
+        outs.append((o.detach(), qt.grad, kt.grad, vt.grad))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_decoder_model_vs_reference(golden, device):
+    from data.schemas import TokenizedSeqBatch
+    from modules.model import EncoderDecoderRetrievalModel
+    z = golden("decoder_small")
+    E, A_, H, nl, K, L1, n_max, seed = (int(z[k]) for k in ("E", "A", "H", "n_layers", "K", "L1", "n_max", "seed"))
+    model = EncoderDecoderRetrievalModel(embedding_dim=E, attn_dim=A_, dropout=0.0, num_heads=H, n_layers=nl,
+                                         num_embeddings=K, sem_id_dim=L1, inference_verifier_fn=None,
+                                         max_pos=n_max * L1, jagged_mode=True)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            p.copy_(torch.from_numpy(gi.named_param(name, p.shape, seed)))
+    model = model.to(device).train()
+    keys = ("user_ids", "sem_ids", "sem_ids_fut", "seq_mask", "token_type_ids", "token_type_ids_fut")
+    batch = TokenizedSeqBatch(**{k: torch.from_numpy(z[k]).to(device) for k in keys})
+    out = model(batch)
+    out.loss.backward()
+    assert float(out.loss) == pytest.approx(float(z["loss"]), rel=1e-5)
+    assert np.abs(out.logits.detach().cpu().numpy() - z["logits"]).max() < 1e-4
+    assert np.abs(out.loss_d.detach().cpu().numpy() - z["loss_d"]).max() < 1e-5
+    for name, p in model.named_parameters():
+        key = "grad__" + name
+        if key in z:
+            ref = z[key]
+            got = p.grad.cpu().numpy()
+            assert np.all(np.abs(got - ref) <= 1e-5 + 2e-3 * np.abs(ref)), f"{name}: {np.abs(got - ref).max():.3e}"
+        elif key + "__norm" in z:
+            assert p.grad.double().norm().item() == pytest.approx(float(z[key + "__norm"]), rel=1e-4)
+            assert np.all(np.abs(p.grad[0].cpu().numpy() - z[key + "__row0"]) <= 1e-5 + 2e-3 * np.abs(z[key + "__row0"]))
