@@ -28,6 +28,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rq-vae-recommender_amd"))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))   # seeded input generators (cpu_baseline)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

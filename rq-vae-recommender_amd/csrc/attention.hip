@@ -26,6 +26,22 @@ namespace rqhip {
 
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Head dims below 32 use 32-wide LDS rows / output tiles whose extra columns stay zero.
+template <int HD>
+struct Pad {
+  static constexpr int P = HD < 32 ? 32 : HD;   // padded width
+  static constexpr int LD = P + 4;              // LDS row stride (floats)
+};
+
+// Zero the padding columns [HD, P) of a [32][LD] LDS image once per kernel.
+template <int HD, int NT>
+__device__ __forceinline__ void zero_pad32(float* dst, int tid) {
+  constexpr int P = Pad<HD>::P, LD = Pad<HD>::LD;
+  if constexpr (P > HD) {
+    for (int f = tid; f < 32 * (P - HD); f += NT) dst[(f / (P - HD)) * LD + HD + f % (P - HD)] = 0.f;
+  }
+}
+
 template <int HD>
 __device__ __forceinline__ void load_half_row(const float* p, bool valid, float (&f)[HD / 2]) {
 #pragma unroll
@@ -38,7 +54,7 @@ __device__ __forceinline__ void load_half_row(const float* p, bool valid, float 
 // Stage 32 rows x HD of a strided row source into LDS [32][HD+4]; rows >= n are zero.
 template <int HD, int NT>
 __device__ __forceinline__ void stage32(float* dst, const float* src, int64_t stride, int row0, int n, int tid) {
-  constexpr int F4 = HD / 4, LD = HD + 4;
+  constexpr int F4 = HD / 4, LD = Pad<HD>::LD;
   for (int f = tid; f < 32 * F4; f += NT) {
     const int r = f / F4, c = (f % F4) * 4;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -50,7 +66,7 @@ __device__ __forceinline__ void stage32(float* dst, const float* src, int64_t st
 // acc += Mat[rows i][HD] (LDS, A operand, row = lane&31) x frag (B operand, registers)
 template <int HD>
 __device__ __forceinline__ floatx16 mfma_rows_x_frag(const float* Ms, const float (&frag)[HD / 2], int lane, floatx16 acc) {
-  const float* ap = Ms + (lane & 31) * (HD + 4) + (lane >> 5) * (HD / 2);
+  const float* ap = Ms + (lane & 31) * Pad<HD>::LD + (lane >> 5) * (HD / 2);
 #pragma unroll
   for (int s = 0; s < HD / 2; s += 4) {
     const float4 a = *reinterpret_cast<const float4*>(ap + s);
@@ -62,27 +78,32 @@ __device__ __forceinline__ floatx16 mfma_rows_x_frag(const float* Ms, const floa
   return acc;
 }
 
-// acc[tile] (rows d, cols lane) += Ms^T[d][t-row] * w[t] over the 32 rows of Ms (LDS [32][HD+4]).
+// acc[tile] (rows d, cols lane) += Ms^T[d][t-row] * w[t] over the 32 rows of Ms (LDS [32][LD]).
 template <int HD>
-__device__ __forceinline__ void mfma_colsT_x_regs(const float* Ms, const floatx16& w, int lane, floatx16 (&acc)[HD / 32]) {
+__device__ __forceinline__ void mfma_colsT_x_regs(const float* Ms, const floatx16& w, int lane,
+                                                  floatx16 (&acc)[Pad<HD>::P / 32]) {
   const int h = lane >> 5, c = lane & 31;
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
-    const float* row = Ms + crow(t, h) * (HD + 4) + c;
+    const float* row = Ms + crow(t, h) * Pad<HD>::LD + c;
 #pragma unroll
-    for (int tl = 0; tl < HD / 32; ++tl) acc[tl] = __builtin_amdgcn_mfma_f32_32x32x2f32(row[tl * 32], w[t], acc[tl], 0, 0, 0);
+    for (int tl = 0; tl < Pad<HD>::P / 32; ++tl)
+      acc[tl] = __builtin_amdgcn_mfma_f32_32x32x2f32(row[tl * 32], w[t], acc[tl], 0, 0, 0);
   }
 }
 
 // Write rows-d accumulators for one row (lane) as float4 runs: d = 32 tl + 8 g + 4 h + 0..3.
 template <int HD>
-__device__ __forceinline__ void store_dT(float* rowp, const floatx16 (&acc)[HD / 32], float mul, int h) {
+__device__ __forceinline__ void store_dT(float* rowp, const floatx16 (&acc)[Pad<HD>::P / 32], float mul, int h) {
 #pragma unroll
-  for (int tl = 0; tl < HD / 32; ++tl)
+  for (int tl = 0; tl < Pad<HD>::P / 32; ++tl)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<float4*>(rowp + tl * 32 + 8 * g + 4 * h) =
-          make_float4(acc[tl][4 * g] * mul, acc[tl][4 * g + 1] * mul, acc[tl][4 * g + 2] * mul, acc[tl][4 * g + 3] * mul);
+    for (int g = 0; g < 4; ++g) {
+      const int d = tl * 32 + 8 * g + 4 * h;
+      if (d < HD)
+        *reinterpret_cast<float4*>(rowp + d) =
+            make_float4(acc[tl][4 * g] * mul, acc[tl][4 * g + 1] * mul, acc[tl][4 * g + 2] * mul, acc[tl][4 * g + 3] * mul);
+    }
 }
 
 // ---------------------------------------------------------------------------------------- fwd
@@ -92,11 +113,13 @@ __global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__
                                                         const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
                                                         int causal, float scale, float* __restrict__ out, int64_t so,
                                                         float* __restrict__ lse, int64_t Tq) {
-  constexpr int LD = HD + 4;
+  constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
   __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD];
   float* K_s = smem;
   float* V_s = smem + 32 * LD;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
+  zero_pad32<HD, 128>(K_s, tid);
+  zero_pad32<HD, 128>(V_s, tid);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   const int qbase = blockIdx.x * 64;
@@ -105,9 +128,9 @@ __global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__
   const bool qv = qi < lq;
   float qf[HD / 2];
   load_half_row<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + h * (HD / 2), qv, qf);
-  floatx16 o[HD / 32];
+  floatx16 o[NTL];
 #pragma unroll
-  for (int tl = 0; tl < HD / 32; ++tl)
+  for (int tl = 0; tl < NTL; ++tl)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[tl][r] = 0.f;
   float m = -INFINITY, l = 0.f;
@@ -142,7 +165,7 @@ __global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__
     l = l * alpha + ls;
     m = mn;
 #pragma unroll
-    for (int tl = 0; tl < HD / 32; ++tl)
+    for (int tl = 0; tl < NTL; ++tl)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[tl][r] *= alpha;
     mfma_colsT_x_regs<HD>(V_s, s, lane, o);        // O^T += V^T P^T
@@ -160,13 +183,15 @@ __global__ void __launch_bounds__(128) attn_bwd_dkdv_kernel(
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dk, int64_t sdk, float* __restrict__ dv, int64_t sdv) {
-  constexpr int LD = HD + 4;
+  constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
   __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD + 64];
   float* Q_s = smem;
   float* O_s = smem + 32 * LD;   // dO tile
   float* lse_s = O_s + 32 * LD;
   float* dl_s = lse_s + 32;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
+  zero_pad32<HD, 128>(Q_s, tid);
+  zero_pad32<HD, 128>(O_s, tid);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   const int kbase = blockIdx.x * 64;
@@ -176,9 +201,9 @@ __global__ void __launch_bounds__(128) attn_bwd_dkdv_kernel(
   float kf[HD / 2], vf[HD / 2];
   load_half_row<HD>(k + (k0 + (kv ? kj : 0)) * sk + hh * HD + h * (HD / 2), kv, kf);
   load_half_row<HD>(v + (k0 + (kv ? kj : 0)) * sv + hh * HD + h * (HD / 2), kv, vf);
-  floatx16 dka[HD / 32], dva[HD / 32];
+  floatx16 dka[NTL], dva[NTL];
 #pragma unroll
-  for (int tl = 0; tl < HD / 32; ++tl)
+  for (int tl = 0; tl < NTL; ++tl)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dka[tl][r] = 0.f; dva[tl][r] = 0.f; }
   const int qstart = causal ? (kbase / 32) * 32 : 0;
@@ -229,11 +254,13 @@ __global__ void __launch_bounds__(128) attn_bwd_dq_kernel(
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dq, int64_t sdq) {
-  constexpr int LD = HD + 4;
+  constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
   __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD];
   float* K_s = smem;
   float* V_s = smem + 32 * LD;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
+  zero_pad32<HD, 128>(K_s, tid);
+  zero_pad32<HD, 128>(V_s, tid);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   const int qbase = blockIdx.x * 64;
@@ -252,9 +279,9 @@ __global__ void __launch_bounds__(128) attn_bwd_dq_kernel(
     delta += __shfl_xor(delta, 32, 64);
   }
   const float lq_lse = qv ? lse[(int64_t)hh * Tq + qrow] : 0.f;
-  floatx16 dqa[HD / 32];
+  floatx16 dqa[NTL];
 #pragma unroll
-  for (int tl = 0; tl < HD / 32; ++tl)
+  for (int tl = 0; tl < NTL; ++tl)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dqa[tl][r] = 0.f;
   const int kend = causal ? min(lk, qbase + 64) : lk;
@@ -303,7 +330,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 }
 
 static bool attn_args_ok(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k) {
-  return B >= 0 && B <= 65535 && H >= 1 && H <= 65535 && (hd == 32 || hd == 64 || hd == 128) && max_q >= 0 &&
+  return B >= 0 && B <= 65535 && H >= 1 && H <= 65535 && (hd == 16 || hd == 32 || hd == 64 || hd == 128) && max_q >= 0 &&
          max_k >= 0;
 }
 
@@ -317,12 +344,13 @@ int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
   RQ_CHECK_ARG(q && k && v && cu_q && cu_k && out && lse, "varlen_attn_fwd: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 32/64/128, B<=65535)");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<=65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
   if (B == 0 || max_q == 0) return 0;
   dim3 g((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
+    case 16: launch_fwd<16>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
     case 32: launch_fwd<32>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
     case 64: launch_fwd<64>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
     case 128: launch_fwd<128>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
@@ -336,13 +364,14 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, void* stream) {
   RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv, "varlen_attn_bwd: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd: bad shape (hd must be 32/64/128, B<=65535)");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd: bad shape (hd must be 16/32/64/128, B<=65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0 && sdo % 4 == 0 && sdq % 4 == 0 &&
                    sdk % 4 == 0 && sdv % 4 == 0,
                "varlen_attn_bwd: row strides must be x4");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
+    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
     case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
     case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
     case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;

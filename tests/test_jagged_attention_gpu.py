@@ -3,7 +3,7 @@ with the reference's golden vectors and the pinned oracle.
 
 Jagged values / offsets / grads: bit-exact (byte-moving kernels; `+1-1` rounding reproduced).
 Attention: fp32 MFMA vs float64 oracle, |err| <= 2e-5 + 2e-4 |ref| (fwd) and 1e-4 + 1e-3 |ref| (bwd).
-Decoder model (reference fixture, dropout 0): loss rel 1e-5, logits atol 1e-4, grads rtol 2e-3.
+Decoder model (reference fixture, dropout 0): loss rel 1e-5, logits |err| <= 2e-4 max|logit|, grads rtol 2e-3.
 """
 import numpy as np
 import pytest
@@ -72,6 +72,8 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (3, 300, 300, 6, 64, False, True),   # long context (DM-like)
     (4, 70, 70, 4, 32, True, True),
     (2, 40, 90, 2, 128, False, False),
+    (5, 30, 30, 4, 16, True, True),      # small head dim (decoder fixtures: A=64, H=4)
+    (4, 20, 33, 4, 16, False, False),
 ])
 def test_varlen_attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
     from rqvae_hip import ops
@@ -132,8 +134,10 @@ def test_decoder_model_vs_reference(golden, device):
     out = model(batch)
     out.loss.backward()
     assert float(out.loss) == pytest.approx(float(z["loss"]), rel=1e-5)
-    assert np.abs(out.logits.detach().cpu().numpy() - z["logits"]).max() < 1e-4
-    assert np.abs(out.loss_d.detach().cpu().numpy() - z["loss_d"]).max() < 1e-5
+    # fixture logits reach |400|: fp32 summation-order noise through 4 blocks scales with them
+    scale = np.abs(z["logits"]).max()
+    assert np.abs(out.logits.detach().cpu().numpy() - z["logits"]).max() <= 2e-4 * scale
+    assert np.allclose(out.loss_d.detach().cpu().numpy(), z["loss_d"], rtol=2e-5, atol=0)
     for name, p in model.named_parameters():
         key = "grad__" + name
         if key in z:
