@@ -254,7 +254,57 @@ def measure_extras(model, device, x):
         opt.step()
     dt = time_region(small, 20, 5, sync)
     out["b64_step_ms"] = round(dt / 20 * 1e3, 3)
+    out.update(measure_decoder(device))
     return out
+
+
+DEC = dict(B=256, max_items=20, E=128, A=512, H=8, layers=8, K=256, sem_id_dim=4, dropout=0.3, lr=3e-4, wd=0.035)
+
+
+def measure_decoder(device, steps=10, warmup=3):
+    """BASELINE configs[2]: decoder train step at Amazon dims (decoder_amazon.gin), synthetic
+    tokenized batches (n_items ~ U{2..20}), HIP jagged conversion + varlen attention."""
+    from rqvae_hip import ops
+    from data.processed import synthetic_tokenized_batch
+    from modules.model import EncoderDecoderRetrievalModel
+    torch.manual_seed(3)
+    m = EncoderDecoderRetrievalModel(embedding_dim=DEC["E"], attn_dim=DEC["A"], dropout=DEC["dropout"],
+                                     num_heads=DEC["H"], n_layers=DEC["layers"], num_embeddings=DEC["K"],
+                                     sem_id_dim=DEC["sem_id_dim"], inference_verifier_fn=None,
+                                     max_pos=DEC["max_items"] * DEC["sem_id_dim"]).to(device).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"], foreach=True)
+    batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + i, device)
+               for i in range(4)]
+    ctx_tokens = [int(b.seq_mask.sum()) + DEC["B"] for b in batches]
+    it = [0]
+
+    def step():
+        b = batches[it[0] % len(batches)]
+        it[0] += 1
+        opt.zero_grad(set_to_none=True)
+        o = m(b)
+        o.loss.backward()
+        opt.step()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ops.TIMER.reset()
+    ops.TIMER.enabled = True
+    it[0] = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ops.TIMER.enabled = False
+    toks = sum(ctx_tokens[i % len(batches)] for i in range(steps))
+    fut = steps * DEC["B"] * (DEC["sem_id_dim"] + 1)
+    return {"decoder_amazon": {
+        "ctx_tokens_per_s": round(toks / dt, 1), "ctx_plus_fut_tokens_per_s": round((toks + fut) / dt, 1),
+        "ms_per_step": round(dt / steps * 1e3, 3), "batch": DEC["B"],
+        "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
+        "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
+        "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}}
 
 
 if __name__ == "__main__":

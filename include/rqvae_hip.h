@@ -52,6 +52,12 @@ int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks
                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
                     float* emb_sum, void* stream);
 
+/* Same as rq_quantize_fwd with an explicit kernel choice (benchmarking / A-B testing):
+ * impl 0 = auto, 1 = LDS-tiled kernel (any D), 2 = register-resident kernel (D <= 64). */
+int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
+                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
+                         float* qloss, float* emb_sum, int impl, void* stream);
+
 /* Backward of rq_quantize_fwd (the autograd graph of modules/quantize.py:99-156 chained by
  * modules/rqvae.py:129): grads of emb_out (g_emb, (L,B,D) or NULL), of sum_l emb_out
  * (g_emb_sum, (B,D) or NULL), of residuals (g_res, (L,B,D) or NULL) and of qloss (g_qloss,
@@ -88,7 +94,7 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
  * (modules/transformer/attention.py:113-124), dropout 0, is_causal top-left.
  *   q[t][h][d] at q + t*sq + h*hd + d (likewise k, v, out, dout, dq, dk, dv with their strides);
  *   cu_q, cu_k (B+1) int64 offsets; max_q / max_k >= the longest segment (grid bound);
- *   lse (H, Tq) fp32 log-sum-exp per query (written by fwd, read by bwd). hd in {32, 64, 128}.
+ *   lse (H, Tq) fp32 log-sum-exp per query (written by fwd, read by bwd). hd in {16, 32, 64, 128}.
  * Backward is deterministic (no atomics): dk/dv per key block, dq per query block. */
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,

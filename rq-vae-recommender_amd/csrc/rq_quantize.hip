@@ -468,6 +468,186 @@ __global__ void __launch_bounds__(64) rq_cb_segsum_kernel(const float* __restric
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Register-resident forward for small D (D <= 64): items stay on the MFMA lane axis for the
+// whole L-level chain. Lane (j, h) holds item j's half-row x[j][h*D/2 .. +D/2) — exactly its
+// B-operand fragment — so the distance GEMM reads only codewords from LDS, the argmin is a
+// register scan, and the epilogue (rotation trick / STE / eval, VQ loss, next residual) runs on
+// the same registers with one xor-32 lane swap per row reduction. The next level's residual never
+// leaves the VGPRs; the codeword row for the epilogue comes from the LDS copy of the level.
+// RESIDENT: the whole level codebook fits one LDS image (K rows); otherwise it is streamed in
+// chunks of NB rows and the epilogue reads the chosen codeword from global memory (L2).
+template <int D, bool RESIDENT>
+__global__ void __launch_bounds__(256, 2)
+rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ cbs, const float* __restrict__ csq,
+                  int K, int L, int mode, float beta, int NB, int64_t* __restrict__ ids, float* __restrict__ emb_out,
+                  float* __restrict__ res, float* __restrict__ qloss, float* __restrict__ emb_sum) {
+  constexpr int H2 = D / 2, LD = D + 4;
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  float* A_s = dsm;              // [NB][LD] codewords of the current level / chunk
+  float* cs_s = dsm + NB * LD;   // [NB]     |c|^2
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
+  const int b = blockIdx.x * kTB + wave * 32 + (lane & 31);
+  const bool valid = b < B;
+  const int64_t BD = (int64_t)B * D;
+  const int64_t o = (int64_t)(valid ? b : 0) * D + h * H2;
+  float xv[H2], es[H2];
+#pragma unroll
+  for (int k = 0; k < H2; k += 4) {
+    const float4 v = valid ? *reinterpret_cast<const float4*>(x + o + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xv[k] = v.x; xv[k + 1] = v.y; xv[k + 2] = v.z; xv[k + 3] = v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < H2; ++k) es[k] = 0.f;
+  float ql = 0.f;
+
+  for (int l = 0; l < L; ++l) {
+    const float* cb = cbs + (int64_t)l * K * D;
+    if (valid) {   // residuals[l] = input of level l
+#pragma unroll
+      for (int k = 0; k < H2; k += 4)
+        *reinterpret_cast<float4*>(res + (int64_t)l * BD + o + k) = make_float4(xv[k], xv[k + 1], xv[k + 2], xv[k + 3]);
+    }
+    float xs = 0.f;
+#pragma unroll
+    for (int k = 0; k < H2; ++k) xs += xv[k] * xv[k];
+    xs += __shfl_xor(xs, 32, 64);
+    float best_d = INFINITY;
+    int best_i = 0;
+    for (int n0 = 0; n0 < K; n0 += NB) {
+      const int nrows = min(NB, K - n0);
+      __syncthreads();   // previous level / chunk fully consumed (incl. epilogue codeword reads)
+      for (int f = tid; f < nrows * (D / 4); f += 256) {
+        const int r = f / (D / 4), c = (f % (D / 4)) * 4;
+        *reinterpret_cast<float4*>(A_s + r * LD + c) = *reinterpret_cast<const float4*>(cb + (int64_t)(n0 + r) * D + c);
+      }
+      for (int r = tid; r < nrows; r += 256) cs_s[r] = csq[(int64_t)l * K + n0 + r];
+      __syncthreads();
+      for (int t0 = 0; t0 < nrows; t0 += 32) {
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        // rows past nrows read stale LDS; their distances are masked below (i < n0 + nrows)
+        const float* ap = A_s + (t0 + (lane & 31)) * LD + h * H2;
+#pragma unroll
+        for (int s4 = 0; s4 < H2; s4 += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(ap + s4);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, xv[s4], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, xv[s4 + 1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, xv[s4 + 2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, xv[s4 + 3], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int il = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float d = (xs + cs_s[il < NB ? il : 0]) - 2.f * acc[r];
+          const int i = n0 + il;
+          if (il < nrows && (d < best_d || (d == best_d && i < best_i))) { best_d = d; best_i = i; }
+        }
+      }
+    }
+    {
+      const float od = __shfl_xor(best_d, 32, 64);
+      const int oi = __shfl_xor(best_i, 32, 64);
+      if (od < best_d || (od == best_d && oi < best_i)) { best_d = od; best_i = oi; }
+    }
+    const int id = best_i;
+    // ---- epilogue on the item's two lanes
+    float ev[H2];
+    const float* er = RESIDENT ? (A_s + id * LD + h * H2) : (cb + (int64_t)id * D + h * H2);
+#pragma unroll
+    for (int k = 0; k < H2; k += 4) {
+      const float4 c = *reinterpret_cast<const float4*>(er + k);
+      ev[k] = c.x; ev[k + 1] = c.y; ev[k + 2] = c.z; ev[k + 3] = c.w;
+    }
+    float x2 = 0.f, e2 = 0.f, dl = 0.f;
+#pragma unroll
+    for (int k = 0; k < H2; ++k) {
+      x2 += xv[k] * xv[k];
+      e2 += ev[k] * ev[k];
+      const float t = xv[k] - ev[k];
+      dl += t * t;
+    }
+    x2 += __shfl_xor(x2, 32, 64);
+    e2 += __shfl_xor(e2, 32, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    float out[H2];
+    if (mode == kRotation) {
+      const float xn = sqrtf(x2), en = sqrtf(e2);
+      const float xd = xn + 1e-8f, ed = en + 1e-8f;
+      float u[H2], q[H2];
+      float s2 = 0.f, eu = 0.f;
+#pragma unroll
+      for (int k = 0; k < H2; ++k) {
+        u[k] = xv[k] / xd;
+        q[k] = ev[k] / ed;
+        const float sk = u[k] + q[k];
+        out[k] = sk;   // holds u+q until normalised
+        s2 += sk * sk;
+        eu += xv[k] * u[k];
+      }
+      s2 += __shfl_xor(s2, 32, 64);
+      eu += __shfl_xor(eu, 32, 64);
+      const float sn = fmaxf(sqrtf(s2), 1e-6f);
+      float ew = 0.f;
+#pragma unroll
+      for (int k = 0; k < H2; ++k) {
+        out[k] = out[k] / sn;   // w
+        ew += xv[k] * out[k];
+      }
+      ew += __shfl_xor(ew, 32, 64);
+      const float lam = en / (xn + 1e-6f);
+#pragma unroll
+      for (int k = 0; k < H2; ++k) out[k] = ((xv[k] - 2.f * (ew * out[k])) + 2.f * (eu * q[k])) * lam;
+    } else if (mode == kSte) {
+#pragma unroll
+      for (int k = 0; k < H2; ++k) out[k] = xv[k] + (ev[k] - xv[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < H2; ++k) out[k] = ev[k];
+    }
+    ql = ql + (dl + beta * dl);
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < H2; k += 4)
+        *reinterpret_cast<float4*>(emb_out + (int64_t)l * BD + o + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+      if (h == 0) ids[(int64_t)b * L + l] = id;
+    }
+#pragma unroll
+    for (int k = 0; k < H2; ++k) {
+      es[k] = es[k] + out[k];
+      xv[k] = xv[k] - out[k];   // next level's residual stays in registers
+    }
+  }
+  if (valid) {
+    if (h == 0) qloss[b] = ql;
+    if (emb_sum != nullptr) {
+#pragma unroll
+      for (int k = 0; k < H2; k += 4)
+        *reinterpret_cast<float4*>(emb_sum + o + k) = make_float4(es[k], es[k + 1], es[k + 2], es[k + 3]);
+    }
+  }
+}
+
+template <int D>
+static void launch_fwd_reg(int B, hipStream_t s, const float* x, const float* cbs, const float* csq, int K, int L,
+                           int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
+  constexpr int LD = D + 4;
+  constexpr int kMaxLds = 76 * 1024;              // two workgroups per CU
+  const int fit = kMaxLds / ((LD + 1) * 4);
+  const bool resident = K <= fit;
+  const int NB = resident ? K : (fit / 32) * 32;
+  const size_t lds = (size_t)NB * (LD + 1) * sizeof(float);
+  dim3 g((B + kTB - 1) / kTB);
+  if (resident)
+    hipLaunchKernelGGL((rq_fwd_reg_kernel<D, true>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB, ids, eo,
+                       res, ql, es);
+  else
+    hipLaunchKernelGGL((rq_fwd_reg_kernel<D, false>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB, ids,
+                       eo, res, ql, es);
+}
+
 // ---------------------------------------------------------------------------------------
 static bool row_split(int D, int& lpi, int& epl) {
   if (D < 8 || D > 1024 || (D & (D - 1)) != 0) return false;
@@ -508,9 +688,20 @@ int rq_codebook_sqnorm(const float* rows, int64_t n, int64_t D, float* out, void
   return 0;
 }
 
+int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
+                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
+                         float* qloss, float* emb_sum, int impl, void* stream);
+
 int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
                     float* emb_sum, void* stream) {
+  return rq_quantize_fwd_impl(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss, emb_sum,
+                              0, stream);
+}
+
+int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
+                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
+                         float* qloss, float* emb_sum, int impl, void* stream) {
   int lpi, epl;
   RQ_CHECK_ARG(x && codebooks && cb_sqnorm && ids && emb_out && residuals && qloss, "rq_quantize_fwd: null pointer");
   RQ_CHECK_ARG(row_split((int)D, lpi, epl), "rq_quantize_fwd: D=%lld must be a power of two in [8, 1024]", (long long)D);
@@ -522,6 +713,19 @@ int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks
   hipStream_t s = (hipStream_t)stream;
   dim3 g((unsigned)((B + kTB - 1) / kTB));
   const int b = (int)B, d = (int)D, k = (int)K, l = (int)L;
+  RQ_CHECK_ARG(impl >= 0 && impl <= 2, "rq_quantize_fwd_impl: impl must be 0 (auto), 1 (tiled) or 2 (register)");
+  if (impl == 0) impl = D <= 64 ? 2 : 1;
+  RQ_CHECK_ARG(impl == 1 || D <= 64, "rq_quantize_fwd_impl: register kernel needs D <= 64");
+  if (impl == 2) {
+    switch (D) {
+      case 8: launch_fwd_reg<8>(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;
+      case 16: launch_fwd_reg<16>(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;
+      case 32: launch_fwd_reg<32>(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;
+      case 64: launch_fwd_reg<64>(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;
+    }
+    RQ_LAUNCH_CHECK("rq_quantize_fwd(register)");
+    return 0;
+  }
   switch (D) {
 #define RQ_FWD_CASE(DD, BK, LPI, EPL) \
   case DD: launch_fwd<BK, LPI, EPL>(g, s, x, b, d, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;

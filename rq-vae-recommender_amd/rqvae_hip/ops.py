@@ -25,6 +25,7 @@ class KernelTimer:
     def __init__(self):
         self.enabled = False
         self.events = {}
+        self.bytes = {}
 
     def around(self, name, fn, *args):
         if not self.enabled:
@@ -37,6 +38,13 @@ class KernelTimer:
 
     def reset(self):
         self.events = {}
+        self.bytes = {}
+
+    def gbps(self, name):
+        """Algorithmic bytes / device time over all recorded launches of `name`."""
+        ev = self.events.get(name, [])
+        t = sum(a.elapsed_time(b) for a, b in ev) * 1e-3
+        return (sum(self.bytes.get(name, [])) / t / 1e9) if t > 0 else 0.0
 
     def mean_ms(self, name):
         ev = self.events.get(name, [])
@@ -135,8 +143,10 @@ class PaddedToJaggedValues(torch.autograd.Function):
         assert x.dim() == 3 and x.is_contiguous()
         B, N, D = x.shape
         vals = torch.empty((total, D), device=x.device, dtype=x.dtype)
-        call("jagged_from_padded", ptr(x), B, N, D, ptr(offsets), ptr(vals), _DTYPES[x.dtype], int(add_one_sub_one),
-             stream_handle(x.device))
+        TIMER.around("jagged_from_padded", call, "jagged_from_padded", ptr(x), B, N, D, ptr(offsets), ptr(vals),
+                     _DTYPES[x.dtype], int(add_one_sub_one), stream_handle(x.device))
+        if TIMER.enabled:
+            TIMER.bytes.setdefault("jagged_from_padded", []).append(2 * total * D * x.element_size())
         ctx.save_for_backward(offsets)
         ctx.shape = (B, N, D)
         return vals
@@ -147,8 +157,10 @@ class PaddedToJaggedValues(torch.autograd.Function):
         B, N, D = ctx.shape
         g_vals = g_vals.contiguous()
         gx = torch.empty((B, N, D), device=g_vals.device, dtype=g_vals.dtype)
-        call("jagged_to_padded", ptr(g_vals), ptr(offsets), B, N, D, ptr(gx), _DTYPES[g_vals.dtype],
-             stream_handle(g_vals.device))
+        TIMER.around("jagged_to_padded", call, "jagged_to_padded", ptr(g_vals), ptr(offsets), B, N, D, ptr(gx),
+                     _DTYPES[g_vals.dtype], stream_handle(g_vals.device))
+        if TIMER.enabled:
+            TIMER.bytes.setdefault("jagged_to_padded", []).append((g_vals.numel() + gx.numel()) * gx.element_size())
         return gx, None, None, None
 
 

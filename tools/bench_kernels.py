@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Kernel-level A/B timing in ONE process (guide §5.4 rule 24): interleaved rounds, HIP events.
+
+  python tools/bench_kernels.py [--rounds 5]
+
+Times rq_quantize_fwd_impl (1 = LDS-tiled, 2 = register-resident) at the BASELINE quantize
+shapes, the backward (rows + codebook reduction), jagged gather/scatter and varlen attention.
+Prints one JSON object per measurement.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rq-vae-recommender_amd"))
+
+import torch  # noqa: E402
+
+from rqvae_hip import ops  # noqa: E402
+from rqvae_hip._lib import call, ptr, stream_handle  # noqa: E402
+
+
+def ev_time(fn, iters=20):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def quantize_case(B, D, K, L, dev):
+    g = torch.Generator(device=dev).manual_seed(B + D)
+    x = torch.randn(B, D, generator=g, device=dev) / D ** 0.5
+    cbs = torch.randn(L, K, D, generator=g, device=dev) / D ** 0.5
+    csq = (cbs * cbs).sum(-1).contiguous()
+    outs = dict(ids=torch.empty(B, L, dtype=torch.int64, device=dev), emb=torch.empty(L, B, D, device=dev),
+                res=torch.empty(L, B, D, device=dev), ql=torch.empty(B, device=dev), es=torch.empty(B, D, device=dev))
+    return x, cbs, csq, outs
+
+
+def run_impl(x, cbs, csq, o, impl, mode=3):
+    B, D = x.shape
+    L, K, _ = cbs.shape
+    call("rq_quantize_fwd_impl", ptr(x), B, D, ptr(cbs), ptr(csq), K, L, mode, 0.25, ptr(o["ids"]), ptr(o["emb"]),
+         ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    results = []
+    shapes = [(65536, 64, 256, 3), (65536, 32, 256, 3), (262144, 64, 256, 3), (64, 64, 256, 3),
+              (16384, 1024, 2048, 4)]
+    for (B, D, K, L) in shapes:
+        x, cbs, csq, o = quantize_case(B, D, K, L, dev)
+        impls = [1, 2] if D <= 64 else [1]
+        ref = None
+        for impl in impls:
+            run_impl(x, cbs, csq, o, impl)
+            ids = o["ids"].clone()
+            if ref is None:
+                ref = ids
+            else:
+                results.append(dict(check="ids_equal_impl1_vs_%d" % impl, shape=[B, D, K, L],
+                                    frac_equal=float((ids == ref).all(1).float().mean())))
+        times = {i: [] for i in impls}
+        for _ in range(args.rounds):
+            for impl in impls:
+                times[impl].append(ev_time(lambda: run_impl(x, cbs, csq, o, impl), 10))
+        flops = 2.0 * K * D * L * B
+        for impl in impls:
+            ms = sorted(times[impl])
+            results.append(dict(kernel="rq_quantize_fwd", impl=impl, shape=[B, D, K, L], median_ms=ms[len(ms) // 2],
+                                min_ms=ms[0], tflops=flops / (ms[len(ms) // 2] * 1e-3) / 1e12))
+        # backward
+        xr = x.clone().requires_grad_(True)
+        cr = cbs.clone().requires_grad_(True)
+        emb, res, ids, ql, es = ops.rq_quantize(xr, cr, ops.MODE_ROTATION, 0.25)
+        ges, gq = torch.randn_like(es), torch.rand_like(ql)
+        nbytes = ops._lib.load().rq_quantize_bwd_workspace(B, D, K, L)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        gx, gcb = torch.empty_like(x), torch.empty_like(cbs)
+
+        def bwd():
+            call("rq_quantize_bwd", ptr(res), ptr(ids), ptr(cbs), B, D, K, L, 3, 0.25, None, ptr(ges), None, ptr(gq),
+                 ptr(gx), ptr(gcb), ptr(ws), nbytes, stream_handle())
+        ms = sorted(ev_time(bwd, 10) for _ in range(args.rounds))
+        results.append(dict(kernel="rq_quantize_bwd", shape=[B, D, K, L], median_ms=ms[len(ms) // 2]))
+        del x, cbs, csq, o, xr, cr, emb, res, ws
+        torch.cuda.empty_cache()
+    for r in results:
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
