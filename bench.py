@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     return ap.parse_args()
 
 
@@ -128,6 +129,9 @@ def main():
     rk, ws, lr = dp.init_from_env()
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs an MI355X (no GPU visible)")
+    if args.decoder_only:
+        print(json.dumps(measure_decoder(torch.device("cuda", lr))), flush=True)
+        return
     device = torch.device("cuda", lr)
     torch.cuda.set_device(device)
     B = args.batch
@@ -243,17 +247,26 @@ def measure_extras(model, device, x):
     dt = time_region(tok, 10, 3, sync)
     out["eval_tokenize_items_per_s"] = round(10 * x.shape[0] / dt, 1)
     model.train()
-    # config batch B=64 step latency (eager)
+    # config batch B=64 step latency: eager, and the whole step replayed as one hipGraph
+    from rqvae_hip.graph import CapturedStep
     xs = x[:64].contiguous()
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True, capturable=True)
 
     def small():
         opt.zero_grad(set_to_none=False)
         o = model(SeqBatch(None, None, None, xs, None, None), gumbel_t=0.2)
         o.loss.backward()
         opt.step()
+        return o.loss
     dt = time_region(small, 20, 5, sync)
     out["b64_step_ms"] = round(dt / 20 * 1e3, 3)
+    try:
+        g = CapturedStep(small)
+        dt = time_region(g, 50, 5, sync)
+        out["b64_step_ms_hipgraph"] = round(dt / 50 * 1e3, 4)
+        out["b64_items_per_s_hipgraph"] = round(50 * 64 / dt, 1)
+    except Exception as e:  # report, never hide
+        out["b64_hipgraph_error"] = repr(e)[:300]
     out.update(measure_decoder(device))
     return out
 

@@ -361,7 +361,7 @@ rq_bwd_rows_kernel(const float* __restrict__ res, const int64_t* __restrict__ id
       gn[k] = gn[k] + gx[k];
       if (g_res) gn[k] += g_res[(int64_t)l * BD + o + k];
     }
-    if (valid) {
+    if (valid && contrib != nullptr) {   // eval mode only: the codeword also gets the emb_out grad
 #pragma unroll
       for (int k = 0; k < EPL; k += 4)
         *reinterpret_cast<float4*>(contrib + (int64_t)l * BD + o + k) = make_float4(cc[k], cc[k + 1], cc[k + 2], cc[k + 3]);
@@ -375,9 +375,10 @@ rq_bwd_rows_kernel(const float* __restrict__ res, const int64_t* __restrict__ id
 }
 
 // ---------------------------------------------------------------------------------------
-// Stable counting sort of ids per level (keys < K <= 4096): per-block histograms, a
-// key-major exclusive scan, then an in-order scatter (ballot ranks) — deterministic order
-// (ascending row index within each key).
+// Stable counting sort of ids per level (keys < K <= 4096) -> perm (rows grouped by codeword,
+// ascending row index inside a codeword): per-block histograms hist[l][blk][k] (key fastest,
+// coalesced), a per-key scan over blocks, an exclusive scan over keys, then an in-order scatter
+// with ballot ranks. Deterministic by construction (no atomics decide any order).
 constexpr int kSortRows = 256;   // rows per sort block
 
 __global__ void __launch_bounds__(256) sort_hist_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
@@ -387,43 +388,61 @@ __global__ void __launch_bounds__(256) sort_hist_kernel(const int64_t* __restric
   for (int k = threadIdx.x; k < K; k += 256) cnt[k] = 0;
   __syncthreads();
   const int r = blk * kSortRows + threadIdx.x;
-  if (r < B) atomicAdd(&cnt[(int)ids[(int64_t)r * L + l]], 1);
+  if (r < B) atomicAdd(&cnt[(int)ids[(int64_t)r * L + l]], 1);   // counts only: order-free
   __syncthreads();
-  for (int k = threadIdx.x; k < K; k += 256) hist[((int64_t)l * K + k) * nblk + blk] = cnt[k];
+  int* h = hist + ((int64_t)l * nblk + blk) * K;
+  for (int k = threadIdx.x; k < K; k += 256) h[k] = cnt[k];
 }
 
-// Exclusive scan of hist[l] (K*nblk ints) in place; key_off[l][k] = first slot of key k.
-__global__ void __launch_bounds__(1024) sort_scan_kernel(int* __restrict__ hist, int K, int nblk, int B,
-                                                          int* __restrict__ key_off) {
+// Per key: exclusive scan over blocks (in place) and the key's total -> key_off[l][k].
+__global__ void __launch_bounds__(256) sort_keyscan_kernel(int* __restrict__ hist, int K, int nblk,
+                                                            int* __restrict__ key_off) {
+  const int l = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  int* h = hist + (int64_t)l * nblk * K + k;
+  int run = 0;
+  int blk = 0;
+  for (; blk + 8 <= nblk; blk += 8) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = h[(int64_t)(blk + u) * K];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { h[(int64_t)(blk + u) * K] = run; run += v[u]; }
+  }
+  for (; blk < nblk; ++blk) { const int v = h[(int64_t)blk * K]; h[(int64_t)blk * K] = run; run += v; }
+  key_off[(int64_t)l * (K + 1) + k] = run;
+}
+
+// Exclusive scan of the per-key totals in place: key_off[l][k] = first slot of key k; [K] = B.
+__global__ void __launch_bounds__(1024) sort_offsets_kernel(int* __restrict__ key_off, int K, int B) {
   __shared__ int part[1024];
   const int l = blockIdx.x, t = threadIdx.x;
-  const int64_t n = (int64_t)K * nblk;
-  int* h = hist + (int64_t)l * n;
-  const int64_t per = (n + 1023) / 1024;
-  const int64_t a = t * per, e = a + per < n ? a + per : n;
+  int* ko = key_off + (int64_t)l * (K + 1);
+  const int per = (K + 1023) / 1024;
+  const int a = t * per, e = min(a + per, K);
   int s = 0;
-  for (int64_t i = a; i < e; ++i) s += h[i];
+  for (int i = a; i < e; ++i) s += ko[i];
   part[t] = s;
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan of the partials
+  for (int o = 1; o < 1024; o <<= 1) {
     const int v = t >= o ? part[t - o] : 0;
     __syncthreads();
     part[t] += v;
     __syncthreads();
   }
   int run = part[t] - s;
-  for (int64_t i = a; i < e; ++i) { const int c = h[i]; h[i] = run; run += c; }
-  __syncthreads();
-  for (int k = t; k < K; k += 1024) key_off[(int64_t)l * (K + 1) + k] = h[(int64_t)k * nblk];
-  if (t == 0) key_off[(int64_t)l * (K + 1) + K] = B;
+  for (int i = a; i < e; ++i) { const int c = ko[i]; ko[i] = run; run += c; }
+  if (t == 0) ko[K] = B;
 }
 
 __global__ void __launch_bounds__(64) sort_scatter_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
                                                           int nblk, const int* __restrict__ hist,
-                                                          int* __restrict__ perm) {
+                                                          const int* __restrict__ key_off, int* __restrict__ perm) {
   extern __shared__ int base[];
   const int l = blockIdx.y, blk = blockIdx.x, lane = threadIdx.x;
-  for (int k = lane; k < K; k += 64) base[k] = hist[((int64_t)l * K + k) * nblk + blk];
+  const int* h = hist + ((int64_t)l * nblk + blk) * K;
+  const int* ko = key_off + (int64_t)l * (K + 1);
+  for (int k = lane; k < K; k += 64) base[k] = ko[k] + h[k];
   __syncthreads();
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int c = 0; c < kSortRows; c += 64) {
@@ -436,7 +455,7 @@ __global__ void __launch_bounds__(64) sort_scatter_kernel(const int64_t* __restr
       const int k = __shfl(key, leader, 64);
       const unsigned long long m = __ballot(v && key == k) & rem;
       if (v && key == k) perm[(int64_t)l * B + base[k] + __popcll(m & lt)] = r;
-      __syncthreads();   // single wave: orders the LDS read above before the update below
+      __syncthreads();   // single wave: the LDS read above retires before the update below
       if (lane == leader) base[k] += __popcll(m);
       __syncthreads();
       rem &= ~m;
@@ -444,30 +463,60 @@ __global__ void __launch_bounds__(64) sort_scatter_kernel(const int64_t* __restr
   }
 }
 
-// grad_cb[l][k] = sum over rows with id k (ascending row order) of contrib[l][row].
-__global__ void __launch_bounds__(64) rq_cb_segsum_kernel(const float* __restrict__ contrib, const int* __restrict__ perm,
-                                                          const int* __restrict__ key_off, int B, int D, int K,
-                                                          float* __restrict__ grad_cb) {
-  const int k = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
+// grad_cb[l][k] = sum over the rows b of codeword k of c_b, with
+//   c_b = (2 gl_b) (e_k - x_b)            (rotation / STE: recomputed from residuals, no buffer)
+//   c_b = contrib[l][b]                   (eval mode: includes the emb_out gradient)
+// One workgroup (4 waves) per codeword; wave w reduces the w-th contiguous quarter of the
+// segment, RPW rows per wave-step when D < 64; partials are combined in a fixed order.
+__global__ void __launch_bounds__(256) rq_cb_segsum_kernel(const float* __restrict__ res, const float* __restrict__ cbs,
+                                                           const float* __restrict__ g_qloss,
+                                                           const float* __restrict__ contrib, const int* __restrict__ perm,
+                                                           const int* __restrict__ key_off, int B, int D, int K,
+                                                           float* __restrict__ grad_cb) {
+  __shared__ float part[4 * 1024];
+  const int k = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int a = key_off[(int64_t)l * (K + 1) + k], e = key_off[(int64_t)l * (K + 1) + k + 1];
+  const int n = e - a, q = (n + 3) / 4;
+  const int wa = a + min(n, wave * q), we = a + min(n, (wave + 1) * q);
   const int* p = perm + (int64_t)l * B;
-  const float* cbase = contrib + (int64_t)l * B * D;
-  float* out = grad_cb + ((int64_t)l * K + k) * D;
+  const int64_t BD = (int64_t)B * D;
+  const float* xb = contrib ? contrib + (int64_t)l * BD : res + (int64_t)l * BD;
+  const float* ek = cbs + ((int64_t)l * K + k) * D;
+  const int cpw = D < 64 ? D : 64, rpw = 64 / cpw;
+  const int rs = lane / cpw, dl = lane % cpw;
   for (int d0 = 0; d0 < D; d0 += 64) {
-    const int d = d0 + lane;
-    if (d >= D) break;
+    const int d = d0 + dl;
+    const float e_d = (contrib || d >= D) ? 0.f : ek[d];
     float acc = 0.f;
-    int i = a;
-    for (; i + 4 <= e; i += 4) {
-      const float v0 = cbase[(int64_t)p[i] * D + d], v1 = cbase[(int64_t)p[i + 1] * D + d];
-      const float v2 = cbase[(int64_t)p[i + 2] * D + d], v3 = cbase[(int64_t)p[i + 3] * D + d];
-      acc += v0; acc += v1; acc += v2; acc += v3;
+    int i = wa + rs;
+    for (; i + 3 * rpw < we; i += 4 * rpw) {
+      int rr[4];
+      float v[4], g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rr[u] = p[i + u * rpw];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = xb[(int64_t)rr[u] * D + d];
+        g[u] = contrib ? 1.f : (g_qloss ? g_qloss[rr[u]] : 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += contrib ? v[u] : (2.f * g[u]) * (e_d - v[u]);
     }
-    for (; i < e; ++i) acc += cbase[(int64_t)p[i] * D + d];
-    out[d] = acc;
+    for (; i < we; i += rpw) {
+      const int r = p[i];
+      const float v = xb[(int64_t)r * D + d];
+      acc += contrib ? v : (2.f * (g_qloss ? g_qloss[r] : 0.f)) * (e_d - v);
+    }
+    part[(wave * rpw + rs) * 64 + dl] = acc;
+    __syncthreads();
+    if (tid < cpw) {
+      float s = 0.f;
+      for (int j = 0; j < 4 * rpw; ++j) s += part[j * 64 + tid];
+      grad_cb[((int64_t)l * K + k) * D + d0 + tid] = s;
+    }
+    __syncthreads();
   }
 }
-
 
 // ---------------------------------------------------------------------------------------
 // Register-resident forward for small D (D <= 64): items stay on the MFMA lane axis for the
@@ -478,18 +527,25 @@ __global__ void __launch_bounds__(64) rq_cb_segsum_kernel(const float* __restric
 // leaves the VGPRs; the codeword row for the epilogue comes from the LDS copy of the level.
 // RESIDENT: the whole level codebook fits one LDS image (K rows); otherwise it is streamed in
 // chunks of NB rows and the epilogue reads the chosen codeword from global memory (L2).
-template <int D, bool RESIDENT>
+template <int D, bool RESIDENT, int WPI>
 __global__ void __launch_bounds__(256, 2)
 rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ cbs, const float* __restrict__ csq,
                   int K, int L, int mode, float beta, int NB, int64_t* __restrict__ ids, float* __restrict__ emb_out,
                   float* __restrict__ res, float* __restrict__ qloss, float* __restrict__ emb_sum) {
+  // WPI waves share one 32-item tile and split its codeword tiles (small-B latency mode);
+  // items per workgroup = 128 / WPI. All WPI waves run the (cheap) epilogue redundantly so each
+  // keeps the next residual in its own registers; only sub-wave 0 stores.
   constexpr int H2 = D / 2, LD = D + 4;
   extern __shared__ __attribute__((aligned(16))) float dsm[];
-  float* A_s = dsm;              // [NB][LD] codewords of the current level / chunk
-  float* cs_s = dsm + NB * LD;   // [NB]     |c|^2
+  float* A_s = dsm;                                  // [NB][LD] codewords of the current level / chunk
+  float* cs_s = dsm + NB * LD;                       // [NB]     |c|^2
+  float* rd_s = cs_s + NB;                           // [4][32]  per-wave best distance (WPI > 1)
+  int* ri_s = reinterpret_cast<int*>(rd_s + 128);    // [4][32]  per-wave best index
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  const int b = blockIdx.x * kTB + wave * 32 + (lane & 31);
+  const int tile = wave / WPI, wsub = wave % WPI;
+  const int b = blockIdx.x * (128 / WPI) + tile * 32 + (lane & 31);
   const bool valid = b < B;
+  const bool writer = valid && wsub == 0;
   const int64_t BD = (int64_t)B * D;
   const int64_t o = (int64_t)(valid ? b : 0) * D + h * H2;
   float xv[H2], es[H2];
@@ -504,7 +560,7 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
 
   for (int l = 0; l < L; ++l) {
     const float* cb = cbs + (int64_t)l * K * D;
-    if (valid) {   // residuals[l] = input of level l
+    if (writer) {   // residuals[l] = input of level l
 #pragma unroll
       for (int k = 0; k < H2; k += 4)
         *reinterpret_cast<float4*>(res + (int64_t)l * BD + o + k) = make_float4(xv[k], xv[k + 1], xv[k + 2], xv[k + 3]);
@@ -524,11 +580,11 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
       }
       for (int r = tid; r < nrows; r += 256) cs_s[r] = csq[(int64_t)l * K + n0 + r];
       __syncthreads();
-      for (int t0 = 0; t0 < nrows; t0 += 32) {
+      for (int t0 = wsub * 32; t0 < nrows; t0 += 32 * WPI) {
         floatx16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        // rows past nrows read stale LDS; their distances are masked below (i < n0 + nrows)
+        // rows past nrows read stale LDS; their distances are masked below (il < nrows)
         const float* ap = A_s + (t0 + (lane & 31)) * LD + h * H2;
 #pragma unroll
         for (int s4 = 0; s4 < H2; s4 += 4) {
@@ -551,6 +607,18 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
       const float od = __shfl_xor(best_d, 32, 64);
       const int oi = __shfl_xor(best_i, 32, 64);
       if (od < best_d || (od == best_d && oi < best_i)) { best_d = od; best_i = oi; }
+    }
+    if constexpr (WPI > 1) {   // combine the sub-waves' candidates in a fixed order
+      if (h == 0) { rd_s[wave * 32 + lane] = best_d; ri_s[wave * 32 + lane] = best_i; }
+      __syncthreads();
+      best_d = INFINITY;
+      best_i = 0;
+#pragma unroll
+      for (int w = 0; w < WPI; ++w) {
+        const float od = rd_s[(tile * WPI + w) * 32 + (lane & 31)];
+        const int oi = ri_s[(tile * WPI + w) * 32 + (lane & 31)];
+        if (od < best_d || (od == best_d && oi < best_i)) { best_d = od; best_i = oi; }
+      }
     }
     const int id = best_i;
     // ---- epilogue on the item's two lanes
@@ -608,7 +676,7 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
       for (int k = 0; k < H2; ++k) out[k] = ev[k];
     }
     ql = ql + (dl + beta * dl);
-    if (valid) {
+    if (writer) {
 #pragma unroll
       for (int k = 0; k < H2; k += 4)
         *reinterpret_cast<float4*>(emb_out + (int64_t)l * BD + o + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
@@ -620,7 +688,7 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
       xv[k] = xv[k] - out[k];   // next level's residual stays in registers
     }
   }
-  if (valid) {
+  if (writer) {
     if (h == 0) qloss[b] = ql;
     if (emb_sum != nullptr) {
 #pragma unroll
@@ -630,22 +698,34 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
   }
 }
 
+template <int D, int WPI>
+static void launch_fwd_reg_w(int B, hipStream_t s, const float* x, const float* cbs, const float* csq, int K, int L,
+                             int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
+  constexpr int LD = D + 4;
+  constexpr int kMaxLds = 75 * 1024;              // two workgroups per CU
+  const int fit = (kMaxLds - 1024) / ((LD + 1) * 4);
+  const bool resident = K <= fit;
+  const int NB = resident ? K : (fit / 32) * 32;
+  const size_t lds = (size_t)NB * (LD + 1) * sizeof(float) + 1024;
+  dim3 g((B + 128 / WPI - 1) / (128 / WPI));
+  if (resident)
+    hipLaunchKernelGGL((rq_fwd_reg_kernel<D, true, WPI>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB,
+                       ids, eo, res, ql, es);
+  else
+    hipLaunchKernelGGL((rq_fwd_reg_kernel<D, false, WPI>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB,
+                       ids, eo, res, ql, es);
+}
+
 template <int D>
 static void launch_fwd_reg(int B, hipStream_t s, const float* x, const float* cbs, const float* csq, int K, int L,
                            int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
-  constexpr int LD = D + 4;
-  constexpr int kMaxLds = 76 * 1024;              // two workgroups per CU
-  const int fit = kMaxLds / ((LD + 1) * 4);
-  const bool resident = K <= fit;
-  const int NB = resident ? K : (fit / 32) * 32;
-  const size_t lds = (size_t)NB * (LD + 1) * sizeof(float);
-  dim3 g((B + kTB - 1) / kTB);
-  if (resident)
-    hipLaunchKernelGGL((rq_fwd_reg_kernel<D, true>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB, ids, eo,
-                       res, ql, es);
+  // fewer 128-item workgroups than CUs: let 2 or 4 waves split each 32-item tile's codewords
+  if (B <= 256 * 32)
+    launch_fwd_reg_w<D, 4>(B, s, x, cbs, csq, K, L, mode, beta, ids, eo, res, ql, es);
+  else if (B <= 256 * 128)
+    launch_fwd_reg_w<D, 2>(B, s, x, cbs, csq, K, L, mode, beta, ids, eo, res, ql, es);
   else
-    hipLaunchKernelGGL((rq_fwd_reg_kernel<D, false>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB, ids,
-                       eo, res, ql, es);
+    launch_fwd_reg_w<D, 1>(B, s, x, cbs, csq, K, L, mode, beta, ids, eo, res, ql, es);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -779,7 +859,7 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   }
   switch (D) {
 #define RQ_BWD_CASE(DD, LPI, EPL) \
-  case DD: launch_bwd<LPI, EPL>(b, s, residuals, ids, codebooks, d, k, l, mode, beta, g_emb, g_emb_sum, g_res, g_qloss, grad_x, contrib); break;
+  case DD: launch_bwd<LPI, EPL>(b, s, residuals, ids, codebooks, d, k, l, mode, beta, g_emb, g_emb_sum, g_res, g_qloss, grad_x, mode == kEval ? contrib : nullptr); break;
     RQ_BWD_CASE(8, 2, 4)
     RQ_BWD_CASE(16, 4, 4)
     RQ_BWD_CASE(32, 8, 4)
@@ -793,9 +873,12 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   }
   RQ_LAUNCH_CHECK("rq_bwd_rows");
   hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, l), dim3(256), k * sizeof(int), s, ids, b, l, k, nblk, hist);
-  hipLaunchKernelGGL(sort_scan_kernel, dim3(l), dim3(1024), 0, s, hist, k, nblk, b, key_off);
-  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, l), dim3(64), k * sizeof(int), s, ids, b, l, k, nblk, hist, perm);
-  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, l), dim3(64), 0, s, contrib, perm, key_off, b, d, k, grad_codebooks);
+  hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 255) / 256, l), dim3(256), 0, s, hist, k, nblk, key_off);
+  hipLaunchKernelGGL(sort_offsets_kernel, dim3(l), dim3(1024), 0, s, key_off, k, b);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, l), dim3(64), k * sizeof(int), s, ids, b, l, k, nblk, hist, key_off,
+                     perm);
+  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, l), dim3(256), 0, s, residuals, codebooks, g_qloss,
+                     mode == kEval ? contrib : nullptr, perm, key_off, b, d, k, grad_codebooks);
   RQ_LAUNCH_CHECK("rq_codebook_grad");
   return 0;
 }

@@ -22,7 +22,7 @@ from modules.embedding.id_embedder import SemIdEmbedder, UserIdEmbedder
 from modules.normalize import RMSNorm
 from modules.transformer.model import TransformerEncoderDecoder
 from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
-from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged_tensor
+from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged
 
 
 class ModelOutput(NamedTuple):
@@ -78,11 +78,12 @@ class EncoderDecoderRetrievalModel(nn.Module):
         if fut_emb is not None:
             fut = torch.cat([fut, fut_emb + self.tte(batch.token_type_ids_fut)], dim=1)
         ctx_lengths = batch.seq_mask.sum(axis=1) + 1
-        ctx_nt = padded_to_jagged_tensor(ctx.contiguous(), lengths=ctx_lengths, max_len=ctx.shape[1])
-        fut_lengths = torch.full((B,), fut.shape[1], device=fut.device, dtype=torch.int64)
-        fut_nt = padded_to_jagged_tensor(fut.contiguous(), lengths=fut_lengths, max_len=fut.shape[1])
-        transformer_context = self.in_proj_context(self.do(self.norm(ctx_nt)))
-        transformer_input = self.in_proj(self.do(self.norm_cxt(fut_nt)))
+        ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1])          # one host sync (total)
+        nf = fut.shape[1]                                                                # fixed length: no sync
+        fut_lengths = torch.full((B,), nf, device=fut.device, dtype=torch.int64)
+        fut_j = padded_to_jagged(fut.contiguous(), fut_lengths, nf, total=B * nf, known_max=nf)
+        transformer_context = ctx_j.with_values(self.in_proj_context(self.do(self.norm(ctx_j.values()))))
+        transformer_input = fut_j.with_values(self.in_proj(self.do(self.norm_cxt(fut_j.values()))))
         return self.transformer(x=transformer_input, context=transformer_context, padding_mask=batch.seq_mask,
                                 jagged=True)
 
@@ -90,16 +91,16 @@ class EncoderDecoderRetrievalModel(nn.Module):
         B = batch.seq_mask.shape[0]
         trnsf_out = self._predict(batch)
         if self.training or not self.enable_generation:
-            predict_out = self.out_proj(trnsf_out)
+            predict_out = self.out_proj(jagged_to_flattened_tensor(trnsf_out))
             # sem_ids_fut is fixed length, so the jagged values reshape to (B, L+2, K)
-            logits = jagged_to_flattened_tensor(predict_out).view(B, -1, self.num_embeddings)[:, :-1, :].flatten(end_dim=1)
+            logits = predict_out.view(B, -1, self.num_embeddings)[:, :-1, :].flatten(end_dim=1)
             target = batch.sem_ids_fut.flatten(end_dim=1)
             unred_loss = F.cross_entropy(logits, target, reduction="none", ignore_index=-1).view(B, -1)
             loss = unred_loss.sum(axis=1).mean()
             if not self.training:
                 self.transformer.cached_enc_output = None
             return ModelOutput(loss=loss, logits=logits, loss_d=unred_loss.mean(axis=0))
-        last = jagged_to_flattened_tensor(trnsf_out.contiguous()).view(B, -1, self.attn_dim)[:, -1, :]
+        last = jagged_to_flattened_tensor(trnsf_out).contiguous().view(B, -1, self.attn_dim)[:, -1, :]
         return ModelOutput(loss=None, logits=self.out_proj(last), loss_d=None)
 
     @eval_mode
@@ -149,7 +150,7 @@ class EncoderDecoderRetrievalModel(nn.Module):
                 n_ctx = cur.sem_ids.shape[1] + 1
                 padded = jagged_to_padded_tensor(enc, n_ctx).repeat_interleave(k, dim=0)
                 lengths = enc.offsets().diff().repeat_interleave(k)
-                self.transformer.cached_enc_output = padded_to_jagged_tensor(padded.contiguous(), lengths, max_len=n_ctx)
+                self.transformer.cached_enc_output = padded_to_jagged(padded.contiguous(), lengths, n_ctx)
                 cur = TokenizedSeqBatch(user_ids=cur.user_ids.repeat_interleave(k, dim=0),
                                         sem_ids=cur.sem_ids.repeat_interleave(k, dim=0), sem_ids_fut=nxt,
                                         token_type_ids_fut=torch.zeros_like(nxt),

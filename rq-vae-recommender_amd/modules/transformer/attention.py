@@ -18,16 +18,10 @@ import torch
 from torch import nn
 from torch import Tensor
 
+from ops.jagged import Jagged, as_jagged
 from rqvae_hip import ops as hip_ops
 
-AttentionInput = Union[Tensor, "torch.nested.Tensor"]
-
-
-def _max_seqlen(nt) -> int:
-    m = getattr(nt, "_maybe_max_seqlen", None)
-    if m is None:
-        m = nt._get_max_seqlen()
-    return int(m)
+AttentionInput = Union[Tensor, "torch.nested.Tensor", Jagged]
 
 
 def _wrap_like(values: Tensor, like):
@@ -49,11 +43,13 @@ class Attend(nn.Module):
         self.dropout = dropout
 
     def jagged_forward(self, qu, ke, va, is_causal: bool):
-        """softmax(q k^T / sqrt(head_dim)) v per sequence; NJT (B, j, H*hd) in and out."""
+        """softmax(q k^T / sqrt(head_dim)) v per sequence; NJT (B, j, H*hd) in and out (a dense
+        ``Jagged`` in gives a ``Jagged`` out)."""
         assert not (self.training and self.dropout), "attention dropout is not supported (reference forces 0)"
-        out = hip_ops.varlen_attention(qu.values(), ke.values(), va.values(), qu.offsets(), ke.offsets(),
-                                       self.num_heads, bool(is_causal), _max_seqlen(qu), _max_seqlen(ke))
-        return _wrap_like(out, qu)
+        jq, jk, jv = as_jagged(qu), as_jagged(ke), as_jagged(va)
+        out = hip_ops.varlen_attention(jq.values(), jk.values(), jv.values(), jq.offsets(), jk.offsets(),
+                                       self.num_heads, bool(is_causal), jq.max_len, jk.max_len)
+        return jq.with_values(out) if isinstance(qu, Jagged) else _wrap_like(out, qu)
 
     def forward(self, qkv: Tensor, is_causal: bool = False) -> Tensor:
         raise Exception("Unjagged attention currently not supported.")
@@ -88,10 +84,15 @@ class MultiHeadAttention(nn.Module):
         assert not self.cross_attn or x_kv is not None, "Found null x_kv in cross attn. layer"
         if not jagged:
             raise Exception("Unjagged attention currently not supported.")
+        jx = as_jagged(x)
         if self.cross_attn:
-            queries = self.q(x)
-            keys, values = self.kv(x_kv).chunk(2, dim=-1)
+            jkv = as_jagged(x_kv)
+            q = self.q(jx.values())
+            k, v = self.kv(jkv.values()).chunk(2, dim=-1)
         else:
-            queries, keys, values = self.qkv(x).chunk(3, dim=-1)
-        context_vec = self.attend.jagged_forward(queries, keys, values, is_causal=is_causal)
-        return self.proj(context_vec)
+            jkv = jx
+            q, k, v = self.qkv(jx.values()).chunk(3, dim=-1)   # strided row views, consumed in place
+        ctx = hip_ops.varlen_attention(q, k, v, jx.offsets(), jkv.offsets(), self.num_heads, bool(is_causal),
+                                       jx.max_len, jkv.max_len)
+        out = self.proj(ctx)
+        return jx.with_values(out) if isinstance(x, Jagged) else _wrap_like(out, x)

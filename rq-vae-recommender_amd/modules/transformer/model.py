@@ -8,6 +8,10 @@ Block semantics reproduced exactly (SURVEY A-11):
   h  += CrossAttn(Dropout(cross_attn_norm(x)), context)      # norm of x, not h
   out = h + Dropout(MLP(RMSNorm(h)))                          # `ffn_norm` exists but is unused
 The encoder output is cached in eval mode (`cached_enc_output`) exactly like the reference.
+
+Jagged inputs may be torch NJTs (drop-in) or dense ``ops.jagged.Jagged`` views; NJTs are
+unwrapped once at the module boundary and every row-wise op (RMSNorm, dropout, Linear, residual
+adds) runs on the dense (T, C) values, avoiding NJT's per-op Python dispatch.
 """
 from typing import List, Optional
 
@@ -16,7 +20,8 @@ from torch import Tensor
 
 from modules.encoder import MLP
 from modules.normalize import RMSNorm
-from modules.transformer.attention import AttentionInput, MultiHeadAttention
+from modules.transformer.attention import AttentionInput, MultiHeadAttention, _wrap_like
+from ops.jagged import Jagged, as_jagged
 
 
 class KVCacheOpsMixin:
@@ -53,13 +58,22 @@ class TransformerBlock(nn.Module):
 
     def forward(self, x: AttentionInput, x_kv: Optional[Tensor] = None, padding_mask: Optional[Tensor] = None,
                 is_causal: Optional[bool] = True, jagged: Optional[bool] = False) -> AttentionInput:
+        if not jagged:
+            raise Exception("Unjagged attention currently not supported.")
+        jx = as_jagged(x)
+        jkv = as_jagged(x_kv) if x_kv is not None else None
+        out = self._forward_jagged(jx, jkv, is_causal)
+        return out if isinstance(x, Jagged) else _wrap_like(out.values(), x)
+
+    def _forward_jagged(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool) -> Jagged:
         use_cache = not self.training and self.enable_kv_cache
-        h = x + self.attention(self.do(self.attn_norm(x)), padding_mask=padding_mask, is_causal=is_causal,
-                               jagged=jagged, use_cache=use_cache)
+        xv = jx.values()
+        h = xv + self.attention(jx.with_values(self.do(self.attn_norm(xv))), is_causal=is_causal, jagged=True,
+                                use_cache=use_cache).values()
         if self.do_cross_attn:
-            h = h + self.cross_attention(x=self.do(self.cross_attn_norm(x)), x_kv=x_kv, padding_mask=padding_mask,
-                                         is_causal=False, jagged=jagged, use_cache=use_cache)
-        return h + self.ff(h)
+            h = h + self.cross_attention(x=jx.with_values(self.do(self.cross_attn_norm(xv))), x_kv=jkv,
+                                         is_causal=False, jagged=True, use_cache=use_cache).values()
+        return jx.with_values(h + self.ff(h))
 
     def reset_kv_cache(self):
         raise NotImplementedError("KV Cache currently not supported")
@@ -81,9 +95,13 @@ class TransformerDecoder(nn.Module, KVCacheOpsMixin):
 
     def forward(self, x: AttentionInput, padding_mask: Optional[Tensor] = None, is_causal: Optional[bool] = True,
                 context: Optional[Tensor] = None, jagged: Optional[bool] = None) -> AttentionInput:
+        if not jagged:
+            raise Exception("Unjagged attention currently not supported.")
+        h = as_jagged(x)
+        ctx = as_jagged(context) if context is not None else None
         for layer in self.layers:
-            x = layer(x=x, x_kv=context, padding_mask=padding_mask, is_causal=is_causal, jagged=jagged)
-        return x
+            h = layer._forward_jagged(h, ctx, is_causal)
+        return h if isinstance(x, Jagged) else _wrap_like(h.values(), x)
 
 
 class TransformerEncoderDecoder(nn.Module, KVCacheOpsMixin):

@@ -16,21 +16,75 @@ from torch import Tensor
 
 from rqvae_hip import ops as hip_ops
 
-__all__ = ["padded_to_jagged_tensor", "jagged_to_flattened_tensor", "jagged_to_padded_tensor"]
+__all__ = ["padded_to_jagged_tensor", "jagged_to_flattened_tensor", "jagged_to_padded_tensor", "Jagged",
+           "padded_to_jagged", "as_jagged"]
+
+
+class Jagged:
+    """Dense view of a jagged batch: values (T, C) + int64 offsets (B+1) + length bounds.
+
+    The model internals run on this (every op on the jagged axis is row-wise, so it applies to
+    ``values`` directly) instead of torch NJT, whose per-op Python dispatch dominated the decoder
+    step on the host. Exposes ``values()`` / ``offsets()`` like an NJT; ``to_nested()`` converts.
+    """
+
+    __slots__ = ("_values", "_offsets", "max_len", "min_len")
+
+    def __init__(self, values: Tensor, offsets: Tensor, max_len: int, min_len: int = 0):
+        self._values, self._offsets, self.max_len, self.min_len = values, offsets, int(max_len), int(min_len)
+
+    def values(self) -> Tensor:
+        return self._values
+
+    def offsets(self) -> Tensor:
+        return self._offsets
+
+    def with_values(self, values: Tensor) -> "Jagged":
+        return Jagged(values, self._offsets, self.max_len, self.min_len)
+
+    def to_nested(self):
+        return torch.nested.nested_tensor_from_jagged(self._values, self._offsets, min_seqlen=self.min_len,
+                                                      max_seqlen=self.max_len)
+
+    @property
+    def shape(self):
+        return (self._offsets.shape[0] - 1, None, self._values.shape[-1])
+
+
+def as_jagged(x) -> Jagged:
+    """NJT or Jagged -> Jagged (no copy)."""
+    if isinstance(x, Jagged):
+        return x
+    mx = getattr(x, "_maybe_max_seqlen", None)
+    mn = getattr(x, "_maybe_min_seqlen", None)
+    if mx is None:
+        mx = x._get_max_seqlen()
+    return Jagged(x.values(), x.offsets(), int(mx), int(mn or 0))
+
+
+def padded_to_jagged(x: Tensor, lengths: Tensor, max_len: int, total: int = None, add_one_sub_one: bool = True,
+                     known_max: int = None) -> Jagged:
+    """HIP padded -> jagged gather. `total` / `known_max` (host ints) skip the host sync when the
+    caller already knows them (e.g. fixed-length decoder inputs)."""
+    assert x.dim() == 3 and x.is_contiguous()
+    hip_ops.require_gpu(x, lengths, what="padded_to_jagged")
+    B, N, _ = x.shape
+    n = min(int(max_len), N)
+    offsets = hip_ops.jagged_offsets(lengths, n)
+    if total is None:
+        total, lmin, lmax = torch.stack([offsets[-1], lengths.clamp(0, n).min(), lengths.clamp(0, n).max()]).tolist()
+    else:
+        lmin = lmax = known_max if known_max is not None else n
+    values = hip_ops.PaddedToJaggedValues.apply(x, offsets, int(total), add_one_sub_one)
+    return Jagged(values, offsets, int(lmax), int(lmin))
 
 
 def padded_to_jagged_tensor(x: Tensor, lengths: Tensor, max_len: int):
     assert x.dim() == 3
     assert lengths.shape[0] == x.shape[0]
     assert x.is_contiguous()
-    hip_ops.require_gpu(x, lengths, what="padded_to_jagged_tensor")
-    B, N, _ = x.shape
-    n = min(int(max_len), N)
-    offsets = hip_ops.jagged_offsets(lengths, n)
     # one host sync (the reference's torch.empty(lengths.sum()) has the same one)
-    total, lmin, lmax = torch.stack([offsets[-1], lengths.clamp(0, n).min(), lengths.clamp(0, n).max()]).tolist()
-    values = hip_ops.PaddedToJaggedValues.apply(x, offsets, int(total), True)
-    return torch.nested.nested_tensor_from_jagged(values, offsets, min_seqlen=int(lmin), max_seqlen=int(lmax))
+    return padded_to_jagged(x, lengths, max_len).to_nested()
 
 
 def jagged_to_flattened_tensor(x) -> Tensor:
@@ -38,5 +92,6 @@ def jagged_to_flattened_tensor(x) -> Tensor:
 
 
 def jagged_to_padded_tensor(x, max_len: int) -> Tensor:
+    # accepts an NJT or a Jagged
     """NJT (B, j, D) -> zero-padded (B, max_len, D) via the HIP scatter kernel (differentiable)."""
     return hip_ops.JaggedToPaddedValues.apply(x.values(), x.offsets(), int(max_len))

@@ -58,15 +58,16 @@ def seq_lengths(B: int, max_items: int, seed: int, min_items: int = 2) -> np.nda
 def named_param(name: str, shape, seed: int) -> np.ndarray:
     """Deterministic value for a named parameter (decoder fixtures), independent of init code.
 
-    RMSNorm weights ~ 1 + U(-0.1, 0.1); embeddings / bos ~ N(0, 0.5^2);
-    2-D Linear weights ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)).
+    1-D weights (RMSNorm, incl. ``ff.0.weight``) ~ 1 + U(-0.1, 0.1); ``bos_emb`` and embedding
+    tables (``*emb.weight``, ``wpe``, ``tte``, ``tte_fut``) ~ N(0, 0.3^2); 2-D Linear weights ~
+    U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (torch default bound).
     """
     import zlib
     g = rng(seed * 100003 + zlib.crc32(name.encode()))
     shape = tuple(int(s) for s in shape)
-    if "norm" in name:
+    if name == "bos_emb" or name.endswith(("emb.weight", "wpe.weight", "tte.weight", "tte_fut.weight")):
+        return (0.3 * g.standard_normal(shape)).astype(np.float32)
+    if len(shape) == 1:
         return (1.0 + g.uniform(-0.1, 0.1, size=shape)).astype(np.float32)
-    if "emb" in name or "wpe" in name or "tte" in name:
-        return (0.5 * g.standard_normal(shape)).astype(np.float32)
     b = 1.0 / np.sqrt(shape[-1])
     return g.uniform(-b, b, size=shape).astype(np.float32)

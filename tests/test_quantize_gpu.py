@@ -109,7 +109,7 @@ def test_rqvae_vs_reference(golden, device, tag):
 
 
 @pytest.mark.parametrize("B,D,K,L", [(65536, 64, 256, 3), (4096, 1024, 2048, 4), (1000, 32, 256, 3), (1, 64, 256, 3),
-                                     (129, 16, 40, 2)])
+                                     (129, 16, 40, 2), (20000, 64, 256, 3), (64, 64, 256, 3)])
 def test_fused_levels_vs_oracle_full_size(device, B, D, K, L):
     """Full BASELINE sizes vs the pinned oracle: ids exact off near-ties, outputs within fp32 tol,
     plus size-independent properties (residual chain identity, loss = (1+beta)|res - e|^2)."""

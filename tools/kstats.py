@@ -1,0 +1,12 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 *_kernel_stats.csv: top kernels by total time."""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 25
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:n]:
+    print(f"{float(r['TotalDurationNs'])/1e6:9.3f} ms {float(r['Percentage']):6.2f}% n={r['Calls']:>6} "
+          f"avg={float(r['AverageNs'])/1e3:9.2f}us  {r['Name'][:100]}")
+print(f"total {tot/1e6:.3f} ms")
