@@ -179,7 +179,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     q_ms, q_n = ops.TIMER.mean_ms("rq_quantize_fwd")
-    loss = float(last.loss)
+    loss = float(last.loss.detach())
+    del last
 
     extras = {}
     if not args.no_extras and rk == 0:
@@ -250,11 +251,12 @@ def measure_extras(model, device, x):
     # config batch B=64 step latency: eager, and the whole step replayed as one hipGraph
     from rqvae_hip.graph import CapturedStep
     xs = x[:64].contiguous()
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True, capturable=True)
+    m64 = build_model(device, seed=5)   # fresh module: no autograd state from the timed region
+    opt = torch.optim.AdamW(m64.parameters(), lr=1e-4, weight_decay=0.01, foreach=True, capturable=True)
 
     def small():
         opt.zero_grad(set_to_none=False)
-        o = model(SeqBatch(None, None, None, xs, None, None), gumbel_t=0.2)
+        o = m64(SeqBatch(None, None, None, xs, None, None), gumbel_t=0.2)
         o.loss.backward()
         opt.step()
         return o.loss

@@ -78,6 +78,15 @@ size_t rq_unique_workspace(int64_t B);
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
                     size_t ws_bytes, void* stream);
 
+/* Fused decoder head of RqVae.forward (modules/rqvae.py:145-150): x_hat = l2norm(pre) (decoder MLP's
+ * final L2NormalizationLayer, F.normalize eps 1e-12) and recon[b] = sum_c (x_hat - x)^2
+ * (modules/loss.py:5-10). pre, x: (B, C) fp32, C % 4 == 0, C <= 4096. fwd writes recon (B,) and
+ * norms (B,) = |pre_b| (saved for bwd); bwd writes g_pre (B, C) from g_recon (B,). */
+int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
+                        void* stream);
+int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
+                        int64_t C, float* g_pre, void* stream);
+
 /* Jagged (NJT) conversion — ops/triton/jagged.py. dtype: 0 fp32, 1 bf16, 2 fp16.
  * jagged_offsets: offsets (B+1) int64 = [0, cumsum(clamp(lengths, 0, N))]   (jagged.py:30-33)
  * jagged_from_padded: values[offsets[b]+t] = x[b,t] (+1-1 rounding when add_one_sub_one, as

@@ -18,7 +18,7 @@ from torch import Tensor
 from data.schemas import SeqBatch
 from modules.encoder import MLP
 from modules.loss import CategoricalReconstuctionLoss, ReconstructionLoss
-from modules.normalize import l2norm
+from modules.normalize import L2NormalizationLayer, l2norm
 from modules.quantize import Quantize, QuantizeDistance, QuantizeForwardMode, fused_mode
 from rqvae_hip import ops as hip_ops
 
@@ -138,11 +138,16 @@ class RqVae(nn.Module):
     def forward(self, batch: SeqBatch, gumbel_t: float) -> RqVaeComputedLosses:
         x = batch.x
         emb, _, ids, qloss, emb_sum = self.quantize_levels(self.encode(x), gumbel_t)
-        x_hat = self.decode(emb_sum)
         n = self.n_cat_feats
-        if n > 0:   # the reference's cat is a no-op for n == 0 (SURVEY A-10)
-            x_hat = torch.cat([l2norm(x_hat[..., :-n]), x_hat[..., -n:]], axis=-1)
-        reconstruction = self.reconstruction_loss(x_hat, x)
+        head = self.decoder.mlp
+        if n == 0 and isinstance(head[-1], L2NormalizationLayer) and x.dtype == torch.float32:
+            # decoder's final l2norm + ReconstructionLoss fused into one HIP row kernel (fwd + bwd)
+            reconstruction = hip_ops.l2norm_recon_loss(head[:-1](emb_sum), x)
+        else:
+            x_hat = self.decode(emb_sum)
+            if n > 0:   # the reference's cat is a no-op for n == 0 (SURVEY A-10)
+                x_hat = torch.cat([l2norm(x_hat[..., :-n]), x_hat[..., -n:]], axis=-1)
+            reconstruction = self.reconstruction_loss(x_hat, x)
         loss = (reconstruction + qloss).mean()
         with torch.no_grad():
             embs_norm = emb.norm(dim=-1).T

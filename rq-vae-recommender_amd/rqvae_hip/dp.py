@@ -63,12 +63,13 @@ class GradBuckets:
                  overlap: bool = True):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         self.average = average
+        self.active = world() > 1   # single process: no flat views (AccumulateGrad steals, no add_)
         self.overlap = overlap and world() > 1
         self.buckets = []
         self._handles = []
         self._pending = {}
         by_dtype = {}
-        for p in self.params:
+        for p in (self.params if self.active else []):
             by_dtype.setdefault((p.dtype, p.device), []).append(p)
         for (dt, dev), ps in by_dtype.items():
             # reverse registration order ~= order grads become ready in backward
@@ -114,6 +115,10 @@ class GradBuckets:
         self._pending[bi] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, async_op=True)
 
     def zero_grad(self):
+        if not self.active:
+            for p in self.params:
+                p.grad = None
+            return
         for b in self.buckets:
             b["flat"].zero_()
             b["used"].clear()

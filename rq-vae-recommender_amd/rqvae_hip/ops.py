@@ -124,6 +124,36 @@ def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     return out
 
 
+class L2NormReconFunction(torch.autograd.Function):
+    """recon_b = sum_c (pre_b / max(|pre_b|, 1e-12) - x_b)^2 — the l2norm that ends the RqVae
+    decoder fused with ReconstructionLoss (modules/rqvae.py:145-148). Gradient w.r.t. pre only
+    (x is data)."""
+
+    @staticmethod
+    def forward(ctx, pre, x):
+        require_gpu(pre, x, what="l2norm_recon")
+        pre, x = pre.contiguous(), x.contiguous()
+        B, C = pre.shape
+        recon = torch.empty((B,), device=pre.device, dtype=torch.float32)
+        norms = torch.empty((B,), device=pre.device, dtype=torch.float32)
+        call("rq_l2norm_recon_fwd", ptr(pre), ptr(x), B, C, ptr(recon), ptr(norms), stream_handle(pre.device))
+        ctx.save_for_backward(pre, x, norms)
+        return recon
+
+    @staticmethod
+    def backward(ctx, g_recon):
+        pre, x, norms = ctx.saved_tensors
+        B, C = pre.shape
+        g_pre = torch.empty_like(pre)
+        call("rq_l2norm_recon_bwd", ptr(pre), ptr(x), ptr(norms), ptr(g_recon.contiguous()), B, C, ptr(g_pre),
+             stream_handle(pre.device))
+        return g_pre, None
+
+
+def l2norm_recon_loss(pre, x):
+    return L2NormReconFunction.apply(pre, x)
+
+
 # --------------------------------------------------------------------------------- jagged
 def jagged_offsets(lengths: torch.Tensor, N: int) -> torch.Tensor:
     require_gpu(lengths, what="jagged_offsets")
