@@ -71,6 +71,13 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
                     const float* g_qloss, float* grad_x, float* grad_codebooks, void* workspace, size_t ws_bytes,
                     void* stream);
 
+/* Deterministic segmented sum: out[k] = sum of rows[b] (B, D) over b with keys[b] == k (int64, in
+ * [0, K)), reduced in a fixed order; counts[k] = #rows (or NULL). Used by the k-means codebook
+ * init (init/kmeans.py:40-58 centroid means). D <= 1024, K <= 4096. */
+size_t rq_segment_sum_workspace(int64_t B, int64_t K);
+int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
+                   void* workspace, size_t ws_bytes, void* stream);
+
 /* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
  * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */

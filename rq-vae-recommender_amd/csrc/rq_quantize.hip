@@ -728,6 +728,12 @@ static void launch_fwd_reg(int B, hipStream_t s, const float* x, const float* cb
     launch_fwd_reg_w<D, 1>(B, s, x, cbs, csq, K, L, mode, beta, ids, eo, res, ql, es);
 }
 
+__global__ void __launch_bounds__(256) segment_counts_kernel(const int* __restrict__ key_off, int K,
+                                                             int64_t* __restrict__ counts) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < K) counts[k] = key_off[k + 1] - key_off[k];
+}
+
 // ---------------------------------------------------------------------------------------
 static bool row_split(int D, int& lpi, int& epl) {
   if (D < 8 || D > 1024 || (D & (D - 1)) != 0) return false;
@@ -880,6 +886,42 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, l), dim3(256), 0, s, residuals, codebooks, g_qloss,
                      mode == kEval ? contrib : nullptr, perm, key_off, b, d, k, grad_codebooks);
   RQ_LAUNCH_CHECK("rq_codebook_grad");
+  return 0;
+}
+
+
+// Deterministic segmented sum by key (k-means centroid update, generic scatter-add):
+// out[k] = sum of rows[b] over b with keys[b] == k (fixed reduction order), counts[k] = #rows.
+size_t rq_segment_sum_workspace(int64_t B, int64_t K) {
+  const int64_t nblk = (B + kSortRows - 1) / kSortRows;
+  return (size_t)(K * nblk + (K + 1) + B) * sizeof(int) + 256;
+}
+
+int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
+                   void* workspace, size_t ws_bytes, void* stream) {
+  RQ_CHECK_ARG(rows && keys && out && workspace, "rq_segment_sum: null pointer");
+  RQ_CHECK_ARG(B >= 0 && B < (1ll << 31) && D >= 1 && D <= 1024 && K >= 1 && K <= 4096, "rq_segment_sum: bad shape");
+  RQ_CHECK_ARG(ws_bytes >= rq_segment_sum_workspace(B, K), "rq_segment_sum: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  if (B == 0) {
+    RQ_HIP(hipMemsetAsync(out, 0, (size_t)(K * D) * sizeof(float), s));
+    if (counts) RQ_HIP(hipMemsetAsync(counts, 0, (size_t)K * sizeof(int64_t), s));
+    return 0;
+  }
+  const int b = (int)B, d = (int)D, k = (int)K;
+  const int nblk = (b + kSortRows - 1) / kSortRows;
+  int* hist = (int*)workspace;
+  int* key_off = hist + (size_t)K * nblk;
+  int* perm = key_off + (K + 1);
+  hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, 1), dim3(256), k * sizeof(int), s, keys, b, 1, k, nblk, hist);
+  hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 255) / 256, 1), dim3(256), 0, s, hist, k, nblk, key_off);
+  hipLaunchKernelGGL(sort_offsets_kernel, dim3(1), dim3(1024), 0, s, key_off, k, b);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, 1), dim3(64), k * sizeof(int), s, keys, b, 1, k, nblk, hist, key_off,
+                     perm);
+  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, 1), dim3(256), 0, s, (const float*)nullptr, (const float*)nullptr,
+                     (const float*)nullptr, rows, perm, key_off, b, d, k, out);
+  if (counts) hipLaunchKernelGGL(segment_counts_kernel, dim3((k + 255) / 256), dim3(256), 0, s, key_off, k, counts);
+  RQ_LAUNCH_CHECK("rq_segment_sum");
   return 0;
 }
 

@@ -54,8 +54,9 @@ class Kmeans:
 
     def _update_centroids(self, x: torch.Tensor) -> None:
         idx = self._assign(x)
-        sums = torch.zeros_like(self.centroids).index_add_(0, idx, x)
-        counts = torch.bincount(idx, minlength=self.k)
+        # deterministic per-cluster sums: a fixed point of Lloyd's map reproduces the centroids
+        # bit-for-bit, so the reference's exact stop test (move < 1e-10) terminates
+        sums, counts = hip_ops.segment_sum(x, idx, self.k)
         new = sums / counts.clamp_min(1).unsqueeze(1).to(x.dtype)
         empty = torch.nonzero(counts == 0).flatten().tolist()
         for c in empty:   # rare; same rule as the reference (random row)
@@ -69,7 +70,8 @@ class Kmeans:
         x = x.detach().float().contiguous()
         self._init_centroids(x)
         i = 0
-        while self.iters is None or i < self.iters:
+        cap = self.iters if self.iters is not None else 100000   # reference: unbounded (safety cap only)
+        while i < cap:
             old = self.centroids.clone()
             self._update_centroids(x)
             if torch.norm(self.centroids - old, dim=1).max() < self.stop_threshold:

@@ -112,6 +112,21 @@ def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25):
     return RqQuantizeFunction.apply(x, codebooks, mode, beta)
 
 
+def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int):
+    """(sums (K, D), counts (K,)) of `rows` grouped by `keys` — deterministic (no float atomics)."""
+    require_gpu(rows, keys, what="segment_sum")
+    rows = rows.contiguous().float()
+    keys = keys.contiguous().to(torch.int64)
+    B, D = rows.shape
+    out = torch.empty((K, D), device=rows.device, dtype=torch.float32)
+    counts = torch.empty((K,), device=rows.device, dtype=torch.int64)
+    nbytes = _lib.load().rq_segment_sum_workspace(B, K)
+    ws = torch.empty((nbytes,), device=rows.device, dtype=torch.uint8)
+    call("rq_segment_sum", ptr(rows), ptr(keys), B, D, int(K), ptr(out), ptr(counts), ptr(ws), nbytes,
+         stream_handle(rows.device))
+    return out, counts
+
+
 def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     """Number of distinct rows of ids (B, L) as a device int64 scalar (modules/rqvae.py:152-157)."""
     require_gpu(ids, what="unique_count")

@@ -68,6 +68,22 @@ def test_dedup_rank_large(device):
     assert np.array_equal(got, U.dedup_rank(ids))
 
 
+@pytest.mark.parametrize("B,D,K", [(20000, 8, 16), (65536, 64, 256), (3, 1024, 7), (1000, 16, 4096)])
+def test_segment_sum(device, B, D, K):
+    from rqvae_hip import ops
+    g = gi.rng(B + D + K)
+    rows = g.standard_normal((B, D), dtype=np.float32)
+    keys = g.integers(0, K, size=B)
+    ref = np.zeros((K, D))
+    np.add.at(ref, keys, rows.astype(np.float64))
+    r, k = torch.from_numpy(rows).to(device), torch.from_numpy(keys).to(device)
+    s1, c1 = ops.segment_sum(r, k, K)
+    s2, _ = ops.segment_sum(r, k, K)
+    assert torch.equal(s1, s2), "deterministic"
+    assert np.array_equal(c1.cpu().numpy(), np.bincount(keys, minlength=K))
+    assert np.allclose(s1.cpu().numpy(), ref, rtol=1e-5, atol=1e-4)
+
+
 def test_kmeans_vs_reference(golden, device):
     from init.kmeans import Kmeans
     z = golden("kmeans")
