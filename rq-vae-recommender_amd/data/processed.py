@@ -24,11 +24,9 @@ class RecDataset(Enum):
     ML_32M = 3
 
 
-try:  # pragma: no cover - gin is optional
-    import gin as _gin
-    _gin.constants_from_enum(RecDataset)
-except ImportError:
-    pass
+from modules.ginlite import gin as _gin   # noqa: E402  (gin-config or the built-in subset)
+
+_gin.constants_from_enum(RecDataset, module="data.processed")
 
 DATASET_NAME_TO_MAX_SEQ_LEN = {RecDataset.AMAZON: 20, RecDataset.ML_1M: 200, RecDataset.ML_32M: 200}
 # public corpus sizes used for the synthetic stand-ins
@@ -113,7 +111,7 @@ class SeqData(Dataset):
         fut = torch.tensor([sample[-1]], dtype=torch.int64)
         x = self.item_data[item_ids.clamp_min(0), :768]
         x[item_ids == -1] = -1
-        return SeqBatch(user_ids=torch.tensor(idx), ids=item_ids, ids_fut=fut, x=x,
+        return SeqBatch(user_ids=torch.tensor([idx]), ids=item_ids, ids_fut=fut, x=x,
                         x_fut=self.item_data[fut, :768], seq_mask=item_ids >= 0)
 
 

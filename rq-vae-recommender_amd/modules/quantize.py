@@ -25,10 +25,7 @@ from modules.loss import QuantizeLoss
 from modules.normalize import L2NormalizationLayer
 from rqvae_hip import ops as hip_ops
 
-try:  # gin is optional (not installed in this image); register the enum when present
-    import gin as _gin
-except ImportError:  # pragma: no cover
-    _gin = None
+from modules.ginlite import gin as _gin   # gin-config, or the built-in subset when gin is absent
 
 
 class QuantizeForwardMode(Enum):
@@ -42,8 +39,7 @@ class QuantizeDistance(Enum):
     COSINE = 2
 
 
-if _gin is not None:  # pragma: no cover
-    _gin.constants_from_enum(QuantizeForwardMode)
+_gin.constants_from_enum(QuantizeForwardMode, module="modules.quantize")
 
 
 class QuantizeOutput(NamedTuple):

@@ -1,0 +1,108 @@
+"""Decoder (generative retrieval) training entry point — drop-in for reference train_decoder.py
+(same gin-configurable `train(...)` signature; `python train_decoder.py configs/decoder_amazon.gin`).
+
+MI355X path: frozen RQ-VAE tokenizer (fused eval quantize + device dedup), decoder on the HIP jagged
+conversion + varlen attention kernels, one process per GPU with rqvae_hip.dp (disjoint shards of
+each global batch, bucketed RCCL all-reduce overlapped with backward, loss averaged over ranks).
+The reference rejects non-AMAZON datasets and its ML-32M gin binds a non-existent parameter
+(SURVEY A-8); this entry accepts every RecDataset (the ML-32M config still fails on
+`train.attn_dropout`, exactly like gin). Checkpoints: plain state dicts with "scheduler".
+"""
+import json
+import os
+import time
+
+import torch
+from torch.utils.data import DataLoader
+
+from data.processed import ItemData, RecDataset, SeqData
+from data.utils import batch_to, cycle
+from modules.ginlite import gin
+from modules.model import EncoderDecoderRetrievalModel
+from modules.scheduler.inv_sqrt import InverseSquareRootScheduler
+from modules.tokenizer.semids import SemanticIdTokenizer
+from modules.utils import parse_config
+from rqvae_hip import dp
+
+
+@gin.configurable
+def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.01, dataset_folder="dataset/ml-1m",
+          save_dir_root="out/", dataset=RecDataset.ML_1M, pretrained_rqvae_path=None, pretrained_decoder_path=None,
+          split_batches=True, amp=False, swanlab_logging=False, force_dataset_process=False,
+          mixed_precision_type="fp16", gradient_accumulate_every=1, save_model_every=1000000,
+          partial_eval_every=1000, full_eval_every=10000, vae_input_dim=18, vae_embed_dim=16,
+          vae_hidden_dims=[18, 18], vae_codebook_size=32, vae_codebook_normalize=False, vae_sim_vq=False,
+          vae_n_cat_feats=18, vae_n_layers=3, decoder_embed_dim=64, dropout_p=0.1, attn_heads=8,
+          attn_embed_dim=64, attn_layers=4, dataset_split="beauty", push_vae_to_hf=False,
+          train_data_subsample=True, model_jagged_mode=True, vae_hf_model_name="edobotta/rqvae-amazon-beauty",
+          data_path=None, log_every=100, seed=0):
+    if amp:
+        raise NotImplementedError("amp: this build's decoder path is fp32 (reference default amp=False)")
+    if push_vae_to_hf:
+        raise NotImplementedError("HF hub upload is out of scope (network)")
+    rank, world, local_rank = dp.init_from_env()
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    item_ds = ItemData(root=dataset_folder, dataset=dataset, data_path=data_path, seed=seed)
+    train_ds = SeqData(root=dataset_folder, dataset=dataset, is_train=True, subsample=train_data_subsample,
+                       data_path=data_path, seed=seed)
+    global_batch = batch_size if split_batches else batch_size * world
+    lo, hi = dp.shard_range(global_batch, rank, world)
+    g = torch.Generator().manual_seed(seed + 5)
+    loader = cycle(DataLoader(train_ds, batch_size=global_batch, shuffle=True, generator=g))
+
+    tokenizer = SemanticIdTokenizer(input_dim=vae_input_dim, hidden_dims=vae_hidden_dims, output_dim=vae_embed_dim,
+                                    codebook_size=vae_codebook_size, n_layers=vae_n_layers, n_cat_feats=vae_n_cat_feats,
+                                    rqvae_weights_path=pretrained_rqvae_path,
+                                    rqvae_codebook_normalize=vae_codebook_normalize, rqvae_sim_vq=vae_sim_vq).to(device)
+    tokenizer.precompute_corpus_ids(item_ds)   # not DDP-wrapped (reference A-7)
+    torch.manual_seed(seed)
+    model = EncoderDecoderRetrievalModel(embedding_dim=decoder_embed_dim, attn_dim=attn_embed_dim, dropout=dropout_p,
+                                         num_heads=attn_heads, n_layers=attn_layers, num_embeddings=vae_codebook_size,
+                                         inference_verifier_fn=lambda x: tokenizer.exists_prefix(x),
+                                         sem_id_dim=tokenizer.sem_ids_dim,
+                                         max_pos=train_ds.max_seq_len * tokenizer.sem_ids_dim,
+                                         jagged_mode=model_jagged_mode).to(device)
+    opt = torch.optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay)
+    sched = InverseSquareRootScheduler(optimizer=opt, warmup_steps=10000)
+    start_iter = 0
+    if pretrained_decoder_path is not None:
+        ck = torch.load(pretrained_decoder_path, map_location=device, weights_only=True)
+        model.load_state_dict(ck["model"])
+        opt.load_state_dict(ck["optimizer"])
+        if "scheduler" in ck:
+            sched.load_state_dict(ck["scheduler"])
+        start_iter = ck["iter"] + 1
+    buckets = dp.GradBuckets(model.parameters())
+    buckets.broadcast_params()
+    t0, hist = time.time(), []
+    for it in range(start_iter, iterations):
+        model.train()
+        buckets.zero_grad()
+        total = 0.0
+        for _ in range(gradient_accumulate_every):
+            data = next(loader)
+            data = batch_to(type(data)(*[v[lo:hi] for v in data]), device)
+            out = model(tokenizer(data))
+            # mean over the GLOBAL batch: the average of equal-size shard means (ranks average grads)
+            loss = out.loss / gradient_accumulate_every
+            loss.backward()
+            total = total + loss.detach()
+        buckets.synchronize()
+        opt.step()
+        sched.step()
+        hist.append(total)
+        if rank == 0 and (it % log_every == 0 or it + 1 == iterations):
+            print(json.dumps({"iter": it, "loss": float(torch.stack(hist).mean()), "lr": opt.param_groups[0]["lr"],
+                              "elapsed_s": round(time.time() - t0, 2)}), flush=True)
+            hist = []
+        if rank == 0 and ((it + 1) % save_model_every == 0 or it + 1 == iterations):
+            os.makedirs(save_dir_root, exist_ok=True)
+            torch.save({"iter": it, "model": model.state_dict(), "optimizer": opt.state_dict(),
+                        "scheduler": sched.state_dict()}, os.path.join(save_dir_root, f"checkpoint_{it}.pt"))
+    return model
+
+
+if __name__ == "__main__":
+    parse_config()
+    train()

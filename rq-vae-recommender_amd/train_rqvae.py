@@ -1,0 +1,131 @@
+"""RQ-VAE training entry point — drop-in for reference train_rqvae.py (same gin-configurable
+`train(...)` signature, `python train_rqvae.py configs/rqvae_ml32m.gin`).
+
+Differences from the reference loop (train_rqvae.py:24-250), all on the MI355X path:
+  * one process per GPU (torchrun env) with rqvae_hip.dp instead of accelerate/DDP: each rank
+    draws a DISJOINT shard of every global batch (`split_batches` semantics), k-means init runs
+    on rank 0 and is broadcast, gradients are all-reduced over RCCL;
+  * no per-step `.item()` host syncs — losses are read back every `log_every` iterations;
+  * checkpoints are plain state dicts {"iter", "model", "model_config", "optimizer"} (loadable with
+    weights_only=True); swanlab logging is replaced by printed JSON lines (out of scope);
+  * the loop runs `iterations + 1` times like the reference (SURVEY A-4).
+Data: `data.processed.ItemData` (seeded synthetic corpus unless `data_path` names a feature file).
+"""
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from data.processed import ItemData, RecDataset
+from data.schemas import SeqBatch
+from modules.ginlite import gin
+from modules.quantize import QuantizeForwardMode
+from modules.rqvae import RqVae
+from modules.tokenizer.semids import SemanticIdTokenizer
+from modules.utils import parse_config
+from rqvae_hip import dp
+
+
+@gin.configurable
+def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.01, dataset_folder="dataset/ml-1m",
+          dataset=RecDataset.ML_1M, pretrained_rqvae_path=None, save_dir_root="out/", use_kmeans_init=True,
+          split_batches=True, amp=False, swanlab_logging=False, do_eval=True, force_dataset_process=False,
+          mixed_precision_type="fp16", gradient_accumulate_every=1, save_model_every=1000000, eval_every=50000,
+          commitment_weight=0.25, vae_n_cat_feats=18, vae_input_dim=18, vae_embed_dim=16, vae_hidden_dims=[18, 18],
+          vae_codebook_size=32, vae_codebook_normalize=False, vae_codebook_mode=QuantizeForwardMode.GUMBEL_SOFTMAX,
+          vae_sim_vq=False, vae_n_layers=3, dataset_split="beauty", data_path=None, log_every=100, seed=0):
+    if amp:
+        raise NotImplementedError("amp: the RQ-VAE hot path is fp32 (reference default amp=False)")
+    rank, world, local_rank = dp.init_from_env()
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    train_ds = ItemData(root=dataset_folder, dataset=dataset, train_test_split="train" if do_eval else "all",
+                        data_path=data_path, seed=seed)
+    eval_ds = ItemData(root=dataset_folder, dataset=dataset, train_test_split="eval", data_path=data_path,
+                       seed=seed) if do_eval else None
+    index_ds = ItemData(root=dataset_folder, dataset=dataset, train_test_split="all", data_path=data_path,
+                        seed=seed) if do_eval else train_ds
+    items = train_ds.item_data[:, :vae_input_dim].to(device)      # resident corpus
+    n_items = items.shape[0]
+    global_batch = batch_size if split_batches else batch_size * world
+    lo, hi = dp.shard_range(global_batch, rank, world)
+
+    torch.manual_seed(seed)
+    model = RqVae(input_dim=vae_input_dim, embed_dim=vae_embed_dim, hidden_dims=vae_hidden_dims,
+                  codebook_size=vae_codebook_size, codebook_kmeans_init=use_kmeans_init and pretrained_rqvae_path is None,
+                  codebook_normalize=vae_codebook_normalize, codebook_sim_vq=vae_sim_vq, codebook_mode=vae_codebook_mode,
+                  n_layers=vae_n_layers, n_cat_features=vae_n_cat_feats, commitment_weight=commitment_weight).to(device)
+    opt = torch.optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay)
+    start_iter = 0
+    if pretrained_rqvae_path is not None:
+        state = torch.load(pretrained_rqvae_path, map_location=device, weights_only=True)
+        model.load_state_dict(state["model"])
+        opt.load_state_dict(state["optimizer"])
+        start_iter = state["iter"] + 1
+
+    tokenizer = SemanticIdTokenizer(input_dim=vae_input_dim, hidden_dims=vae_hidden_dims, output_dim=vae_embed_dim,
+                                    codebook_size=vae_codebook_size, n_layers=vae_n_layers, n_cat_feats=vae_n_cat_feats,
+                                    rqvae_codebook_normalize=vae_codebook_normalize, rqvae_sim_vq=vae_sim_vq).to(device)
+    tokenizer.rq_vae = model
+
+    # k-means init on rank 0 over the first min(20000, N) items (reference :139-141), then broadcast
+    if start_iter == 0 and use_kmeans_init and pretrained_rqvae_path is None:
+        if rank == 0:
+            with torch.no_grad():
+                model(SeqBatch(None, None, None, items[: min(20000, n_items)], None, None), 0.2)
+        for layer in model.layers:
+            layer.kmeans_initted = True
+    buckets = dp.GradBuckets(model.parameters())
+    buckets.broadcast_params()
+
+    gen = torch.Generator(device=device).manual_seed(seed + 17)   # same stream on every rank
+    hist = []
+    t0 = time.time()
+    for it in range(start_iter, start_iter + 1 + iterations):
+        model.train()
+        buckets.zero_grad()
+        total = 0.0
+        for _ in range(gradient_accumulate_every):
+            idx = torch.randint(0, n_items, (global_batch,), generator=gen, device=device)[lo:hi]
+            out = model(SeqBatch(None, None, None, items[idx], None, None), gumbel_t=0.2)
+            loss = out.loss / gradient_accumulate_every
+            loss.backward()
+            total = total + loss.detach()
+        buckets.synchronize()
+        opt.step()
+        hist.append(torch.stack([total, out.reconstruction_loss.detach(), out.rqvae_loss.detach(),
+                                 out.p_unique_ids.detach()]))
+        if rank == 0 and (it % log_every == 0 or it == start_iter + iterations):
+            vals = torch.stack(hist).mean(0).tolist()
+            hist = []
+            print(json.dumps({"iter": it, "loss": vals[0], "rl": vals[1], "vl": vals[2], "p_unique_ids": vals[3],
+                              "elapsed_s": round(time.time() - t0, 2)}), flush=True)
+        if do_eval and ((it + 1) % eval_every == 0 or it + 1 == iterations) and rank == 0:
+            model.eval()
+            with torch.no_grad():
+                ev = [model(SeqBatch(None, None, None, eval_ds.item_data[a:a + 4096, :vae_input_dim].to(device), None,
+                                     None), gumbel_t=0.2).loss for a in range(0, len(eval_ds), 4096)]
+            print(json.dumps({"iter": it, "eval_total_loss": float(torch.stack(ev).mean())}), flush=True)
+        if rank == 0 and ((it + 1) % save_model_every == 0 or it + 1 == iterations):
+            os.makedirs(save_dir_root, exist_ok=True)
+            torch.save({"iter": it, "model": model.state_dict(), "model_config": model.config,
+                        "optimizer": opt.state_dict()}, os.path.join(save_dir_root, f"checkpoint_{it}.pt"))
+            tokenizer.reset()
+            model.eval()
+            corpus_ids = tokenizer.precompute_corpus_ids(index_ds)
+            _, counts = torch.unique(corpus_ids[:, :-1], dim=0, return_counts=True)
+            p = counts / corpus_ids.shape[0]
+            stats = {"iter": it, "rqvae_entropy": float(-(p * torch.log(p)).sum()),
+                     "max_id_duplicates": float(corpus_ids[:, -1].max() / corpus_ids.shape[0])}
+            for cid in range(vae_n_layers):
+                stats[f"codebook_usage_{cid}"] = len(torch.unique(corpus_ids[:, cid])) / vae_codebook_size
+            print(json.dumps(stats), flush=True)
+    return model
+
+
+if __name__ == "__main__":
+    parse_config()
+    train()

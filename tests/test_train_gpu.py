@@ -1,0 +1,40 @@
+"""Drop-in training entry points (train_rqvae.train / train_decoder.train) run end to end on the GPU
+with the reference configs' shapes (few iterations), incl. k-means init, eval, checkpoint + resume."""
+import glob
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_train_rqvae_amazon_dims(tmp_path, device):
+    import numpy as np
+    import train_rqvae
+    from data.processed import RecDataset
+    from modules.quantize import QuantizeForwardMode
+    np.random.seed(0)
+    kw = dict(iterations=30, batch_size=64, learning_rate=0.0005, weight_decay=0.01, dataset=RecDataset.AMAZON,
+              vae_input_dim=768, vae_n_cat_feats=0, vae_hidden_dims=[512, 256, 128], vae_embed_dim=32,
+              vae_codebook_size=256, vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK, vae_n_layers=3,
+              save_dir_root=str(tmp_path) + "/", save_model_every=15, eval_every=30, do_eval=True, log_every=10)
+    model = train_rqvae.train(**kw)
+    assert all(layer.kmeans_initted for layer in model.layers)
+    ckpts = sorted(glob.glob(str(tmp_path / "checkpoint_*.pt")))
+    assert ckpts
+    state = torch.load(ckpts[-1], map_location="cpu", weights_only=True)
+    assert "layers.0.embedding.weight" in state["model"] and "encoder.mlp.0.weight" in state["model"]
+    # resume from the checkpoint (pretrained path disables k-means, loads optimizer state)
+    kw.update(iterations=3, pretrained_rqvae_path=ckpts[-1], save_model_every=10 ** 9, do_eval=False)
+    train_rqvae.train(**kw)
+
+
+def test_train_decoder_small(tmp_path, device):
+    import train_decoder
+    from data.processed import RecDataset
+    m = train_decoder.train(iterations=4, batch_size=32, learning_rate=0.0003, dataset=RecDataset.AMAZON,
+                            vae_input_dim=768, vae_embed_dim=32, vae_hidden_dims=[512, 256, 128], vae_codebook_size=256,
+                            vae_n_cat_feats=0, vae_n_layers=3, decoder_embed_dim=64, dropout_p=0.3, attn_heads=4,
+                            attn_embed_dim=128, attn_layers=4, save_dir_root=str(tmp_path) + "/", log_every=2)
+    assert m.sem_id_embedder.emb.weight.grad is not None
+    assert glob.glob(str(tmp_path / "checkpoint_*.pt"))
