@@ -14,6 +14,7 @@ Data: `data.processed.ItemData` (seeded synthetic corpus unless `data_path` name
 import json
 import os
 import time
+from enum import Enum
 
 import numpy as np
 import torch
@@ -111,7 +112,8 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
             print(json.dumps({"iter": it, "eval_total_loss": float(torch.stack(ev).mean())}), flush=True)
         if rank == 0 and ((it + 1) % save_model_every == 0 or it + 1 == iterations):
             os.makedirs(save_dir_root, exist_ok=True)
-            torch.save({"iter": it, "model": model.state_dict(), "model_config": model.config,
+            config = {k: (v.name if isinstance(v, Enum) else v) for k, v in model.config.items()}   # tensors/plain only
+            torch.save({"iter": it, "model": model.state_dict(), "model_config": config,
                         "optimizer": opt.state_dict()}, os.path.join(save_dir_root, f"checkpoint_{it}.pt"))
             tokenizer.reset()
             model.eval()

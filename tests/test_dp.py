@@ -54,8 +54,10 @@ def _worker(rank, world, port, gb, bucket_bytes, q):
             buckets.zero_grad()
             _loss(model, x[a:b]).backward()
             buckets.synchronize()
-        grads = {n: p.grad.clone() for n, p in model.named_parameters()}
-        params = {n: p.detach().clone() for n, p in model.named_parameters()}
+        # numpy copies: tensors sent through a torch.multiprocessing queue are shared-memory handles
+        # that die with this process (the parent may read after we exit)
+        grads = {n: p.grad.detach().numpy().copy() for n, p in model.named_parameters()}
+        params = {n: p.detach().numpy().copy() for n, p in model.named_parameters()}
         q.put((r, (a, b), params, grads, len(buckets.buckets)))
     finally:
         if dist.is_initialized():
@@ -78,6 +80,8 @@ def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes):
     spans = [r[1] for r in res]
     assert spans[0][0] == 0 and spans[-1][1] == gb and all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
     # params identical on all ranks (rank-0 broadcast)
+    res = [(r[0], r[1], {n: torch.from_numpy(v) for n, v in r[2].items()},
+            {n: torch.from_numpy(v) for n, v in r[3].items()}, r[4]) for r in res]
     for r in res[1:]:
         for n in r[2]:
             assert torch.equal(r[2][n], res[0][2][n])
