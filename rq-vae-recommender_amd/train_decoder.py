@@ -55,7 +55,11 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
                                     codebook_size=vae_codebook_size, n_layers=vae_n_layers, n_cat_feats=vae_n_cat_feats,
                                     rqvae_weights_path=pretrained_rqvae_path,
                                     rqvae_codebook_normalize=vae_codebook_normalize, rqvae_sim_vq=vae_sim_vq).to(device)
-    tokenizer.precompute_corpus_ids(item_ds)   # not DDP-wrapped (reference A-7)
+    corpus_ids = tokenizer.precompute_corpus_ids(item_ds)   # not DDP-wrapped (reference A-7)
+    top = int(corpus_ids.max())
+    if top >= vae_codebook_size:   # would index past the SemIdEmbedder table on the device
+        raise ValueError(f"semantic id / dedup value {top} >= codebook size {vae_codebook_size}: the tokenizer's "
+                         "RQ-VAE maps too many items to one tuple (pass a trained pretrained_rqvae_path)")
     torch.manual_seed(seed)
     model = EncoderDecoderRetrievalModel(embedding_dim=decoder_embed_dim, attn_dim=attn_embed_dim, dropout=dropout_p,
                                          num_heads=attn_heads, n_layers=attn_layers, num_embeddings=vae_codebook_size,

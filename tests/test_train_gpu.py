@@ -30,11 +30,22 @@ def test_train_rqvae_amazon_dims(tmp_path, device):
 
 
 def test_train_decoder_small(tmp_path, device):
+    import numpy as np
     import train_decoder
+    import train_rqvae
     from data.processed import RecDataset
+    from modules.quantize import QuantizeForwardMode
+    vae = dict(vae_input_dim=768, vae_embed_dim=32, vae_hidden_dims=[512, 256, 128], vae_codebook_size=256,
+               vae_n_cat_feats=0, vae_n_layers=3)
+    np.random.seed(1)
+    train_rqvae.train(iterations=10, batch_size=256, dataset=RecDataset.AMAZON, do_eval=False, save_model_every=10,
+                      vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK, save_dir_root=str(tmp_path / "vae") + "/",
+                      **vae)
+    ckpt = sorted(glob.glob(str(tmp_path / "vae" / "checkpoint_*.pt")))[-1]
+    with pytest.raises(ValueError, match="codebook size"):   # untrained tokenizer: fails loudly on the host
+        train_decoder.train(iterations=1, batch_size=8, dataset=RecDataset.AMAZON, **vae)
     m = train_decoder.train(iterations=4, batch_size=32, learning_rate=0.0003, dataset=RecDataset.AMAZON,
-                            vae_input_dim=768, vae_embed_dim=32, vae_hidden_dims=[512, 256, 128], vae_codebook_size=256,
-                            vae_n_cat_feats=0, vae_n_layers=3, decoder_embed_dim=64, dropout_p=0.3, attn_heads=4,
-                            attn_embed_dim=128, attn_layers=4, save_dir_root=str(tmp_path) + "/", log_every=2)
+                            pretrained_rqvae_path=ckpt, decoder_embed_dim=64, dropout_p=0.3, attn_heads=4,
+                            attn_embed_dim=128, attn_layers=4, save_dir_root=str(tmp_path) + "/", log_every=2, **vae)
     assert m.sem_id_embedder.emb.weight.grad is not None
     assert glob.glob(str(tmp_path / "checkpoint_*.pt"))
