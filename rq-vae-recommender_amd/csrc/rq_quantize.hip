@@ -58,19 +58,29 @@ struct RowRot {
   __device__ __forceinline__ void build(const float (&x)[EPL], const float (&e)[EPL], float xn, float en) {
     // u = x/(|x|+1e-8), q = e/(|e|+1e-8), w = normalize(u+q, eps 1e-6)   (quantize.py:34-39,135-138)
     const float xd = xn + 1e-8f, ed = en + 1e-8f;
-    float s2 = 0.f;
+    const float rx = 1.0f / xd, re = 1.0f / ed;
+    float mnx = INFINITY, mxx = 0.f, mne = INFINITY, mxe = 0.f;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
-      u[k] = x[k] / xd;
-      q[k] = e[k] / ed;
+      mnx = fminf(mnx, fabsf(x[k])); mxx = fmaxf(mxx, fabsf(x[k]));
+      mne = fminf(mne, fabsf(e[k])); mxe = fmaxf(mxe, fabsf(e[k]));
+    }
+    const bool fast = div_rn_ok(mnx, mxx, xd) && div_rn_ok(mne, mxe, ed);
+    float s2 = 0.f, mns = INFINITY, mxs = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      u[k] = fast ? div_rn(x[k], xd, rx) : x[k] / xd;
+      q[k] = fast ? div_rn(e[k], ed, re) : e[k] / ed;
       const float s = u[k] + q[k];
       w[k] = s;
       s2 += s * s;
+      mns = fminf(mns, fabsf(s)); mxs = fmaxf(mxs, fabsf(s));
     }
     s2 = group_sum<LPI>(s2);
-    const float sn = fmaxf(sqrtf(s2), 1e-6f);
+    const float sn = fmaxf(sqrtf(s2), 1e-6f), rs = 1.0f / sn;
+    const bool fast_w = div_rn_ok(mns, mxs, sn);
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) w[k] = w[k] / sn;
+    for (int k = 0; k < EPL; ++k) w[k] = fast_w ? div_rn(w[k], sn, rs) : w[k] / sn;
     lam = en / (xn + 1e-6f);   // (|emb| / (|x| + 1e-6)).detach()   (quantize.py:140-142)
   }
 };
@@ -181,10 +191,14 @@ rq_fwd_kernel(const float* __restrict__ x, int B, int D, const float* __restrict
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
+          // indices visited in increasing order per lane: strict '<' keeps the lowest one
           const int il = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           const int i = n0 + il;
-          const float d = (xs + cs_s[il]) - 2.f * acc[t][r];
-          if (i < K && (d < best_d || (d == best_d && i < best_i))) { best_d = d; best_i = i; }
+          float d = (xs + cs_s[il]) - 2.f * acc[t][r];
+          d = i < K ? d : INFINITY;
+          const bool lt = d < best_d;
+          best_d = lt ? d : best_d;
+          best_i = lt ? i : best_i;
         }
       }
     }
@@ -537,9 +551,10 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
   // keeps the next residual in its own registers; only sub-wave 0 stores.
   constexpr int H2 = D / 2, LD = D + 4;
   extern __shared__ __attribute__((aligned(16))) float dsm[];
-  float* A_s = dsm;                                  // [NB][LD] codewords of the current level / chunk
-  float* cs_s = dsm + NB * LD;                       // [NB]     |c|^2
-  float* rd_s = cs_s + NB;                           // [4][32]  per-wave best distance (WPI > 1)
+  const int NBp = (NB + 31) & ~31;
+  float* A_s = dsm;                                  // [NBp][LD] codewords of the current level / chunk
+  float* cs_s = dsm + NBp * LD;                      // [NBp]     |c|^2
+  float* rd_s = cs_s + NBp;                          // [4][32]  per-wave best distance (WPI > 1)
   int* ri_s = reinterpret_cast<int*>(rd_s + 128);    // [4][32]  per-wave best index
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
   const int tile = wave / WPI, wsub = wave % WPI;
@@ -558,16 +573,29 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
   for (int k = 0; k < H2; ++k) es[k] = 0.f;
   float ql = 0.f;
 
-  for (int l = 0; l < L; ++l) {
-    const float* cb = cbs + (int64_t)l * K * D;
-    if (writer) {   // residuals[l] = input of level l
+  // Stores are deferred until the NEXT level's codebook staging has landed in LDS: gfx950 has one
+  // in-order vmcnt for loads and stores, so a store issued before the staging loads would make
+  // their wait drain it (HBM write latency on the critical path). Issued after, the stores drain
+  // under the level's MFMA phase. pend_e = emb_out[l-1] still to store.
+  float pend_e[H2];
+  auto flush = [&](int l) {   // residuals[l] (= current xv) and emb_out[l-1]
+    if (!writer) return;
+#pragma unroll
+    for (int k = 0; k < H2; k += 4)
+      *reinterpret_cast<float4*>(res + (int64_t)l * BD + o + k) = make_float4(xv[k], xv[k + 1], xv[k + 2], xv[k + 3]);
+    if (l > 0) {
 #pragma unroll
       for (int k = 0; k < H2; k += 4)
-        *reinterpret_cast<float4*>(res + (int64_t)l * BD + o + k) = make_float4(xv[k], xv[k + 1], xv[k + 2], xv[k + 3]);
+        *reinterpret_cast<float4*>(emb_out + (int64_t)(l - 1) * BD + o + k) =
+            make_float4(pend_e[k], pend_e[k + 1], pend_e[k + 2], pend_e[k + 3]);
     }
+  };
+
+  for (int l = 0; l < L; ++l) {
+    const float* cb = cbs + (int64_t)l * K * D;
     float xs = 0.f;
 #pragma unroll
-    for (int k = 0; k < H2; ++k) xs += xv[k] * xv[k];
+    for (int k = 0; k < H2; ++k) xs = __builtin_fmaf(xv[k], xv[k], xs);
     xs += __shfl_xor(xs, 32, 64);
     float best_d = INFINITY;
     int best_i = 0;
@@ -579,12 +607,31 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
         *reinterpret_cast<float4*>(A_s + r * LD + c) = *reinterpret_cast<const float4*>(cb + (int64_t)(n0 + r) * D + c);
       }
       for (int r = tid; r < nrows; r += 256) cs_s[r] = csq[(int64_t)l * K + n0 + r];
+      if (n0 == 0) flush(l);
       __syncthreads();
-      for (int t0 = wsub * 32; t0 < nrows; t0 += 32 * WPI) {
-        floatx16 acc;
+      // One-tile software pipeline: the argmin scan of tile t (VALU) is independent of tile
+      // t+1's MFMA chain, so it fills the 64-cycle dependent-MFMA gaps instead of draining them.
+      // Rows past nrows (last partial tile) read stale LDS; their distances are forced to +inf.
+      // Each lane visits its codeword indices in increasing order, so a strict '<' keeps the
+      // lowest index among equal distances (torch.argmin); the lane-pair merge below breaks ties.
+      auto scan = [&](const floatx16& a, const float4 (&c)[4], int t0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int il = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float cr = (r & 3) == 0 ? c[r >> 2].x : (r & 3) == 1 ? c[r >> 2].y : (r & 3) == 2 ? c[r >> 2].z
+                                                                                                  : c[r >> 2].w;
+          float d = (xs + cr) - 2.f * a[r];
+          d = il < nrows ? d : INFINITY;
+          const bool lt = d < best_d;
+          best_d = lt ? d : best_d;
+          best_i = lt ? n0 + il : best_i;
+        }
+      };
+      auto chain = [&](int t0, floatx16& acc, float4 (&c)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = *reinterpret_cast<const float4*>(cs_s + t0 + 8 * j + 4 * h);
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        // rows past nrows read stale LDS; their distances are masked below (il < nrows)
         const float* ap = A_s + (t0 + (lane & 31)) * LD + h * H2;
 #pragma unroll
         for (int s4 = 0; s4 < H2; s4 += 4) {
@@ -594,13 +641,33 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, xv[s4 + 2], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, xv[s4 + 3], acc, 0, 0, 0);
         }
+      };
+      int t0 = wsub * 32;
+      if (t0 < nrows) {
+        floatx16 acc_p;
+        float4 cp[4];
+        chain(t0, acc_p, cp);
+        int tp = t0;
+        for (t0 += 32 * WPI; t0 < nrows; t0 += 32 * WPI) {
+          floatx16 acc;
+          float4 cn[4];
+          chain(t0, acc, cn);
+          scan(acc_p, cp, tp);
+          // interleave: 2 MFMAs (128 cycles of matrix work) then a slice of the previous
+          // tile's scan, with the codeword ds_reads spread ahead of the MFMAs that use them
+          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int il = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float d = (xs + cs_s[il < NB ? il : 0]) - 2.f * acc[r];
-          const int i = n0 + il;
-          if (il < nrows && (d < best_d || (d == best_d && i < best_i))) { best_d = d; best_i = i; }
+          for (int i = 0; i < H2 / 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+            if (i < H2 / 4 - 2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          acc_p = acc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cp[j] = cn[j];
+          tp = t0;
         }
+        scan(acc_p, cp, tp);
       }
     }
     {
@@ -629,45 +696,58 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
       const float4 c = *reinterpret_cast<const float4*>(er + k);
       ev[k] = c.x; ev[k + 1] = c.y; ev[k + 2] = c.z; ev[k + 3] = c.w;
     }
-    float x2 = 0.f, e2 = 0.f, dl = 0.f;
+    // Row sums use fma (one rounding per term); |x|^2 is the level's xs. The reference's torch
+    // reductions round in their own order, so parity here is tolerance-level for the embeddings
+    // (ids: exact up to reference top-2 ties within that tolerance), as for every reduction.
+    float e2 = 0.f, dl = 0.f;
 #pragma unroll
     for (int k = 0; k < H2; ++k) {
-      x2 += xv[k] * xv[k];
-      e2 += ev[k] * ev[k];
+      e2 = __builtin_fmaf(ev[k], ev[k], e2);
       const float t = xv[k] - ev[k];
-      dl += t * t;
+      dl = __builtin_fmaf(t, t, dl);
     }
-    x2 += __shfl_xor(x2, 32, 64);
     e2 += __shfl_xor(e2, 32, 64);
     dl += __shfl_xor(dl, 32, 64);
     float out[H2];
     if (mode == kRotation) {
-      const float xn = sqrtf(x2), en = sqrtf(e2);
+      const float xn = sqrtf(xs), en = sqrtf(e2);
       const float xd = xn + 1e-8f, ed = en + 1e-8f;
-      float u[H2], q[H2];
-      float s2 = 0.f, eu = 0.f;
+      const float rx = 1.0f / xd, re = 1.0f / ed;
+      float mnx = INFINITY, mxx = 0.f, mne = INFINITY, mxe = 0.f;
 #pragma unroll
       for (int k = 0; k < H2; ++k) {
-        u[k] = xv[k] / xd;
-        q[k] = ev[k] / ed;
+        mnx = fminf(mnx, fabsf(xv[k])); mxx = fmaxf(mxx, fabsf(xv[k]));
+        mne = fminf(mne, fabsf(ev[k])); mxe = fmaxf(mxe, fabsf(ev[k]));
+      }
+      const bool fast = div_rn_ok(mnx, mxx, xd) && div_rn_ok(mne, mxe, ed);
+      float u[H2], q[H2];
+      float s2 = 0.f, eu = 0.f, mns = INFINITY, mxs = 0.f;
+#pragma unroll
+      for (int k = 0; k < H2; ++k) {
+        u[k] = fast ? div_rn(xv[k], xd, rx) : xv[k] / xd;
+        q[k] = fast ? div_rn(ev[k], ed, re) : ev[k] / ed;
         const float sk = u[k] + q[k];
         out[k] = sk;   // holds u+q until normalised
-        s2 += sk * sk;
-        eu += xv[k] * u[k];
+        s2 = __builtin_fmaf(sk, sk, s2);
+        eu = __builtin_fmaf(xv[k], u[k], eu);
+        mns = fminf(mns, fabsf(sk)); mxs = fmaxf(mxs, fabsf(sk));
       }
       s2 += __shfl_xor(s2, 32, 64);
       eu += __shfl_xor(eu, 32, 64);
-      const float sn = fmaxf(sqrtf(s2), 1e-6f);
+      const float sn = fmaxf(sqrtf(s2), 1e-6f), rs = 1.0f / sn;
+      const bool fast_w = div_rn_ok(mns, mxs, sn);
       float ew = 0.f;
 #pragma unroll
       for (int k = 0; k < H2; ++k) {
-        out[k] = out[k] / sn;   // w
-        ew += xv[k] * out[k];
+        out[k] = fast_w ? div_rn(out[k], sn, rs) : out[k] / sn;   // w
+        ew = __builtin_fmaf(xv[k], out[k], ew);
       }
       ew += __shfl_xor(ew, 32, 64);
       const float lam = en / (xn + 1e-6f);
+      const float m2ew = -2.f * ew, p2eu = 2.f * eu;
+      // (x - 2 (x.w) w + 2 (x.u) q) * lam   (quantize.py:41-45,140-142)
 #pragma unroll
-      for (int k = 0; k < H2; ++k) out[k] = ((xv[k] - 2.f * (ew * out[k])) + 2.f * (eu * q[k])) * lam;
+      for (int k = 0; k < H2; ++k) out[k] = __builtin_fmaf(p2eu, q[k], __builtin_fmaf(m2ew, out[k], xv[k])) * lam;
     } else if (mode == kSte) {
 #pragma unroll
       for (int k = 0; k < H2; ++k) out[k] = xv[k] + (ev[k] - xv[k]);
@@ -676,19 +756,19 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
       for (int k = 0; k < H2; ++k) out[k] = ev[k];
     }
     ql = ql + (dl + beta * dl);
-    if (writer) {
-#pragma unroll
-      for (int k = 0; k < H2; k += 4)
-        *reinterpret_cast<float4*>(emb_out + (int64_t)l * BD + o + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
-      if (h == 0) ids[(int64_t)b * L + l] = id;
-    }
+    if (writer && h == 0) ids[(int64_t)b * L + l] = id;
 #pragma unroll
     for (int k = 0; k < H2; ++k) {
+      pend_e[k] = out[k];
       es[k] = es[k] + out[k];
       xv[k] = xv[k] - out[k];   // next level's residual stays in registers
     }
   }
   if (writer) {
+#pragma unroll
+    for (int k = 0; k < H2; k += 4)
+      *reinterpret_cast<float4*>(emb_out + (int64_t)(L - 1) * BD + o + k) =
+          make_float4(pend_e[k], pend_e[k + 1], pend_e[k + 2], pend_e[k + 3]);
     if (h == 0) qloss[b] = ql;
     if (emb_sum != nullptr) {
 #pragma unroll
@@ -704,9 +784,10 @@ static void launch_fwd_reg_w(int B, hipStream_t s, const float* x, const float* 
   constexpr int LD = D + 4;
   constexpr int kMaxLds = 75 * 1024;              // two workgroups per CU
   const int fit = (kMaxLds - 1024) / ((LD + 1) * 4);
-  const bool resident = K <= fit;
+  const bool resident = K <= fit - 31;
   const int NB = resident ? K : (fit / 32) * 32;
-  const size_t lds = (size_t)NB * (LD + 1) * sizeof(float) + 1024;
+  // rows / |c|^2 entries up to the next multiple of 32 are read (masked) by the last tile
+  const size_t lds = (size_t)((NB + 31) / 32 * 32) * (LD + 1) * sizeof(float) + 1024;
   dim3 g((B + 128 / WPI - 1) / (128 / WPI));
   if (resident)
     hipLaunchKernelGGL((rq_fwd_reg_kernel<D, true, WPI>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB,

@@ -53,9 +53,20 @@ def run_impl(x, cbs, csq, o, impl, mode=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--sweep", action="store_true", help="mode / level sweep of the ML-32M shape only")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     results = []
+    if args.sweep:
+        for (B, D, K, L) in [(65536, 64, 256, 3), (65536, 64, 256, 1), (65536, 64, 256, 6)]:
+            x, cbs, csq, o = quantize_case(B, D, K, L, dev)
+            for impl in (1, 2):
+                for mode in (0, 2, 3):
+                    ms = sorted(ev_time(lambda: run_impl(x, cbs, csq, o, impl, mode), 10) for _ in range(args.rounds))
+                    med = ms[len(ms) // 2]
+                    print(json.dumps(dict(kernel="rq_quantize_fwd", impl=impl, mode=mode, shape=[B, D, K, L],
+                                          median_ms=med, tflops=2.0 * K * D * L * B / (med * 1e-3) / 1e12)), flush=True)
+        return
     shapes = [(65536, 64, 256, 3), (65536, 32, 256, 3), (262144, 64, 256, 3), (64, 64, 256, 3),
               (16384, 1024, 2048, 4)]
     for (B, D, K, L) in shapes:
