@@ -78,6 +78,15 @@ size_t rq_segment_sum_workspace(int64_t B, int64_t K);
 int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
                    void* workspace, size_t ws_bytes, void* stream);
 
+/* Weight / bias gradient of a Linear layer over a large batch: dW (O,I) = g^T x, db (O,) = sum_b g
+ * (or NULL). g: (Bn, O) rows of stride ldg, x: (Bn, I) rows of stride ldx, fp32, O, I, ld % 4 == 0,
+ * 16-byte aligned. Replaces torch autograd's grad_weight = grad_out^T @ input for the nn.Linear
+ * layers of modules/encoder.py:7-36 (RQ-VAE encoder/decoder MLPs): split-K over the batch with a
+ * fixed-order reduction (deterministic). workspace >= rq_linear_wgrad_workspace(Bn, O, I) bytes. */
+size_t rq_linear_wgrad_workspace(int64_t Bn, int64_t O, int64_t I);
+int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, int64_t Bn, int64_t O, int64_t I,
+                    float* dW, float* db, void* workspace, size_t ws_bytes, void* stream);
+
 /* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
  * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */

@@ -1,13 +1,15 @@
 """Bias-free MLP — reference semantics: modules/encoder.py:7-36.
 
 Layer order inside ``self.mlp`` (and therefore the state-dict keys ``mlp.{i}.weight``) is the
-reference's: Linear, SiLU, [Dropout], ..., Linear, then L2 norm or Identity. The GEMMs run on
-hipBLASLt through torch; the RQ hot path around them is HIP (rqvae_hip.ops).
+reference's: Linear, SiLU, [Dropout], ..., Linear, then L2 norm or Identity. Forward and data-grad
+GEMMs run on hipBLASLt through torch; weight gradients on the split-K HIP kernel
+(modules.linear.Linear); the RQ hot path around them is HIP (rqvae_hip.ops).
 """
 from typing import List
 
 from torch import nn
 
+from modules.linear import Linear
 from modules.normalize import L2NormalizationLayer
 
 
@@ -15,7 +17,7 @@ def _layer_stack(dims, dropout, normalize):
     seq = nn.Sequential()
     last = len(dims) - 2
     for i in range(last + 1):
-        seq.append(nn.Linear(dims[i], dims[i + 1], bias=False))
+        seq.append(Linear(dims[i], dims[i + 1], bias=False))
         if i < last:
             seq.append(nn.SiLU())
             if dropout:

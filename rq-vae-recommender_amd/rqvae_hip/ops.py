@@ -12,7 +12,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream_handle, require_gpu
+from ._lib import RqHipError, call, ptr, stream_handle, require_gpu
 
 MODE_EVAL, MODE_GUMBEL, MODE_STE, MODE_ROTATION = 0, 1, 2, 3
 
@@ -125,6 +125,61 @@ def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int):
     call("rq_segment_sum", ptr(rows), ptr(keys), B, D, int(K), ptr(out), ptr(counts), ptr(ws), nbytes,
          stream_handle(rows.device))
     return out, counts
+
+
+def linear_wgrad(g: torch.Tensor, x: torch.Tensor, with_bias: bool):
+    """(dW = g^T x (O, I), db = g.sum(0) (O,) or None) for g (N, O), x (N, I) fp32 — split-K MFMA
+    kernel with a fixed-order reduction (rq_linear_wgrad)."""
+    require_gpu(g, x, what="linear_wgrad")
+    g = g.contiguous()
+    x = x.contiguous()
+    N, O = g.shape
+    I = x.shape[1]
+    dW = torch.empty((O, I), device=g.device, dtype=torch.float32)
+    db = torch.empty((O,), device=g.device, dtype=torch.float32) if with_bias else None
+    nbytes = _lib.load().rq_linear_wgrad_workspace(N, O, I)
+    ws = torch.empty((nbytes,), device=g.device, dtype=torch.uint8)
+    call("rq_linear_wgrad", ptr(g), O, ptr(x), I, N, O, I, ptr(dW), ptr(db), ptr(ws), nbytes,
+         stream_handle(g.device))
+    return dW, db
+
+
+def wgrad_supported(weight: torch.Tensor) -> bool:
+    O, I = weight.shape
+    return weight.dtype == torch.float32 and O % 4 == 0 and I % 4 == 0
+
+
+class LinearFunction(torch.autograd.Function):
+    """y = x W^T + b (torch.nn.functional.linear, hipBLASLt) whose backward takes the data gradient
+    from hipBLASLt (g @ W: large M, well tiled) and the weight / bias gradient from rq_linear_wgrad
+    (reduction over the whole batch, where the library GEMM leaves most CUs idle)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        O, I = weight.shape
+        g2 = g.reshape(-1, O)
+        gx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            gx = (g2 @ weight).view(x.shape)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dW, db = linear_wgrad(g2, x.reshape(-1, I), ctx.has_bias)
+        return gx, dW, db if ctx.has_bias else None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+    """Drop-in for F.linear on the device path (fp32, O and I multiples of 4)."""
+    require_gpu(x, weight, bias, what="linear")
+    if not wgrad_supported(weight) or x.dtype != torch.float32:
+        raise RqHipError(f"linear: fp32 weights with both dims % 4 == 0 required, got {tuple(weight.shape)} "
+                         f"{weight.dtype}")
+    return LinearFunction.apply(x, weight, bias)
 
 
 def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
