@@ -10,8 +10,9 @@
 //   pass 1  wgrad_partial_kernel: workgroup (s, tile) computes the 128 x 128 output tile over
 //           rows [s*chunk, (s+1)*chunk) on v_mfma_f32_32x32x2_f32, operands staged through a
 //           double-buffered LDS ring (rows stay in their HBM layout: b-major, coalesced float4
-//           loads, conflict-free b32 operand reads). Tile-column-0 workgroups also sum g over
-//           their rows for db. Partials go to a workspace [S][O][I] (+ [S][O]).
+//           loads; one conflict-free ds_read_b64 per operand feeds two MFMA tiles).
+//           Tile-column-0 workgroups also sum g over their rows for db. Partials go to a
+//           workspace [S][O][I] (+ [S][O]).
 //   pass 2  wgrad_reduce_kernel: fixed-order sum over s — deterministic, no atomics.
 //
 // Workgroups that share a row chunk are placed on the same XCD (blockIdx % 8 selects the XCD)
@@ -21,9 +22,12 @@
 namespace rqhip {
 
 constexpr int kWT = 128;    // output tile (o and i)
-constexpr int kWBK = 16;    // rows per LDS stage
-constexpr int kWLD = 160;   // LDS row stride in floats: the two lane halves (rows k, k+1) hit disjoint banks
+constexpr int kWBK = 32;    // rows per LDS stage
+constexpr int kWLD = 128;   // LDS row stride in floats (float2 operand reads: 32 lanes x 8 B = all 64 banks)
 
+// Operand mapping: a wave owns a 64 (o) x 64 (i) block as 2 x 2 MFMA tiles, interleaved so that
+// one ds_read_b64 feeds both tiles of a pair: tile p's MFMA row m is o = 2m + p (and tile q's
+// column n is i = 2n + q). The MFMA k index is the lane half (rows b = 2kp, 2kp+1 of the stage).
 __global__ void __launch_bounds__(256, 2)
 wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, int64_t ldx, int64_t Bn,
                      int O, int I, int tiles_i, int tiles, int S, int64_t chunk, int per, float* __restrict__ P,
@@ -41,10 +45,11 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
   const int wo = wave >> 1, wi = wave & 1;
   const bool do_bias = Pb != nullptr && (t % tiles_i) == 0 && wi == 0;
 
-  float4 ra[2], rb[2];
+  constexpr int kF = kWBK * kWT / 4 / 256;   // float4 per thread per operand per stage
+  float4 ra[kF], rb[kF];
   auto load = [&](int64_t b0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < kF; ++j) {
       const int f = tid + 256 * j, r = f >> 5, c = (f & 31) * 4;
       const int64_t b = b0 + r;
       const bool okb = b < b_hi;
@@ -54,7 +59,7 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
   };
   auto stash = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < kF; ++j) {
       const int f = tid + 256 * j, r = f >> 5, c = (f & 31) * 4;
       *reinterpret_cast<float4*>(&As[buf][r][c]) = ra[j];
       *reinterpret_cast<float4*>(&Bs[buf][r][c]) = rb[j];
@@ -79,13 +84,13 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
     if (st + 1 < nst) load(b_lo + (int64_t)(st + 1) * kWBK);   // in flight during the MFMAs
 #pragma unroll
     for (int kp = 0; kp < kWBK / 2; ++kp) {
-      const int k = 2 * kp + h;   // MFMA k index = lane half: A[o][k] = g[b][o], B[k][i] = x[b][i]
-      const float a0 = As[buf][k][wo * 64 + c32], a1 = As[buf][k][wo * 64 + 32 + c32];
-      const float v0 = Bs[buf][k][wi * 64 + c32], v1 = Bs[buf][k][wi * 64 + 32 + c32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v1, acc[1][1], 0, 0, 0);
+      const int k = 2 * kp + h;   // A[o][k] = g[b][o], B[k][i] = x[b][i]
+      const float2 a = *reinterpret_cast<const float2*>(&As[buf][k][wo * 64 + 2 * c32]);
+      const float2 v = *reinterpret_cast<const float2*>(&Bs[buf][k][wi * 64 + 2 * c32]);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, v.x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, v.y, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, v.x, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, v.y, acc[1][1], 0, 0, 0);
     }
     if (do_bias) {
 #pragma unroll
@@ -95,20 +100,18 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
     __syncthreads();
   }
 
-  // C/D map: row = (r&3) + 8(r>>2) + 4h within the 32-row block, col = lane&31.
+  // C/D map: MFMA row m = (r&3) + 8(r>>2) + 4h, column n = lane&31; o = 2m + p, i = 2n + q.
   float* Ps = P + (int64_t)s * O * I;
+  const int i = i0 + wi * 64 + 2 * c32;
+  if (i < I) {
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = i0 + wi * 64 + q * 32 + c32;
-      if (i >= I) continue;
+    for (int p = 0; p < 2; ++p)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int o = o0 + wo * 64 + p * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (o < O) Ps[(int64_t)o * I + i] = acc[p][q][r];
+        const int o = o0 + wo * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * h) + p;
+        if (o < O) *reinterpret_cast<float2*>(Ps + (int64_t)o * I + i) = make_float2(acc[p][0][r], acc[p][1][r]);
       }
-    }
+  }
   if (do_bias) {
     const int o = o0 + wo * 64 + lane;
     if (o < O) Pb[(int64_t)s * O + o] = bsum;

@@ -784,7 +784,7 @@ static void launch_fwd_reg_w(int B, hipStream_t s, const float* x, const float* 
   constexpr int LD = D + 4;
   constexpr int kMaxLds = 75 * 1024;              // two workgroups per CU
   const int fit = (kMaxLds - 1024) / ((LD + 1) * 4);
-  const bool resident = K <= fit - 31;
+  const bool resident = (K + 31) / 32 * 32 <= fit;
   const int NB = resident ? K : (fit / 32) * 32;
   // rows / |c|^2 entries up to the next multiple of 32 are read (masked) by the last tile
   const size_t lds = (size_t)((NB + 31) / 32 * 32) * (LD + 1) * sizeof(float) + 1024;

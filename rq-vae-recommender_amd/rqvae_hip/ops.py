@@ -144,6 +144,9 @@ def linear_wgrad(g: torch.Tensor, x: torch.Tensor, with_bias: bool):
     return dW, db
 
 
+WGRAD_MIN_ROWS = 1024
+
+
 def wgrad_supported(weight: torch.Tensor) -> bool:
     O, I = weight.shape
     return weight.dtype == torch.float32 and O % 4 == 0 and I % 4 == 0
@@ -169,7 +172,12 @@ class LinearFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (g2 @ weight).view(x.shape)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dW, db = linear_wgrad(g2, x.reshape(-1, I), ctx.has_bias)
+            x2 = x.reshape(-1, I)
+            if g2.shape[0] >= WGRAD_MIN_ROWS:
+                dW, db = linear_wgrad(g2, x2, ctx.has_bias)
+            else:   # a few hundred rows: one library GEMM launch beats split-K + reduction
+                dW = g2.t() @ x2
+                db = g2.sum(0) if ctx.has_bias else None
         return gx, dW, db if ctx.has_bias else None
 
 
