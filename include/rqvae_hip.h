@@ -78,6 +78,17 @@ size_t rq_segment_sum_workspace(int64_t B, int64_t K);
 int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
                    void* workspace, size_t ws_bytes, void* stream);
 
+/* RMSNorm (modules/normalize.py:22-32): y = (x * rstd) * w, rstd = rsqrt(mean_j x^2 + eps) per row.
+ * x, y: (B, D) fp32 rows, D % 4 == 0, D <= 4096; rstd (B,) saved for the backward. bwd: gx (B, D)
+ * and gw (D,) = sum_b gy_b x_b rstd_b (fixed-order reduction; workspace >=
+ * rq_rmsnorm_bwd_workspace(B, D) bytes). Replaces torch's pow/mean/rsqrt/mul chain (6 kernels fwd,
+ * ~10 bwd) in the decoder (modules/model.py:54-55, modules/transformer/model.py:47-57). */
+int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float* y, float* rstd,
+                   void* stream);
+size_t rq_rmsnorm_bwd_workspace(int64_t B, int64_t D);
+int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
+                   float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream);
+
 /* Weight / bias gradient of a Linear layer over a large batch: dW (O,I) = g^T x, db (O,) = sum_b g
  * (or NULL). g: (Bn, O) rows of stride ldg, x: (Bn, I) rows of stride ldx, fp32, O, I, ld % 4 == 0,
  * 16-byte aligned. Replaces torch autograd's grad_weight = grad_out^T @ input for the nn.Linear

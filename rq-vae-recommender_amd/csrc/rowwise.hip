@@ -90,6 +90,148 @@ __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __re
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// RMSNorm (modules/normalize.py:22-32): t = x * rsqrt(mean(x^2) + eps), y = t * w.
+// fwd: one wave per row, saves rstd. bwd: gx = r (w gy) - x (r^3 / D) sum_j (w gy x)_j per row;
+// gw = sum_b gy_b t_b reduced deterministically: each 4-wave workgroup owns kRmsRows rows and writes
+// a [D] partial (waves combined in order through LDS), rms_reduce_kernel sums partials in order.
+constexpr int kRmsRows = 64;
+
+template <int VPL>
+__global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          int64_t B, int D, float eps, float* __restrict__ y,
+                                                          float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const float* p = x + r * D;
+  float4 xv[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    xv[v] = c < D ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s = __builtin_fmaf(xv[v].x, xv[v].x, s);
+    s = __builtin_fmaf(xv[v].y, xv[v].y, s);
+    s = __builtin_fmaf(xv[v].z, xv[v].z, s);
+    s = __builtin_fmaf(xv[v].w, xv[v].w, s);
+  }
+  s = group_sum<64>(s);
+  const float rs = rsqrtf(s / (float)D + eps);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    if (c >= D) continue;
+    const float4 wv = *reinterpret_cast<const float4*>(w + c);
+    *reinterpret_cast<float4*>(y + r * D + c) =
+        make_float4((xv[v].x * rs) * wv.x, (xv[v].y * rs) * wv.y, (xv[v].z * rs) * wv.z, (xv[v].w * rs) * wv.w);
+  }
+  if (lane == 0) rstd[r] = rs;
+}
+
+template <int VPL>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ rstd, const float* __restrict__ gy,
+                                                          int64_t B, int D, float* __restrict__ gx,
+                                                          float* __restrict__ gw_part) {
+  __shared__ float4 part[4][VPL * 64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float4 wv[VPL], gwa[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    wv[v] = c < D ? *reinterpret_cast<const float4*>(w + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gwa[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float invD = 1.f / (float)D;
+  for (int i = wave; i < kRmsRows; i += 4) {
+    const int64_t r = (int64_t)blockIdx.x * kRmsRows + i;
+    if (r >= B) break;
+    const float rs = rstd[r];
+    float4 xv[VPL], gt[VPL];
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      const bool ok = c < D;
+      xv[v] = ok ? *reinterpret_cast<const float4*>(x + r * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g = ok ? *reinterpret_cast<const float4*>(gy + r * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      gt[v] = make_float4(wv[v].x * g.x, wv[v].y * g.y, wv[v].z * g.z, wv[v].w * g.w);
+      dot = __builtin_fmaf(gt[v].x, xv[v].x, dot);
+      dot = __builtin_fmaf(gt[v].y, xv[v].y, dot);
+      dot = __builtin_fmaf(gt[v].z, xv[v].z, dot);
+      dot = __builtin_fmaf(gt[v].w, xv[v].w, dot);
+      gwa[v].x = __builtin_fmaf(g.x, xv[v].x * rs, gwa[v].x);
+      gwa[v].y = __builtin_fmaf(g.y, xv[v].y * rs, gwa[v].y);
+      gwa[v].z = __builtin_fmaf(g.z, xv[v].z * rs, gwa[v].z);
+      gwa[v].w = __builtin_fmaf(g.w, xv[v].w * rs, gwa[v].w);
+    }
+    dot = group_sum<64>(dot);
+    const float k = rs * rs * rs * invD * dot;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      if (c >= D) continue;
+      *reinterpret_cast<float4*>(gx + r * D + c) =
+          make_float4(rs * gt[v].x - xv[v].x * k, rs * gt[v].y - xv[v].y * k, rs * gt[v].z - xv[v].z * k,
+                      rs * gt[v].w - xv[v].w * k);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) part[wave][v * 64 + lane] = gwa[v];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      if (c >= D) continue;
+      float4 a = part[0][v * 64 + lane];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const float4 b = part[q][v * 64 + lane];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      *reinterpret_cast<float4*>(gw_part + (int64_t)blockIdx.x * D + c) = a;
+    }
+  }
+}
+
+// out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): 64 float4 columns per workgroup,
+// wave q sums s = q, q+4, ..., the four wave partials are added in order through LDS.
+__global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict__ P, int S, int64_t n,
+                                                         float* __restrict__ out) {
+  __shared__ float4 red[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t j = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const bool ok = j < n;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    int s = wave;
+    for (; s + 12 < S; s += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+    }
+    for (; s < S; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[wave][lane] = a;
+  __syncthreads();
+  if (wave == 0 && ok) {
+    float4 r = red[0][lane];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float4 v = red[q][lane];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + j) = r;
+  }
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -129,6 +271,55 @@ int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, co
 #undef L2R_CASE
   }
   RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd");
+  return 0;
+}
+
+size_t rq_rmsnorm_bwd_workspace(int64_t B, int64_t D) {
+  if (B <= 0 || D <= 0) return 0;
+  return (size_t)((B + kRmsRows - 1) / kRmsRows) * (size_t)D * sizeof(float);
+}
+
+#define RMS_SWITCH(VPL_EXPR, LAUNCH)                                                                      \
+  switch (VPL_EXPR) {                                                                                     \
+    case 1: LAUNCH(1) break; case 2: LAUNCH(2) break; case 3: LAUNCH(3) break; case 4: LAUNCH(4) break;  \
+    case 5: LAUNCH(5) break; case 6: LAUNCH(6) break; case 7: LAUNCH(7) break; case 8: LAUNCH(8) break;  \
+    case 9: LAUNCH(9) break; case 10: LAUNCH(10) break; case 11: LAUNCH(11) break;                       \
+    case 12: LAUNCH(12) break; case 13: LAUNCH(13) break; case 14: LAUNCH(14) break;                     \
+    case 15: LAUNCH(15) break; case 16: LAUNCH(16) break;                                                 \
+  }
+
+int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float* y, float* rstd,
+                   void* stream) {
+  RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_fwd: need D %% 4 == 0, D <= 4096");
+  if (B == 0) return 0;
+  RQ_CHECK_ARG(x && w && y && rstd, "rq_rmsnorm_fwd: null pointer");
+  dim3 g((unsigned)((B + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+#define RMS_F(V) hipLaunchKernelGGL((rmsnorm_fwd_kernel<V>), g, dim3(256), 0, s, x, w, B, (int)D, eps, y, rstd);
+  RMS_SWITCH((int)((D + 255) / 256), RMS_F)
+#undef RMS_F
+  RQ_LAUNCH_CHECK("rq_rmsnorm_fwd");
+  return 0;
+}
+
+int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
+                   float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream) {
+  RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_bwd: need D %% 4 == 0, D <= 4096");
+  RQ_CHECK_ARG(gw && (B == 0 || (x && w && rstd && gy && gx)), "rq_rmsnorm_bwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (B == 0) {
+    RQ_HIP(hipMemsetAsync(gw, 0, (size_t)D * sizeof(float), s));
+    return 0;
+  }
+  RQ_CHECK_ARG(workspace && ws_bytes >= rq_rmsnorm_bwd_workspace(B, D), "rq_rmsnorm_bwd: workspace too small");
+  float* part = static_cast<float*>(workspace);
+  const int nblk = (int)((B + kRmsRows - 1) / kRmsRows);
+#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, gx, part);
+  RMS_SWITCH((int)((D + 255) / 256), RMS_B)
+#undef RMS_B
+  RQ_LAUNCH_CHECK("rq_rmsnorm_bwd");
+  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + 63) / 64)), dim3(256), 0, s, part, nblk, D, gw);
+  RQ_LAUNCH_CHECK("rq_rmsnorm_bwd(reduce)");
   return 0;
 }
 

@@ -18,6 +18,7 @@ from torch import Tensor
 from torch.nn import functional as F
 
 from data.schemas import TokenizedSeqBatch
+from modules.linear import Linear
 from modules.embedding.id_embedder import SemIdEmbedder, UserIdEmbedder
 from modules.normalize import RMSNorm
 from modules.transformer.model import TransformerEncoderDecoder
@@ -63,9 +64,9 @@ class EncoderDecoderRetrievalModel(nn.Module):
         self.transformer = TransformerEncoderDecoder(d_in=attn_dim, d_out=attn_dim, dropout=dropout,
                                                      num_heads=num_heads, encoder_layers=n_layers // 2,
                                                      decoder_layers=n_layers // 2)
-        self.in_proj = nn.Linear(embedding_dim, attn_dim, bias=False)
-        self.in_proj_context = nn.Linear(embedding_dim, attn_dim, bias=False)
-        self.out_proj = nn.Linear(attn_dim, num_embeddings, bias=False)
+        self.in_proj = Linear(embedding_dim, attn_dim, bias=False)
+        self.in_proj_context = Linear(embedding_dim, attn_dim, bias=False)
+        self.out_proj = Linear(attn_dim, num_embeddings, bias=False)
 
     def _predict(self, batch: TokenizedSeqBatch):
         user_emb = self.user_id_embedder(batch.user_ids)                  # (B, 1, E)

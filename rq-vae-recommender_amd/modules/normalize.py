@@ -2,12 +2,15 @@
 
 * ``l2norm``: divide by max(||x||_2, eps) along ``dim`` (eps 1e-12), i.e. F.normalize.
 * ``RMSNorm``: y = w * x / sqrt(mean(x^2, -1) + eps), evaluated in fp32 and cast back to the
-  input dtype before the weight multiply. Works on dense tensors and on jagged NJTs (it only
-  touches the last, dense axis).
+  input dtype before the weight multiply. Dense fp32 device tensors run the fused HIP kernels
+  (rqvae_hip.ops.rmsnorm: one HBM pass each way); jagged NJTs and CPU tensors take torch's ops
+  (it only touches the last, dense axis).
 """
 import torch
 from torch import nn
 from torch.nn import functional as F
+
+from rqvae_hip import ops as hip_ops
 
 __all__ = ["l2norm", "L2NormalizationLayer", "RMSNorm"]
 
@@ -36,5 +39,7 @@ class RMSNorm(nn.Module):
         return x * inv_rms
 
     def forward(self, x):
+        if hip_ops.rmsnorm_supported(x, self.weight):
+            return hip_ops.rmsnorm(x, self.weight, self.eps)
         y = self._norm(x.float()).type_as(x)
         return y * self.weight

@@ -20,6 +20,7 @@ from torch import Tensor
 
 from ops.jagged import Jagged, as_jagged
 from rqvae_hip import ops as hip_ops
+from modules.linear import Linear
 
 AttentionInput = Union[Tensor, "torch.nested.Tensor", Jagged]
 
@@ -67,11 +68,11 @@ class MultiHeadAttention(nn.Module):
         self.d_out = d_out
         self.enable_kv_cache = enable_kv_cache
         if cross_attn:
-            self.q = nn.Linear(d_in, d_out, bias=qkv_bias)
-            self.kv = nn.Linear(d_in, 2 * d_out, bias=qkv_bias)
+            self.q = Linear(d_in, d_out, bias=qkv_bias)
+            self.kv = Linear(d_in, 2 * d_out, bias=qkv_bias)
         else:
-            self.qkv = nn.Linear(d_in, 3 * d_out, bias=qkv_bias)
-        self.proj = nn.Linear(d_out, d_out, bias=False)
+            self.qkv = Linear(d_in, 3 * d_out, bias=qkv_bias)
+        self.proj = Linear(d_out, d_out, bias=False)
         self.attend = Attend(self.d_out, self.num_heads, self.head_dim, dropout=False)
         self._kv_cache = None
 

@@ -31,6 +31,9 @@ _SIGS = {
     "rq_quantize_bwd": ([_P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I),
     "rq_segment_sum_workspace": ([_I64, _I64], _SZ),
     "rq_segment_sum": ([_P, _P, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
+    "rq_rmsnorm_fwd": ([_P, _P, _I64, _I64, _F, _P, _P, _P], _I),
+    "rq_rmsnorm_bwd_workspace": ([_I64, _I64], _SZ),
+    "rq_rmsnorm_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_linear_wgrad_workspace": ([_I64, _I64, _I64], _SZ),
     "rq_linear_wgrad": ([_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_unique_workspace": ([_I64], _SZ),

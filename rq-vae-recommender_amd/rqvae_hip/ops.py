@@ -190,6 +190,47 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     return LinearFunction.apply(x, weight, bias)
 
 
+class RMSNormFunction(torch.autograd.Function):
+    """y = (x * rsqrt(mean(x^2, -1) + eps)) * w over the last axis (modules/normalize.py:22-32), one
+    HBM pass forward (rq_rmsnorm_fwd) and one backward (rq_rmsnorm_bwd: gx and a deterministic gw)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps: float):
+        require_gpu(x, weight, what="rmsnorm")
+        D = x.shape[-1]
+        x2 = x.contiguous().view(-1, D)
+        B = x2.shape[0]
+        y = torch.empty_like(x2)
+        rstd = torch.empty((B,), device=x.device, dtype=torch.float32)
+        call("rq_rmsnorm_fwd", ptr(x2), ptr(weight), B, D, float(eps), ptr(y), ptr(rstd), stream_handle(x.device))
+        ctx.save_for_backward(x2, weight, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight, rstd = ctx.saved_tensors
+        B, D = x2.shape
+        gy2 = gy.contiguous().view(B, D)
+        gx = torch.empty_like(x2)
+        gw = torch.empty((D,), device=x2.device, dtype=torch.float32)
+        nbytes = _lib.load().rq_rmsnorm_bwd_workspace(B, D)
+        ws = torch.empty((nbytes,), device=x2.device, dtype=torch.uint8)
+        call("rq_rmsnorm_bwd", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2), B, D, ptr(gx), ptr(gw), ptr(ws), nbytes,
+             stream_handle(x2.device))
+        return gx.view(ctx.shape), gw, None
+
+
+def rmsnorm_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    D = x.shape[-1]
+    return (x.is_cuda and not x.is_nested and x.dtype == torch.float32 and weight.dtype == torch.float32
+            and D % 4 == 0 and D <= 4096)
+
+
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    return RMSNormFunction.apply(x, weight, eps)
+
+
 def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     """Number of distinct rows of ids (B, L) as a device int64 scalar (modules/rqvae.py:152-157)."""
     require_gpu(ids, what="unique_count")

@@ -26,3 +26,35 @@ def test_l2norm_recon_vs_torch(device, B, C):
     assert torch.allclose(r, rr, rtol=1e-5, atol=1e-6)
     assert torch.allclose(a.grad, b.grad, rtol=1e-4, atol=1e-7)
     assert torch.isfinite(a.grad).all()
+
+
+@pytest.mark.parametrize("shape", [(11000, 512), (7, 128), (3, 5, 4096), (1, 4), (0, 64)])
+def test_rmsnorm_fused_matches_fp64(device, shape):
+    """Fused RMSNorm vs the reference formula (modules/normalize.py:22-32) in fp64.
+    Tolerance: y, gx 2e-5 * max|ref|; gw 2e-5 * sum_b |gy x rstd| (fp32 row sums)."""
+    from modules.normalize import RMSNorm
+    from rqvae_hip import ops
+    D = shape[-1]
+    gen = torch.Generator(device=device).manual_seed(D + len(shape))
+    x = torch.randn(*shape, generator=gen, device=device) * 3
+    m = RMSNorm(D).to(device)
+    with torch.no_grad():
+        m.weight.copy_(1 + 0.1 * torch.randn(D, generator=gen, device=device))
+    assert ops.rmsnorm_supported(x, m.weight)
+    xr = x.clone().requires_grad_(True)
+    y = m(xr)
+    gy = torch.randn(*shape, generator=gen, device=device)
+    (y * gy).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    w64 = m.weight.detach().double().requires_grad_(True)
+    y64 = x64 * torch.rsqrt(x64.pow(2).mean(-1, keepdim=True) + m.eps) * w64
+    (y64 * gy.double()).sum().backward()
+    if x.numel() == 0:
+        assert y.shape == x.shape and not m.weight.grad.any()
+        return
+    def ok(a, b, scale):
+        return ((a.double() - b).abs() <= 2e-5 * scale + 1e-7).all()
+    assert ok(y, y64, y64.abs().max())
+    assert ok(xr.grad, x64.grad, x64.grad.abs().max())
+    r = torch.rsqrt(x.double().pow(2).mean(-1, keepdim=True) + m.eps)
+    assert ok(m.weight.grad, w64.grad, (gy.double() * x.double() * r).abs().reshape(-1, D).sum(0))
