@@ -107,8 +107,8 @@ __device__ __forceinline__ void store_dT(float* rowp, const floatx16 (&acc)[Pad<
 }
 
 // ---------------------------------------------------------------------------------------- fwd
-template <int HD>
-__global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__ q, int64_t sq, const float* __restrict__ k,
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restrict__ q, int64_t sq, const float* __restrict__ k,
                                                         int64_t sk, const float* __restrict__ v, int64_t sv,
                                                         const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
                                                         int causal, float scale, float* __restrict__ out, int64_t so,
@@ -118,11 +118,11 @@ __global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__
   float* K_s = smem;
   float* V_s = smem + 32 * LD;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  zero_pad32<HD, 128>(K_s, tid);
-  zero_pad32<HD, 128>(V_s, tid);
+  zero_pad32<HD, 64 * NW>(K_s, tid);
+  zero_pad32<HD, 64 * NW>(V_s, tid);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int qbase = blockIdx.x * 64;
+  const int qbase = blockIdx.x * 32 * NW;
   if (qbase >= lq) return;
   const int qi = qbase + wave * 32 + (lane & 31);
   const bool qv = qi < lq;
@@ -134,11 +134,11 @@ __global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[tl][r] = 0.f;
   float m = -INFINITY, l = 0.f;
-  const int kend = causal ? min(lk, qbase + 64) : lk;
+  const int kend = causal ? min(lk, qbase + 32 * NW) : lk;
   for (int kt = 0; kt < kend; kt += 32) {
     __syncthreads();
-    stage32<HD, 128>(K_s, k + k0 * sk + hh * HD, sk, kt, lk, tid);
-    stage32<HD, 128>(V_s, v + k0 * sv + hh * HD, sv, kt, lk, tid);
+    stage32<HD, 64 * NW>(K_s, k + k0 * sk + hh * HD, sk, kt, lk, tid);
+    stage32<HD, 64 * NW>(V_s, v + k0 * sv + hh * HD, sv, kt, lk, tid);
     __syncthreads();
     floatx16 s;
 #pragma unroll
@@ -177,8 +177,8 @@ __global__ void __launch_bounds__(128) attn_fwd_kernel(const float* __restrict__
 }
 
 // ------------------------------------------------------------------------------- bwd: dK, dV
-template <int HD>
-__global__ void __launch_bounds__(128) attn_bwd_dkdv_kernel(
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
@@ -190,11 +190,11 @@ __global__ void __launch_bounds__(128) attn_bwd_dkdv_kernel(
   float* lse_s = O_s + 32 * LD;
   float* dl_s = lse_s + 32;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  zero_pad32<HD, 128>(Q_s, tid);
-  zero_pad32<HD, 128>(O_s, tid);
+  zero_pad32<HD, 64 * NW>(Q_s, tid);
+  zero_pad32<HD, 64 * NW>(O_s, tid);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int kbase = blockIdx.x * 64;
+  const int kbase = blockIdx.x * 32 * NW;
   if (kbase >= lk) return;
   const int kj = kbase + wave * 32 + (lane & 31);
   const bool kv = kj < lk;
@@ -209,9 +209,9 @@ __global__ void __launch_bounds__(128) attn_bwd_dkdv_kernel(
   const int qstart = causal ? (kbase / 32) * 32 : 0;
   for (int qt = qstart; qt < lq; qt += 32) {
     __syncthreads();
-    stage32<HD, 128>(Q_s, q + q0 * sq + hh * HD, sq, qt, lq, tid);
-    stage32<HD, 128>(O_s, dout + q0 * sdo + hh * HD, sdo, qt, lq, tid);
-    if (tid < 64) {   // delta_q = sum_d dO*O and lse for the 32 queries of this tile
+    stage32<HD, 64 * NW>(Q_s, q + q0 * sq + hh * HD, sq, qt, lq, tid);
+    stage32<HD, 64 * NW>(O_s, dout + q0 * sdo + hh * HD, sdo, qt, lq, tid);
+    if (tid < 64) {   // delta_q = sum_d dO*O and lse for the 32 queries of this tile (wave 0)
       const int qr = tid & 31, half = tid >> 5, qq = qt + qr;
       float dsum = 0.f;
       if (qq < lq) {
@@ -248,8 +248,8 @@ __global__ void __launch_bounds__(128) attn_bwd_dkdv_kernel(
 }
 
 // ------------------------------------------------------------------------------------ bwd: dQ
-template <int HD>
-__global__ void __launch_bounds__(128) attn_bwd_dq_kernel(
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
@@ -259,11 +259,11 @@ __global__ void __launch_bounds__(128) attn_bwd_dq_kernel(
   float* K_s = smem;
   float* V_s = smem + 32 * LD;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  zero_pad32<HD, 128>(K_s, tid);
-  zero_pad32<HD, 128>(V_s, tid);
+  zero_pad32<HD, 64 * NW>(K_s, tid);
+  zero_pad32<HD, 64 * NW>(V_s, tid);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int qbase = blockIdx.x * 64;
+  const int qbase = blockIdx.x * 32 * NW;
   if (qbase >= lq) return;
   const int qi = qbase + wave * 32 + (lane & 31);
   const bool qv = qi < lq;
@@ -284,11 +284,11 @@ __global__ void __launch_bounds__(128) attn_bwd_dq_kernel(
   for (int tl = 0; tl < NTL; ++tl)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dqa[tl][r] = 0.f;
-  const int kend = causal ? min(lk, qbase + 64) : lk;
+  const int kend = causal ? min(lk, qbase + 32 * NW) : lk;
   for (int kt = 0; kt < kend; kt += 32) {
     __syncthreads();
-    stage32<HD, 128>(K_s, k + k0 * sk + hh * HD, sk, kt, lk, tid);
-    stage32<HD, 128>(V_s, v + k0 * sv + hh * HD, sv, kt, lk, tid);
+    stage32<HD, 64 * NW>(K_s, k + k0 * sk + hh * HD, sk, kt, lk, tid);
+    stage32<HD, 64 * NW>(V_s, v + k0 * sv + hh * HD, sv, kt, lk, tid);
     __syncthreads();
     floatx16 s, dp;
 #pragma unroll
@@ -308,12 +308,22 @@ __global__ void __launch_bounds__(128) attn_bwd_dq_kernel(
   store_dT<HD>(dq + (q0 + qi) * sdq + hh * HD, dqa, scale, h);
 }
 
+// Short sequences (<= 96 rows, e.g. Amazon contexts of <= 81 tokens) run one wave (32 rows) per
+// workgroup so no wave idles on a padded 32-row half; longer ones share each staged K/V (Q/dO)
+// tile between two waves.
 template <int HD>
-static void launch_fwd(dim3 g, hipStream_t st, const float* q, int64_t sq, const float* k, int64_t sk, const float* v,
-                       int64_t sv, const int64_t* cq, const int64_t* ck, int causal, float scale, float* out, int64_t so,
-                       float* lse, int64_t Tq) {
-  hipLaunchKernelGGL((attn_fwd_kernel<HD>), g, dim3(128), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse,
-                     Tq);
+static void launch_fwd(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
+                       int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
+                       float scale, float* out, int64_t so, float* lse, int64_t Tq) {
+  if (max_q <= 96) {
+    dim3 g((unsigned)((max_q + 31) / 32), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
+                       so, lse, Tq);
+  } else {
+    dim3 g((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, 2>), g, dim3(128), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
+                       so, lse, Tq);
+  }
 }
 
 template <int HD>
@@ -321,12 +331,24 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                        const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
                        const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck,
                        int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv) {
-  dim3 gk((unsigned)((max_k + 63) / 64), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD>), gk, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq,
-                     cq, ck, causal, scale, dk, sdk, dv, sdv);
-  dim3 gq((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD>), gq, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq,
-                     ck, causal, scale, dq, sdq);
+  if (max_k <= 96) {
+    dim3 gk((unsigned)((max_k + 31) / 32), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), gk, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
+                       lse, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
+  } else {
+    dim3 gk((unsigned)((max_k + 63) / 64), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 2>), gk, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
+                       lse, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
+  }
+  if (max_q <= 96) {
+    dim3 gq((unsigned)((max_q + 31) / 32), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), gq, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
+                       Tq, cq, ck, causal, scale, dq, sdq);
+  } else {
+    dim3 gq((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 2>), gq, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
+                       Tq, cq, ck, causal, scale, dq, sdq);
+  }
 }
 
 static bool attn_args_ok(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k) {
@@ -347,13 +369,12 @@ int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<=65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
   if (B == 0 || max_q == 0) return 0;
-  dim3 g((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
-    case 16: launch_fwd<16>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 32: launch_fwd<32>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 64: launch_fwd<64>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 128: launch_fwd<128>(g, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 16: launch_fwd<16>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 32: launch_fwd<32>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 64: launch_fwd<64>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 128: launch_fwd<128>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_fwd");
   return 0;

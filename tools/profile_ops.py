@@ -14,7 +14,37 @@ import bench  # noqa: E402
 from data.schemas import SeqBatch  # noqa: E402
 
 
+def decoder():
+    """Decoder train step (bench.measure_decoder config) with input shapes recorded."""
+    from data.processed import synthetic_tokenized_batch
+    from modules.model import EncoderDecoderRetrievalModel
+    D = bench.DEC
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    m = EncoderDecoderRetrievalModel(embedding_dim=D["E"], attn_dim=D["A"], dropout=D["dropout"], num_heads=D["H"],
+                                     n_layers=D["layers"], num_embeddings=D["K"], sem_id_dim=D["sem_id_dim"],
+                                     inference_verifier_fn=None, max_pos=D["max_items"] * D["sem_id_dim"]).to(dev).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=D["lr"], weight_decay=D["wd"], foreach=True)
+    b = synthetic_tokenized_batch(D["B"], D["max_items"], D["sem_id_dim"], D["K"], 50, dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        m(b).loss.backward()
+        opt.step()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=45,
+                                                             max_name_column_width=40, max_shapes_column_width=70))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "decoder":
+        return decoder()
     dev = torch.device("cuda", 0)
     model = bench.build_model(dev)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
