@@ -276,7 +276,7 @@ def measure_extras(model, device, x):
 DEC = dict(B=256, max_items=20, E=128, A=512, H=8, layers=8, K=256, sem_id_dim=4, dropout=0.3, lr=3e-4, wd=0.035)
 
 
-def measure_decoder(device, steps=10, warmup=3):
+def measure_decoder(device, steps=20, warmup=5):
     """BASELINE configs[2]: decoder train step at Amazon dims (decoder_amazon.gin), synthetic
     tokenized batches (n_items ~ U{2..20}), HIP jagged conversion + varlen attention."""
     from rqvae_hip import ops
@@ -287,7 +287,7 @@ def measure_decoder(device, steps=10, warmup=3):
                                      num_heads=DEC["H"], n_layers=DEC["layers"], num_embeddings=DEC["K"],
                                      sem_id_dim=DEC["sem_id_dim"], inference_verifier_fn=None,
                                      max_pos=DEC["max_items"] * DEC["sem_id_dim"]).to(device).train()
-    opt = torch.optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"], foreach=True)
+    opt = torch.optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"], fused=True)
     batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + i, device)
                for i in range(4)]
     ctx_tokens = [int(b.seq_mask.sum()) + DEC["B"] for b in batches]

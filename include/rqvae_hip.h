@@ -131,14 +131,16 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
  *   q[t][h][d] at q + t*sq + h*hd + d (likewise k, v, out, dout, dq, dk, dv with their strides);
  *   cu_q, cu_k (B+1) int64 offsets; max_q / max_k >= the longest segment (grid bound);
  *   lse (H, Tq) fp32 log-sum-exp per query (written by fwd, read by bwd). hd in {16, 32, 64, 128}.
- * Backward is deterministic (no atomics): dk/dv per key block, dq per query block. */
+ * Backward is deterministic (no atomics): dq per query block (also writes delta (H, Tq) = rowsum(dO*O),
+ * caller-provided scratch), then dk/dv per key block. */
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream);
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
-                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, void* stream);
+                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, float* delta,
+                    void* stream);
 
 #ifdef __cplusplus
 }

@@ -16,11 +16,15 @@
 // tile, no LDS round trip. The dK/dV pass puts keys on lanes the same way. P / dS feed the
 // next MFMA straight from the accumulator registers (register t of the 32x32 tile is the
 // k-slice of MFMA step t with key index (t&3)+8(t>>2)+4*(lane>>5)).
-// Backward = two launches (dK,dV per key block; dQ per query block) with recomputed P:
-// no atomics, bitwise deterministic.
+// Backward = two launches (dQ per query block, which also stores delta = rowsum(dO*O); then
+// dK,dV per key block) with recomputed P: no atomics, bitwise deterministic.
 #include "common.h"
 
 #include <math.h>
+
+#ifndef RQ_ATTN_ONE_WAVE_MAX
+#define RQ_ATTN_ONE_WAVE_MAX 96   // longest sequence served by one-wave workgroups
+#endif
 
 namespace rqhip {
 
@@ -181,8 +185,9 @@ template <int HD, int NW>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
-    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
-    int causal, float scale, float* __restrict__ dk, int64_t sdk, float* __restrict__ dv, int64_t sdv) {
+    const float* __restrict__ lse, const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q,
+    const int64_t* __restrict__ cu_k, int causal, float scale, float* __restrict__ dk, int64_t sdk,
+    float* __restrict__ dv, int64_t sdv) {
   constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
   __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD + 64];
   float* Q_s = smem;
@@ -211,19 +216,11 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
     __syncthreads();
     stage32<HD, 64 * NW>(Q_s, q + q0 * sq + hh * HD, sq, qt, lq, tid);
     stage32<HD, 64 * NW>(O_s, dout + q0 * sdo + hh * HD, sdo, qt, lq, tid);
-    if (tid < 64) {   // delta_q = sum_d dO*O and lse for the 32 queries of this tile (wave 0)
-      const int qr = tid & 31, half = tid >> 5, qq = qt + qr;
-      float dsum = 0.f;
-      if (qq < lq) {
-        const float* orow = out + (q0 + qq) * so + hh * HD + half * (HD / 2);
-        const float* drow = dout + (q0 + qq) * sdo + hh * HD + half * (HD / 2);
-        for (int d = 0; d < HD / 2; ++d) dsum += drow[d] * orow[d];
-      }
-      dsum += __shfl_xor(dsum, 32, 64);
-      if (half == 0) {
-        dl_s[qr] = dsum;
-        lse_s[qr] = qq < lq ? lse[(int64_t)hh * Tq + q0 + qq] : 0.f;
-      }
+    if (tid < 32) {   // delta_q = sum_d dO*O (written by the dQ pass) and lse for the 32 queries
+      const int qq = qt + tid;
+      const bool ok = qq < lq;
+      dl_s[tid] = ok ? delta[(int64_t)hh * Tq + q0 + qq] : 0.f;
+      lse_s[tid] = ok ? lse[(int64_t)hh * Tq + q0 + qq] : 0.f;
     }
     __syncthreads();
     floatx16 s, dp;
@@ -253,7 +250,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
-    int causal, float scale, float* __restrict__ dq, int64_t sdq) {
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ delta_out) {
   constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
   __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD];
   float* K_s = smem;
@@ -277,6 +274,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
     if (qv)
       for (int d = 0; d < HD / 2; ++d) delta += dof[d] * orow[d];
     delta += __shfl_xor(delta, 32, 64);
+    if (qv && h == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;   // reused by the dK/dV pass
   }
   const float lq_lse = qv ? lse[(int64_t)hh * Tq + qrow] : 0.f;
   floatx16 dqa[NTL];
@@ -315,7 +313,7 @@ template <int HD>
 static void launch_fwd(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
                        float scale, float* out, int64_t so, float* lse, int64_t Tq) {
-  if (max_q <= 96) {
+  if (max_q <= RQ_ATTN_ONE_WAVE_MAX) {
     dim3 g((unsigned)((max_q + 31) / 32), (unsigned)H, (unsigned)B);
     hipLaunchKernelGGL((attn_fwd_kernel<HD, 1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
                        so, lse, Tq);
@@ -330,24 +328,26 @@ template <int HD>
 static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q, int64_t sq,
                        const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
                        const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck,
-                       int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv) {
-  if (max_k <= 96) {
-    dim3 gk((unsigned)((max_k + 31) / 32), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), gk, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
-                       lse, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
-  } else {
-    dim3 gk((unsigned)((max_k + 63) / 64), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 2>), gk, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
-                       lse, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
-  }
-  if (max_q <= 96) {
+                       int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv,
+                       float* delta) {
+  // dQ pass first: it also writes delta_q = dO.O, which the dK/dV pass reads per query tile
+  if (max_q <= RQ_ATTN_ONE_WAVE_MAX) {
     dim3 gq((unsigned)((max_q + 31) / 32), (unsigned)H, (unsigned)B);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), gq, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
-                       Tq, cq, ck, causal, scale, dq, sdq);
+                       Tq, cq, ck, causal, scale, dq, sdq, delta);
   } else {
     dim3 gq((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 2>), gq, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
-                       Tq, cq, ck, causal, scale, dq, sdq);
+                       Tq, cq, ck, causal, scale, dq, sdq, delta);
+  }
+  if (max_k <= RQ_ATTN_ONE_WAVE_MAX) {
+    dim3 gk((unsigned)((max_k + 31) / 32), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), gk, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
+                       lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
+  } else {
+    dim3 gk((unsigned)((max_k + 63) / 64), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 2>), gk, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
+                       lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
   }
 }
 
@@ -383,8 +383,10 @@ int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
-                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, void* stream) {
-  RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv, "varlen_attn_bwd: null pointer");
+                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, float* delta,
+                    void* stream) {
+  RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv && delta,
+               "varlen_attn_bwd: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd: bad shape (hd must be 16/32/64/128, B<=65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0 && sdo % 4 == 0 && sdq % 4 == 0 &&
                    sdk % 4 == 0 && sdv % 4 == 0,
@@ -392,10 +394,10 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
-    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
-    case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
-    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
-    case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv); break;
+    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
+    case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
+    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
+    case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_bwd");
   return 0;

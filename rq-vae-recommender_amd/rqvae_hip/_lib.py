@@ -46,7 +46,7 @@ _SIGS = {
     "varlen_attn_fwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
                          _I64, _P], _I),
     "varlen_attn_bwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
-                         _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _P], _I),
+                         _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -367,9 +367,10 @@ class VarlenAttentionFunction(torch.autograd.Function):
         dq = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         dk = torch.empty((k.shape[0], A), device=q.device, dtype=torch.float32)
         dv = torch.empty((v.shape[0], A), device=q.device, dtype=torch.float32)
+        delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
         call("varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
              out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
-             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0),
+             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), ptr(delta),
              stream_handle(q.device))
         return dq, dk, dv, None, None, None, None, None, None, None
 

@@ -67,7 +67,7 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
                                          sem_id_dim=tokenizer.sem_ids_dim,
                                          max_pos=train_ds.max_seq_len * tokenizer.sem_ids_dim,
                                          jagged_mode=model_jagged_mode).to(device)
-    opt = torch.optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay)
+    opt = torch.optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay, fused=True)
     sched = InverseSquareRootScheduler(optimizer=opt, warmup_steps=10000)
     start_iter = 0
     if pretrained_decoder_path is not None:

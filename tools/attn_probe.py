@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Varlen attention fwd / bwd timing at the decoder configs' shapes (HIP events, one process).
+
+  Amazon:  B=256 sequences, ctx len 4*U{2..20}+1 (<= 81), H=8, hd=64 (attn_dim 512)
+  ML-32M:  B=64 sequences,  ctx len 4*U{2..200}+1 (<= 801), H=6, hd=64 (attn_dim 384)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rq-vae-recommender_amd"))
+from rqvae_hip import ops  # noqa: E402
+
+
+def t(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def case(name, B, H, hd, max_items, dev):
+    g = np.random.Generator(np.random.PCG64(7))
+    lens = 4 * g.integers(2, max_items + 1, size=B) + 1
+    cu = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).to(dev)
+    T = int(lens.sum())
+    A = H * hd
+    qkv = torch.randn(T, 3 * A, device=dev, requires_grad=True)
+    q, k, v = qkv[:, :A], qkv[:, A:2 * A], qkv[:, 2 * A:]
+    mx = int(lens.max())
+    fwd = lambda: ops.varlen_attention(q, k, v, cu, cu, H, False, mx, mx)  # noqa: E731
+    out = fwd()
+    go = torch.randn_like(out)
+    fb = lambda: torch.autograd.grad(fwd(), qkv, go)  # noqa: E731
+    ms_f, ms_fb = t(fwd), t(fb)
+    fl = 4.0 * hd * H * float((lens.astype(np.float64) ** 2).sum())
+    print(json.dumps(dict(case=name, tokens=T, max_len=mx, fwd_ms=round(ms_f, 4), fwd_bwd_ms=round(ms_fb, 4),
+                          fwd_tflops=round(fl / ms_f / 1e9, 1), fwd_bwd_tflops=round(3.5 * fl / ms_fb / 1e9, 1))),
+          flush=True)
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    if len(sys.argv) > 1:   # A/B: time an alternative build of the library
+        from rqvae_hip import _lib
+        _lib._lib = _lib.load(sys.argv[1])
+        print(json.dumps(dict(lib=sys.argv[1])))
+    case("amazon", 256, 8, 64, 20, dev)
+    case("ml32m", 64, 6, 64, 200, dev)
+
+
+if __name__ == "__main__":
+    main()
