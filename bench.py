@@ -9,6 +9,7 @@ beside it): encoder MLP -> fused HIP L-level quantize -> decoder MLP -> losses -
 (HIP quantize VJP) -> RCCL gradient all-reduce (N>1) -> AdamW.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline] [--no-extras]
+                  [--no-pmc]
 
 N>1 is launched by torch.distributed.run (one process per GPU); every rank processes its own
 disjoint 65,536-item shard ("weak" scaling) and rank 0 prints ONE JSON line.
@@ -16,8 +17,9 @@ disjoint 65,536-item shard ("weak" scaling) and rank 0 prints ONE JSON line.
 roofline: the fused quantize forward kernel (rq_quantize_fwd), algorithmic FLOPs
 2*K*D*L per item divided by its mean device time, measured with HIP events on
 the launching stream inside the timed region; peak = fp32 MFMA 157.3 TFLOP/s (gfx950 has no
-xf32). cpu_baseline: the pinned numpy oracle of the same train step (oracle/rqvae.py) on a
-bounded sample, timed on this host.
+xf32). traffic: HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+child processes, N=1 only) next to the algorithmic bytes. cpu_baseline: the pinned numpy oracle
+of the same train step (oracle/rqvae.py) on a bounded sample, timed on this host.
 """
 import argparse
 import json
@@ -48,6 +50,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=65536, help="items per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     return ap.parse_args()
@@ -84,6 +87,45 @@ def time_region(fn, steps, warmup, sync_all):
         fn()
     sync_all()
     return time.perf_counter() - t0
+
+
+def quantize_algorithmic_bytes(B, D, K, L):
+    """Bytes one rq_quantize_fwd launch must move: x and the codebooks (+|c|^2) in; residuals and
+    emb_out (L,B,D, saved for the VJP), emb_sum (B,D), ids (B,L) int64 and qloss (B,) out."""
+    return 4 * B * D + 4 * L * K * (D + 1) + 4 * B * (2 * L * D + D + 1) + 8 * B * L
+
+
+def pmc_traffic(timeout_s=75):
+    """HBM bytes per rq_quantize_fwd launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE:
+    they do not fit one TCC pass) over tools/pmc_quantize.py — the same kernel at the same shape —
+    run as child processes (this process never execs). Both counters are in KiB; FETCH_SIZE is
+    doubled (gfx950 tallies 128-B streaming reads at 64 B, MI355X_MICROARCH.md 'HBM')."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return None, "skipped: already running under rocprofv3"
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--kernel-include-regex", "rq_fwd",
+                   "-f", "csv", "-d", d, "-o", ctr, "--", sys.executable, os.path.join(ROOT, "tools", "pmc_quantize.py"),
+                   "5"]
+            r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True)
+            path = os.path.join(d, f"{ctr}_counter_collection.csv")
+            if r.returncode != 0 or not os.path.exists(path):
+                return None, f"{ctr} pass failed (exit {r.returncode}): {r.stderr[-200:]}"
+            v = sorted(float(row["Counter_Value"]) for row in csv.DictReader(open(path)) if row["Counter_Name"] == ctr)
+            if not v:
+                return None, f"{ctr}: no rq_fwd dispatches recorded"
+            vals[ctr] = v[len(v) // 2]
+    fetch = 2.0 * vals["FETCH_SIZE"] * 1024
+    write = vals["WRITE_SIZE"] * 1024
+    return dict(bytes=fetch + write, fetch_bytes_x2=fetch, write_bytes=write), None
 
 
 def cpu_baseline(budget_s, B=2048):
@@ -192,6 +234,10 @@ def main():
         return
     flops_per_item = 2 * CFG["K"] * CFG["D"] * CFG["L"]
     achieved = flops_per_item * B / (q_ms * 1e-3) / 1e12
+    alg_bytes = quantize_algorithmic_bytes(B, CFG["D"], CFG["K"], CFG["L"])
+    traffic, traffic_note = (None, "skipped (--no-pmc or N>1)")
+    if not args.no_pmc and ws == 1 and B == 65536:
+        traffic, traffic_note = pmc_traffic()
     line = {
         "metric": "decoder-train tokens/sec + RQ-VAE items/sec at 1/2/4/8 MI355X; achieved HBM %",
         "value": round(ws * B * args.steps / elapsed, 1),
@@ -210,8 +256,10 @@ def main():
                    "parallelism": f"dp{ws}"},
         "roofline": {"kernel": "rq_quantize_fwd", "bound": "mfma", "achieved": round(achieved, 3),
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": None, "launch_ms": round(q_ms, 4), "launches": q_n,
-                     "flops_per_launch": flops_per_item * B},
+                     "traffic": round(traffic["bytes"]) if traffic else None, "launch_ms": round(q_ms, 4),
+                     "launches": q_n, "flops_per_launch": flops_per_item * B, "algorithmic_bytes": alg_bytes,
+                     "traffic_detail": traffic if traffic else traffic_note,
+                     "hbm_GBps_at_algorithmic_bytes": round(alg_bytes / (q_ms * 1e-3) / 1e9, 1)},
         "loss_last": round(loss, 5),
     }
     line.update(extras)

@@ -1,0 +1,54 @@
+#!/bin/bash
+# One GPU-box pass: parity suite, bench line, rocprofv3 kernel stats of the bench, and HBM-traffic
+# PMC passes (FETCH_SIZE / WRITE_SIZE in separate runs) on the quantize forward.
+#   gpurun --timeout 1100 -- bash tools/gpu_check.sh [tests|bench|prof|pmc ...]
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -u
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+O="$R/gpurun_out"
+mkdir -p "$O"
+steps="${*:-tests bench prof pmc}"
+export TMPDIR=/tmp
+
+run() {   # name, seconds, command...
+  local name="$1" secs="$2"; shift 2
+  echo "[$(date +%T)] $name: $*"
+  timeout -k 10 "$secs" "$@"
+  local rc=$?
+  echo "[$(date +%T)] $name exit $rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+
+for s in $steps; do
+  case "$s" in
+    tests)
+      run tests 600 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$O/gpu_tests.log" 2>&1 || exit 1
+      tail -3 "$O/gpu_tests.log" ;;
+    bench)
+      run bench 400 python -u "$R/bench.py" > "$O/bench.json" 2> "$O/bench.err"
+      cat "$O/bench.json" ;;
+    prof)
+      cd /tmp
+      run prof 400 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o bench -- \
+        python3 "$R/bench.py" --no-cpu-baseline --no-pmc > "$O/prof_bench.json" 2> "$O/prof_bench.err"
+      run prof_rq 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o rqvae -- \
+        python3 "$R/bench.py" --no-cpu-baseline --no-pmc --no-extras > "$O/prof_rqvae.json" 2> "$O/prof_rqvae.err"
+      run prof_dec 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o decoder -- \
+        python3 "$R/bench.py" --decoder-only > "$O/prof_decoder.json" 2> "$O/prof_decoder.err"
+      cd "$R"
+      cat "$O/prof_bench.json" ;;
+    pmc)
+      cd /tmp
+      run pmc_fetch 90 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rq_fwd -f csv -d "$O/pmc_fetch" -o q -- \
+        python3 "$R/tools/pmc_quantize.py" 10 > "$O/pmc_fetch.log" 2>&1
+      run pmc_write 90 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rq_fwd -f csv -d "$O/pmc_write" -o q -- \
+        python3 "$R/tools/pmc_quantize.py" 10 > "$O/pmc_write.log" 2>&1
+      cd "$R" ;;
+    kern)
+      run kern 300 python -u "$R/tools/bench_kernels.py" > "$O/kernels.jsonl" 2> "$O/kernels.err"
+      cat "$O/kernels.jsonl" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
