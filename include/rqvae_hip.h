@@ -53,7 +53,10 @@ int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks
                     float* emb_sum, void* stream);
 
 /* Same as rq_quantize_fwd with an explicit kernel choice (benchmarking / A-B testing):
- * impl 0 = auto, 1 = LDS-tiled kernel (any D), 2 = register-resident kernel (D <= 64). */
+ * impl 0 = auto (2 for D <= 64, else 3 when allowed, else 1), 1 = fused LDS-tiled kernel (any D),
+ * 2 = register-resident kernel (D <= 64), 3 = split path for D >= 128 with 2*ceil(K/128)+1 <= D
+ * (per level: distance GEMM + partial argmin over 128x128 tiles, then a row epilogue; emb_out
+ * doubles as the level's scratch before it is written). */
 int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
                          int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
                          float* qloss, float* emb_sum, int impl, void* stream);

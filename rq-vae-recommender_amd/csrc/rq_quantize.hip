@@ -809,6 +809,306 @@ static void launch_fwd_reg(int B, hipStream_t s, const float* x, const float* cb
     launch_fwd_reg_w<D, 1>(B, s, x, cbs, csq, K, L, mode, beta, ids, eo, res, ql, es);
 }
 
+// ---------------------------------------------------------------------------------------
+// Split path for large D / K (D >= 128, e.g. the synthetic roofline shape D=1024, K=2048, L=4).
+// The fused kernel above gives one workgroup per 128 items, so B=16,384 leaves half the CUs
+// idle and every workgroup walks all K codewords alone. Here each level runs as
+//   rq_dist_argmin_kernel  one workgroup per (128-item tile, 128-codeword block): the distance
+//                          GEMM on v_mfma_f32_32x32x2_f32 (register-prefetched LDS stages of
+//                          32 D-columns, conflict-free ds_read_b128) with the argmin over its
+//                          block fused into the epilogue -> one (dist, index) partial per item
+//   rq_level_epi_kernel    LPI lanes per item: merge the partials (lowest index among equal
+//                          minima, as torch.min), then the same row epilogue as the fused kernel
+//                          (rotation trick / STE / eval, VQ loss, next residual and its |r|^2)
+// Workgroup order is XCD-major (T1) so the 16 codeword blocks of one item tile share an L2.
+// Scratch: level l's (dist, index) partials and its |res_l|^2 live in item b's own emb_out[l]
+// row (columns [0, 2*nblk] — needs 2*nblk + 1 <= D) until the epilogue overwrites that row.
+constexpr int kSB = 128;           // items per tile
+constexpr int kSN = 128;           // codewords per block
+constexpr int kSK = 32;            // D columns per LDS stage
+constexpr int kSLD = kSK + 4;      // padded LDS row: ds_read_b128 over 32 rows hits 16 distinct 4-bank groups
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+rq_dist_argmin_kernel(const float* __restrict__ res, const float* __restrict__ cb, const float* __restrict__ csq, int B,
+                      int D, int K, int nblk, int tilesB, float* __restrict__ scratch) {
+  __shared__ __attribute__((aligned(16))) float A_s[kSN * kSLD];   // codeword stage [128][36]
+  __shared__ __attribute__((aligned(16))) float X_s[kSB * kSLD];   // residual stage [128][36]
+  __shared__ float cs_s[kSN];
+  __shared__ float xs_s[kSB];
+  __shared__ float md_s[kSB];
+  __shared__ int mi_s[kSB];
+  const int n = tilesB * nblk, o = blockIdx.x, xcd = o & 7, q = n >> 3, rr = n & 7;
+  const int w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (o >> 3);
+  const int tb = w / nblk, cbk = w % nblk;
+  const int b0 = tb * kSB, n0 = cbk * kSN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int wr = wave >> 1, wc = wave & 1;   // wave block: codewords wr*64.., items wc*64..
+
+  // stage loads: thread t moves rows t/8 + 32j (j < 4), 16 B at column (t%8)*4 of each operand;
+  // rows past K / B are clamped (their results are masked later), so no load sits behind a
+  // runtime branch. Plain unrolled code (no captured arrays) keeps the staging in VGPRs.
+  const int srow = tid >> 3, scol = (tid & 7) * 4;
+  const float* ag = cb + (int64_t)min(n0 + srow, K - 1) * D + scol;
+  const float* xg = res + (int64_t)min(b0 + srow, B - 1) * D + scol;
+  int64_t aoff[4], xoff[4];
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    aoff[j] = (int64_t)(min(n0 + srow + 32 * j, K - 1) - min(n0 + srow, K - 1)) * D;
+    xoff[j] = (int64_t)(min(b0 + srow + 32 * j, B - 1) - min(b0 + srow, B - 1)) * D;
+  }
+  aoff[0] = xoff[0] = 0;
+  float* as_w = A_s + srow * kSLD + scol;
+  float* xs_w = X_s + srow * kSLD + scol;
+  float4 ra0, ra1, ra2, ra3, rx0, rx1, rx2, rx3;
+#define RQ_SPLIT_LOAD(k0)                                                        \
+  ra0 = *reinterpret_cast<const float4*>(ag + aoff[0] + (k0));                   \
+  ra1 = *reinterpret_cast<const float4*>(ag + aoff[1] + (k0));                   \
+  ra2 = *reinterpret_cast<const float4*>(ag + aoff[2] + (k0));                   \
+  ra3 = *reinterpret_cast<const float4*>(ag + aoff[3] + (k0));                   \
+  rx0 = *reinterpret_cast<const float4*>(xg + xoff[0] + (k0));                   \
+  rx1 = *reinterpret_cast<const float4*>(xg + xoff[1] + (k0));                   \
+  rx2 = *reinterpret_cast<const float4*>(xg + xoff[2] + (k0));                   \
+  rx3 = *reinterpret_cast<const float4*>(xg + xoff[3] + (k0));
+#define RQ_SPLIT_STASH()                                                         \
+  *reinterpret_cast<float4*>(as_w) = ra0;                                        \
+  *reinterpret_cast<float4*>(as_w + 32 * kSLD) = ra1;                            \
+  *reinterpret_cast<float4*>(as_w + 64 * kSLD) = ra2;                            \
+  *reinterpret_cast<float4*>(as_w + 96 * kSLD) = ra3;                            \
+  *reinterpret_cast<float4*>(xs_w) = rx0;                                        \
+  *reinterpret_cast<float4*>(xs_w + 32 * kSLD) = rx1;                            \
+  *reinterpret_cast<float4*>(xs_w + 64 * kSLD) = rx2;                            \
+  *reinterpret_cast<float4*>(xs_w + 96 * kSLD) = rx3;
+
+  RQ_SPLIT_LOAD(0)
+  if (tid < kSN) cs_s[tid] = csq[min(n0 + tid, K - 1)];
+  else xs_s[tid - kSN] = scratch[(int64_t)min(b0 + tid - kSN, B - 1) * D + 2 * nblk];
+  RQ_SPLIT_STASH()
+  __syncthreads();
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+
+  // lane half h supplies physical columns h*16 + s of each stage for logical k = h (same
+  // permutation for both operands: the dot products are unchanged)
+  const float* ap = A_s + (wr * 64 + c32) * kSLD + h * (kSK / 2);
+  const float* bp = X_s + (wc * 64 + c32) * kSLD + h * (kSK / 2);
+  for (int k0 = 0; k0 < D; k0 += kSK) {
+    {
+      const int kn = k0 + kSK < D ? k0 + kSK : k0;   // last stage: a harmless reload, no branch
+      RQ_SPLIT_LOAD(kn)                       // in flight under this stage's MFMAs
+    }
+    __builtin_amdgcn_sched_barrier(0);        // keep the loads ahead of the MFMAs (no sinking)
+#pragma unroll
+    for (int s4 = 0; s4 < kSK / 2; s4 += 4) {
+      const float4 a0 = *reinterpret_cast<const float4*>(ap + s4);
+      const float4 a1 = *reinterpret_cast<const float4*>(ap + 32 * kSLD + s4);
+      const float4 x0 = *reinterpret_cast<const float4*>(bp + s4);
+      const float4 x1 = *reinterpret_cast<const float4*>(bp + 32 * kSLD + s4);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, x0.x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, x1.x, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, x0.x, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, x1.x, acc[1][1], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, x0.y, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, x1.y, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, x0.y, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, x1.y, acc[1][1], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, x0.z, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, x1.z, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, x0.z, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, x1.z, acc[1][1], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, x0.w, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, x1.w, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, x0.w, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, x1.w, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();   // stage consumed
+    RQ_SPLIT_STASH()   // unconditional (last stage: a harmless rewrite) so the loads stay above the MFMAs
+    __syncthreads();
+  }
+#undef RQ_SPLIT_LOAD
+#undef RQ_SPLIT_STASH
+
+  // dist = (|x|^2 + |c|^2) - 2 x.c (quantize.py:108-112); C/D map: row = codeword, column = item.
+  // Each lane scans its codewords in increasing index order (strict '<' keeps the lowest).
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int jl = wc * 64 + c * 32 + c32;
+    const float xs = xs_s[jl];
+    float bd = INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int il = wr * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float d = (xs + cs_s[il]) - 2.f * acc[a][c][r];
+        d = n0 + il < K ? d : INFINITY;
+        const bool lt = d < bd;
+        bd = lt ? d : bd;
+        bi = lt ? n0 + il : bi;
+      }
+    const float od = __shfl_xor(bd, 32, 64);
+    const int oi = __shfl_xor(bi, 32, 64);
+    if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    if (wr == 1 && h == 0) { md_s[jl] = bd; mi_s[jl] = bi; }
+    __syncthreads();
+    if (wr == 0 && h == 0) {
+      const float od2 = md_s[jl];
+      const int oi2 = mi_s[jl];
+      if (od2 < bd || (od2 == bd && oi2 < bi)) { bd = od2; bi = oi2; }
+      const int b = b0 + jl;
+      if (b < B) *reinterpret_cast<float2*>(scratch + (int64_t)b * D + 2 * cbk) = make_float2(bd, __int_as_float(bi));
+    }
+  }
+}
+
+// Level-0 prologue of the split path: residuals[0] = x and |x|^2 into the level-0 scratch slot.
+template <int LPI, int EPL>
+__global__ void __launch_bounds__(256) rq_split_prep_kernel(const float* __restrict__ x, int B, int D, int nblk,
+                                                            float* __restrict__ res0, float* __restrict__ scratch0) {
+  constexpr int G = 64 / LPI;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPI, grp = lane / LPI;
+  const int b = (blockIdx.x * 4 + wave) * G + grp;
+  const bool valid = b < B;
+  const int64_t o = (int64_t)(valid ? b : B - 1) * D + sub * EPL;
+  float xv[EPL];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < EPL; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(x + o + k);
+    xv[k] = v.x; xv[k + 1] = v.y; xv[k + 2] = v.z; xv[k + 3] = v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) s += xv[k] * xv[k];
+  s = group_sum<LPI>(s);
+  if (valid) {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4)
+      *reinterpret_cast<float4*>(res0 + o + k) = make_float4(xv[k], xv[k + 1], xv[k + 2], xv[k + 3]);
+    if (sub == 0) scratch0[(int64_t)b * D + 2 * nblk] = s;
+  }
+}
+
+// Level-l epilogue of the split path (same row math as rq_fwd_kernel's epilogue).
+template <int LPI, int EPL>
+__global__ void __launch_bounds__(256) rq_level_epi_kernel(const float* __restrict__ res_l, const float* __restrict__ cb,
+                                                           int B, int D, int L, int l, int nblk, int mode, float beta,
+                                                           int64_t* __restrict__ ids, float* __restrict__ emb_out,
+                                                           float* __restrict__ res_next, float* __restrict__ qloss,
+                                                           float* __restrict__ emb_sum) {
+  constexpr int G = 64 / LPI;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPI, grp = lane / LPI;
+  const int b = (blockIdx.x * 4 + wave) * G + grp;
+  const bool valid = b < B;
+  const int64_t BD = (int64_t)B * D;
+  const int64_t o = (int64_t)(valid ? b : B - 1) * D + sub * EPL;
+  float* eo = emb_out + (int64_t)l * BD;
+  // merge the per-block partials of this item (read before the row is overwritten below)
+  float bd = INFINITY;
+  int bi = 0;
+  for (int p = sub; p < nblk; p += LPI) {
+    const float2 v = *reinterpret_cast<const float2*>(eo + (o - sub * EPL) + 2 * p);
+    const int vi = __float_as_int(v.y);
+    if (v.x < bd || (v.x == bd && vi < bi)) { bd = v.x; bi = vi; }
+  }
+#pragma unroll
+  for (int s = LPI / 2; s >= 1; s >>= 1) {
+    const float od = __shfl_xor(bd, s, 64);
+    const int oi = __shfl_xor(bi, s, 64);
+    if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+  }
+  const int id = bi;
+  const float* cr = cb + (int64_t)id * D + sub * EPL;
+  float xv[EPL], ev[EPL], out[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; k += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(res_l + o + k);
+    const float4 c = *reinterpret_cast<const float4*>(cr + k);
+    xv[k] = a.x; xv[k + 1] = a.y; xv[k + 2] = a.z; xv[k + 3] = a.w;
+    ev[k] = c.x; ev[k + 1] = c.y; ev[k + 2] = c.z; ev[k + 3] = c.w;
+  }
+  float dl = 0.f;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) { const float t = xv[k] - ev[k]; dl += t * t; }
+  dl = group_sum<LPI>(dl);
+  if (mode == kRotation) {
+    float x2 = 0.f, e2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) { x2 += xv[k] * xv[k]; e2 += ev[k] * ev[k]; }
+    x2 = group_sum<LPI>(x2);
+    e2 = group_sum<LPI>(e2);
+    RowRot<LPI, EPL> rot;
+    rot.build(xv, ev, sqrtf(x2), sqrtf(e2));
+    float ew = 0.f, eu = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) { ew += xv[k] * rot.w[k]; eu += xv[k] * rot.u[k]; }
+    ew = group_sum<LPI>(ew);
+    eu = group_sum<LPI>(eu);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) out[k] = ((xv[k] - 2.f * (ew * rot.w[k])) + 2.f * (eu * rot.q[k])) * rot.lam;
+  } else if (mode == kSte) {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) out[k] = xv[k] + (ev[k] - xv[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) out[k] = ev[k];
+  }
+  float r2 = 0.f;
+  float nr[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) { nr[k] = xv[k] - out[k]; r2 += nr[k] * nr[k]; }
+  r2 = group_sum<LPI>(r2);
+  if (!valid) return;
+#pragma unroll
+  for (int k = 0; k < EPL; k += 4) {
+    *reinterpret_cast<float4*>(eo + o + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+    if (res_next != nullptr)
+      *reinterpret_cast<float4*>(res_next + o + k) = make_float4(nr[k], nr[k + 1], nr[k + 2], nr[k + 3]);
+  }
+  if (emb_sum != nullptr && l == L - 1) {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      float4 s = *reinterpret_cast<const float4*>(emb_out + o + k);
+      for (int m = 1; m < L; ++m) {
+        const float4 v = (m == l) ? make_float4(out[k], out[k + 1], out[k + 2], out[k + 3])
+                                  : *reinterpret_cast<const float4*>(emb_out + (int64_t)m * BD + o + k);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      if (L == 1) s = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+      *reinterpret_cast<float4*>(emb_sum + o + k) = s;
+    }
+  }
+  if (sub == 0) {
+    ids[(int64_t)b * L + l] = id;
+    const float lq = dl + beta * dl;
+    qloss[b] = l == 0 ? 0.f + lq : qloss[b] + lq;
+    if (l + 1 < L) emb_out[(int64_t)(l + 1) * BD + (int64_t)b * D + 2 * nblk] = r2;   // next level's |res|^2
+  }
+}
+
+template <int LPI, int EPL>
+static void launch_split(int B, hipStream_t s, const float* x, int D, const float* cbs, const float* csq, int K, int L,
+                         int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
+  constexpr int G = 64 / LPI;
+  const int nblk = (K + kSN - 1) / kSN, tilesB = (B + kSB - 1) / kSB;
+  const int64_t BD = (int64_t)B * D;
+  const dim3 gr((B + 4 * G - 1) / (4 * G));
+  hipLaunchKernelGGL((rq_split_prep_kernel<LPI, EPL>), gr, dim3(256), 0, s, x, B, D, nblk, res, eo);
+  for (int l = 0; l < L; ++l) {
+    hipLaunchKernelGGL(rq_dist_argmin_kernel, dim3(tilesB * nblk), dim3(256), 0, s, res + l * BD, cbs + (int64_t)l * K * D,
+                       csq + (int64_t)l * K, B, D, K, nblk, tilesB, eo + l * BD);
+    hipLaunchKernelGGL((rq_level_epi_kernel<LPI, EPL>), gr, dim3(256), 0, s, res + l * BD, cbs + (int64_t)l * K * D, B,
+                       D, L, l, nblk, mode, beta, ids, eo, l + 1 < L ? res + (l + 1) * BD : nullptr, ql, es);
+  }
+}
+
 __global__ void __launch_bounds__(256) segment_counts_kernel(const int* __restrict__ key_off, int K,
                                                              int64_t* __restrict__ counts) {
   const int k = blockIdx.x * 256 + threadIdx.x;
@@ -880,9 +1180,25 @@ int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* code
   hipStream_t s = (hipStream_t)stream;
   dim3 g((unsigned)((B + kTB - 1) / kTB));
   const int b = (int)B, d = (int)D, k = (int)K, l = (int)L;
-  RQ_CHECK_ARG(impl >= 0 && impl <= 2, "rq_quantize_fwd_impl: impl must be 0 (auto), 1 (tiled) or 2 (register)");
-  if (impl == 0) impl = D <= 64 ? 2 : 1;
-  RQ_CHECK_ARG(impl == 1 || D <= 64, "rq_quantize_fwd_impl: register kernel needs D <= 64");
+  RQ_CHECK_ARG(impl >= 0 && impl <= 3,
+               "rq_quantize_fwd_impl: impl must be 0 (auto), 1 (tiled), 2 (register) or 3 (split)");
+  const bool split_ok = D >= 128 && 2 * ((K + kSN - 1) / kSN) + 1 <= D;
+  if (impl == 0) impl = D <= 64 ? 2 : (split_ok ? 3 : 1);
+  RQ_CHECK_ARG(impl != 2 || D <= 64, "rq_quantize_fwd_impl: register kernel needs D <= 64");
+  RQ_CHECK_ARG(impl != 3 || split_ok, "rq_quantize_fwd_impl: split path needs D >= 128 and 2*ceil(K/128)+1 <= D");
+  if (impl == 3) {
+    switch (D) {
+#define RQ_SPLIT_CASE(DD, LPI, EPL) \
+  case DD: launch_split<LPI, EPL>(b, s, x, d, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;
+      RQ_SPLIT_CASE(128, 32, 4)
+      RQ_SPLIT_CASE(256, 64, 4)
+      RQ_SPLIT_CASE(512, 64, 8)
+      RQ_SPLIT_CASE(1024, 64, 16)
+#undef RQ_SPLIT_CASE
+    }
+    RQ_LAUNCH_CHECK("rq_quantize_fwd(split)");
+    return 0;
+  }
   if (impl == 2) {
     switch (D) {
       case 8: launch_fwd_reg<8>(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum); break;

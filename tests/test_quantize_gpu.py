@@ -216,3 +216,38 @@ def test_tiled_and_register_kernels_agree(device, B, D, K, L):
         _close(o["emb"][:, ok], f["emb"][:, ok], 1e-4, 1e-5, f"impl{impl} emb")
         _close(o["ql"][ok], f["qloss"][ok], 1e-4, 1e-6, f"impl{impl} qloss")
         assert np.array_equal(o["res"][0], x)
+
+
+@pytest.mark.parametrize("B,D,K,L", [(1000, 128, 300, 2), (4097, 256, 2048, 3), (300, 1024, 2048, 4),
+                                     (2000, 512, 1000, 3), (1, 1024, 129, 2)])
+@pytest.mark.parametrize("mode", [0, 2, 3])
+def test_split_path_vs_oracle(device, B, D, K, L, mode):
+    """Split path (impl 3: per-level distance GEMM + partial argmin over 128x128 tiles, then the row
+    epilogue) against the oracle and the fused tiled kernel (impl 1), ragged B and K included."""
+    from rqvae_hip._lib import call, ptr, stream_handle
+    g = gi.rng(B + 7 * D + K + mode)
+    x = (g.standard_normal((B, D), dtype=np.float32) / np.sqrt(D)).astype(np.float32)
+    cbs = (g.standard_normal((L, K, D), dtype=np.float32) / np.sqrt(D)).astype(np.float32)
+    f = Q.rq_fwd(x, cbs, mode)
+    xt, ct = torch.from_numpy(x).to(device), torch.from_numpy(cbs).to(device)
+    csq = (ct * ct).sum(-1).contiguous()
+    outs = {}
+    for impl in (1, 3):
+        o = dict(ids=torch.empty(B, L, dtype=torch.int64, device=device), emb=torch.empty(L, B, D, device=device),
+                 res=torch.empty(L, B, D, device=device), ql=torch.empty(B, device=device),
+                 es=torch.empty(B, D, device=device))
+        call("rq_quantize_fwd_impl", ptr(xt), B, D, ptr(ct), ptr(csq), K, L, mode, 0.25, ptr(o["ids"]), ptr(o["emb"]),
+             ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle(device))
+        outs[impl] = {k: v.cpu().numpy() for k, v in o.items()}
+    o = outs[3]
+    ok = (o["ids"] == f["ids"]).all(1)
+    assert ok.mean() > 0.998, ok.mean()
+    _close(o["emb"][:, ok], f["emb"][:, ok], 1e-4, 1e-5, "split emb")
+    _close(o["ql"][ok], f["qloss"][ok], 1e-4, 1e-6, "split qloss")
+    assert np.array_equal(o["res"][0], x)
+    for l in range(L - 1):   # residual chain identity, bit-exact
+        assert np.array_equal(o["res"][l + 1], (o["res"][l] - o["emb"][l]).astype(np.float32))
+    _close(o["es"], o["emb"].sum(0), 1e-6, 1e-6, "emb_sum")
+    same = (o["ids"] == outs[1]["ids"]).all(1)
+    assert same.mean() > 0.998
+    _close(o["emb"][:, same], outs[1]["emb"][:, same], 1e-5, 1e-6, "split vs tiled emb")

@@ -68,10 +68,10 @@ def main():
                                           median_ms=med, tflops=2.0 * K * D * L * B / (med * 1e-3) / 1e12)), flush=True)
         return
     shapes = [(65536, 64, 256, 3), (65536, 32, 256, 3), (262144, 64, 256, 3), (64, 64, 256, 3),
-              (16384, 1024, 2048, 4)]
+              (16384, 1024, 2048, 4), (65536, 1024, 2048, 4), (65536, 256, 1024, 3)]
     for (B, D, K, L) in shapes:
         x, cbs, csq, o = quantize_case(B, D, K, L, dev)
-        impls = [1, 2] if D <= 64 else [1]
+        impls = [1, 2] if D <= 64 else [1, 3]
         ref = None
         for impl in impls:
             run_impl(x, cbs, csq, o, impl)
