@@ -92,6 +92,30 @@ size_t rq_rmsnorm_bwd_workspace(int64_t B, int64_t D);
 int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
                    float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream);
 
+/* RMSNorm followed by nn.Dropout(p) (modules/transformer/model.py:71,74 `self.do(self.attn_norm(x))`,
+ * modules/model.py:128-129 `self.do(self.norm(...))`): y = keep * scale * rmsnorm(x), keep drawn from
+ * a counter-based generator keyed by `seed` (element e of y keeps iff word e of SplitMix64(seed) >=
+ * round(p 2^32); kept values scaled by 1/(1-p)), so the backward regenerates the mask from
+ * (seed, e) instead of storing it. p = 0 is plain RMSNorm. */
+int rq_rmsnorm_dropout_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float p, uint64_t seed,
+                           float* y, float* rstd, void* stream);
+int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
+                           float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
+                           void* stream);
+
+/* Elementwise dropout fusions over n fp32 elements (n % 4 == 0, 16-byte aligned), same mask
+ * generator as above (element index = position in the buffer):
+ *   rq_silu_dropout_fwd  h = Dropout(SiLU(z))         the MLP hidden layer (modules/encoder.py:20-28)
+ *   rq_silu_dropout_bwd  gz = SiLU'(z) * keep * scale * g
+ *   rq_dropout_add_fwd   out = h + Dropout(y)          the block output (modules/transformer/model.py:82)
+ *   rq_dropout_bwd       gy = keep * scale * g         (grad of y; h's grad is g itself)
+ * rq_dropout_params returns the (threshold, scale) pair the kernels use for p. */
+int rq_dropout_params(float p, uint32_t* thr, float* scale);
+int rq_silu_dropout_fwd(const float* z, int64_t n, float p, uint64_t seed, float* h, void* stream);
+int rq_silu_dropout_bwd(const float* g, const float* z, int64_t n, float p, uint64_t seed, float* gz, void* stream);
+int rq_dropout_add_fwd(const float* h, const float* y, int64_t n, float p, uint64_t seed, float* out, void* stream);
+int rq_dropout_bwd(const float* g, int64_t n, float p, uint64_t seed, float* gy, void* stream);
+
 /* Weight / bias gradient of a Linear layer over a large batch: dW (O,I) = g^T x, db (O,) = sum_b g
  * (or NULL). g: (Bn, O) rows of stride ldg, x: (Bn, I) rows of stride ldx, fp32, O, I, ld % 4 == 0,
  * 16-byte aligned. Replaces torch autograd's grad_weight = grad_out^T @ input for the nn.Linear

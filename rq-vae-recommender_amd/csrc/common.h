@@ -70,4 +70,36 @@ __device__ __forceinline__ bool div_rn_ok(float min_abs, float max_abs, float b)
   return min_abs >= 0x1p-90f && max_abs <= 0x1p90f && b >= 0x1p-60f && b <= 0x1p60f;
 }
 
+// Counter-based dropout mask (stateless, so a backward kernel regenerates the forward's mask from
+// (seed, element index) instead of storing it). SplitMix64 output for counter c under key seed;
+// element e = 4q + j of a tensor draws 32-bit word j of (mix(2q), mix(2q + 1)) and is kept iff
+// word >= thr, thr = round(p * 2^32), i.e. with probability 1 - p (nn.Dropout semantics, kept
+// values scaled by 1 / (1 - p)). thr == 0 means no dropout.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t c) {
+  uint64_t z = seed + (c + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// thr / scale of nn.Dropout(p) for the kernels below (dropout.hip).
+void dropout_params(float p, uint32_t* thr, float* scale);
+struct Keep4 {
+  bool k[4];
+};
+__device__ __forceinline__ Keep4 keep4(uint64_t seed, uint64_t q, uint32_t thr) {
+  const uint64_t a = splitmix64(seed, 2 * q), b = splitmix64(seed, 2 * q + 1);
+  Keep4 r;
+  r.k[0] = (uint32_t)a >= thr;
+  r.k[1] = (uint32_t)(a >> 32) >= thr;
+  r.k[2] = (uint32_t)b >= thr;
+  r.k[3] = (uint32_t)(b >> 32) >= thr;
+  return r;
+}
+__device__ __forceinline__ float4 drop4(float4 v, uint64_t seed, uint64_t q, uint32_t thr, float scale) {
+  if (thr == 0) return v;
+  const Keep4 m = keep4(seed, q, thr);
+  return make_float4(m.k[0] ? v.x * scale : 0.f, m.k[1] ? v.y * scale : 0.f, m.k[2] ? v.z * scale : 0.f,
+                     m.k[3] ? v.w * scale : 0.f);
+}
+
 }  // namespace rqhip

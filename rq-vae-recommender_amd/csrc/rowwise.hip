@@ -95,11 +95,12 @@ __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __re
 // fwd: one wave per row, saves rstd. bwd: gx = r (w gy) - x (r^3 / D) sum_j (w gy x)_j per row;
 // gw = sum_b gy_b t_b reduced deterministically: each 4-wave workgroup owns kRmsRows rows and writes
 // a [D] partial (waves combined in order through LDS), rms_reduce_kernel sums partials in order.
-constexpr int kRmsRows = 64;
+constexpr int kRmsRows = 16;   // rows per workgroup: T=11.6k decoder rows -> 725 workgroups
 
 template <int VPL>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                          int64_t B, int D, float eps, float* __restrict__ y,
+                                                          int64_t B, int D, float eps, uint32_t thr, float dscale,
+                                                          uint64_t seed, float* __restrict__ y,
                                                           float* __restrict__ rstd) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -124,7 +125,8 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restric
     if (c >= D) continue;
     const float4 wv = *reinterpret_cast<const float4*>(w + c);
     *reinterpret_cast<float4*>(y + r * D + c) =
-        make_float4((xv[v].x * rs) * wv.x, (xv[v].y * rs) * wv.y, (xv[v].z * rs) * wv.z, (xv[v].w * rs) * wv.w);
+        drop4(make_float4((xv[v].x * rs) * wv.x, (xv[v].y * rs) * wv.y, (xv[v].z * rs) * wv.z, (xv[v].w * rs) * wv.w),
+              seed, (uint64_t)(r * D + c) / 4, thr, dscale);
   }
   if (lane == 0) rstd[r] = rs;
 }
@@ -132,8 +134,8 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restric
 template <int VPL>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ rstd, const float* __restrict__ gy,
-                                                          int64_t B, int D, float* __restrict__ gx,
-                                                          float* __restrict__ gw_part) {
+                                                          int64_t B, int D, uint32_t thr, float dscale, uint64_t seed,
+                                                          float* __restrict__ gx, float* __restrict__ gw_part) {
   __shared__ float4 part[4][VPL * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float4 wv[VPL], gwa[VPL];
@@ -155,7 +157,9 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
       const int c = (v * 64 + lane) * 4;
       const bool ok = c < D;
       xv[v] = ok ? *reinterpret_cast<const float4*>(x + r * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 g = ok ? *reinterpret_cast<const float4*>(gy + r * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g = ok ? drop4(*reinterpret_cast<const float4*>(gy + r * D + c), seed, (uint64_t)(r * D + c) / 4, thr,
+                                  dscale)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
       gt[v] = make_float4(wv[v].x * g.x, wv[v].y * g.y, wv[v].z * g.z, wv[v].w * g.w);
       dot = __builtin_fmaf(gt[v].x, xv[v].x, dot);
       dot = __builtin_fmaf(gt[v].y, xv[v].y, dot);
@@ -196,36 +200,37 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
   }
 }
 
-// out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): 64 float4 columns per workgroup,
-// wave q sums s = q, q+4, ..., the four wave partials are added in order through LDS.
+// out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): a workgroup owns 16 float4 columns;
+// its 16 row lanes q sum s = q, q+16, ... (4 loads in flight), then the 16 partials are added in q
+// order through LDS. Deterministic, no atomics; D/64 workgroups of long independent sums.
 __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict__ P, int S, int64_t n,
                                                          float* __restrict__ out) {
-  __shared__ float4 red[4][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t j = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  __shared__ float4 red[16][16];
+  const int c = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const int64_t j = ((int64_t)blockIdx.x * 16 + c) * 4;
   const bool ok = j < n;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
-    int s = wave;
-    for (; s + 12 < S; s += 16) {
+    int s = q;
+    for (; s + 48 < S; s += 64) {
       float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 16 * u) * n + j);
 #pragma unroll
       for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
     }
-    for (; s < S; s += 4) {
+    for (; s < S; s += 16) {
       const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
   }
-  red[wave][lane] = a;
+  red[q][c] = a;
   __syncthreads();
-  if (wave == 0 && ok) {
-    float4 r = red[0][lane];
+  if (q == 0 && ok) {
+    float4 r = red[0][c];
 #pragma unroll
-    for (int q = 1; q < 4; ++q) {
-      const float4 v = red[q][lane];
+    for (int w = 1; w < 16; ++w) {
+      const float4 v = red[w][c];
       r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
     *reinterpret_cast<float4*>(out + j) = r;
@@ -288,22 +293,31 @@ size_t rq_rmsnorm_bwd_workspace(int64_t B, int64_t D) {
     case 15: LAUNCH(15) break; case 16: LAUNCH(16) break;                                                 \
   }
 
-int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float* y, float* rstd,
-                   void* stream) {
+int rq_rmsnorm_dropout_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float p, uint64_t seed,
+                           float* y, float* rstd, void* stream) {
   RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_fwd: need D %% 4 == 0, D <= 4096");
   if (B == 0) return 0;
   RQ_CHECK_ARG(x && w && y && rstd, "rq_rmsnorm_fwd: null pointer");
+  uint32_t thr;
+  float dscale;
+  dropout_params(p, &thr, &dscale);
   dim3 g((unsigned)((B + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
-#define RMS_F(V) hipLaunchKernelGGL((rmsnorm_fwd_kernel<V>), g, dim3(256), 0, s, x, w, B, (int)D, eps, y, rstd);
+#define RMS_F(V) hipLaunchKernelGGL((rmsnorm_fwd_kernel<V>), g, dim3(256), 0, s, x, w, B, (int)D, eps, thr, dscale, seed, y, rstd);
   RMS_SWITCH((int)((D + 255) / 256), RMS_F)
 #undef RMS_F
   RQ_LAUNCH_CHECK("rq_rmsnorm_fwd");
   return 0;
 }
 
-int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
-                   float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream) {
+int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float* y, float* rstd,
+                   void* stream) {
+  return rq_rmsnorm_dropout_fwd(x, w, B, D, eps, 0.f, 0, y, rstd, stream);
+}
+
+int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
+                           float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
+                           void* stream) {
   RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_bwd: need D %% 4 == 0, D <= 4096");
   RQ_CHECK_ARG(gw && (B == 0 || (x && w && rstd && gy && gx)), "rq_rmsnorm_bwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
@@ -312,15 +326,23 @@ int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const floa
     return 0;
   }
   RQ_CHECK_ARG(workspace && ws_bytes >= rq_rmsnorm_bwd_workspace(B, D), "rq_rmsnorm_bwd: workspace too small");
+  uint32_t thr;
+  float dscale;
+  dropout_params(p, &thr, &dscale);
   float* part = static_cast<float*>(workspace);
   const int nblk = (int)((B + kRmsRows - 1) / kRmsRows);
-#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, gx, part);
+#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, thr, dscale, seed, gx, part);
   RMS_SWITCH((int)((D + 255) / 256), RMS_B)
 #undef RMS_B
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd");
-  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + 63) / 64)), dim3(256), 0, s, part, nblk, D, gw);
+  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + 15) / 16)), dim3(256), 0, s, part, nblk, D, gw);
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd(reduce)");
   return 0;
+}
+
+int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
+                   float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream) {
+  return rq_rmsnorm_dropout_bwd(x, w, rstd, gy, B, D, 0.f, 0, gx, gw, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

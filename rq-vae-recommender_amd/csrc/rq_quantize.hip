@@ -392,7 +392,7 @@ rq_bwd_rows_kernel(const float* __restrict__ res, const int64_t* __restrict__ id
 // Stable counting sort of ids per level (keys < K <= 4096) -> perm (rows grouped by codeword,
 // ascending row index inside a codeword): per-block histograms hist[l][blk][k] (key fastest,
 // coalesced), a per-key scan over blocks, an exclusive scan over keys, then an in-order scatter
-// with ballot ranks. Deterministic by construction (no atomics decide any order).
+// (per-block LDS bitonic sort of (key, row) pairs). Deterministic by construction (no atomics decide any order).
 constexpr int kSortRows = 256;   // rows per sort block
 
 __global__ void __launch_bounds__(256) sort_hist_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
@@ -402,7 +402,10 @@ __global__ void __launch_bounds__(256) sort_hist_kernel(const int64_t* __restric
   for (int k = threadIdx.x; k < K; k += 256) cnt[k] = 0;
   __syncthreads();
   const int r = blk * kSortRows + threadIdx.x;
-  if (r < B) atomicAdd(&cnt[(int)ids[(int64_t)r * L + l]], 1);   // counts only: order-free
+  if (r < B) {
+    const int64_t key = ids[(int64_t)r * L + l];
+    if (key >= 0 && key < K) atomicAdd(&cnt[(int)key], 1);   // counts only: order-free; bad keys dropped
+  }
   __syncthreads();
   int* h = hist + ((int64_t)l * nblk + blk) * K;
   for (int k = threadIdx.x; k < K; k += 256) h[k] = cnt[k];
@@ -446,89 +449,145 @@ __global__ void __launch_bounds__(1024) sort_offsets_kernel(int* __restrict__ ke
   }
   int run = part[t] - s;
   for (int i = a; i < e; ++i) { const int c = ko[i]; ko[i] = run; run += c; }
-  if (t == 0) ko[K] = B;
+  if (t == 1023) ko[K] = part[1023];   // rows placed (B unless out-of-range keys were dropped)
 }
 
-__global__ void __launch_bounds__(64) sort_scatter_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
-                                                          int nblk, const int* __restrict__ hist,
-                                                          const int* __restrict__ key_off, int* __restrict__ perm) {
-  extern __shared__ int base[];
-  const int l = blockIdx.y, blk = blockIdx.x, lane = threadIdx.x;
+// Stable placement of one block's 256 rows: a bitonic sort of (key << 8 | row-in-block) in LDS
+// orders the rows by key then row index; a row's rank inside its key run is its sorted position
+// minus the run's first position. 36 compare-exchange stages, no per-key serial loop.
+__global__ void __launch_bounds__(256) sort_scatter_kernel(const int64_t* __restrict__ ids, int B, int L, int K,
+                                                           int nblk, const int* __restrict__ hist,
+                                                           const int* __restrict__ key_off, int* __restrict__ perm) {
+  extern __shared__ int sm[];
+  int* base = sm;                                          // [K] first output slot of key k for this block
+  int* first = sm + K;                                     // [K] sorted position where key k's run starts
+  unsigned* sk = reinterpret_cast<unsigned*>(sm + 2 * K);  // [256]
+  const int l = blockIdx.y, blk = blockIdx.x, t = threadIdx.x;
   const int* h = hist + ((int64_t)l * nblk + blk) * K;
   const int* ko = key_off + (int64_t)l * (K + 1);
-  for (int k = lane; k < K; k += 64) base[k] = ko[k] + h[k];
+  for (int k = t; k < K; k += 256) base[k] = ko[k] + h[k];
+  const int r = blk * kSortRows + t;
+  const int64_t k64 = r < B ? ids[(int64_t)r * L + l] : -1;
+  const bool valid = k64 >= 0 && k64 < K;   // rows with out-of-range keys are not placed
+  sk[t] = valid ? ((unsigned)k64 << 8) | (unsigned)t : 0xFFFFFFFFu;
   __syncthreads();
-  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int c = 0; c < kSortRows; c += 64) {
-    const int r = blk * kSortRows + c + lane;
-    const bool v = r < B;
-    const int key = v ? (int)ids[(int64_t)r * L + l] : -1;
-    unsigned long long rem = __ballot(v);
-    while (rem) {
-      const int leader = __builtin_ctzll(rem);
-      const int k = __shfl(key, leader, 64);
-      const unsigned long long m = __ballot(v && key == k) & rem;
-      if (v && key == k) perm[(int64_t)l * B + base[k] + __popcll(m & lt)] = r;
-      __syncthreads();   // single wave: the LDS read above retires before the update below
-      if (lane == leader) base[k] += __popcll(m);
+  for (int size = 2; size <= kSortRows; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int j = t ^ stride;
+      if (j > t) {
+        const unsigned a = sk[t], b = sk[j];
+        if ((a > b) == ((t & size) == 0)) { sk[t] = b; sk[j] = a; }
+      }
       __syncthreads();
-      rem &= ~m;
     }
   }
+  const unsigned v = sk[t];
+  const bool placed = v != 0xFFFFFFFFu;
+  const int key = (int)(v >> 8);
+  if (placed && (t == 0 || (sk[t - 1] >> 8) != (unsigned)key)) first[key] = t;
+  __syncthreads();
+  if (placed) perm[(int64_t)l * B + base[key] + (t - first[key])] = blk * kSortRows + (int)(v & 255u);
 }
 
 // grad_cb[l][k] = sum over the rows b of codeword k of c_b, with
 //   c_b = (2 gl_b) (e_k - x_b)            (rotation / STE: recomputed from residuals, no buffer)
-//   c_b = contrib[l][b]                   (eval mode: includes the emb_out gradient)
-// One workgroup (4 waves) per codeword; wave w reduces the w-th contiguous quarter of the
-// segment, RPW rows per wave-step when D < 64; partials are combined in a fixed order.
+//   c_b = contrib[l][b]                   (eval mode / generic segment sum: the given rows)
+// Workgroup (k, g, l), 4 waves: a segment of at most kSegDirect rows is reduced entirely by g = 0
+// and written to grad_cb; a longer one (e.g. the dedup-column token every item shares) is cut into
+// kSegSplit contiguous parts whose partial sums go to scratch[g][l][k] and rq_segsum_finalize adds
+// them in g order. Inside a workgroup wave w reduces the w-th contiguous quarter of its rows, lanes
+// hold float4 columns (RPW rows per wave-step when D < 256), partials combine in a fixed order:
+// bitwise deterministic for any placement.
+constexpr int kSegSplit = 8;
+constexpr int kSegDirect = 256;
+
 __global__ void __launch_bounds__(256) rq_cb_segsum_kernel(const float* __restrict__ res, const float* __restrict__ cbs,
                                                            const float* __restrict__ g_qloss,
                                                            const float* __restrict__ contrib, const int* __restrict__ perm,
                                                            const int* __restrict__ key_off, int B, int D, int K,
-                                                           float* __restrict__ grad_cb) {
-  __shared__ float part[4 * 1024];
-  const int k = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int a = key_off[(int64_t)l * (K + 1) + k], e = key_off[(int64_t)l * (K + 1) + k + 1];
+                                                           float* __restrict__ grad_cb, float* __restrict__ scratch) {
+  __shared__ float4 part[4 * 64];
+  const int k = blockIdx.x, g = blockIdx.y, l = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int L = gridDim.z;
+  const int a0 = key_off[(int64_t)l * (K + 1) + k], e0 = key_off[(int64_t)l * (K + 1) + k + 1];
+  const int n0 = e0 - a0;
+  const bool direct = n0 <= kSegDirect;
+  if (direct && g > 0) return;
+  const int a = direct ? a0 : a0 + (int)((int64_t)n0 * g / kSegSplit);
+  const int e = direct ? e0 : a0 + (int)((int64_t)n0 * (g + 1) / kSegSplit);
   const int n = e - a, q = (n + 3) / 4;
   const int wa = a + min(n, wave * q), we = a + min(n, (wave + 1) * q);
   const int* p = perm + (int64_t)l * B;
   const int64_t BD = (int64_t)B * D;
   const float* xb = contrib ? contrib + (int64_t)l * BD : res + (int64_t)l * BD;
-  const float* ek = cbs + ((int64_t)l * K + k) * D;
-  const int cpw = D < 64 ? D : 64, rpw = 64 / cpw;
-  const int rs = lane / cpw, dl = lane % cpw;
-  for (int d0 = 0; d0 < D; d0 += 64) {
-    const int d = d0 + dl;
-    const float e_d = (contrib || d >= D) ? 0.f : ek[d];
-    float acc = 0.f;
+  const float* ek = cbs ? cbs + ((int64_t)l * K + k) * D : nullptr;
+  float* dst = direct ? grad_cb + ((int64_t)l * K + k) * D : scratch + (((int64_t)g * L + l) * K + k) * D;
+  const int D4 = D / 4;
+  const int cpw = D4 < 64 ? D4 : 64, rpw = 64 / cpw;
+  const int rs = lane / cpw, c4 = lane % cpw;
+  for (int d0 = 0; d0 < D4; d0 += 64) {
+    const int d = d0 + c4;
+    const bool dok = d < D4;
+    const float4 e_d = (contrib || !dok) ? make_float4(0.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4*>(ek)[d];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int i = wa + rs;
-    for (; i + 3 * rpw < we; i += 4 * rpw) {
-      int rr[4];
-      float v[4], g[4];
+    for (; i + 7 * rpw < we; i += 8 * rpw) {
+      int rr[8];
+      float4 v[8];
+      float gg[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) rr[u] = p[i + u * rpw];
+      for (int u = 0; u < 8; ++u) rr[u] = p[i + u * rpw];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[u] = xb[(int64_t)rr[u] * D + d];
-        g[u] = contrib ? 1.f : (g_qloss ? g_qloss[rr[u]] : 0.f);
+      for (int u = 0; u < 8; ++u) {
+        v[u] = dok ? reinterpret_cast<const float4*>(xb + (int64_t)rr[u] * D)[d] : make_float4(0.f, 0.f, 0.f, 0.f);
+        gg[u] = contrib ? 1.f : 2.f * (g_qloss ? g_qloss[rr[u]] : 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc += contrib ? v[u] : (2.f * g[u]) * (e_d - v[u]);
+      for (int u = 0; u < 8; ++u) {
+        if (contrib) {
+          acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+        } else {
+          acc.x += gg[u] * (e_d.x - v[u].x); acc.y += gg[u] * (e_d.y - v[u].y);
+          acc.z += gg[u] * (e_d.z - v[u].z); acc.w += gg[u] * (e_d.w - v[u].w);
+        }
+      }
     }
     for (; i < we; i += rpw) {
       const int r = p[i];
-      const float v = xb[(int64_t)r * D + d];
-      acc += contrib ? v : (2.f * (g_qloss ? g_qloss[r] : 0.f)) * (e_d - v);
+      const float4 v = dok ? reinterpret_cast<const float4*>(xb + (int64_t)r * D)[d] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (contrib) {
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      } else {
+        const float gr = 2.f * (g_qloss ? g_qloss[r] : 0.f);
+        acc.x += gr * (e_d.x - v.x); acc.y += gr * (e_d.y - v.y); acc.z += gr * (e_d.z - v.z); acc.w += gr * (e_d.w - v.w);
+      }
     }
-    part[(wave * rpw + rs) * 64 + dl] = acc;
+    part[(wave * rpw + rs) * cpw + c4] = acc;
     __syncthreads();
-    if (tid < cpw) {
-      float s = 0.f;
-      for (int j = 0; j < 4 * rpw; ++j) s += part[j * 64 + tid];
-      grad_cb[((int64_t)l * K + k) * D + d0 + tid] = s;
+    if (tid < cpw && d0 + tid < D4) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = 0; j < 4 * rpw; ++j) {
+        const float4 v = part[j * cpw + tid];
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+      }
+      reinterpret_cast<float4*>(dst)[d0 + tid] = t;
     }
     __syncthreads();
+  }
+}
+
+// Heavy segments: grad_cb[l][k] = sum_g scratch[g][l][k] in g order.
+__global__ void __launch_bounds__(256) rq_segsum_finalize_kernel(const int* __restrict__ key_off, int D, int K,
+                                                                 const float* __restrict__ scratch,
+                                                                 float* __restrict__ grad_cb) {
+  const int k = blockIdx.x, l = blockIdx.y, L = gridDim.y;
+  const int n = key_off[(int64_t)l * (K + 1) + k + 1] - key_off[(int64_t)l * (K + 1) + k];
+  if (n <= kSegDirect) return;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < kSegSplit; ++g) s += scratch[(((int64_t)g * L + l) * K + k) * D + d];
+    grad_cb[((int64_t)l * K + k) * D + d] = s;
   }
 }
 
@@ -1234,6 +1293,7 @@ size_t rq_quantize_bwd_workspace(int64_t B, int64_t D, int64_t K, int64_t L) {
   bytes += (size_t)(L * K * nblk) * sizeof(int);         // hist / scanned positions
   bytes += (size_t)(L * (K + 1)) * sizeof(int);          // key offsets
   bytes += (size_t)(L * B) * sizeof(int);                // perm
+  bytes += (size_t)(kSegSplit * L * K * D) * sizeof(float);   // heavy-segment partials
   return bytes + 256;
 }
 
@@ -1255,7 +1315,8 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   float* contrib = (float*)w; w += (size_t)(L * B * D) * sizeof(float);
   int* hist = (int*)w;        w += (size_t)(L * K * nblk) * sizeof(int);
   int* key_off = (int*)w;     w += (size_t)(L * (K + 1)) * sizeof(int);
-  int* perm = (int*)w;
+  int* perm = (int*)w;        w += (size_t)(L * B) * sizeof(int);
+  float* segs = (float*)(((uintptr_t)w + 15) & ~(uintptr_t)15);
   if (B == 0) {
     RQ_HIP(hipMemsetAsync(grad_codebooks, 0, (size_t)(L * K * D) * sizeof(float), s));
     return 0;
@@ -1278,10 +1339,11 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, l), dim3(256), k * sizeof(int), s, ids, b, l, k, nblk, hist);
   hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 255) / 256, l), dim3(256), 0, s, hist, k, nblk, key_off);
   hipLaunchKernelGGL(sort_offsets_kernel, dim3(l), dim3(1024), 0, s, key_off, k, b);
-  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, l), dim3(64), k * sizeof(int), s, ids, b, l, k, nblk, hist, key_off,
-                     perm);
-  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, l), dim3(256), 0, s, residuals, codebooks, g_qloss,
-                     mode == kEval ? contrib : nullptr, perm, key_off, b, d, k, grad_codebooks);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, l), dim3(256), (2 * k + kSortRows) * sizeof(int), s, ids, b, l, k,
+                     nblk, hist, key_off, perm);
+  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, kSegSplit, l), dim3(256), 0, s, residuals, codebooks, g_qloss,
+                     mode == kEval ? contrib : nullptr, perm, key_off, b, d, k, grad_codebooks, segs);
+  hipLaunchKernelGGL(rq_segsum_finalize_kernel, dim3(k, l), dim3(256), 0, s, key_off, d, k, segs, grad_codebooks);
   RQ_LAUNCH_CHECK("rq_codebook_grad");
   return 0;
 }
@@ -1291,13 +1353,15 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
 // out[k] = sum of rows[b] over b with keys[b] == k (fixed reduction order), counts[k] = #rows.
 size_t rq_segment_sum_workspace(int64_t B, int64_t K) {
   const int64_t nblk = (B + kSortRows - 1) / kSortRows;
-  return (size_t)(K * nblk + (K + 1) + B) * sizeof(int) + 256;
+  return (size_t)(K * nblk + (K + 1) + B) * sizeof(int) + 256 + (size_t)(kSegSplit * K) * 1024 * sizeof(float);
 }
 
 int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
                    void* workspace, size_t ws_bytes, void* stream) {
   RQ_CHECK_ARG(rows && keys && out && workspace, "rq_segment_sum: null pointer");
-  RQ_CHECK_ARG(B >= 0 && B < (1ll << 31) && D >= 1 && D <= 1024 && K >= 1 && K <= 4096, "rq_segment_sum: bad shape");
+  RQ_CHECK_ARG(B >= 0 && B < (1ll << 31) && D >= 4 && D <= 1024 && D % 4 == 0 && K >= 1 && K <= 4096,
+               "rq_segment_sum: bad shape (need D %% 4 == 0, 4 <= D <= 1024, K <= 4096)");
+  RQ_CHECK_ARG(((uintptr_t)rows | (uintptr_t)out) % 16 == 0, "rq_segment_sum: rows / out must be 16-byte aligned");
   RQ_CHECK_ARG(ws_bytes >= rq_segment_sum_workspace(B, K), "rq_segment_sum: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   if (B == 0) {
@@ -1310,13 +1374,15 @@ int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D,
   int* hist = (int*)workspace;
   int* key_off = hist + (size_t)K * nblk;
   int* perm = key_off + (K + 1);
+  float* segs = (float*)(((uintptr_t)(perm + B) + 15) & ~(uintptr_t)15);
   hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, 1), dim3(256), k * sizeof(int), s, keys, b, 1, k, nblk, hist);
   hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 255) / 256, 1), dim3(256), 0, s, hist, k, nblk, key_off);
   hipLaunchKernelGGL(sort_offsets_kernel, dim3(1), dim3(1024), 0, s, key_off, k, b);
-  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, 1), dim3(64), k * sizeof(int), s, keys, b, 1, k, nblk, hist, key_off,
-                     perm);
-  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, 1), dim3(256), 0, s, (const float*)nullptr, (const float*)nullptr,
-                     (const float*)nullptr, rows, perm, key_off, b, d, k, out);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, 1), dim3(256), (2 * k + kSortRows) * sizeof(int), s, keys, b, 1, k,
+                     nblk, hist, key_off, perm);
+  hipLaunchKernelGGL(rq_cb_segsum_kernel, dim3(k, kSegSplit, 1), dim3(256), 0, s, (const float*)nullptr,
+                     (const float*)nullptr, (const float*)nullptr, rows, perm, key_off, b, d, k, out, segs);
+  hipLaunchKernelGGL(rq_segsum_finalize_kernel, dim3(k, 1), dim3(256), 0, s, key_off, d, k, segs, out);
   if (counts) hipLaunchKernelGGL(segment_counts_kernel, dim3((k + 255) / 256), dim3(256), 0, s, key_off, k, counts);
   RQ_LAUNCH_CHECK("rq_segment_sum");
   return 0;

@@ -10,6 +10,19 @@ import torch
 from torch import nn
 from torch import Tensor
 
+from rqvae_hip import ops as hip_ops
+
+
+class Embedding(nn.Embedding):
+    """nn.Embedding (same parameter, init and state-dict key) whose backward on the device is the
+    deterministic segmented sum rqvae_hip.ops.embedding (sort by index, fixed-order row sums) instead
+    of torch's sort + scatter kernels."""
+
+    def forward(self, idx: Tensor) -> Tensor:
+        if hip_ops.embedding_supported(self.weight) and idx.is_cuda and self.max_norm is None:
+            return hip_ops.embedding(idx, self.weight, self.padding_idx)
+        return super().forward(idx)
+
 
 class SemIdEmbeddingBatch(NamedTuple):
     seq: Tensor
@@ -22,8 +35,8 @@ class SemIdEmbedder(nn.Module):
         self.sem_ids_dim = sem_ids_dim
         self.num_embeddings = num_embeddings
         self.padding_idx = sem_ids_dim * num_embeddings
-        self.emb = nn.Embedding(num_embeddings=self.padding_idx + 1, embedding_dim=embeddings_dim,
-                                padding_idx=self.padding_idx)
+        self.emb = Embedding(num_embeddings=self.padding_idx + 1, embedding_dim=embeddings_dim,
+                             padding_idx=self.padding_idx)
 
     def _rows(self, type_ids, sem_ids):
         return type_ids * self.num_embeddings + sem_ids
@@ -31,17 +44,19 @@ class SemIdEmbedder(nn.Module):
     def forward(self, batch) -> SemIdEmbeddingBatch:
         rows = torch.where(batch.seq_mask, self._rows(batch.token_type_ids, batch.sem_ids),
                            torch.full_like(batch.sem_ids, self.padding_idx))
-        fut = None
-        if batch.sem_ids_fut is not None:
-            fut = self.emb(self._rows(batch.token_type_ids_fut, batch.sem_ids_fut))
-        return SemIdEmbeddingBatch(seq=self.emb(rows), fut=fut)
+        if batch.sem_ids_fut is None:
+            return SemIdEmbeddingBatch(seq=self.emb(rows), fut=None)
+        # one gather (and one backward reduction) for the context and future tokens of the table
+        N = rows.shape[1]
+        both = self.emb(torch.cat([rows, self._rows(batch.token_type_ids_fut, batch.sem_ids_fut)], dim=1))
+        return SemIdEmbeddingBatch(seq=both[:, :N], fut=both[:, N:])
 
 
 class UserIdEmbedder(nn.Module):
     def __init__(self, num_buckets, embedding_dim) -> None:
         super().__init__()
         self.num_buckets = num_buckets
-        self.emb = nn.Embedding(num_buckets, embedding_dim)
+        self.emb = Embedding(num_buckets, embedding_dim)
 
     def forward(self, x: Tensor) -> Tensor:
         return self.emb(torch.remainder(x, self.num_buckets))

@@ -10,6 +10,7 @@ from typing import List
 from torch import nn
 
 from modules.linear import Linear
+from rqvae_hip import ops as hip_ops
 from modules.normalize import L2NormalizationLayer
 
 
@@ -35,4 +36,16 @@ class MLP(nn.Module):
 
     def forward(self, x):
         assert x.shape[-1] == self.input_dim, f"Invalid input dim: Expected {self.input_dim}, found {x.shape[-1]}"
-        return self.mlp(x)
+        mods = self.mlp
+        i, n = 0, len(mods)
+        while i < n:
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < n else None
+            if (isinstance(m, nn.SiLU) and isinstance(nxt, nn.Dropout) and nxt.training and nxt.p > 0
+                    and hip_ops.dropout_fusable(x)):
+                x = hip_ops.silu_dropout(x, nxt.p)   # SiLU + Dropout in one HIP pass
+                i += 2
+                continue
+            x = m(x)
+            i += 1
+        return x

@@ -19,7 +19,7 @@ from torch.nn import functional as F
 
 from data.schemas import TokenizedSeqBatch
 from modules.linear import Linear
-from modules.embedding.id_embedder import SemIdEmbedder, UserIdEmbedder
+from modules.embedding.id_embedder import Embedding, SemIdEmbedder, UserIdEmbedder
 from modules.normalize import RMSNorm
 from modules.transformer.model import TransformerEncoderDecoder
 from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
@@ -58,9 +58,9 @@ class EncoderDecoderRetrievalModel(nn.Module):
         self.sem_id_embedder = SemIdEmbedder(num_embeddings=num_embeddings, sem_ids_dim=sem_id_dim,
                                              embeddings_dim=embedding_dim)
         self.user_id_embedder = UserIdEmbedder(2000, embedding_dim)
-        self.wpe = nn.Embedding(num_embeddings=max_pos, embedding_dim=embedding_dim)
-        self.tte = nn.Embedding(num_embeddings=sem_id_dim, embedding_dim=embedding_dim)
-        self.tte_fut = nn.Embedding(num_embeddings=sem_id_dim, embedding_dim=embedding_dim)  # unused (reference)
+        self.wpe = Embedding(num_embeddings=max_pos, embedding_dim=embedding_dim)
+        self.tte = Embedding(num_embeddings=sem_id_dim, embedding_dim=embedding_dim)
+        self.tte_fut = Embedding(num_embeddings=sem_id_dim, embedding_dim=embedding_dim)  # unused (reference)
         self.transformer = TransformerEncoderDecoder(d_in=attn_dim, d_out=attn_dim, dropout=dropout,
                                                      num_heads=num_heads, encoder_layers=n_layers // 2,
                                                      decoder_layers=n_layers // 2)
@@ -83,8 +83,8 @@ class EncoderDecoderRetrievalModel(nn.Module):
         nf = fut.shape[1]                                                                # fixed length: no sync
         fut_lengths = torch.full((B,), nf, device=fut.device, dtype=torch.int64)
         fut_j = padded_to_jagged(fut.contiguous(), fut_lengths, nf, total=B * nf, known_max=nf)
-        transformer_context = ctx_j.with_values(self.in_proj_context(self.do(self.norm(ctx_j.values()))))
-        transformer_input = fut_j.with_values(self.in_proj(self.do(self.norm_cxt(fut_j.values()))))
+        transformer_context = ctx_j.with_values(self.in_proj_context(self.norm.forward_dropout(ctx_j.values(), self.do)))
+        transformer_input = fut_j.with_values(self.in_proj(self.norm_cxt.forward_dropout(fut_j.values(), self.do)))
         return self.transformer(x=transformer_input, context=transformer_context, padding_mask=batch.seq_mask,
                                 jagged=True)
 

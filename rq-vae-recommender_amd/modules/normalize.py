@@ -43,3 +43,10 @@ class RMSNorm(nn.Module):
             return hip_ops.rmsnorm(x, self.weight, self.eps)
         y = self._norm(x.float()).type_as(x)
         return y * self.weight
+
+    def forward_dropout(self, x, dropout: nn.Dropout):
+        """dropout(self(x)) — one fused HIP pass (mask regenerated in backward) when training on the
+        device; the two separate ops otherwise."""
+        if dropout.training and dropout.p > 0 and hip_ops.rmsnorm_supported(x, self.weight):
+            return hip_ops.rmsnorm(x, self.weight, self.eps, dropout.p)
+        return dropout(self(x))

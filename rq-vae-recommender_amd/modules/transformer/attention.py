@@ -86,14 +86,15 @@ class MultiHeadAttention(nn.Module):
         if not jagged:
             raise Exception("Unjagged attention currently not supported.")
         jx = as_jagged(x)
+        # q/k/v stay column blocks of the packed projection outputs (read in place through row
+        # strides); the backward writes their gradients into one buffer per projection (no cat)
         if self.cross_attn:
             jkv = as_jagged(x_kv)
-            q = self.q(jx.values())
-            k, v = self.kv(jkv.values()).chunk(2, dim=-1)
+            ctx = hip_ops.varlen_attention_packed(self.q(jx.values()), self.kv(jkv.values()), jx.offsets(),
+                                                  jkv.offsets(), self.num_heads, bool(is_causal), jx.max_len,
+                                                  jkv.max_len)
         else:
-            jkv = jx
-            q, k, v = self.qkv(jx.values()).chunk(3, dim=-1)   # strided row views, consumed in place
-        ctx = hip_ops.varlen_attention(q, k, v, jx.offsets(), jkv.offsets(), self.num_heads, bool(is_causal),
-                                       jx.max_len, jkv.max_len)
+            ctx = hip_ops.varlen_attention_packed(self.qkv(jx.values()), None, jx.offsets(), jx.offsets(),
+                                                  self.num_heads, bool(is_causal), jx.max_len, jx.max_len)
         out = self.proj(ctx)
         return jx.with_values(out) if isinstance(x, Jagged) else _wrap_like(out, x)

@@ -22,6 +22,7 @@ from modules.encoder import MLP
 from modules.normalize import RMSNorm
 from modules.transformer.attention import AttentionInput, MultiHeadAttention, _wrap_like
 from ops.jagged import Jagged, as_jagged
+from rqvae_hip import ops as hip_ops
 
 
 class KVCacheOpsMixin:
@@ -68,12 +69,16 @@ class TransformerBlock(nn.Module):
     def _forward_jagged(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool) -> Jagged:
         use_cache = not self.training and self.enable_kv_cache
         xv = jx.values()
-        h = xv + self.attention(jx.with_values(self.do(self.attn_norm(xv))), is_causal=is_causal, jagged=True,
-                                use_cache=use_cache).values()
+        h = xv + self.attention(jx.with_values(self.attn_norm.forward_dropout(xv, self.do)), is_causal=is_causal,
+                                jagged=True, use_cache=use_cache).values()
         if self.do_cross_attn:
-            h = h + self.cross_attention(x=jx.with_values(self.do(self.cross_attn_norm(xv))), x_kv=jkv,
+            h = h + self.cross_attention(x=jx.with_values(self.cross_attn_norm.forward_dropout(xv, self.do)), x_kv=jkv,
                                          is_causal=False, jagged=True, use_cache=use_cache).values()
-        return jx.with_values(h + self.ff(h))
+        norm, mlp, drop = self.ff
+        y = mlp(norm(h))
+        if drop.training and drop.p > 0 and hip_ops.dropout_fusable(h) and hip_ops.dropout_fusable(y):
+            return jx.with_values(hip_ops.dropout_add(h, y, drop.p))   # h + Dropout(ff) in one pass
+        return jx.with_values(h + drop(y))
 
     def reset_kv_cache(self):
         raise NotImplementedError("KV Cache currently not supported")

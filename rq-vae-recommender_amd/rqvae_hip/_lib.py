@@ -20,6 +20,7 @@ _I64 = ctypes.c_int64
 _I = ctypes.c_int
 _F = ctypes.c_float
 _SZ = ctypes.c_size_t
+_U64 = ctypes.c_uint64
 
 _SIGS = {
     "rq_abi_version": ([], _I),
@@ -34,6 +35,13 @@ _SIGS = {
     "rq_rmsnorm_fwd": ([_P, _P, _I64, _I64, _F, _P, _P, _P], _I),
     "rq_rmsnorm_bwd_workspace": ([_I64, _I64], _SZ),
     "rq_rmsnorm_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
+    "rq_rmsnorm_dropout_fwd": ([_P, _P, _I64, _I64, _F, _F, _U64, _P, _P, _P], _I),
+    "rq_rmsnorm_dropout_bwd": ([_P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _P, _SZ, _P], _I),
+    "rq_dropout_params": ([_F, _P, _P], _I),
+    "rq_silu_dropout_fwd": ([_P, _I64, _F, _U64, _P, _P], _I),
+    "rq_silu_dropout_bwd": ([_P, _P, _I64, _F, _U64, _P, _P], _I),
+    "rq_dropout_add_fwd": ([_P, _P, _I64, _F, _U64, _P, _P], _I),
+    "rq_dropout_bwd": ([_P, _I64, _F, _U64, _P, _P], _I),
     "rq_linear_wgrad_workspace": ([_I64, _I64, _I64], _SZ),
     "rq_linear_wgrad": ([_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_unique_workspace": ([_I64], _SZ),

@@ -112,14 +112,15 @@ def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25):
     return RqQuantizeFunction.apply(x, codebooks, mode, beta)
 
 
-def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int):
-    """(sums (K, D), counts (K,)) of `rows` grouped by `keys` — deterministic (no float atomics)."""
+def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int, with_counts: bool = True):
+    """(sums (K, D), counts (K,) or None) of `rows` grouped by `keys` — deterministic (no float
+    atomics). Rows whose key is outside [0, K) are skipped."""
     require_gpu(rows, keys, what="segment_sum")
     rows = rows.contiguous().float()
     keys = keys.contiguous().to(torch.int64)
     B, D = rows.shape
     out = torch.empty((K, D), device=rows.device, dtype=torch.float32)
-    counts = torch.empty((K,), device=rows.device, dtype=torch.int64)
+    counts = torch.empty((K,), device=rows.device, dtype=torch.int64) if with_counts else None
     nbytes = _lib.load().rq_segment_sum_workspace(B, K)
     ws = torch.empty((nbytes,), device=rows.device, dtype=torch.uint8)
     call("rq_segment_sum", ptr(rows), ptr(keys), B, D, int(K), ptr(out), ptr(counts), ptr(ws), nbytes,
@@ -191,20 +192,23 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
 
 
 class RMSNormFunction(torch.autograd.Function):
-    """y = (x * rsqrt(mean(x^2, -1) + eps)) * w over the last axis (modules/normalize.py:22-32), one
-    HBM pass forward (rq_rmsnorm_fwd) and one backward (rq_rmsnorm_bwd: gx and a deterministic gw)."""
+    """y = Dropout_p((x * rsqrt(mean(x^2, -1) + eps)) * w) over the last axis (modules/normalize.py:22-32,
+    followed by the nn.Dropout the decoder applies to every norm output it feeds to attention), one HBM
+    pass forward (rq_rmsnorm_dropout_fwd) and one backward (gx and a deterministic gw); the dropout
+    mask is regenerated from `seed` in the backward, never stored. p = 0: plain RMSNorm."""
 
     @staticmethod
-    def forward(ctx, x, weight, eps: float):
+    def forward(ctx, x, weight, eps: float, p: float = 0.0, seed: int = 0):
         require_gpu(x, weight, what="rmsnorm")
         D = x.shape[-1]
         x2 = x.contiguous().view(-1, D)
         B = x2.shape[0]
         y = torch.empty_like(x2)
         rstd = torch.empty((B,), device=x.device, dtype=torch.float32)
-        call("rq_rmsnorm_fwd", ptr(x2), ptr(weight), B, D, float(eps), ptr(y), ptr(rstd), stream_handle(x.device))
+        call("rq_rmsnorm_dropout_fwd", ptr(x2), ptr(weight), B, D, float(eps), float(p), int(seed), ptr(y), ptr(rstd),
+             stream_handle(x.device))
         ctx.save_for_backward(x2, weight, rstd)
-        ctx.shape = x.shape
+        ctx.shape, ctx.p, ctx.seed = x.shape, float(p), int(seed)
         return y.view(x.shape)
 
     @staticmethod
@@ -216,9 +220,9 @@ class RMSNormFunction(torch.autograd.Function):
         gw = torch.empty((D,), device=x2.device, dtype=torch.float32)
         nbytes = _lib.load().rq_rmsnorm_bwd_workspace(B, D)
         ws = torch.empty((nbytes,), device=x2.device, dtype=torch.uint8)
-        call("rq_rmsnorm_bwd", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2), B, D, ptr(gx), ptr(gw), ptr(ws), nbytes,
-             stream_handle(x2.device))
-        return gx.view(ctx.shape), gw, None
+        call("rq_rmsnorm_dropout_bwd", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2), B, D, ctx.p, ctx.seed, ptr(gx),
+             ptr(gw), ptr(ws), nbytes, stream_handle(x2.device))
+        return gx.view(ctx.shape), gw, None, None, None
 
 
 def rmsnorm_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -227,8 +231,109 @@ def rmsnorm_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
             and D % 4 == 0 and D <= 4096)
 
 
-def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
-    return RMSNormFunction.apply(x, weight, eps)
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, p: float = 0.0) -> torch.Tensor:
+    return RMSNormFunction.apply(x, weight, eps, float(p), next_seed() if p > 0 else 0)
+
+
+# ------------------------------------------------------------------------------- dropout
+_SEED = {"base": None, "n": 0}
+
+
+def next_seed() -> int:
+    """Key of the next dropout mask: a counter under torch.initial_seed(), so torch.manual_seed makes
+    the masks reproducible (the generator is counter-based; masks are never stored). Host-only: no
+    device sync. A hipGraph capture freezes the key of each captured call."""
+    base = torch.initial_seed()
+    if _SEED["base"] != base:
+        _SEED["base"], _SEED["n"] = base, 0
+    _SEED["n"] += 1
+    return (base * 0x9E3779B97F4A7C15 + _SEED["n"] * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
+
+
+def dropout_fusable(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
+
+
+class SiluDropoutFunction(torch.autograd.Function):
+    """h = Dropout_p(SiLU(z)) in one pass (the MLP hidden layer, modules/encoder.py:20-28)."""
+
+    @staticmethod
+    def forward(ctx, z, p: float, seed: int):
+        require_gpu(z, what="silu_dropout")
+        h = torch.empty_like(z)
+        call("rq_silu_dropout_fwd", ptr(z), z.numel(), float(p), int(seed), ptr(h), stream_handle(z.device))
+        ctx.save_for_backward(z)
+        ctx.p, ctx.seed = float(p), int(seed)
+        return h
+
+    @staticmethod
+    def backward(ctx, g):
+        (z,) = ctx.saved_tensors
+        g = g.contiguous()
+        gz = torch.empty_like(z)
+        call("rq_silu_dropout_bwd", ptr(g), ptr(z), z.numel(), ctx.p, ctx.seed, ptr(gz), stream_handle(z.device))
+        return gz, None, None
+
+
+def silu_dropout(z: torch.Tensor, p: float) -> torch.Tensor:
+    return SiluDropoutFunction.apply(z.contiguous(), float(p), next_seed())
+
+
+class DropoutAddFunction(torch.autograd.Function):
+    """out = h + Dropout_p(y) in one pass (the block output, modules/transformer/model.py:76/82)."""
+
+    @staticmethod
+    def forward(ctx, h, y, p: float, seed: int):
+        require_gpu(h, y, what="dropout_add")
+        out = torch.empty_like(h)
+        call("rq_dropout_add_fwd", ptr(h), ptr(y), h.numel(), float(p), int(seed), ptr(out), stream_handle(h.device))
+        ctx.p, ctx.seed = float(p), int(seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        gy = torch.empty_like(g)
+        call("rq_dropout_bwd", ptr(g), g.numel(), ctx.p, ctx.seed, ptr(gy), stream_handle(g.device))
+        return g, gy, None, None
+
+
+def dropout_add(h: torch.Tensor, y: torch.Tensor, p: float) -> torch.Tensor:
+    return DropoutAddFunction.apply(h.contiguous(), y.contiguous(), float(p), next_seed())
+
+
+# ------------------------------------------------------------------------------ embedding
+class EmbeddingFunction(torch.autograd.Function):
+    """F.embedding forward (a row gather); backward = deterministic segmented sum of the output
+    gradient rows by index (rq_segment_sum: stable counting sort + fixed-order per-row sums), with the
+    padding row's gradient zero as in nn.Embedding(padding_idx). Replaces torch's sort + scatter
+    embedding backward (~4 launches and a data-dependent atomic reduction per table)."""
+
+    @staticmethod
+    def forward(ctx, weight, idx, padding_idx):
+        require_gpu(weight, idx, what="embedding")
+        ctx.save_for_backward(idx)
+        ctx.K, ctx.padding_idx = weight.shape[0], padding_idx
+        return torch.nn.functional.embedding(idx, weight, padding_idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        E = g.shape[-1]
+        keys = idx.reshape(-1)
+        if ctx.padding_idx is not None:   # padding rows are skipped (key -1): their row's grad is 0
+            keys = torch.where(keys == ctx.padding_idx, -1, keys)
+        sums, _ = segment_sum(g.reshape(-1, E), keys, ctx.K, with_counts=False)
+        return sums, None, None
+
+
+def embedding_supported(weight: torch.Tensor) -> bool:
+    K, E = weight.shape
+    return weight.is_cuda and weight.dtype == torch.float32 and K <= 4096 and E <= 1024
+
+
+def embedding(idx: torch.Tensor, weight: torch.Tensor, padding_idx=None) -> torch.Tensor:
+    return EmbeddingFunction.apply(weight, idx, padding_idx)
 
 
 def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
@@ -373,6 +478,72 @@ class VarlenAttentionFunction(torch.autograd.Function):
              int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), ptr(delta),
              stream_handle(q.device))
         return dq, dk, dv, None, None, None, None, None, None, None
+
+
+class PackedVarlenAttentionFunction(torch.autograd.Function):
+    """Varlen attention on the packed projection outputs: self-attention reads q/k/v as the three
+    column blocks of qkv (T, 3A); cross-attention reads q (Tq, A) and k/v as the two column blocks
+    of kv (Tk, 2A). The backward writes dq/dk/dv straight into one gradient buffer per projection
+    output (row-strided), so autograd never concatenates the three chunk gradients."""
+
+    @staticmethod
+    def forward(ctx, qsrc, kvsrc, cu_q, cu_k, num_heads: int, causal: bool, max_q: int, max_k: int, scale: float):
+        require_gpu(qsrc, cu_q, cu_k, what="varlen_attention")
+        self_attn = kvsrc is None
+        A = qsrc.shape[1] // 3 if self_attn else qsrc.shape[1]
+        src_kv = qsrc if self_attn else kvsrc
+        koff = A if self_attn else 0
+        for t in (qsrc, src_kv):
+            assert t.dim() == 2 and t.stride(1) == 1 and t.dtype == torch.float32
+        q = qsrc[:, :A]
+        k = src_kv[:, koff:koff + A]
+        v = src_kv[:, koff + A:koff + 2 * A]
+        Tq = q.shape[0]
+        hd = A // num_heads
+        B = cu_q.shape[0] - 1
+        out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
+        lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
+        call("varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
+             B, num_heads, hd, int(max_q), int(max_k), int(causal), float(scale), ptr(out), out.stride(0), ptr(lse), Tq,
+             stream_handle(q.device))
+        if self_attn:
+            ctx.save_for_backward(qsrc, out, lse, cu_q, cu_k)
+        else:
+            ctx.save_for_backward(qsrc, kvsrc, out, lse, cu_q, cu_k)
+        ctx.cfg = (self_attn, A, num_heads, bool(causal), int(max_q), int(max_k), float(scale))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        self_attn, A, H, causal, max_q, max_k, scale = ctx.cfg
+        if self_attn:
+            qsrc, out, lse, cu_q, cu_k = ctx.saved_tensors
+            kvsrc = None
+        else:
+            qsrc, kvsrc, out, lse, cu_q, cu_k = ctx.saved_tensors
+        src_kv = qsrc if self_attn else kvsrc
+        koff = A if self_attn else 0
+        dout = dout.contiguous()
+        gq_src = torch.empty_like(qsrc)
+        gkv_src = gq_src if self_attn else torch.empty_like(kvsrc)
+        q, k, v = qsrc[:, :A], src_kv[:, koff:koff + A], src_kv[:, koff + A:koff + 2 * A]
+        dq, dk, dv = gq_src[:, :A], gkv_src[:, koff:koff + A], gkv_src[:, koff + A:koff + 2 * A]
+        Tq = q.shape[0]
+        B = cu_q.shape[0] - 1
+        delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
+        call("varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+             out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
+             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), ptr(delta),
+             stream_handle(q.device))
+        return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None
+
+
+def varlen_attention_packed(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):
+    """qsrc = qkv (T, 3A) with kvsrc None (self-attention), or q (Tq, A) with kv (Tk, 2A) (cross)."""
+    A = qsrc.shape[1] // 3 if kvsrc is None else qsrc.shape[1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(A // num_heads)
+    return PackedVarlenAttentionFunction.apply(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale)
 
 
 def varlen_attention(q, k, v, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):

@@ -1,0 +1,180 @@
+"""Decoder-side fusions against plain PyTorch fp32 references of the same ops:
+RMSNorm + Dropout, SiLU + Dropout, residual + Dropout (counter-based masks regenerated in the
+backward), the segmented-sum embedding backward, and packed-projection attention (no chunk cat).
+
+Dropout masks are random by design, so the reference recovers the kernel's mask from its output
+(kept elements are exactly value * 1/(1-p), dropped ones exactly 0) and checks the rest of the op
+and its gradient against torch with that mask; the keep rate is checked statistically."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rms_ref(x, w, eps):
+    return (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps)) * w
+
+
+def _kernel_scale(p, device):
+    """The kernels' 1/(1-p) (fp32, computed by the library) for bitwise comparisons."""
+    import ctypes
+    from rqvae_hip import _lib
+    thr, scale = ctypes.c_uint32(), ctypes.c_float()
+    assert _lib.load().rq_dropout_params(ctypes.c_float(p), ctypes.byref(thr), ctypes.byref(scale)) == 0
+    return torch.tensor(scale.value, dtype=torch.float32, device=device)
+
+
+def _check_rate(mask, p):
+    n = mask.numel()
+    rate = 1.0 - mask.float().mean().item()
+    assert abs(rate - p) < 6 * np.sqrt(p * (1 - p) / n) + 1e-6, (rate, p)
+
+
+@pytest.mark.parametrize("T,D,p", [(1000, 512, 0.3), (257, 128, 0.5), (64, 1024, 0.1)])
+def test_rmsnorm_dropout(device, T, D, p):
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(T + D)
+    x = torch.randn(T, D, device=device, generator=g)
+    w = torch.rand(D, device=device, generator=g) + 0.5
+    gy = torch.randn(T, D, device=device, generator=g)
+    plain = ops.rmsnorm(x, w, 1e-6)
+    seed = 1234567
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = ops.RMSNormFunction.apply(xr, wr, 1e-6, p, seed)
+    y.backward(gy)
+    scale = _kernel_scale(p, device)
+    mask = y != 0
+    _check_rate(mask, p)
+    assert torch.equal(y[mask], plain[mask] * scale), "kept values = rmsnorm * 1/(1-p), bitwise"
+    y2 = ops.RMSNormFunction.apply(x, w, 1e-6, p, seed)
+    assert torch.equal(y, y2), "same seed -> same mask"
+    assert not torch.equal(y != 0, ops.RMSNormFunction.apply(x, w, 1e-6, p, seed + 1) != 0)
+    xt, wt = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ref = _rms_ref(xt, wt, 1e-6) * mask * scale
+    ref.backward(gy)
+    torch.testing.assert_close(xr.grad, xt.grad, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(wr.grad, wt.grad, rtol=2e-5, atol=2e-5)
+
+
+def test_rmsnorm_dropout_p0_is_rmsnorm(device):
+    from rqvae_hip import ops
+    x = torch.randn(300, 512, device=device)
+    w = torch.rand(512, device=device)
+    assert torch.equal(ops.RMSNormFunction.apply(x, w, 1e-6, 0.0, 99), ops.rmsnorm(x, w, 1e-6))
+
+
+@pytest.mark.parametrize("n,p", [(11600 * 1024, 0.3), (4096, 0.5)])
+def test_silu_dropout(device, n, p):
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(n)
+    z = torch.randn(n, device=device, generator=g) * 3
+    z[z == 0] = 1.0   # silu(0) == 0 would read as a dropped element below
+    gh = torch.randn(n, device=device, generator=g)
+    zr = z.clone().requires_grad_(True)
+    h = ops.SiluDropoutFunction.apply(zr, p, 42)
+    h.backward(gh)
+    mask = h != 0
+    _check_rate(mask, p)
+    zt = z.clone().requires_grad_(True)
+    ref = torch.nn.functional.silu(zt) * mask * _kernel_scale(p, device)
+    ref.backward(gh)
+    torch.testing.assert_close(h, ref, rtol=2e-6, atol=1e-7)
+    torch.testing.assert_close(zr.grad, zt.grad, rtol=2e-6, atol=1e-7)
+    # p = 0: plain SiLU
+    torch.testing.assert_close(ops.SiluDropoutFunction.apply(z, 0.0, 1), torch.nn.functional.silu(z), rtol=2e-6, atol=0)
+
+
+def test_dropout_add(device):
+    from rqvae_hip import ops
+    T, D, p = 5000, 512, 0.3
+    g = torch.Generator(device=device).manual_seed(21)
+    hh = torch.randn(T, D, device=device, generator=g)
+    y = torch.randn(T, D, device=device, generator=g)
+    go = torch.randn(T, D, device=device, generator=g)
+    go[go == 0] = 1.0   # a zero gradient would read as a dropped element below
+    hr, yr = hh.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    out = ops.DropoutAddFunction.apply(hr, yr, p, 7)
+    out.backward(go)
+    scale = _kernel_scale(p, device)
+    mask = yr.grad != 0   # gradient of y carries the mask
+    _check_rate(mask, p)
+    assert torch.equal(out, hh + torch.where(mask, y * scale, torch.zeros_like(y)))
+    assert torch.equal(hr.grad, go)
+    assert torch.equal(yr.grad, torch.where(mask, go * scale, torch.zeros_like(go)))
+
+
+def test_embedding_segment_sum_backward(device):
+    from rqvae_hip import ops
+    K, E = 1025, 128
+    g = torch.Generator(device=device).manual_seed(5)
+    w = torch.randn(K, E, device=device, generator=g)
+    idx = torch.randint(0, K, (256, 80), device=device, generator=g)
+    idx[:, 40:] = K - 1   # padding rows
+    idx[:, 3:40:4] = 768  # a heavy key (the dedup-column token): 2,560 rows, split across workgroups
+    go = torch.randn(256, 80, E, device=device, generator=g)
+    wr = w.clone().requires_grad_(True)
+    out = ops.embedding(idx, wr, K - 1)
+    out.backward(go)
+    wt = w.clone().requires_grad_(True)
+    ref = torch.nn.functional.embedding(idx, wt, padding_idx=K - 1)
+    ref.backward(go)
+    assert torch.equal(out, ref)
+    torch.testing.assert_close(wr.grad, wt.grad, rtol=1e-5, atol=1e-4)   # 2,560-row sums, other order
+    assert torch.all(wr.grad[K - 1] == 0)
+    # bitwise deterministic
+    wr2 = w.clone().requires_grad_(True)
+    ops.embedding(idx, wr2, K - 1).backward(go)
+    assert torch.equal(wr.grad, wr2.grad)
+
+
+@pytest.mark.parametrize("N,D,K", [(20000, 128, 1025), (5000, 64, 7), (3, 8, 4096), (65536, 1024, 300)])
+def test_segment_sum_vs_index_add(device, N, D, K):
+    """Deterministic segmented sum (light segments in one workgroup, heavy ones split and finalized)
+    against torch index_add_ in fp64; out-of-range keys are skipped."""
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(N + K)
+    rows = torch.randn(N, D, device=device, generator=g)
+    keys = torch.randint(0, K, (N,), device=device, generator=g)
+    keys[: N // 3] = min(5, K - 1)    # heavy segment
+    keys[N // 3: N // 3 + 7] = -1     # skipped
+    sums, counts = ops.segment_sum(rows, keys, K)
+    ok = keys >= 0
+    ref = torch.zeros(K, D, device=device, dtype=torch.float64).index_add_(0, keys[ok], rows[ok].double())
+    torch.testing.assert_close(sums.double(), ref, rtol=1e-5, atol=max(1e-4, 5e-8 * N))   # fp32 sums of N/3 rows
+    assert torch.equal(counts, torch.bincount(keys[ok], minlength=K))
+    sums2, _ = ops.segment_sum(rows, keys, K)
+    assert torch.equal(sums, sums2)
+
+
+@pytest.mark.parametrize("cross", [False, True])
+def test_packed_attention_matches_unpacked(device, cross):
+    from rqvae_hip import ops
+    H, A = 8, 512
+    g = torch.Generator(device=device).manual_seed(11)
+    lens_q = torch.tensor([5, 5, 5, 5], device=device) if cross else torch.tensor([45, 1, 81, 17], device=device)
+    lens_k = torch.tensor([45, 1, 81, 17], device=device)
+    cu_q = torch.cat([torch.zeros(1, device=device, dtype=torch.int64), lens_q.cumsum(0)])
+    cu_k = torch.cat([torch.zeros(1, device=device, dtype=torch.int64), lens_k.cumsum(0)])
+    Tq, Tk = int(cu_q[-1]), int(cu_k[-1])
+    if cross:
+        qs = torch.randn(Tq, A, device=device, generator=g).requires_grad_(True)
+        kvs = torch.randn(Tk, 2 * A, device=device, generator=g).requires_grad_(True)
+        out = ops.varlen_attention_packed(qs, kvs, cu_q, cu_k, H, False, 5, 81)
+        q2, kv2 = qs.detach().clone().requires_grad_(True), kvs.detach().clone().requires_grad_(True)
+        k, v = kv2.chunk(2, dim=-1)
+        ref = ops.varlen_attention(q2, k, v, cu_q, cu_k, H, False, 5, 81)
+    else:
+        qs = torch.randn(Tq, 3 * A, device=device, generator=g).requires_grad_(True)
+        kvs = None
+        out = ops.varlen_attention_packed(qs, None, cu_q, cu_q, H, True, 81, 81)
+        q2 = qs.detach().clone().requires_grad_(True)
+        q, k, v = q2.chunk(3, dim=-1)
+        ref = ops.varlen_attention(q, k, v, cu_q, cu_q, H, True, 81, 81)
+    go = torch.randn_like(out)
+    out.backward(go)
+    ref.backward(go)
+    assert torch.equal(out, ref)
+    assert torch.equal(qs.grad, q2.grad)
+    if cross:
+        assert torch.equal(kvs.grad, kv2.grad)

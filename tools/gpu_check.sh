@@ -45,6 +45,12 @@ for s in $steps; do
       run pmc_write 90 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rq_fwd -f csv -d "$O/pmc_write" -o q -- \
         python3 "$R/tools/pmc_quantize.py" 10 > "$O/pmc_write.log" 2>&1
       cd "$R" ;;
+    profdec)
+      cd /tmp
+      run prof_dec 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o decoder -- \
+        python3 "$R/bench.py" --decoder-only > "$O/prof_decoder.json" 2> "$O/prof_decoder.err"
+      cd "$R"
+      cat "$O/prof_decoder.json" ;;
     kern)
       run kern 300 python -u "$R/tools/bench_kernels.py" > "$O/kernels.jsonl" 2> "$O/kernels.err"
       cat "$O/kernels.jsonl" ;;
