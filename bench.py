@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-decoder", action="store_true", help="skip the data-parallel decoder measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     return ap.parse_args()
@@ -172,7 +173,7 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs an MI355X (no GPU visible)")
     if args.decoder_only:
-        print(json.dumps(measure_decoder(torch.device("cuda", lr))), flush=True)
+        print(json.dumps({"decoder_amazon": measure_decoder(torch.device("cuda", lr), ws, rk)}), flush=True)
         return
     device = torch.device("cuda", lr)
     torch.cuda.set_device(device)
@@ -224,8 +225,10 @@ def main():
     loss = float(last.loss.detach())
     del last
 
+    # decoder-train tokens/s (BASELINE metric, second half): data parallel over the same ranks
+    dec = None if args.no_decoder else measure_decoder(device, ws, rk)
     extras = {}
-    if not args.no_extras and rk == 0:
+    if not args.no_extras and rk == 0 and ws == 1:
         extras = measure_extras(model, device, pool[0])
 
     if rk != 0:
@@ -262,8 +265,10 @@ def main():
                      "hbm_GBps_at_algorithmic_bytes": round(alg_bytes / (q_ms * 1e-3) / 1e9, 1)},
         "loss_last": round(loss, 5),
     }
+    if dec is not None:
+        line["decoder_amazon"] = dec
     line.update(extras)
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and ws == 1:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(line), flush=True)
     if ws > 1:
@@ -317,17 +322,43 @@ def measure_extras(model, device, x):
         out["b64_items_per_s_hipgraph"] = round(50 * 64 / dt, 1)
     except Exception as e:  # report, never hide
         out["b64_hipgraph_error"] = repr(e)[:300]
-    out.update(measure_decoder(device))
+    out["quantize_synthetic"] = measure_quantize_synthetic(device)
     return out
+
+
+def measure_quantize_synthetic(device, B=16384, D=1024, K=2048, L=4):
+    """BASELINE configs[4] quantize roofline shape (synthetic D=1024, K=2048, L=4) on one GPU: the
+    fused forward (auto path = split distance GEMM + partial argmin) timed with HIP events."""
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(77)
+    x = torch.randn(B, D, generator=g, device=device)
+    x = x / x.norm(dim=1, keepdim=True)
+    cbs = torch.randn(L, K, D, generator=g, device=device)
+    cbs = cbs / cbs.norm(dim=2, keepdim=True) * torch.tensor([1.0, 0.5, 0.25, 0.125], device=device).view(L, 1, 1)
+    for _ in range(3):
+        ops.rq_quantize(x, cbs, ops.MODE_ROTATION, 0.25)
+    torch.cuda.synchronize()
+    ops.TIMER.reset()
+    ops.TIMER.enabled = True
+    for _ in range(10):
+        ops.rq_quantize(x, cbs, ops.MODE_ROTATION, 0.25)
+    torch.cuda.synchronize()
+    ops.TIMER.enabled = False
+    ms, n = ops.TIMER.mean_ms("rq_quantize_fwd")
+    tf = 2.0 * K * D * L * B / (ms * 1e-3) / 1e12
+    return {"shape": [B, D, K, L], "fwd_ms": round(ms, 4), "items_per_s": round(B / (ms * 1e-3), 1),
+            "achieved_TFLOPs": round(tf, 2), "frac_fp32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
 DEC = dict(B=256, max_items=20, E=128, A=512, H=8, layers=8, K=256, sem_id_dim=4, dropout=0.3, lr=3e-4, wd=0.035)
 
 
-def measure_decoder(device, steps=20, warmup=5):
-    """BASELINE configs[2]: decoder train step at Amazon dims (decoder_amazon.gin), synthetic
-    tokenized batches (n_items ~ U{2..20}), HIP jagged conversion + varlen attention."""
-    from rqvae_hip import ops
+def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
+    """BASELINE configs[2] (decoder_amazon.gin dims, dropout 0.3), data parallel over the ranks: each
+    rank trains on its own synthetic tokenized batches (n_items ~ U{2..20}, 256 sequences per rank,
+    weak scaling), gradients all-reduced by GradBuckets (RCCL), fused AdamW. HIP jagged conversion,
+    varlen attention and fused dropout kernels. Tokens/s = context tokens of all ranks / max time."""
+    from rqvae_hip import dp, ops
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel
     torch.manual_seed(3)
@@ -335,39 +366,54 @@ def measure_decoder(device, steps=20, warmup=5):
                                      num_heads=DEC["H"], n_layers=DEC["layers"], num_embeddings=DEC["K"],
                                      sem_id_dim=DEC["sem_id_dim"], inference_verifier_fn=None,
                                      max_pos=DEC["max_items"] * DEC["sem_id_dim"]).to(device).train()
+    buckets = dp.GradBuckets(m.parameters())
+    buckets.broadcast_params()
     opt = torch.optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"], fused=True)
-    batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + i, device)
-               for i in range(4)]
+    batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + 97 * rk + i,
+                                         device) for i in range(4)]
     ctx_tokens = [int(b.seq_mask.sum()) + DEC["B"] for b in batches]
     it = [0]
 
     def step():
         b = batches[it[0] % len(batches)]
         it[0] += 1
-        opt.zero_grad(set_to_none=True)
+        buckets.zero_grad()
         o = m(b)
         o.loss.backward()
+        buckets.synchronize()
         opt.step()
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    sync_all()
     ops.TIMER.reset()
     ops.TIMER.enabled = True
     it[0] = 0
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    sync_all()
     dt = time.perf_counter() - t0
     ops.TIMER.enabled = False
     toks = sum(ctx_tokens[i % len(batches)] for i in range(steps))
-    fut = steps * DEC["B"] * (DEC["sem_id_dim"] + 1)
-    return {"decoder_amazon": {
-        "ctx_tokens_per_s": round(toks / dt, 1), "ctx_plus_fut_tokens_per_s": round((toks + fut) / dt, 1),
-        "ms_per_step": round(dt / steps * 1e3, 3), "batch": DEC["B"],
-        "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
-        "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
-        "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}}
+    tot = torch.tensor([dt, float(toks)], device=device, dtype=torch.float64)
+    if ws > 1:
+        mx = tot[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dt, toks = float(mx), float(tot[1])
+    fut = ws * steps * DEC["B"] * (DEC["sem_id_dim"] + 1)
+    return {"ctx_tokens_per_s": round(toks / dt, 1), "ctx_plus_fut_tokens_per_s": round((toks + fut) / dt, 1),
+            "ms_per_step": round(dt / steps * 1e3, 3), "per_gpu_batch": DEC["B"], "n_gpus": ws,
+            "parallelism": f"dp{ws}", "scaling": "weak",
+            "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
+            "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
+            "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}
 
 
 if __name__ == "__main__":
