@@ -608,7 +608,12 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
   // WPI waves share one 32-item tile and split its codeword tiles (small-B latency mode);
   // items per workgroup = 128 / WPI. All WPI waves run the (cheap) epilogue redundantly so each
   // keeps the next residual in its own registers; only sub-wave 0 stores.
-  constexpr int H2 = D / 2, LD = D + 4;
+  // SWZ: the resident D=64 image is filled by LDS-DMA (global_load_lds_dwordx4, no VGPR staging)
+  // into unpadded 256-B rows whose 16-B chunks are XOR-swizzled by (row & 15): chunk c of row r
+  // sits at c ^ (r & 15), so the 16 rows a ds_read_b128 lane group touches hit 16 distinct
+  // 4-bank groups. Otherwise rows are padded to D + 4 floats and filled through registers.
+  constexpr bool SWZ = RESIDENT && D == 64;
+  constexpr int H2 = D / 2, LD = SWZ ? D : D + 4;
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   const int NBp = (NB + 31) & ~31;
   float* A_s = dsm;                                  // [NBp][LD] codewords of the current level / chunk
@@ -661,40 +666,73 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
     for (int n0 = 0; n0 < K; n0 += NB) {
       const int nrows = min(NB, K - n0);
       __syncthreads();   // previous level / chunk fully consumed (incl. epilogue codeword reads)
-      for (int f = tid; f < nrows * (D / 4); f += 256) {
-        const int r = f / (D / 4), c = (f % (D / 4)) * 4;
-        *reinterpret_cast<float4*>(A_s + r * LD + c) = *reinterpret_cast<const float4*>(cb + (int64_t)(n0 + r) * D + c);
+      if constexpr (SWZ) {
+        // wave-instruction q moves rows 4q..4q+3 (1 KiB): lane i lands at LDS chunk i%16 of row
+        // 4q + i/16 and therefore loads logical chunk (i%16) ^ (row & 15) of that row
+        const int nq = (nrows + 3) / 4;
+        for (int q = wave; q < nq; q += 4) {
+          const int row = min(4 * q + (lane >> 4), nrows - 1);
+          const int c = (lane & 15) ^ (row & 15);
+          __builtin_amdgcn_global_load_lds(cb + (int64_t)(n0 + row) * D + 4 * c, A_s + q * 256, 16, 0, 0);
+        }
+      } else {
+        // 8 float4 loads in flight per thread before their LDS writes (a plain strided loop
+        // compiles to load -> vmcnt(0) -> ds_write per element); indices past the chunk are
+        // clamped, so neither the loads nor the writes sit behind a branch
+        const int total = nrows * (D / 4);
+        const float* cbn = cb + (int64_t)n0 * D;
+        for (int f0 = 0; f0 < total; f0 += 256 * 8) {
+          float4 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int f = min(f0 + u * 256 + tid, total - 1);
+            v[u] = *reinterpret_cast<const float4*>(cbn + (int64_t)(f / (D / 4)) * D + (f % (D / 4)) * 4);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {   // clamped lanes rewrite the last element with its own value
+            const int f = min(f0 + u * 256 + tid, total - 1);
+            *reinterpret_cast<float4*>(A_s + (f / (D / 4)) * LD + (f % (D / 4)) * 4) = v[u];
+          }
+        }
       }
-      for (int r = tid; r < nrows; r += 256) cs_s[r] = csq[(int64_t)l * K + n0 + r];
-      if (n0 == 0) flush(l);
+      for (int r = tid; r < NBp; r += 256) cs_s[r] = r < nrows ? csq[(int64_t)l * K + n0 + r] : INFINITY;
       __syncthreads();
+      if (n0 == 0) flush(l);   // after the barrier: the stores drain under this level's MFMAs
       // One-tile software pipeline: the argmin scan of tile t (VALU) is independent of tile
       // t+1's MFMA chain, so it fills the 64-cycle dependent-MFMA gaps instead of draining them.
       // Rows past nrows (last partial tile) read stale LDS; their distances are forced to +inf.
       // Each lane visits its codeword indices in increasing order, so a strict '<' keeps the
       // lowest index among equal distances (torch.argmin); the lane-pair merge below breaks ties.
+      // d = (|x|^2 + |c|^2) - 2 x.c as fma(-2, x.c, |x|^2 + |c|^2): 2 x.c is exact, so this is the
+      // reference expression's rounding. The tile's best (d, register) is found first, then merged
+      // into the running best once per tile (strict '<' keeps the earlier tile on ties).
       auto scan = [&](const floatx16& a, const float4 (&c)[4], int t0) {
+        float td = INFINITY;
+        int tr = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int il = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
           const float cr = (r & 3) == 0 ? c[r >> 2].x : (r & 3) == 1 ? c[r >> 2].y : (r & 3) == 2 ? c[r >> 2].z
                                                                                                   : c[r >> 2].w;
-          float d = (xs + cr) - 2.f * a[r];
-          d = il < nrows ? d : INFINITY;
-          const bool lt = d < best_d;
-          best_d = lt ? d : best_d;
-          best_i = lt ? n0 + il : best_i;
+          const float d = __builtin_fmaf(-2.f, a[r], xs + cr);
+          const bool lt = d < td;
+          td = lt ? d : td;
+          tr = lt ? r : tr;
         }
+        const bool lt = td < best_d;
+        best_d = lt ? td : best_d;
+        best_i = lt ? n0 + t0 + (tr & 3) + 8 * (tr >> 2) + 4 * h : best_i;
       };
       auto chain = [&](int t0, floatx16& acc, float4 (&c)[4]) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) c[j] = *reinterpret_cast<const float4*>(cs_s + t0 + 8 * j + 4 * h);
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        const float* ap = A_s + (t0 + (lane & 31)) * LD + h * H2;
+        const int arow = t0 + (lane & 31);
+        const float* ap = A_s + arow * LD + h * H2;
 #pragma unroll
         for (int s4 = 0; s4 < H2; s4 += 4) {
-          const float4 a = *reinterpret_cast<const float4*>(ap + s4);
+          const float4 a = SWZ ? *reinterpret_cast<const float4*>(A_s + arow * LD + 4 * (((h * H2 + s4) >> 2) ^ (arow & 15)))
+                               : *reinterpret_cast<const float4*>(ap + s4);
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, xv[s4], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, xv[s4 + 1], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, xv[s4 + 2], acc, 0, 0, 0);
@@ -752,7 +790,8 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
     const float* er = RESIDENT ? (A_s + id * LD + h * H2) : (cb + (int64_t)id * D + h * H2);
 #pragma unroll
     for (int k = 0; k < H2; k += 4) {
-      const float4 c = *reinterpret_cast<const float4*>(er + k);
+      const float4 c = SWZ ? *reinterpret_cast<const float4*>(A_s + id * LD + 4 * (((h * H2 + k) >> 2) ^ (id & 15)))
+                           : *reinterpret_cast<const float4*>(er + k);
       ev[k] = c.x; ev[k + 1] = c.y; ev[k + 2] = c.z; ev[k + 3] = c.w;
     }
     // Row sums use fma (one rounding per term); |x|^2 is the level's xs. The reference's torch
@@ -845,8 +884,9 @@ static void launch_fwd_reg_w(int B, hipStream_t s, const float* x, const float* 
   const int fit = (kMaxLds - 1024) / ((LD + 1) * 4);
   const bool resident = (K + 31) / 32 * 32 <= fit;
   const int NB = resident ? K : (fit / 32) * 32;
-  // rows / |c|^2 entries up to the next multiple of 32 are read (masked) by the last tile
-  const size_t lds = (size_t)((NB + 31) / 32 * 32) * (LD + 1) * sizeof(float) + 1024;
+  const int LDk = (resident && D == 64) ? D : LD;   // swizzled unpadded image (kernel's SWZ)
+  // rows / |c|^2 entries up to the next multiple of 32 are read (|c|^2 = +inf) by the last tile
+  const size_t lds = (size_t)((NB + 31) / 32 * 32) * (LDk + 1) * sizeof(float) + 1024;
   dim3 g((B + 128 / WPI - 1) / (128 / WPI));
   if (resident)
     hipLaunchKernelGGL((rq_fwd_reg_kernel<D, true, WPI>), g, dim3(256), lds, s, x, B, cbs, csq, K, L, mode, beta, NB,

@@ -51,6 +51,13 @@ for s in $steps; do
         python3 "$R/bench.py" --decoder-only > "$O/prof_decoder.json" 2> "$O/prof_decoder.err"
       cd "$R"
       cat "$O/prof_decoder.json" ;;
+    sqpmc)
+      cd /tmp
+      run pmc_sq 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \
+        --kernel-include-regex "rq_fwd|rq_dist" -f csv -d "$O/pmc_sq" -o q -- python3 "$R/tools/pmc_quantize.py" 5 > "$O/pmc_sq.log" 2>&1
+      run pmc_sq2 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE \
+        --kernel-include-regex "rq_fwd|rq_dist" -f csv -d "$O/pmc_sq2" -o q -- python3 "$R/tools/pmc_quantize.py" 5 > "$O/pmc_sq2.log" 2>&1
+      cd "$R" ;;
     kern)
       run kern 300 python -u "$R/tools/bench_kernels.py" > "$O/kernels.jsonl" 2> "$O/kernels.err"
       cat "$O/kernels.jsonl" ;;
