@@ -247,7 +247,7 @@ def next_seed() -> int:
     if _SEED["base"] != base:
         _SEED["base"], _SEED["n"] = base, 0
     _SEED["n"] += 1
-    return (base * 0x9E3779B97F4A7C15 + _SEED["n"] * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
+    return (base * 0x9E3779B97F4A7C15 + _SEED["n"] * 0xD1B54A32D192ED03) & 0x7FFFFFFFFFFFFFFF   # fits int64
 
 
 def dropout_fusable(t: torch.Tensor) -> bool:
