@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-decoder", action="store_true", help="skip the data-parallel decoder measurement")
+    ap.add_argument("--no-tunable", action="store_true", help="library GEMMs on their default heuristic")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     return ap.parse_args()
@@ -172,6 +173,11 @@ def main():
     rk, ws, lr = dp.init_from_env()
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs an MI355X (no GPU visible)")
+    if not args.no_tunable:
+        # library GEMMs (fwd / data-grad) dispatched to the fastest measured hipBLASLt/rocBLAS
+        # solution per shape; shapes missing from the shipped table are tuned in the warmup
+        from rqvae_hip import gemm_tuning
+        gemm_tuning.enable()
     if args.decoder_only:
         print(json.dumps({"decoder_amazon": measure_decoder(torch.device("cuda", lr), ws, rk)}), flush=True)
         return
@@ -264,6 +270,7 @@ def main():
                      "traffic_detail": traffic if traffic else traffic_note,
                      "hbm_GBps_at_algorithmic_bytes": round(alg_bytes / (q_ms * 1e-3) / 1e9, 1)},
         "loss_last": round(loss, 5),
+        "gemm_selection": "default heuristic" if args.no_tunable else "TunableOp (rqvae_hip.gemm_tuning)",
     }
     if dec is not None:
         line["decoder_amazon"] = dec

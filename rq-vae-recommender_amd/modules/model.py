@@ -24,6 +24,7 @@ from modules.normalize import RMSNorm
 from modules.transformer.model import TransformerEncoderDecoder
 from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
 from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged
+from rqvae_hip import gemm_tuning
 
 
 class ModelOutput(NamedTuple):
@@ -79,7 +80,10 @@ class EncoderDecoderRetrievalModel(nn.Module):
         if fut_emb is not None:
             fut = torch.cat([fut, fut_emb + self.tte(batch.token_type_ids_fut)], dim=1)
         ctx_lengths = batch.seq_mask.sum(axis=1) + 1
-        ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1])          # one host sync (total)
+        # one host sync (total); with tuned library GEMMs the row count is bucketed so that the
+        # variable-length context presents a bounded set of GEMM shapes (rqvae_hip.gemm_tuning)
+        bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
+        ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1], row_bucket=bucket)
         nf = fut.shape[1]                                                                # fixed length: no sync
         fut_lengths = torch.full((B,), nf, device=fut.device, dtype=torch.int64)
         fut_j = padded_to_jagged(fut.contiguous(), fut_lengths, nf, total=B * nf, known_max=nf)

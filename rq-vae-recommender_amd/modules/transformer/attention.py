@@ -92,9 +92,10 @@ class MultiHeadAttention(nn.Module):
             jkv = as_jagged(x_kv)
             ctx = hip_ops.varlen_attention_packed(self.q(jx.values()), self.kv(jkv.values()), jx.offsets(),
                                                   jkv.offsets(), self.num_heads, bool(is_causal), jx.max_len,
-                                                  jkv.max_len)
+                                                  jkv.max_len, rows_q=jx.rows, rows_k=jkv.rows)
         else:
             ctx = hip_ops.varlen_attention_packed(self.qkv(jx.values()), None, jx.offsets(), jx.offsets(),
-                                                  self.num_heads, bool(is_causal), jx.max_len, jx.max_len)
+                                                  self.num_heads, bool(is_causal), jx.max_len, jx.max_len,
+                                                  rows_q=jx.rows, rows_k=jx.rows)
         out = self.proj(ctx)
         return jx.with_values(out) if isinstance(x, Jagged) else _wrap_like(out, x)

@@ -28,10 +28,13 @@ class Jagged:
     step on the host. Exposes ``values()`` / ``offsets()`` like an NJT; ``to_nested()`` converts.
     """
 
-    __slots__ = ("_values", "_offsets", "max_len", "min_len")
+    __slots__ = ("_values", "_offsets", "max_len", "min_len", "rows")
 
-    def __init__(self, values: Tensor, offsets: Tensor, max_len: int, min_len: int = 0):
+    def __init__(self, values: Tensor, offsets: Tensor, max_len: int, min_len: int = 0, rows: int = None):
         self._values, self._offsets, self.max_len, self.min_len = values, offsets, int(max_len), int(min_len)
+        # valid rows (= offsets[-1]); values may carry zero tail rows past it (row bucketing, see
+        # rqvae_hip.gemm_tuning), which every row-wise op carries along and attention ignores
+        self.rows = int(values.shape[0]) if rows is None else int(rows)
 
     def values(self) -> Tensor:
         return self._values
@@ -40,10 +43,10 @@ class Jagged:
         return self._offsets
 
     def with_values(self, values: Tensor) -> "Jagged":
-        return Jagged(values, self._offsets, self.max_len, self.min_len)
+        return Jagged(values, self._offsets, self.max_len, self.min_len, self.rows)
 
     def to_nested(self):
-        return torch.nested.nested_tensor_from_jagged(self._values, self._offsets, min_seqlen=self.min_len,
+        return torch.nested.nested_tensor_from_jagged(self._values[:self.rows], self._offsets, min_seqlen=self.min_len,
                                                       max_seqlen=self.max_len)
 
     @property
@@ -55,7 +58,7 @@ def as_jagged(x) -> Jagged:
     """NJT or Jagged -> Jagged (no copy)."""
     if isinstance(x, Jagged):
         return x
-    mx = getattr(x, "_maybe_max_seqlen", None)
+    mx = getattr(x, "_maybe_max_seqlen", None)  # NJT: values rows == offsets[-1]
     mn = getattr(x, "_maybe_min_seqlen", None)
     if mx is None:
         mx = x._get_max_seqlen()
@@ -63,9 +66,10 @@ def as_jagged(x) -> Jagged:
 
 
 def padded_to_jagged(x: Tensor, lengths: Tensor, max_len: int, total: int = None, add_one_sub_one: bool = True,
-                     known_max: int = None) -> Jagged:
+                     known_max: int = None, row_bucket: int = None) -> Jagged:
     """HIP padded -> jagged gather. `total` / `known_max` (host ints) skip the host sync when the
-    caller already knows them (e.g. fixed-length decoder inputs)."""
+    caller already knows them (e.g. fixed-length decoder inputs). `row_bucket`: allocate the values
+    with their row count rounded up to this multiple, tail rows zero (bounded set of GEMM shapes)."""
     assert x.dim() == 3 and x.is_contiguous()
     hip_ops.require_gpu(x, lengths, what="padded_to_jagged")
     B, N, _ = x.shape
@@ -75,8 +79,9 @@ def padded_to_jagged(x: Tensor, lengths: Tensor, max_len: int, total: int = None
         total, lmin, lmax = torch.stack([offsets[-1], lengths.clamp(0, n).min(), lengths.clamp(0, n).max()]).tolist()
     else:
         lmin = lmax = known_max if known_max is not None else n
-    values = hip_ops.PaddedToJaggedValues.apply(x, offsets, int(total), add_one_sub_one)
-    return Jagged(values, offsets, int(lmax), int(lmin))
+    alloc = int(total) if not row_bucket else (int(total) + row_bucket - 1) // row_bucket * row_bucket
+    values = hip_ops.PaddedToJaggedValues.apply(x, offsets, int(total), add_one_sub_one, alloc)
+    return Jagged(values, offsets, int(lmax), int(lmin), int(total))
 
 
 def padded_to_jagged_tensor(x: Tensor, lengths: Tensor, max_len: int):

@@ -392,11 +392,14 @@ class PaddedToJaggedValues(torch.autograd.Function):
     """values (T, D) of the NJT built by ops/triton/jagged.py:11-66; backward = :69-77."""
 
     @staticmethod
-    def forward(ctx, x, offsets, total: int, add_one_sub_one: bool):
+    def forward(ctx, x, offsets, total: int, add_one_sub_one: bool, alloc: int = None):
         require_gpu(x, offsets, what="padded_to_jagged")
         assert x.dim() == 3 and x.is_contiguous()
         B, N, D = x.shape
-        vals = torch.empty((total, D), device=x.device, dtype=x.dtype)
+        alloc = total if alloc is None else alloc
+        vals = torch.empty((alloc, D), device=x.device, dtype=x.dtype)
+        if alloc > total:
+            vals[total:].zero_()   # bucket tail rows (rqvae_hip.gemm_tuning)
         TIMER.around("jagged_from_padded", call, "jagged_from_padded", ptr(x), B, N, D, ptr(offsets), ptr(vals),
                      _DTYPES[x.dtype], int(add_one_sub_one), stream_handle(x.device))
         if TIMER.enabled:
@@ -415,7 +418,7 @@ class PaddedToJaggedValues(torch.autograd.Function):
                      _DTYPES[g_vals.dtype], stream_handle(g_vals.device))
         if TIMER.enabled:
             TIMER.bytes.setdefault("jagged_to_padded", []).append((g_vals.numel() + gx.numel()) * gx.element_size())
-        return gx, None, None, None
+        return gx, None, None, None, None
 
 
 class JaggedToPaddedValues(torch.autograd.Function):
@@ -487,7 +490,8 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
     output (row-strided), so autograd never concatenates the three chunk gradients."""
 
     @staticmethod
-    def forward(ctx, qsrc, kvsrc, cu_q, cu_k, num_heads: int, causal: bool, max_q: int, max_k: int, scale: float):
+    def forward(ctx, qsrc, kvsrc, cu_q, cu_k, num_heads: int, causal: bool, max_q: int, max_k: int, scale: float,
+                rows_q: int = None, rows_k: int = None):
         require_gpu(qsrc, cu_q, cu_k, what="varlen_attention")
         self_attn = kvsrc is None
         A = qsrc.shape[1] // 3 if self_attn else qsrc.shape[1]
@@ -506,11 +510,17 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         call("varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
              B, num_heads, hd, int(max_q), int(max_k), int(causal), float(scale), ptr(out), out.stride(0), ptr(lse), Tq,
              stream_handle(q.device))
+        # rows past the valid count (row-bucket tail) are never written by the kernels: keep them 0
+        rows_q = Tq if rows_q is None else int(rows_q)
+        rows_k = src_kv.shape[0] if rows_k is None else int(rows_k)
+        if rows_q < Tq:
+            out[rows_q:].zero_()
         if self_attn:
             ctx.save_for_backward(qsrc, out, lse, cu_q, cu_k)
         else:
             ctx.save_for_backward(qsrc, kvsrc, out, lse, cu_q, cu_k)
         ctx.cfg = (self_attn, A, num_heads, bool(causal), int(max_q), int(max_k), float(scale))
+        ctx.rows = (rows_q, rows_k)
         return out
 
     @staticmethod
@@ -535,15 +545,23 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
              out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
              int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), ptr(delta),
              stream_handle(q.device))
-        return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None
+        rows_q, rows_k = ctx.rows
+        if rows_q < gq_src.shape[0]:
+            gq_src[rows_q:].zero_()
+        if not self_attn and rows_k < gkv_src.shape[0]:
+            gkv_src[rows_k:].zero_()
+        return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None, None, None
 
 
-def varlen_attention_packed(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):
-    """qsrc = qkv (T, 3A) with kvsrc None (self-attention), or q (Tq, A) with kv (Tk, 2A) (cross)."""
+def varlen_attention_packed(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None, rows_q=None,
+                            rows_k=None):
+    """qsrc = qkv (T, 3A) with kvsrc None (self-attention), or q (Tq, A) with kv (Tk, 2A) (cross).
+    rows_q / rows_k: valid row counts when the buffers carry zero tail rows (row bucketing)."""
     A = qsrc.shape[1] // 3 if kvsrc is None else qsrc.shape[1]
     if scale is None:
         scale = 1.0 / math.sqrt(A // num_heads)
-    return PackedVarlenAttentionFunction.apply(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale)
+    return PackedVarlenAttentionFunction.apply(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale, rows_q,
+                                               rows_k)
 
 
 def varlen_attention(q, k, v, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):

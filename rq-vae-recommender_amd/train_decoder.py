@@ -22,7 +22,7 @@ from modules.model import EncoderDecoderRetrievalModel
 from modules.scheduler.inv_sqrt import InverseSquareRootScheduler
 from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
-from rqvae_hip import dp
+from rqvae_hip import dp, gemm_tuning
 
 
 @gin.configurable
@@ -43,6 +43,7 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     rank, world, local_rank = dp.init_from_env()
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
+    gemm_tuning.enable()   # fastest measured library GEMM per shape (RQVAE_TUNABLE_GEMM=0: heuristic)
     item_ds = ItemData(root=dataset_folder, dataset=dataset, data_path=data_path, seed=seed)
     train_ds = SeqData(root=dataset_folder, dataset=dataset, is_train=True, subsample=train_data_subsample,
                        data_path=data_path, seed=seed)

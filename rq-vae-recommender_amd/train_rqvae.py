@@ -26,7 +26,7 @@ from modules.quantize import QuantizeForwardMode
 from modules.rqvae import RqVae
 from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
-from rqvae_hip import dp
+from rqvae_hip import dp, gemm_tuning
 
 
 @gin.configurable
@@ -42,6 +42,7 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
     rank, world, local_rank = dp.init_from_env()
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
+    gemm_tuning.enable()   # fastest measured library GEMM per shape (RQVAE_TUNABLE_GEMM=0: heuristic)
 
     train_ds = ItemData(root=dataset_folder, dataset=dataset, train_test_split="train" if do_eval else "all",
                         data_path=data_path, seed=seed)

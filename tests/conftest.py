@@ -10,6 +10,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 for p in (ROOT, PKG, GOLDEN):
     if p not in sys.path:
         sys.path.insert(0, p)
+# library-GEMM tuning (rqvae_hip.gemm_tuning) times every candidate solution per new shape: the
+# suite's many tiny shapes would spend minutes tuning, so it runs on the default heuristic except
+# in the test that exercises the tuning itself
+os.environ.setdefault("RQVAE_TUNABLE_GEMM", "0")
 
 
 def pytest_configure(config):

@@ -114,9 +114,14 @@ def test_varlen_attention_deterministic(device):
         assert torch.equal(a, b)
 
 
-def test_decoder_model_vs_reference(golden, device):
+@pytest.mark.parametrize("bucket", [False, True])
+def test_decoder_model_vs_reference(golden, device, monkeypatch, bucket):
+    """Decoder fixture; `bucket` runs the context with its row count padded to the GEMM row bucket
+    (zero tail rows carried through every row-wise op, ignored by attention): same results."""
     from data.schemas import TokenizedSeqBatch
     from modules.model import EncoderDecoderRetrievalModel
+    from rqvae_hip import gemm_tuning
+    monkeypatch.setattr(gemm_tuning, "is_enabled", lambda: bucket)
     z = golden("decoder_small")
     E, A_, H, nl, K, L1, n_max, seed = (int(z[k]) for k in ("E", "A", "H", "n_layers", "K", "L1", "n_max", "seed"))
     model = EncoderDecoderRetrievalModel(embedding_dim=E, attn_dim=A_, dropout=0.0, num_heads=H, n_layers=nl,
@@ -139,6 +144,7 @@ def test_decoder_model_vs_reference(golden, device):
     assert np.abs(out.logits.detach().cpu().numpy() - z["logits"]).max() <= 2e-4 * scale
     assert np.allclose(out.loss_d.detach().cpu().numpy(), z["loss_d"], rtol=2e-5, atol=0)
     for name, p in model.named_parameters():
+        assert p.grad is None or bool(torch.isfinite(p.grad).all()), name
         key = "grad__" + name
         if key in z:
             ref = z[key]
