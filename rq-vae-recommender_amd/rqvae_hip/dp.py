@@ -32,11 +32,18 @@ def rank():
 
 def init_from_env(backend: Optional[str] = None):
     """Initialise torch.distributed from RANK / WORLD_SIZE / MASTER_* (torchrun env). Returns
-    (rank, world, local_rank). No-op for WORLD_SIZE=1."""
+    (rank, world, local_rank). No-op for WORLD_SIZE=1.
+
+    Rehearsal switches (one-GPU box): RQVAE_DIST_BACKEND=gloo selects the backend, and
+    RQVAE_SHARE_DEVICE=1 maps every rank to device 0 (RCCL refuses two ranks on one GPU, gloo
+    moves the CUDA tensors through the host), so the multi-rank code paths run end to end."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rk = int(os.environ.get("RANK", "0"))
     lr = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RQVAE_SHARE_DEVICE", "0") == "1":
+        lr = 0
     if ws > 1 and not dist.is_initialized():
+        backend = backend or os.environ.get("RQVAE_DIST_BACKEND")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":

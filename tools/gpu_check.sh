@@ -58,6 +58,11 @@ for s in $steps; do
       run pmc_sq2 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE \
         --kernel-include-regex "rq_fwd|rq_dist" -f csv -d "$O/pmc_sq2" -o q -- python3 "$R/tools/pmc_quantize.py" 5 > "$O/pmc_sq2.log" 2>&1
       cd "$R" ;;
+    dp2)   # two ranks sharing the one GPU over gloo: exercises every multi-rank code path of bench.py
+      RQVAE_DIST_BACKEND=gloo RQVAE_SHARE_DEVICE=1 run dp2 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$R/bench.py" --gpus 2 --steps 5 --warmup 3 \
+        > "$O/bench_dp2.json" 2> "$O/bench_dp2.err"
+      cat "$O/bench_dp2.json" ;;
     kern)
       run kern 300 python -u "$R/tools/bench_kernels.py" > "$O/kernels.jsonl" 2> "$O/kernels.err"
       cat "$O/kernels.jsonl" ;;
