@@ -876,6 +876,212 @@ rq_fwd_reg_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// D = 64, whole level codebook resident in LDS, large B: the register kernel rebuilt on
+// v_mfma_f32_16x16x4_f32 with 16 items per wave. Lane (j = lane & 15, g = lane >> 4) holds item
+// j's 16 columns {16q + 4g + i : q, i < 4}, which is its B-operand fragment for k-step (q, i)
+// (lane group g supplies k = g; the same k permutation on both operands). Each 16-row tile's
+// distances land 4 per lane (codewords t0 + 4g + r of item j); the four lane groups merge with
+// two xor shuffles at the end of the level. Compared with the 32x32x2 kernel this halves the
+// per-lane row state (16 floats), so the kernel fits 4 waves per SIMD (8-wave workgroups sharing
+// one 64 KiB LDS-DMA-filled codebook image, two per CU) and two independent accumulator chains
+// per wave cover the 16x16x4 dependent-issue latency. The codebook image is XOR-swizzled by
+// (row & 15): with the (q, g) column order the 16 rows of a ds_read_b128 lane group hit 16
+// distinct 4-bank groups.
+constexpr int kR16Items = 128;   // items per 8-wave workgroup
+
+__global__ void __launch_bounds__(512, 2)
+rq_fwd_r16_kernel(const float* __restrict__ x, int B, const float* __restrict__ cbs, const float* __restrict__ csq,
+                  int K, int L, int mode, float beta, int64_t* __restrict__ ids, float* __restrict__ emb_out,
+                  float* __restrict__ res, float* __restrict__ qloss, float* __restrict__ emb_sum) {
+  constexpr int D = 64, QD = 16;
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  const int KP = (K + 31) & ~31;                     // rows padded to whole tile pairs
+  float* A_s = dsm;                                  // [KP][64] swizzled codeword image
+  float* cs_s = dsm + KP * D;                        // [KP] |c|^2 (+inf past K)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int j = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x * kR16Items + wave * 16 + j;
+  const bool valid = b < B;
+  const int64_t BD = (int64_t)B * D;
+  const int64_t ob = (int64_t)(valid ? b : 0) * D + 4 * g;   // + 16 q for column block q
+  float xv[QD], es[QD], pend[QD];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = valid ? *reinterpret_cast<const float4*>(x + ob + 16 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < QD; ++k) es[k] = 0.f;
+  float ql = 0.f;
+  auto store_row = [&](float* dst, const float (&v)[QD]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(dst + ob + 16 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  };
+  auto rsum = [](float v) {   // sum over the item's four lane groups
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+  };
+
+  for (int l = 0; l < L; ++l) {
+    const float* cb = cbs + (int64_t)l * K * D;
+    float xs = 0.f;
+#pragma unroll
+    for (int k = 0; k < QD; ++k) xs = __builtin_fmaf(xv[k], xv[k], xs);
+    xs = rsum(xs);
+    __syncthreads();   // previous level's image fully consumed (incl. epilogue codeword reads)
+    // LDS-DMA: wave-instruction q moves rows 4q..4q+3 (1 KiB); lane i lands at chunk i%16 of row
+    // 4q + i/16, i.e. loads logical chunk (i%16) ^ (row & 15) of that row (rows past K clamp)
+    for (int q = wave; q < KP / 4; q += 8) {
+      const int row = 4 * q + (lane >> 4);
+      const int c = (lane & 15) ^ (row & 15);
+      __builtin_amdgcn_global_load_lds(cb + (int64_t)min(row, K - 1) * D + 4 * c, A_s + q * 256, 16, 0, 0);
+    }
+    for (int r = tid; r < KP; r += 512) cs_s[r] = r < K ? csq[(int64_t)l * K + r] : INFINITY;
+    __syncthreads();
+    if (valid && g < 4 && l > 0) {   // deferred stores of the previous level (drain under the MFMAs)
+      store_row(res + (int64_t)l * BD, xv);
+      store_row(emb_out + (int64_t)(l - 1) * BD, pend);
+    } else if (valid && l == 0) {
+      store_row(res, xv);
+    }
+    float best_d = INFINITY;
+    int best_i = 0;
+    // dist = fma(-2, x.c, |x|^2 + |c|^2): 2 x.c is exact, so this is the reference expression's
+    // rounding; the tile's best (d, r) is merged once per tile, tiles in increasing order
+    auto scan = [&](const floatx4v& a, const float4& c, int t0) {
+      const float cr[4] = {c.x, c.y, c.z, c.w};
+      float td = INFINITY;
+      int tr = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = __builtin_fmaf(-2.f, a[r], xs + cr[r]);
+        const bool lt = d < td;
+        td = lt ? d : td;
+        tr = lt ? r : tr;
+      }
+      const bool lt = td < best_d;
+      best_d = lt ? td : best_d;
+      best_i = lt ? t0 + 4 * g + tr : best_i;
+    };
+    for (int t0 = 0; t0 < KP; t0 += 32) {
+      floatx4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const int r0 = t0 + j, r1 = t0 + 16 + j;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * q + g;
+        const float4 a0 = *reinterpret_cast<const float4*>(A_s + r0 * D + 4 * (c ^ (r0 & 15)));
+        const float4 a1 = *reinterpret_cast<const float4*>(A_s + r1 * D + 4 * (c ^ (r1 & 15)));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, xv[4 * q], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, xv[4 * q], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, xv[4 * q + 1], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, xv[4 * q + 1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, xv[4 * q + 2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, xv[4 * q + 2], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, xv[4 * q + 3], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, xv[4 * q + 3], acc1, 0, 0, 0);
+      }
+      const float4 c0 = *reinterpret_cast<const float4*>(cs_s + t0 + 4 * g);
+      const float4 c1 = *reinterpret_cast<const float4*>(cs_s + t0 + 16 + 4 * g);
+      scan(acc0, c0, t0);
+      scan(acc1, c1, t0 + 16);
+    }
+#pragma unroll
+    for (int s = 16; s <= 32; s <<= 1) {   // merge the four lane groups (lowest index on ties)
+      const float od = __shfl_xor(best_d, s, 64);
+      const int oi = __shfl_xor(best_i, s, 64);
+      if (od < best_d || (od == best_d && oi < best_i)) { best_d = od; best_i = oi; }
+    }
+    const int id = best_i;
+    float ev[QD];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c = *reinterpret_cast<const float4*>(A_s + id * D + 4 * ((4 * q + g) ^ (id & 15)));
+      ev[4 * q] = c.x; ev[4 * q + 1] = c.y; ev[4 * q + 2] = c.z; ev[4 * q + 3] = c.w;
+    }
+    float e2 = 0.f, dl = 0.f;
+#pragma unroll
+    for (int k = 0; k < QD; ++k) {
+      e2 = __builtin_fmaf(ev[k], ev[k], e2);
+      const float t = xv[k] - ev[k];
+      dl = __builtin_fmaf(t, t, dl);
+    }
+    e2 = rsum(e2);
+    dl = rsum(dl);
+    float out[QD];
+    if (mode == kRotation) {
+      const float xn = sqrtf(xs), en = sqrtf(e2);
+      const float xd = xn + 1e-8f, ed = en + 1e-8f;
+      const float rx = 1.0f / xd, re = 1.0f / ed;
+      float mnx = INFINITY, mxx = 0.f, mne = INFINITY, mxe = 0.f;
+#pragma unroll
+      for (int k = 0; k < QD; ++k) {
+        mnx = fminf(mnx, fabsf(xv[k])); mxx = fmaxf(mxx, fabsf(xv[k]));
+        mne = fminf(mne, fabsf(ev[k])); mxe = fmaxf(mxe, fabsf(ev[k]));
+      }
+      // per-lane choice: either branch yields the correctly rounded quotient
+      const bool fast = div_rn_ok(mnx, mxx, xd) && div_rn_ok(mne, mxe, ed);
+      float u[QD], qv[QD];
+      float s2 = 0.f, eu = 0.f, mns = INFINITY, mxs = 0.f;
+#pragma unroll
+      for (int k = 0; k < QD; ++k) {
+        u[k] = fast ? div_rn(xv[k], xd, rx) : xv[k] / xd;
+        qv[k] = fast ? div_rn(ev[k], ed, re) : ev[k] / ed;
+        const float sk = u[k] + qv[k];
+        out[k] = sk;
+        s2 = __builtin_fmaf(sk, sk, s2);
+        eu = __builtin_fmaf(xv[k], u[k], eu);
+        mns = fminf(mns, fabsf(sk)); mxs = fmaxf(mxs, fabsf(sk));
+      }
+      s2 = rsum(s2);
+      eu = rsum(eu);
+      const float sn = fmaxf(sqrtf(s2), 1e-6f), rs = 1.0f / sn;
+      const bool fast_w = div_rn_ok(mns, mxs, sn);
+      float ew = 0.f;
+#pragma unroll
+      for (int k = 0; k < QD; ++k) {
+        out[k] = fast_w ? div_rn(out[k], sn, rs) : out[k] / sn;   // w
+        ew = __builtin_fmaf(xv[k], out[k], ew);
+      }
+      ew = rsum(ew);
+      const float lam = en / (xn + 1e-6f);
+      const float m2ew = -2.f * ew, p2eu = 2.f * eu;
+      // (x - 2 (x.w) w + 2 (x.u) q) * lam   (quantize.py:41-45,140-142)
+#pragma unroll
+      for (int k = 0; k < QD; ++k) out[k] = __builtin_fmaf(p2eu, qv[k], __builtin_fmaf(m2ew, out[k], xv[k])) * lam;
+    } else if (mode == kSte) {
+#pragma unroll
+      for (int k = 0; k < QD; ++k) out[k] = xv[k] + (ev[k] - xv[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < QD; ++k) out[k] = ev[k];
+    }
+    ql = ql + (dl + beta * dl);
+    if (valid && g == 0) ids[(int64_t)b * L + l] = id;
+#pragma unroll
+    for (int k = 0; k < QD; ++k) {
+      pend[k] = out[k];
+      es[k] = es[k] + out[k];
+      xv[k] = xv[k] - out[k];   // next level's residual stays in registers
+    }
+  }
+  if (valid) {
+    store_row(emb_out + (int64_t)(L - 1) * BD, pend);
+    if (g == 0) qloss[b] = ql;
+    if (emb_sum != nullptr) store_row(emb_sum, es);
+  }
+}
+
+static int launch_fwd_r16(int B, hipStream_t s, const float* x, const float* cbs, const float* csq, int K, int L,
+                          int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
+  const int KP = (K + 31) & ~31;
+  const size_t lds = (size_t)KP * (64 + 1) * sizeof(float);
+  hipLaunchKernelGGL(rq_fwd_r16_kernel, dim3((B + kR16Items - 1) / kR16Items), dim3(512), lds, s, x, B, cbs, csq, K, L,
+                     mode, beta, ids, eo, res, ql, es);
+  return 0;
+}
+
 template <int D, int WPI>
 static void launch_fwd_reg_w(int B, hipStream_t s, const float* x, const float* cbs, const float* csq, int K, int L,
                              int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
@@ -1279,10 +1485,17 @@ int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* code
   hipStream_t s = (hipStream_t)stream;
   dim3 g((unsigned)((B + kTB - 1) / kTB));
   const int b = (int)B, d = (int)D, k = (int)K, l = (int)L;
-  RQ_CHECK_ARG(impl >= 0 && impl <= 3,
-               "rq_quantize_fwd_impl: impl must be 0 (auto), 1 (tiled), 2 (register) or 3 (split)");
+  RQ_CHECK_ARG(impl >= 0 && impl <= 4,
+               "rq_quantize_fwd_impl: impl must be 0 (auto), 1 (tiled), 2 (register), 3 (split) or 4 (register 16x16)");
   const bool split_ok = D >= 128 && 2 * ((K + kSN - 1) / kSN) + 1 <= D;
-  if (impl == 0) impl = D <= 64 ? 2 : (split_ok ? 3 : 1);
+  const bool r16_ok = D == 64 && K <= 288;   // two 65 * K * 4-byte images per CU
+  if (impl == 0) impl = (r16_ok && B >= 32768) ? 4 : D <= 64 ? 2 : (split_ok ? 3 : 1);
+  RQ_CHECK_ARG(impl != 4 || r16_ok, "rq_quantize_fwd_impl: 16x16 register kernel needs D == 64 and K <= 288");
+  if (impl == 4) {
+    launch_fwd_r16(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum);
+    RQ_LAUNCH_CHECK("rq_quantize_fwd(register 16x16)");
+    return 0;
+  }
   RQ_CHECK_ARG(impl != 2 || D <= 64, "rq_quantize_fwd_impl: register kernel needs D <= 64");
   RQ_CHECK_ARG(impl != 3 || split_ok, "rq_quantize_fwd_impl: split path needs D >= 128 and 2*ceil(K/128)+1 <= D");
   if (impl == 3) {

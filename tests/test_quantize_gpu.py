@@ -191,9 +191,11 @@ def test_train_step_matches_oracle_trace(golden, device):
         assert float(out.loss) == pytest.approx(float(ref["loss"]), rel=1e-4)
 
 
-@pytest.mark.parametrize("B,D,K,L", [(5000, 64, 256, 3), (3001, 32, 256, 3), (777, 16, 40, 2), (2048, 64, 3000, 2)])
+@pytest.mark.parametrize("B,D,K,L", [(5000, 64, 256, 3), (3001, 32, 256, 3), (777, 16, 40, 2), (2048, 64, 3000, 2),
+                                     (40000, 64, 256, 3), (1000, 64, 100, 4), (131, 64, 288, 1)])
 def test_tiled_and_register_kernels_agree(device, B, D, K, L):
-    """Both forward kernels (LDS-tiled impl 1, register-resident impl 2) vs the oracle."""
+    """Forward kernels (LDS-tiled impl 1, register-resident 32x32 impl 2, 16x16 impl 4 for D=64 with
+    K <= 288) vs the oracle, ragged B and K included."""
     from rqvae_hip._lib import call, ptr, stream_handle
     g = gi.rng(B + 5 * D + K)
     x = (g.standard_normal((B, D), dtype=np.float32) / np.sqrt(D)).astype(np.float32)
@@ -202,14 +204,15 @@ def test_tiled_and_register_kernels_agree(device, B, D, K, L):
     xt, ct = torch.from_numpy(x).to(device), torch.from_numpy(cbs).to(device)
     csq = (ct * ct).sum(-1).contiguous()
     outs = {}
-    for impl in (1, 2):
+    impls = (1, 2, 4) if (D == 64 and K <= 288) else (1, 2)
+    for impl in impls:
         o = dict(ids=torch.empty(B, L, dtype=torch.int64, device=device), emb=torch.empty(L, B, D, device=device),
                  res=torch.empty(L, B, D, device=device), ql=torch.empty(B, device=device),
                  es=torch.empty(B, D, device=device))
         call("rq_quantize_fwd_impl", ptr(xt), B, D, ptr(ct), ptr(csq), K, L, 3, 0.25, ptr(o["ids"]), ptr(o["emb"]),
              ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle(device))
         outs[impl] = {k: v.cpu().numpy() for k, v in o.items()}
-    for impl in (1, 2):
+    for impl in impls:
         o = outs[impl]
         ok = (o["ids"] == f["ids"]).all(1)
         assert ok.mean() > 0.998, (impl, ok.mean())

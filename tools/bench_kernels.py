@@ -71,7 +71,7 @@ def main():
               (16384, 1024, 2048, 4), (65536, 1024, 2048, 4), (65536, 256, 1024, 3)]
     for (B, D, K, L) in shapes:
         x, cbs, csq, o = quantize_case(B, D, K, L, dev)
-        impls = [1, 2] if D <= 64 else [1, 3]
+        impls = ([1, 2, 4] if D == 64 and K <= 288 else [1, 2]) if D <= 64 else [1, 3]
         ref = None
         for impl in impls:
             run_impl(x, cbs, csq, o, impl)
