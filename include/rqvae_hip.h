@@ -53,10 +53,11 @@ int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks
                     float* emb_sum, void* stream);
 
 /* Same as rq_quantize_fwd with an explicit kernel choice (benchmarking / A-B testing):
- * impl 0 = auto (2 for D <= 64, else 3 when allowed, else 1), 1 = fused LDS-tiled kernel (any D),
- * 2 = register-resident kernel (D <= 64), 3 = split path for D >= 128 with 2*ceil(K/128)+1 <= D
- * (per level: distance GEMM + partial argmin over 128x128 tiles, then a row epilogue; emb_out
- * doubles as the level's scratch before it is written). */
+ * impl 0 = auto (4 for D == 64, K <= 288, B >= 32768; else 2 for D <= 64; else 3 when allowed;
+ * else 1), 1 = fused LDS-tiled kernel (any D), 2 = register-resident 32x32x2 kernel (D <= 64),
+ * 3 = split path for D >= 128 with 2*ceil(K/128)+1 <= D (per level: distance GEMM + partial argmin
+ * over 128x128 tiles, then a row epilogue; emb_out doubles as the level's scratch before it is
+ * written), 4 = register-resident 16x16x4 kernel (D == 64, K <= 288; 4 waves per SIMD). */
 int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
                          int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
                          float* qloss, float* emb_sum, int impl, void* stream);
@@ -140,6 +141,13 @@ int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, 
                         void* stream);
 int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
                         int64_t C, float* g_pre, void* stream);
+
+/* RqVae.forward statistics (modules/rqvae.py:151-162):
+ *   rq_row_norms   out[r] = |x_r|_2 for rows (rows, D), D % 4 == 0 — embs_norm = emb.norm(dim=-1)
+ *   rq_loss_means  out[3] = {mean(recon + qloss), mean(recon), mean(qloss)} over B rows, one
+ *                  deterministic pass (the loss and the two logged components). */
+int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream);
+int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out, void* stream);
 
 /* Jagged (NJT) conversion — ops/triton/jagged.py. dtype: 0 fp32, 1 bf16, 2 fp16.
  * jagged_offsets: offsets (B+1) int64 = [0, cumsum(clamp(lengths, 0, N))]   (jagged.py:30-33)

@@ -237,6 +237,52 @@ __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict
   }
 }
 
+// Row L2 norms: out[r] = sqrt(sum_d x[r][d]^2), one wave per row (the RqVae embs_norm statistic,
+// modules/rqvae.py:155: emb.norm(dim=-1) over (L, B, D) embeddings in one pass).
+__global__ void __launch_bounds__(256) row_norm_kernel(const float* __restrict__ x, int64_t rows, int D,
+                                                       float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* p = x + r * D;
+  float s = 0.f;
+  for (int c = lane * 4; c < D; c += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(p + c);
+    s = __builtin_fmaf(v.x, v.x, s);
+    s = __builtin_fmaf(v.y, v.y, s);
+    s = __builtin_fmaf(v.z, v.z, s);
+    s = __builtin_fmaf(v.w, v.w, s);
+  }
+  s = group_sum<64>(s);
+  if (lane == 0) out[r] = sqrtf(s);
+}
+
+// The three scalar losses of RqVae.forward (modules/rqvae.py:151-162) in one pass over (B,) vectors:
+// out = {mean(recon + qloss), mean(recon), mean(qloss)}; one 1024-thread workgroup, each thread a
+// strided slice, then a fixed-order tree in LDS (deterministic).
+__global__ void __launch_bounds__(1024) loss_means_kernel(const float* __restrict__ recon,
+                                                          const float* __restrict__ ql, int64_t B,
+                                                          float* __restrict__ out) {
+  __shared__ float red[3][1024];
+  const int t = threadIdx.x;
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int64_t i = t; i < B; i += 1024) {
+    const float r = recon[i], q = ql[i];
+    a += r + q;
+    b += r;
+    c += q;
+  }
+  red[0][t] = a; red[1][t] = b; red[2][t] = c;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (t < o) {
+      red[0][t] += red[0][t + o]; red[1][t] += red[1][t + o]; red[2][t] += red[2][t + o];
+    }
+    __syncthreads();
+  }
+  if (t < 3) out[t] = red[t][0] / (float)B;
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -276,6 +322,23 @@ int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, co
 #undef L2R_CASE
   }
   RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd");
+  return 0;
+}
+
+int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream) {
+  RQ_CHECK_ARG(rows >= 0 && D > 0 && D % 4 == 0, "rq_row_norms: need D %% 4 == 0");
+  if (rows == 0) return 0;
+  RQ_CHECK_ARG(x && out, "rq_row_norms: null pointer");
+  hipLaunchKernelGGL(row_norm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, rows,
+                     (int)D, out);
+  RQ_LAUNCH_CHECK("rq_row_norms");
+  return 0;
+}
+
+int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out, void* stream) {
+  RQ_CHECK_ARG(B > 0 && recon && qloss && out, "rq_loss_means: bad arguments");
+  hipLaunchKernelGGL(loss_means_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, recon, qloss, B, out);
+  RQ_LAUNCH_CHECK("rq_loss_means");
   return 0;
 }
 

@@ -148,9 +148,10 @@ class RqVae(nn.Module):
             if n > 0:   # the reference's cat is a no-op for n == 0 (SURVEY A-10)
                 x_hat = torch.cat([l2norm(x_hat[..., :-n]), x_hat[..., -n:]], axis=-1)
             reconstruction = self.reconstruction_loss(x_hat, x)
-        loss = (reconstruction + qloss).mean()
+        # loss = mean(recon + qloss) and the two logged means in one deterministic pass
+        loss, recon_mean, rq_mean = hip_ops.loss_means(reconstruction, qloss)
         with torch.no_grad():
-            embs_norm = emb.norm(dim=-1).T
+            embs_norm = hip_ops.row_norms(emb).T     # emb.norm(dim=-1) over (L, B, D)
             p_unique_ids = hip_ops.unique_count(ids, self.codebook_size).to(torch.float32) / ids.shape[0]
-        return RqVaeComputedLosses(loss=loss, reconstruction_loss=reconstruction.mean(), rqvae_loss=qloss.mean(),
+        return RqVaeComputedLosses(loss=loss, reconstruction_loss=recon_mean, rqvae_loss=rq_mean,
                                    embs_norm=embs_norm, p_unique_ids=p_unique_ids)

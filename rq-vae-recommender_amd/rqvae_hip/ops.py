@@ -396,6 +396,43 @@ def l2norm_recon_loss(pre, x):
     return L2NormReconFunction.apply(pre, x)
 
 
+def row_norms(x: torch.Tensor) -> torch.Tensor:
+    """|x_r|_2 over the last axis (no grad): one HBM pass (rq_row_norms)."""
+    require_gpu(x, what="row_norms")
+    x = x.detach().contiguous()
+    D = x.shape[-1]
+    out = torch.empty(x.shape[:-1], device=x.device, dtype=torch.float32)
+    call("rq_row_norms", ptr(x), x.numel() // D, D, ptr(out), stream_handle(x.device))
+    return out
+
+
+class LossMeansFunction(torch.autograd.Function):
+    """(mean(recon + qloss), mean(recon), mean(qloss)) in one deterministic pass; backward
+    broadcasts (g0 + g1) / B to recon and (g0 + g2) / B to qloss."""
+
+    @staticmethod
+    def forward(ctx, recon, qloss):
+        require_gpu(recon, qloss, what="loss_means")
+        recon, qloss = recon.contiguous(), qloss.contiguous()
+        out = torch.empty((3,), device=recon.device, dtype=torch.float32)
+        call("rq_loss_means", ptr(recon), ptr(qloss), recon.numel(), ptr(out), stream_handle(recon.device))
+        ctx.B = recon.numel()
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, g0, g1, g2):
+        z = torch.zeros((), device=g0.device if g0 is not None else g1.device)
+        g0 = z if g0 is None else g0
+        g1 = z if g1 is None else g1
+        g2 = z if g2 is None else g2
+        B = ctx.B
+        return ((g0 + g1) / B).expand(B), ((g0 + g2) / B).expand(B)
+
+
+def loss_means(recon, qloss):
+    return LossMeansFunction.apply(recon, qloss)
+
+
 # --------------------------------------------------------------------------------- jagged
 def jagged_offsets(lengths: torch.Tensor, N: int) -> torch.Tensor:
     require_gpu(lengths, what="jagged_offsets")
