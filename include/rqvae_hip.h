@@ -126,6 +126,20 @@ size_t rq_linear_wgrad_workspace(int64_t Bn, int64_t O, int64_t I);
 int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, int64_t Bn, int64_t O, int64_t I,
                     float* dW, float* db, void* workspace, size_t ws_bytes, void* stream);
 
+/* fp32 GEMM at PyTorch's 'high' matmul precision, which the reference selects at import
+ * (modules/rqvae.py:19, modules/model.py:27): each operand split as a = hi + lo in bf16, products
+ * hi.hi + hi.lo + lo.hi accumulated in fp32 on bf16 MFMA (per-product relative error <= ~2^-17;
+ * TF32's is 2^-11). Replaces the nn.Linear matmuls of modules/encoder.py:7-36 and
+ * modules/transformer/* (forward x W^T, data grad g W, weight grad g^T x).
+ *   C[m*ldc + n] = sum_k A(m,k) B(n,k),  A(m,k) = a_kcontig ? A[m*lda + k] : A[k*lda + m],
+ *                                         B(n,k) = b_kcontig ? B[n*ldb + k] : B[k*ldb + n].
+ * M, N, K and leading dims % 4 == 0, 16-byte aligned pointers. When the output tiles cannot fill
+ * the GPU, K is split across workgroups with a fixed-order reduction (deterministic); that case
+ * needs ldc == N and workspace >= rq_gemm_bf16x3_workspace(M, N, K) bytes (0 = no split). */
+size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K);
+int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
+                   int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream);
+
 /* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
  * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */

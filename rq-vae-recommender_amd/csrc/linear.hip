@@ -47,22 +47,36 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
 
   constexpr int kF = kWBK * kWT / 4 / 256;   // float4 per thread per operand per stage
   float4 ra[kF], rb[kF];
+  bool okm[kF];
+  // Branch-free staging: every load is issued (a guarded load compiles to a branch around it and
+  // a vmcnt(0) per element). Rows past the chunk read row b_lo and are zeroed by a select (they
+  // would add into valid outputs); columns past O / I are clamped in range and left as they are —
+  // they only feed output rows / columns >= O / I, which are never written.
+  const int scol = (tid & 31) * 4;
+  const int64_t gcol = min(o0 + scol, O - 4), xcol = min(i0 + scol, I - 4);
   auto load = [&](int64_t b0) {
 #pragma unroll
     for (int j = 0; j < kF; ++j) {
-      const int f = tid + 256 * j, r = f >> 5, c = (f & 31) * 4;
+      const int r = (tid >> 5) + 8 * j;
       const int64_t b = b0 + r;
       const bool okb = b < b_hi;
-      ra[j] = (okb && o0 + c < O) ? *reinterpret_cast<const float4*>(g + b * ldg + o0 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      rb[j] = (okb && i0 + c < I) ? *reinterpret_cast<const float4*>(x + b * ldx + i0 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int64_t bb = okb ? b : b_lo;
+      ra[j] = *reinterpret_cast<const float4*>(g + bb * ldg + gcol);
+      rb[j] = *reinterpret_cast<const float4*>(x + bb * ldx + xcol);
+      okm[j] = okb;
     }
   };
+  // The zero-select happens here, after the loads have landed (a select right after the load
+  // would wait for it); per component, since a whole-float4 select lowers through scratch.
   auto stash = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < kF; ++j) {
       const int f = tid + 256 * j, r = f >> 5, c = (f & 31) * 4;
-      *reinterpret_cast<float4*>(&As[buf][r][c]) = ra[j];
-      *reinterpret_cast<float4*>(&Bs[buf][r][c]) = rb[j];
+      const bool k = okm[j];
+      const float4 a = make_float4(k ? ra[j].x : 0.f, k ? ra[j].y : 0.f, k ? ra[j].z : 0.f, k ? ra[j].w : 0.f);
+      const float4 v = make_float4(k ? rb[j].x : 0.f, k ? rb[j].y : 0.f, k ? rb[j].z : 0.f, k ? rb[j].w : 0.f);
+      *reinterpret_cast<float4*>(&As[buf][r][c]) = a;
+      *reinterpret_cast<float4*>(&Bs[buf][r][c]) = v;
     }
   };
 
@@ -82,15 +96,30 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
   for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
     if (st + 1 < nst) load(b_lo + (int64_t)(st + 1) * kWBK);   // in flight during the MFMAs
+    // LDS operand pipeline: the two reads for k-pair kp+1 are issued ahead of k-pair kp's four
+    // MFMAs (sched_group_barrier pins that order), so no MFMA group waits on its own ds_read.
+    // A[o][k] = g[b][o], B[k][i] = x[b][i].
+    float2 a = *reinterpret_cast<const float2*>(&As[buf][h][wo * 64 + 2 * c32]);
+    float2 v = *reinterpret_cast<const float2*>(&Bs[buf][h][wi * 64 + 2 * c32]);
 #pragma unroll
     for (int kp = 0; kp < kWBK / 2; ++kp) {
-      const int k = 2 * kp + h;   // A[o][k] = g[b][o], B[k][i] = x[b][i]
-      const float2 a = *reinterpret_cast<const float2*>(&As[buf][k][wo * 64 + 2 * c32]);
-      const float2 v = *reinterpret_cast<const float2*>(&Bs[buf][k][wi * 64 + 2 * c32]);
+      float2 an = a, vn = v;
+      if (kp + 1 < kWBK / 2) {
+        const int k = 2 * (kp + 1) + h;
+        an = *reinterpret_cast<const float2*>(&As[buf][k][wo * 64 + 2 * c32]);
+        vn = *reinterpret_cast<const float2*>(&Bs[buf][k][wi * 64 + 2 * c32]);
+      }
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, v.x, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, v.y, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, v.x, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, v.y, acc[1][1], 0, 0, 0);
+      a = an;
+      v = vn;
+    }
+#pragma unroll
+    for (int kp = 0; kp < kWBK / 2; ++kp) {
+      if (kp + 1 < kWBK / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next k-pair's reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                          // this k-pair's MFMAs
     }
     if (do_bias) {
 #pragma unroll
@@ -191,6 +220,261 @@ static WgradPlan wgrad_plan(int64_t Bn, int64_t O, int64_t I) {
   return p;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 ("bf16x3") GEMM: the fp32 matmul at torch.set_float32_matmul_precision('high'),
+// which the reference selects at import (modules/rqvae.py:19, modules/model.py:27). PyTorch
+// defines 'high' as TF32 or "each float32 as the sum of two bfloat16 numbers"; gfx950 has no
+// xf32 MFMA, so this is the second form on v_mfma_f32_32x32x16_bf16: a = a_hi + a_lo with
+// a_hi = RN_bf16(a), a_lo = RN_bf16(a - a_hi) (the subtraction is exact), and
+//   a.b ~ a_hi.b_hi + a_hi.b_lo + a_lo.b_hi        (fp32 accumulation; a_lo.b_lo dropped)
+// — per-product relative error <= ~2^-17 (TF32: 2^-11), at 3 bf16 MFMAs per product = 5.3x the
+// f32-MFMA rate. 'highest' keeps the exact-f32 path (library GEMM + wgrad_partial_kernel).
+//
+//   C[m][n] = sum_k A(m, k) B(n, k)
+//   A(m, k) = A[m*lda + k] (a_kc: k-contiguous) or A[k*lda + m] (m-contiguous); B likewise.
+//   forward  y = x W^T : A = x (k-contig),  B = W (k-contig)
+//   dgrad   dx = g W   : A = g (k-contig),  B(n=i, k=o) = W[o][i] (n-contig)
+//   wgrad   dW = g^T x : A(m=o, k=b) = g[b][o], B(n=i, k=b) = x[b][i] (both m/n-contig), split-K
+//
+// Tile 128 x 128 x 32 per workgroup (4 waves, 64 x 64 each = 2 x 2 MFMA tiles). Operands are
+// converted to (hi, lo) bf16 planes while staged into LDS (register staging, double-buffered):
+//   k-contig operand -> "row image" [128 rows][32 k] (64-B rows, 16-B chunk c stored at
+//                       c ^ ((row >> 2) & 3)): fragments by conflict-free ds_read_b128;
+//   m/n-contig       -> "column image" [32 k][128 rows] (256-B rows, chunk XOR
+//                       ((k & 3) << 2 | (k >> 2) & 3)): fragments by ds_read_b64_tr_b16 (the
+//                       hardware transpose read), conflict-free per 32-lane half.
+// Both images come from coalesced float4 loads in the operand's HBM layout.
+// ---------------------------------------------------------------------------------------------
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+constexpr int kXT = 128;                       // output tile (m and n)
+constexpr int kXK = 32;                        // k per LDS stage
+constexpr int kXPlane = kXT * kXK * 2;         // bytes of one bf16 plane (8 KiB)
+constexpr int kXOp = 2 * kXPlane;              // hi + lo planes of one operand
+constexpr int kXBuf = 2 * kXOp;                // A + B
+constexpr int kXLds = 2 * kXBuf;               // double buffer: 64 KiB
+
+// (a, b) -> packed bf16 (hi) and packed bf16 of the exact remainders (lo), round-to-nearest-even.
+__device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const f32x2_t v = {a, b};
+  const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+  const f32x2_t hf = {__builtin_bit_cast(float, hb << 16), __builtin_bit_cast(float, hb & 0xffff0000u)};
+  const f32x2_t r = v - hf;
+  hi = hb;
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
+}
+
+__device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+
+// One operand's staging registers: 4 float4 per thread per stage (a 128 x 32 tile / 256 threads).
+template <bool KC>
+struct XStage {
+  float4 v[4];
+  bool ok[4];
+
+  // rows [r0, r0 + 128) of the operand (clamped to R - 1: they feed only outputs >= R, never
+  // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time.
+  __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int r0, int R, int64_t kb,
+                                       int64_t k_lo, int64_t k_hi, int tid) {
+    if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8 (2 float4 each)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = (tid >> 2) + 64 * (j >> 1);
+        const int64_t row = min(r0 + rr, R - 1);
+        const int64_t k = kb + (tid & 3) * 8 + 4 * (j & 1);
+        ok[j] = k < k_hi;
+        v[j] = *reinterpret_cast<const float4*>(X + row * ld + (ok[j] ? k : k_lo));
+      }
+    } else {              // thread: 4 consecutive rows (tid % 32) * 4, k rows tid/32 + 8j
+      const int64_t col = min(r0 + 4 * (tid & 31), R - 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t k = kb + (tid >> 5) + 8 * j;
+        ok[j] = k < k_hi;
+        v[j] = *reinterpret_cast<const float4*>(X + (ok[j] ? k : k_lo) * ld + col);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, int tid) const {
+    float4 w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool k = ok[j];
+      w[j] = make_float4(k ? v[j].x : 0.f, k ? v[j].y : 0.f, k ? v[j].z : 0.f, k ? v[j].w : 0.f);
+    }
+    if constexpr (KC) {
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const int rr = (tid >> 2) + 64 * c2, c = tid & 3;
+        const int off = rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4);
+        uint4 h, l;
+        split_bf16x2(w[2 * c2].x, w[2 * c2].y, h.x, l.x);
+        split_bf16x2(w[2 * c2].z, w[2 * c2].w, h.y, l.y);
+        split_bf16x2(w[2 * c2 + 1].x, w[2 * c2 + 1].y, h.z, l.z);
+        split_bf16x2(w[2 * c2 + 1].z, w[2 * c2 + 1].w, h.w, l.w);
+        *reinterpret_cast<uint4*>(hi_plane + off) = h;
+        *reinterpret_cast<uint4*>(lo_plane + off) = l;
+      }
+    } else {
+      const int m = 4 * (tid & 31);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kr = (tid >> 5) + 8 * j;
+        const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
+        uint2 h, l;
+        split_bf16x2(w[j].x, w[j].y, h.x, l.x);
+        split_bf16x2(w[j].z, w[j].w, h.y, l.y);
+        *reinterpret_cast<uint2*>(hi_plane + off) = h;
+        *reinterpret_cast<uint2*>(lo_plane + off) = l;
+      }
+    }
+  }
+};
+
+// MFMA operand fragment (8 bf16: row rb + lane % 32, k = 16 s + 8 (lane / 32) + 0..7) of a plane.
+template <bool KC>
+__device__ __forceinline__ bf16x8_t xfrag(const char* plane, int rb, int s, int lane) {
+  if constexpr (KC) {
+    const int rr = rb + (lane & 31), c = 2 * s + (lane >> 5);
+    return *reinterpret_cast<const bf16x8_t*>(plane + rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4));
+  } else {
+    // ds_read_b64_tr_b16: 16-lane group G reads a 4 (k) x 16 (row) block; lane 4q + p supplies
+    // the address of k-row q, rows 4p..4p+3, and receives row (lane % 16) of all 4 k-rows.
+    const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int m = rb + 16 * (G & 1) + 4 * p;
+    s16x4_t t[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kr = 16 * s + 8 * (G >> 1) + 4 * u + q;
+      const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
+      t[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4_t*)(plane + off));
+    }
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    const s16x8_t r = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w};
+    return __builtin_bit_cast(bf16x8_t, r);
+  }
+}
+
+template <bool AKC, bool BKC>
+__global__ void __launch_bounds__(256, 2)
+gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int M, int N,
+                   int64_t K, int tiles_n, int tiles, int S, int64_t chunk, int per, float* __restrict__ C,
+                   int64_t ldc) {
+  __shared__ __attribute__((aligned(16))) char lds[kXLds];
+  const int bid = blockIdx.x;
+  const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
+  if (lw >= tiles * S) return;
+  const int s = lw / tiles, t = lw % tiles;
+  const int m0 = (t / tiles_n) * kXT, n0 = (t % tiles_n) * kXT;
+  const int64_t k_lo = (int64_t)s * chunk;
+  const int64_t k_hi = k_lo + chunk < K ? k_lo + chunk : K;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  XStage<AKC> sa;
+  XStage<BKC> sb;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[p][q][r] = 0.f;
+
+  auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
+  const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
+  sa.load(A, lda, m0, M, k_lo, k_lo, k_hi, tid);
+  sb.load(B, ldb, n0, N, k_lo, k_lo, k_hi, tid);
+  sa.store(plane(0, 0, 0), plane(0, 0, 1), tid);
+  sb.store(plane(0, 1, 0), plane(0, 1, 1), tid);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) {   // next stage's loads in flight during this stage's MFMAs
+      const int64_t kb = k_lo + (int64_t)(st + 1) * kXK;
+      sa.load(A, lda, m0, M, kb, k_lo, k_hi, tid);
+      sb.load(B, ldb, n0, N, kb, k_lo, k_hi, tid);
+    }
+    const char* ah = plane(buf, 0, 0);
+    const char* al = plane(buf, 0, 1);
+    const char* bh = plane(buf, 1, 0);
+    const char* bl = plane(buf, 1, 1);
+#pragma unroll
+    for (int ks = 0; ks < kXK / 16; ++ks) {
+      bf16x8_t fa_h[2], fa_l[2], fb_h[2], fb_l[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        fa_h[p] = xfrag<AKC>(ah, wm * 64 + 32 * p, ks, lane);
+        fa_l[p] = xfrag<AKC>(al, wm * 64 + 32 * p, ks, lane);
+        fb_h[p] = xfrag<BKC>(bh, wn * 64 + 32 * p, ks, lane);
+        fb_l[p] = xfrag<BKC>(bl, wn * 64 + 32 * p, ks, lane);
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_l[p], fb_h[q], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_h[p], fb_l[q], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_h[p], fb_h[q], acc[p][q], 0, 0, 0);
+        }
+    }
+    if (st + 1 < nst) {
+      sa.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);
+      sb.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
+    }
+    __syncthreads();
+  }
+
+  // C/D map of the 32x32 tile: row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column lane & 31.
+  float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
+  const int h = lane >> 5, c32 = lane & 31;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int n = n0 + wn * 64 + 32 * q + c32;
+    if (n >= N) continue;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * p + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M) Cs[(int64_t)m * ldc + n] = acc[p][q][r];
+      }
+  }
+}
+
+struct X3Plan {
+  int tiles_n, tiles, S, per;
+  int64_t chunk;
+};
+
+static X3Plan x3_plan(int64_t M, int64_t N, int64_t K) {
+  X3Plan p;
+  p.tiles_n = (int)((N + kXT - 1) / kXT);
+  p.tiles = (int)((M + kXT - 1) / kXT) * p.tiles_n;
+  // split K only when the output tiles cannot fill the chip (weight gradients)
+  int64_t S = 1;
+  if (p.tiles < resident_slots() / 2) {
+    S = resident_slots() / p.tiles;
+    const int64_t max_s = (K + 4 * kXK - 1) / (4 * kXK);   // at least 4 stages per workgroup
+    if (S > max_s) S = max_s;
+    if (S < 1) S = 1;
+  }
+  int64_t chunk = (K + S - 1) / S;
+  chunk = (chunk + kXK - 1) / kXK * kXK;
+  p.chunk = chunk;
+  p.S = (int)((K + chunk - 1) / chunk);
+  if (p.S < 1) p.S = 1;
+  p.per = (p.tiles * p.S + 7) / 8;
+  return p;
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -231,6 +515,58 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
   if (db) {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((O / 4 + 63) / 64)), dim3(256), 0, s, Pb, p.S, O, db);
     RQ_LAUNCH_CHECK("wgrad_reduce_kernel(bias)");
+  }
+  return 0;
+}
+
+
+size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const X3Plan p = x3_plan(M, N, K);
+  return p.S > 1 ? (size_t)p.S * (size_t)(M * N) * sizeof(float) : 0;
+}
+
+int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
+                   int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream) {
+  RQ_CHECK_ARG(((A && B) || K == 0) && C && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30),
+               "rq_gemm_bf16x3: bad arguments");
+  RQ_CHECK_ARG(M % 4 == 0 && N % 4 == 0 && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0,
+               "rq_gemm_bf16x3: M, N, K and leading dims must be multiples of 4 (float4 rows)");
+  RQ_CHECK_ARG(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && ldc >= N,
+               "rq_gemm_bf16x3: leading dimension too small");
+  RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "rq_gemm_bf16x3: pointers must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (K == 0) {
+    RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
+    return 0;
+  }
+  const X3Plan p = x3_plan(M, N, K);
+  float* out = C;
+  if (p.S > 1) {
+    const size_t need = (size_t)p.S * (size_t)(M * N) * sizeof(float);
+    RQ_CHECK_ARG(workspace != nullptr && ws_bytes >= need && ldc == N,
+                 "rq_gemm_bf16x3: split-K needs ldc == N and workspace %zu >= %zu bytes", ws_bytes, need);
+    out = static_cast<float*>(workspace);
+  }
+  const dim3 grid((unsigned)(p.per * 8)), block(256);
+  const int64_t ldo = p.S > 1 ? N : ldc;
+  if (a_kcontig && b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16x3_kernel<true, true>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
+                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
+  else if (a_kcontig)
+    hipLaunchKernelGGL((gemm_bf16x3_kernel<true, false>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
+                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
+  else if (b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16x3_kernel<false, true>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
+                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
+  else
+    hipLaunchKernelGGL((gemm_bf16x3_kernel<false, false>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
+                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
+  RQ_LAUNCH_CHECK("gemm_bf16x3_kernel");
+  if (p.S > 1) {
+    const int64_t n = M * N;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(256), 0, s, out, p.S, n, C);
+    RQ_LAUNCH_CHECK("wgrad_reduce_kernel(gemm_bf16x3)");
   }
   return 0;
 }

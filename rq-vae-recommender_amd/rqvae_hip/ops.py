@@ -171,15 +171,63 @@ def _wgrad_choice(g2: torch.Tensor, x2: torch.Tensor, with_bias: bool) -> str:
     return "hip"
 
 
+def matmul_high() -> bool:
+    """True when fp32 matmuls may run at PyTorch's 'high' precision (split-bf16), which the
+    reference selects at import (modules/rqvae.py:19, modules/model.py:27); 'highest' keeps the
+    exact-fp32 path."""
+    return torch.get_float32_matmul_precision() != "highest"
+
+
+def gemm_bf16x3(a: torch.Tensor, a_kcontig: bool, b: torch.Tensor, b_kcontig: bool, M: int, N: int, K: int,
+                out: torch.Tensor = None) -> torch.Tensor:
+    """C (M, N) = sum_k A(m, k) B(n, k) in split-bf16 ('high' fp32 matmul precision, rq_gemm_bf16x3).
+    A(m, k) is a[m, k] for a k-contiguous a (M, K), else a[k, m] for a (K, M); B likewise."""
+    require_gpu(a, b, what="gemm_bf16x3")
+    a = a.contiguous()
+    b = b.contiguous()
+    lda, ldb = a.shape[1], b.shape[1]
+    C = out if out is not None else torch.empty((M, N), device=a.device, dtype=torch.float32)
+    nbytes = _lib.load().rq_gemm_bf16x3_workspace(M, N, K)
+    ws = torch.empty((nbytes,), device=a.device, dtype=torch.uint8) if nbytes else None
+    call("rq_gemm_bf16x3", ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), M, N, K, ptr(C), N,
+         ptr(ws), nbytes, stream_handle(a.device))
+    return C
+
+
+def linear_fwd_high(x2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """y = x2 W^T (rows, O) at 'high' precision."""
+    O, I = weight.shape
+    return gemm_bf16x3(x2, True, weight, True, x2.shape[0], O, I)
+
+
+def linear_dgrad_high(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """gx = g2 W (rows, I) at 'high' precision."""
+    O, I = weight.shape
+    return gemm_bf16x3(g2, True, weight, False, g2.shape[0], I, O)
+
+
+def linear_wgrad_high(g2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW = g2^T x2 (O, I) at 'high' precision (split-K over the rows, fixed-order reduction)."""
+    return gemm_bf16x3(g2, False, x2, False, g2.shape[1], x2.shape[1], g2.shape[0])
+
+
 class LinearFunction(torch.autograd.Function):
-    """y = x W^T + b (torch.nn.functional.linear, hipBLASLt) whose backward takes the data gradient
-    from hipBLASLt (g @ W: large M, well tiled) and the weight / bias gradient from rq_linear_wgrad
-    (reduction over the whole batch, where the library GEMM leaves most CUs idle)."""
+    """y = x W^T + b. At matmul precision 'high' (the reference's setting) the forward, data and
+    weight gradients all run on the split-bf16 MFMA GEMM (rq_gemm_bf16x3). At 'highest': the
+    forward and data gradient on the fp32 library GEMM (hipBLASLt) and the weight / bias gradient
+    on rq_linear_wgrad (a reduction over the whole batch, where the library leaves CUs idle)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.high = matmul_high()
+        O, I = weight.shape
+        if ctx.high and x.numel() > 0:
+            y = linear_fwd_high(x.reshape(-1, I), weight)
+            if bias is not None:
+                y += bias
+            return y.view(*x.shape[:-1], O)
         return torch.nn.functional.linear(x, weight, bias)
 
     @staticmethod
@@ -188,11 +236,15 @@ class LinearFunction(torch.autograd.Function):
         O, I = weight.shape
         g2 = g.reshape(-1, O)
         gx = dW = db = None
+        high = ctx.high and g2.shape[0] > 0
         if ctx.needs_input_grad[0]:
-            gx = (g2 @ weight).view(x.shape)
+            gx = (linear_dgrad_high(g2, weight) if high else g2 @ weight).view(x.shape)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             x2 = x.reshape(-1, I)
-            if _wgrad_choice(g2, x2, ctx.has_bias) == "hip":
+            if high:
+                dW = linear_wgrad_high(g2, x2)
+                db = g2.sum(0) if ctx.has_bias else None
+            elif _wgrad_choice(g2, x2, ctx.has_bias) == "hip":
                 dW, db = linear_wgrad(g2, x2, ctx.has_bias)
             else:   # library GEMM: small row counts, or measured faster for this shape
                 dW = g2.t() @ x2

@@ -50,13 +50,80 @@ def run_impl(x, cbs, csq, o, impl, mode=3):
          ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle())
 
 
+def wgrad_bench(dev, rounds):
+    """dW = g^T x over N rows for every Linear of the RQ-VAE encoder / decoder (768-512-256-128-64)."""
+    dims = [768, 512, 256, 128, 64]
+    cases = [(65536, o, i) for i, o in zip(dims[:-1], dims[1:])] + [(65536, i, o) for i, o in zip(dims[:-1], dims[1:])]
+    cases += [(262144, 512, 768)]
+    for (N, O, I) in cases:
+        g = torch.Generator(device=dev).manual_seed(N + O + I)
+        gy = torch.randn(N, O, generator=g, device=dev)
+        x = torch.randn(N, I, generator=g, device=dev)
+        ref = gy.t() @ x
+        dW, db = ops.linear_wgrad(gy, x, True)
+        err = float((dW - ref).abs().max() / ref.abs().max())
+        arms = {"hip": lambda: ops.linear_wgrad(gy, x, True), "lib": lambda: (gy.t() @ x, gy.sum(0))}
+        t = {a: [] for a in arms}
+        for _ in range(rounds):
+            for a, fn in arms.items():
+                t[a].append(ev_time(fn, 10))
+        for a in arms:
+            ms = sorted(t[a])[rounds // 2]
+            print(json.dumps(dict(kernel="wgrad", arm=a, shape=[N, O, I], median_ms=ms,
+                                  tflops=2.0 * N * O * I / (ms * 1e-3) / 1e12, rel_err=err)), flush=True)
+        del gy, x, ref
+        torch.cuda.empty_cache()
+
+
+def gemm3_bench(dev, rounds):
+    """Forward / data-grad / weight-grad of every RQ-VAE MLP layer (B = 65,536): split-bf16 GEMM
+    (rq_gemm_bf16x3, precision 'high') vs the fp32 library GEMM ('highest')."""
+    dims = [768, 512, 256, 128, 64]
+    layers = [(i, o) for i, o in zip(dims[:-1], dims[1:])] + [(o, i) for i, o in zip(dims[:-1], dims[1:])]
+    N = 65536
+    tot = {"x3": 0.0, "lib": 0.0}
+    for (I, O) in layers:
+        g = torch.Generator(device=dev).manual_seed(I * O)
+        x = torch.randn(N, I, generator=g, device=dev)
+        W = torch.randn(O, I, generator=g, device=dev) / I ** 0.5
+        gy = torch.randn(N, O, generator=g, device=dev)
+        cases = {"fwd": (lambda: ops.linear_fwd_high(x, W), lambda: x @ W.t(), 2.0 * N * I * O),
+                 "dgrad": (lambda: ops.linear_dgrad_high(gy, W), lambda: gy @ W, 2.0 * N * I * O),
+                 "wgrad": (lambda: ops.linear_wgrad_high(gy, x), lambda: gy.t() @ x, 2.0 * N * I * O)}
+        for name, (f3, fl, flops) in cases.items():
+            r3, rl = f3(), fl()
+            rel = float((r3 - rl).abs().max() / rl.abs().max())
+            t = {"x3": [], "lib": []}
+            for _ in range(rounds):
+                t["x3"].append(ev_time(f3, 10))
+                t["lib"].append(ev_time(fl, 10))
+            rec = dict(kernel="gemm3", op=name, layer=[I, O], rows=N, rel_err_vs_fp32=rel)
+            for a in t:
+                ms = sorted(t[a])[rounds // 2]
+                tot[a] += ms
+                rec[a + "_ms"] = round(ms, 4)
+                rec[a + "_tflops"] = round(flops / (ms * 1e-3) / 1e12, 1)
+            print(json.dumps(rec), flush=True)
+        del x, W, gy
+        torch.cuda.empty_cache()
+    print(json.dumps({"gemm3_total_ms": {a: round(v, 3) for a, v in tot.items()}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sweep", action="store_true", help="mode / level sweep of the ML-32M shape only")
+    ap.add_argument("--wgrad", action="store_true", help="weight-grad kernel vs library g^T x at the RQ-VAE shapes")
+    ap.add_argument("--gemm3", action="store_true", help="split-bf16 GEMM vs fp32 library at the RQ-VAE MLP shapes")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     results = []
+    if args.wgrad:
+        wgrad_bench(dev, args.rounds)
+        return
+    if args.gemm3:
+        gemm3_bench(dev, args.rounds)
+        return
     if args.sweep:
         for (B, D, K, L) in [(65536, 64, 256, 3), (65536, 64, 256, 1), (65536, 64, 256, 6)]:
             x, cbs, csq, o = quantize_case(B, D, K, L, dev)

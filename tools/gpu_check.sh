@@ -66,6 +66,19 @@ for s in $steps; do
     kern)
       run kern 300 python -u "$R/tools/bench_kernels.py" > "$O/kernels.jsonl" 2> "$O/kernels.err"
       cat "$O/kernels.jsonl" ;;
+    gemm3)
+      run gemm3_tests 300 python -u -m pytest "$R/tests/test_gemm_bf16x3_gpu.py" -m gpu -x -q --timeout 120 \
+        --timeout-method thread > "$O/gemm3_tests.log" 2>&1 || { tail -30 "$O/gemm3_tests.log"; exit 1; }
+      tail -3 "$O/gemm3_tests.log"
+      run gemm3 200 python -u "$R/tools/bench_kernels.py" --gemm3 > "$O/gemm3.jsonl" 2> "$O/gemm3.err"
+      cat "$O/gemm3.jsonl" ;;
+    wgrad)
+      run wgrad 200 python -u "$R/tools/bench_kernels.py" --wgrad > "$O/wgrad.jsonl" 2> "$O/wgrad.err"
+      cat "$O/wgrad.jsonl"
+      cd /tmp
+      run prof_wgrad 200 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o wgrad -- \
+        python3 "$R/tools/bench_kernels.py" --wgrad --rounds 3 > "$O/prof_wgrad.log" 2>&1
+      cd "$R" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
