@@ -14,11 +14,17 @@ beside it): encoder MLP -> fused HIP L-level quantize -> decoder MLP -> losses -
 N>1 is launched by torch.distributed.run (one process per GPU); every rank processes its own
 disjoint 65,536-item shard ("weak" scaling) and rank 0 prints ONE JSON line.
 
-roofline: the fused quantize forward kernel (rq_quantize_fwd), algorithmic FLOPs
-2*K*D*L per item divided by its mean device time, measured with HIP events on
-the launching stream inside the timed region; peak = fp32 MFMA 157.3 TFLOP/s (gfx950 has no
-xf32). traffic: HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
-child processes, N=1 only) next to the algorithmic bytes. cpu_baseline: the pinned numpy oracle
+Matmul precision follows the reference: it sets torch.set_float32_matmul_precision('high') at
+import (modules/rqvae.py:19), so the MLP matmuls run on the split-bf16 GEMM (rq_gemm_bf16x3);
+the same step at 'highest' (exact fp32) is reported beside it (exact_fp32_highest).
+
+roofline: the dominant kernel — the split-bf16 GEMM at its largest-time launch shape (fp32-matmul
+FLOPs 2MNK / mean device time, peak = bf16 dense MFMA / 3 products) — measured with HIP events on
+the launching stream inside the timed region; roofline_quantize: the fused quantize forward
+(rq_quantize_fwd), algorithmic FLOPs 2*K*D*L per item, peak = fp32 MFMA 157.3
+TFLOP/s. traffic: HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 +
+WRITE_SIZE, child processes running the same kernel at the same shape, N=1 only) next to the
+algorithmic bytes. cpu_baseline: the pinned numpy oracle
 of the same train step (oracle/rqvae.py) on a bounded sample, timed on this host.
 """
 import argparse
@@ -37,6 +43,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-in MFMA = vector peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 CFG = dict(input_dim=768, hidden=[512, 256, 128], D=64, K=256, L=3, lr=1e-4, wd=0.01, beta=0.25)
@@ -91,17 +98,43 @@ def time_region(fn, steps, warmup, sync_all):
     return time.perf_counter() - t0
 
 
+def gemm_launch_stats(timer, steps=1):
+    """Split-bf16 GEMM launches recorded in the timed region (ops.TIMER keys
+    'gemm_bf16x3:MxNxK:<a_kc><b_kc>'): the shape with the largest total device time, its mean
+    launch time, fp32-matmul TFLOP/s (2MNK / time) and algorithmic bytes (fp32 A, B in, C out),
+    plus the aggregate over every GEMM launch of the step."""
+    keys = [k for k in timer.events if k.startswith("gemm_bf16x3:")]
+    if not keys:
+        return None
+    tot_ms, tot_flops, best = 0.0, 0.0, None
+    for k in keys:
+        ms, n = timer.mean_ms(k)
+        M, N, K = (int(v) for v in k.split(":")[1].split("x"))
+        lay = k.split(":")[2]
+        tot_ms += ms * n
+        tot_flops += 2.0 * M * N * K * n
+        if best is None or ms * n > best[0]:
+            best = (ms * n, ms, n, M, N, K, int(lay[0]), int(lay[1]))
+    _, ms, n, M, N, K, akc, bkc = best
+    return {"shape": [M, N, K, akc, bkc], "launch_ms": round(ms, 4), "launches": n,
+            "flops_per_launch": 2 * M * N * K, "algorithmic_bytes": 4 * (M * K + N * K + M * N),
+            "achieved_tflops": round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 2),
+            "all_gemm_launches": {"count": sum(timer.mean_ms(k)[1] for k in keys), "ms_per_step_total": round(tot_ms / steps, 4),
+                                  "tflops": round(tot_flops / (tot_ms * 1e-3) / 1e12, 2)}}
+
+
 def quantize_algorithmic_bytes(B, D, K, L):
     """Bytes one rq_quantize_fwd launch must move: x and the codebooks (+|c|^2) in; residuals and
     emb_out (L,B,D, saved for the VJP), emb_sum (B,D), ids (B,L) int64 and qloss (B,) out."""
     return 4 * B * D + 4 * L * K * (D + 1) + 4 * B * (2 * L * D + D + 1) + 8 * B * L
 
 
-def pmc_traffic(timeout_s=75):
-    """HBM bytes per rq_quantize_fwd launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE:
-    they do not fit one TCC pass) over tools/pmc_quantize.py — the same kernel at the same shape —
-    run as child processes (this process never execs). Both counters are in KiB; FETCH_SIZE is
-    doubled (gfx950 tallies 128-B streaming reads at 64 B, MI355X_MICROARCH.md 'HBM')."""
+def pmc_traffic(timeout_s=75, regex="rq_fwd", script=("pmc_quantize.py", "5")):
+    """HBM bytes per launch of the kernels matching `regex` from two rocprofv3 --pmc passes
+    (FETCH_SIZE, WRITE_SIZE: they do not fit one TCC pass) over a short driver (tools/pmc_*.py) that
+    runs the same kernel at the same shape, as child processes (this process never execs). Both
+    counters are in KiB; FETCH_SIZE is doubled (gfx950 tallies 128-B streaming reads at 64 B,
+    MI355X_MICROARCH.md 'HBM')."""
     import csv
     import shutil
     import subprocess
@@ -114,16 +147,16 @@ def pmc_traffic(timeout_s=75):
     vals = {}
     with tempfile.TemporaryDirectory(dir="/tmp") as d:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--kernel-include-regex", "rq_fwd",
-                   "-f", "csv", "-d", d, "-o", ctr, "--", sys.executable, os.path.join(ROOT, "tools", "pmc_quantize.py"),
-                   "5"]
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--kernel-include-regex", regex,
+                   "-f", "csv", "-d", d, "-o", ctr, "--", sys.executable, os.path.join(ROOT, "tools", script[0]),
+                   *script[1:]]
             r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True)
             path = os.path.join(d, f"{ctr}_counter_collection.csv")
             if r.returncode != 0 or not os.path.exists(path):
                 return None, f"{ctr} pass failed (exit {r.returncode}): {r.stderr[-200:]}"
             v = sorted(float(row["Counter_Value"]) for row in csv.DictReader(open(path)) if row["Counter_Name"] == ctr)
             if not v:
-                return None, f"{ctr}: no rq_fwd dispatches recorded"
+                return None, f"{ctr}: no {regex} dispatches recorded"
             vals[ctr] = v[len(v) // 2]
     fetch = 2.0 * vals["FETCH_SIZE"] * 1024
     write = vals["WRITE_SIZE"] * 1024
@@ -228,8 +261,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     q_ms, q_n = ops.TIMER.mean_ms("rq_quantize_fwd")
+    gemm = gemm_launch_stats(ops.TIMER, args.steps)
     loss = float(last.loss.detach())
     del last
+    exact = None
+    if not args.no_extras and ws == 1 and torch.get_float32_matmul_precision() != "highest":
+        # the same step with exact-fp32 matmuls ('highest': library fp32 GEMMs + split-K wgrad kernel)
+        prev = torch.get_float32_matmul_precision()
+        torch.set_float32_matmul_precision("highest")
+        try:
+            dt = time_region(step, 10, 3, sync_all)
+        finally:
+            torch.set_float32_matmul_precision(prev)
+        exact = {"ms_per_step": round(dt / 10 * 1e3, 3), "items_per_s": round(B * 10 / dt, 1)}
 
     # decoder-train tokens/s (BASELINE metric, second half): data parallel over the same ranks
     dec = None if args.no_decoder else measure_decoder(device, ws, rk)
@@ -245,8 +289,29 @@ def main():
     achieved = flops_per_item * B / (q_ms * 1e-3) / 1e12
     alg_bytes = quantize_algorithmic_bytes(B, CFG["D"], CFG["K"], CFG["L"])
     traffic, traffic_note = (None, "skipped (--no-pmc or N>1)")
+    gtraffic, gtraffic_note = (None, "skipped (--no-pmc or N>1)")
     if not args.no_pmc and ws == 1 and B == 65536:
         traffic, traffic_note = pmc_traffic()
+        if gemm is not None:
+            M, N, K, akc, bkc = gemm["shape"]
+            gtraffic, gtraffic_note = pmc_traffic(regex="gemm_bf16x3", script=(
+                "pmc_gemm.py", str(M), str(N), str(K), str(akc), str(bkc), "5"))
+    q_roof = {"kernel": "rq_quantize_fwd", "bound": "mfma", "achieved": round(achieved, 3),
+              "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+              "traffic": round(traffic["bytes"]) if traffic else None, "launch_ms": round(q_ms, 4),
+              "launches": q_n, "flops_per_launch": flops_per_item * B, "algorithmic_bytes": alg_bytes,
+              "traffic_detail": traffic if traffic else traffic_note,
+              "hbm_GBps_at_algorithmic_bytes": round(alg_bytes / (q_ms * 1e-3) / 1e9, 1)}
+    roof = q_roof
+    if gemm is not None:   # the split-bf16 GEMM is the dominant kernel at 'high' precision
+        roof = {"kernel": "gemm_bf16x3 (rq_gemm_bf16x3, largest-time launch shape M x N x K)", "bound": "mfma",
+                "achieved": gemm["achieved_tflops"], "peak": round(BF16_MFMA_PEAK_TFLOPS / 3, 1), "unit": "TFLOP/s",
+                "frac": round(gemm["achieved_tflops"] / (BF16_MFMA_PEAK_TFLOPS / 3), 4),
+                "traffic": round(gtraffic["bytes"]) if gtraffic else None,
+                "peak_note": "fp32-matmul FLOPs; the split runs 3 bf16 MFMA products per fp32 product, so the "
+                             "ceiling is the bf16 dense MFMA peak (2.5 PFLOP/s) / 3",
+                **{k: v for k, v in gemm.items() if k != "achieved_tflops"},
+                "traffic_detail": gtraffic if gtraffic else gtraffic_note}
     line = {
         "metric": "decoder-train tokens/sec + RQ-VAE items/sec at 1/2/4/8 MI355X; achieved HBM %",
         "value": round(ws * B * args.steps / elapsed, 1),
@@ -259,19 +324,25 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
+        "matmul_precision": torch.get_float32_matmul_precision(),
+        "matmul_precision_note": "the reference sets torch.set_float32_matmul_precision('high') at import "
+                                 "(modules/rqvae.py:19, model.py:27); gfx950 has no xf32, so 'high' runs the MLP "
+                                 "matmuls as split-bf16 (a = hi + lo, 3 bf16 MFMA products, fp32 accumulate; "
+                                 "per-product rel. error <= ~2^-17 vs TF32's 2^-11). Quantize distances, argmin, "
+                                 "losses and attention stay exact fp32. exact_fp32_highest = the same step at "
+                                 "'highest'.",
         "data": "synthetic (seeded unit-norm 768-d items resident in HBM; random-init MLPs, k-means-like codebooks)",
         "config": {"workload": "RQ-VAE MovieLens-32M train step (configs[1]): 768->[512,256,128]->D64, K256, L3, "
                                "ROTATION_TRICK, AdamW", "global_batch": ws * B, "per_gpu_batch": B,
                    "parallelism": f"dp{ws}"},
-        "roofline": {"kernel": "rq_quantize_fwd", "bound": "mfma", "achieved": round(achieved, 3),
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": round(traffic["bytes"]) if traffic else None, "launch_ms": round(q_ms, 4),
-                     "launches": q_n, "flops_per_launch": flops_per_item * B, "algorithmic_bytes": alg_bytes,
-                     "traffic_detail": traffic if traffic else traffic_note,
-                     "hbm_GBps_at_algorithmic_bytes": round(alg_bytes / (q_ms * 1e-3) / 1e9, 1)},
+        "roofline": roof,
         "loss_last": round(loss, 5),
         "gemm_selection": "default heuristic" if args.no_tunable else "TunableOp (rqvae_hip.gemm_tuning)",
     }
+    if roof is not q_roof:
+        line["roofline_quantize"] = q_roof
+    if exact is not None:
+        line["exact_fp32_highest"] = exact
     if dec is not None:
         line["decoder_amazon"] = dec
     line.update(extras)

@@ -133,7 +133,8 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
  * modules/transformer/* (forward x W^T, data grad g W, weight grad g^T x).
  *   C[m*ldc + n] = sum_k A(m,k) B(n,k),  A(m,k) = a_kcontig ? A[m*lda + k] : A[k*lda + m],
  *                                         B(n,k) = b_kcontig ? B[n*ldb + k] : B[k*ldb + n].
- * M, N, K and leading dims % 4 == 0, 16-byte aligned pointers. When the output tiles cannot fill
+ * The contiguous axis of each operand (K for a k-contiguous one, else M or N) and lda, ldb % 4 == 0,
+ * 16-byte aligned pointers. When the output tiles cannot fill
  * the GPU, K is split across workgroups with a fixed-order reduction (deterministic); that case
  * needs ldc == N and workspace >= rq_gemm_bf16x3_workspace(M, N, K) bytes (0 = no split). */
 size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K);

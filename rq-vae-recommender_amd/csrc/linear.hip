@@ -460,7 +460,7 @@ static X3Plan x3_plan(int64_t M, int64_t N, int64_t K) {
   p.tiles = (int)((M + kXT - 1) / kXT) * p.tiles_n;
   // split K only when the output tiles cannot fill the chip (weight gradients)
   int64_t S = 1;
-  if (p.tiles < resident_slots() / 2) {
+  if (p.tiles < resident_slots() / 2 && (M * N) % 4 == 0) {   // the slab reduction reads float4
     S = resident_slots() / p.tiles;
     const int64_t max_s = (K + 4 * kXK - 1) / (4 * kXK);   // at least 4 stages per workgroup
     if (S > max_s) S = max_s;
@@ -530,8 +530,10 @@ int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, i
                    int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream) {
   RQ_CHECK_ARG(((A && B) || K == 0) && C && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30),
                "rq_gemm_bf16x3: bad arguments");
-  RQ_CHECK_ARG(M % 4 == 0 && N % 4 == 0 && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0,
-               "rq_gemm_bf16x3: M, N, K and leading dims must be multiples of 4 (float4 rows)");
+  RQ_CHECK_ARG((a_kcontig ? K % 4 == 0 : M % 4 == 0) && (b_kcontig ? K % 4 == 0 : N % 4 == 0) && lda % 4 == 0 &&
+                   ldb % 4 == 0,
+               "rq_gemm_bf16x3: the contiguous axis of each operand and the leading dims must be multiples of 4 "
+               "(float4 rows)");
   RQ_CHECK_ARG(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && ldc >= N,
                "rq_gemm_bf16x3: leading dimension too small");
   RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "rq_gemm_bf16x3: pointers must be 16-byte aligned");

@@ -26,6 +26,10 @@ from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cach
 from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged
 from rqvae_hip import gemm_tuning
 
+# As the reference (modules/model.py:27): fp32 matmuls at 'high' precision (split-bf16 GEMM on
+# gfx950, rqvae_hip.ops.gemm_bf16x3); 'highest' restores the exact-fp32 library path.
+torch.set_float32_matmul_precision('high')
+
 
 class ModelOutput(NamedTuple):
     loss: Tensor

@@ -22,6 +22,10 @@ from modules.normalize import L2NormalizationLayer, l2norm
 from modules.quantize import Quantize, QuantizeDistance, QuantizeForwardMode, fused_mode
 from rqvae_hip import ops as hip_ops
 
+# As the reference (modules/rqvae.py:19): fp32 matmuls at 'high' precision. On gfx950 (no xf32)
+# the MLP matmuls then run split-bf16 (rqvae_hip.ops.gemm_bf16x3); 'highest' restores exact fp32.
+torch.set_float32_matmul_precision('high')
+
 
 class RqVaeOutput(NamedTuple):
     embeddings: Tensor      # (B, D, L)

@@ -189,8 +189,9 @@ def gemm_bf16x3(a: torch.Tensor, a_kcontig: bool, b: torch.Tensor, b_kcontig: bo
     C = out if out is not None else torch.empty((M, N), device=a.device, dtype=torch.float32)
     nbytes = _lib.load().rq_gemm_bf16x3_workspace(M, N, K)
     ws = torch.empty((nbytes,), device=a.device, dtype=torch.uint8) if nbytes else None
-    call("rq_gemm_bf16x3", ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), M, N, K, ptr(C), N,
-         ptr(ws), nbytes, stream_handle(a.device))
+    TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}", call, "rq_gemm_bf16x3", ptr(a), lda,
+                 int(a_kcontig), ptr(b), ldb, int(b_kcontig), M, N, K, ptr(C), N, ptr(ws), nbytes,
+                 stream_handle(a.device))
     return C
 
 

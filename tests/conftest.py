@@ -20,6 +20,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")
 
 
+@pytest.fixture(autouse=True)
+def exact_matmul_precision():
+    """Each test starts at 'highest' (exact fp32 matmuls), whatever an earlier import set: the
+    reference's modules set 'high' at import (modules/rqvae.py:19, modules/model.py:27) and so do
+    ours. Tests of the 'high' (split-bf16) path set it themselves."""
+    import torch
+    import modules.model  # noqa: F401  (import-time precision side effect happens before the test)
+    import modules.rqvae  # noqa: F401
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(prev)
+
+
 @pytest.fixture(scope="session")
 def golden():
     cache = {}

@@ -15,7 +15,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(256, 256, 64), (65536, 512, 768), (300, 132, 200), (4, 4, 4), (12, 8, 36), (768, 512, 65536),
-          (132, 260, 4100), (64, 128, 65536)]
+          (132, 260, 4100), (64, 128, 65536), (768, 512, 4099)]
 
 
 def _operands(M, N, K, a_kc, b_kc, gen, device, integer):
@@ -33,6 +33,8 @@ def _operands(M, N, K, a_kc, b_kc, gen, device, integer):
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_bf16x3_exact_on_integers(device, a_kc, b_kc, M, N, K):
+    if (a_kc or b_kc) and K % 4:
+        pytest.skip("k-contiguous operands need K % 4 == 0")
     from rqvae_hip import ops
     if M * N * K > 2 ** 33:
         pytest.skip("large shape: random-data test covers it")
@@ -47,6 +49,8 @@ def test_gemm_bf16x3_exact_on_integers(device, a_kc, b_kc, M, N, K):
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_bf16x3_random_within_bound(device, a_kc, b_kc, M, N, K):
     from rqvae_hip import ops
+    if (a_kc or b_kc) and K % 4:
+        pytest.skip("k-contiguous operands need K % 4 == 0")
     gen = torch.Generator(device=device).manual_seed(M + N + K)
     a, b, A, B = _operands(M, N, K, a_kc, b_kc, gen, device, False)
     C = ops.gemm_bf16x3(a, a_kc, b, b_kc, M, N, K)
@@ -64,6 +68,20 @@ def test_gemm_bf16x3_zero_k(device):
     b = torch.empty(12, 0, device=device)
     C = ops.gemm_bf16x3(a, True, b, True, 8, 12, 0)
     assert C.shape == (8, 12) and not C.any()
+
+
+@pytest.mark.parametrize("rows", [1, 37, 1237, 65535])
+def test_gemm_bf16x3_ragged_rows(device, rows):
+    """Row counts of any size (the batch axis): forward / data grad have M = rows (k-contiguous A),
+    the weight grad K = rows (row-major operands) — exact on small integers."""
+    from rqvae_hip import ops
+    gen = torch.Generator(device=device).manual_seed(rows)
+    x = torch.randint(-8, 9, (rows, 132), generator=gen, device=device).float()
+    W = torch.randint(-8, 9, (68, 132), generator=gen, device=device).float()
+    g = torch.randint(-8, 9, (rows, 68), generator=gen, device=device).float()
+    assert torch.equal(ops.linear_fwd_high(x, W).double(), x.double() @ W.double().t())
+    assert torch.equal(ops.linear_dgrad_high(g, W).double(), g.double() @ W.double())
+    assert torch.equal(ops.linear_wgrad_high(g, x).double(), g.double().t() @ x.double())
 
 
 def test_gemm_bf16x3_rejects_bad_shapes(device):
@@ -104,3 +122,35 @@ def test_linear_high_precision_matches_fp64(device, bias):
     assert close(mine.weight.grad, ref.weight.grad, 1e-4)
     if bias:
         assert close(mine.bias.grad, ref.bias.grad, 1e-5)
+
+
+def test_rqvae_step_high_vs_highest(device):
+    """The RQ-VAE train step (ML-32M dims) at 'high' (split-bf16 MLP matmuls) against the same step
+    at 'highest': loss within 1e-4 relative, MLP gradients within 3 % in norm (dominated by the items whose ids flip), codebook
+    gradients within 5 % in norm, and the semantic ids of >= 99 % of the items identical (near-ties may flip under a 2^-17 perturbation,
+    as they do between TF32 and fp32 in the reference)."""
+    import bench
+    from data.schemas import SeqBatch
+    m = bench.build_model(device)
+    x = bench.make_items(4096, 768, torch.Generator(device=device).manual_seed(4), device)
+    res = {}
+    for prec in ("highest", "high"):
+        torch.set_float32_matmul_precision(prec)
+        m.zero_grad(set_to_none=True)
+        out = m(SeqBatch(None, None, None, x, None, None), gumbel_t=0.2)
+        out.loss.backward()
+        with torch.no_grad():
+            ids = m.get_semantic_ids(x).sem_ids
+        res[prec] = (float(out.loss), {k: p.grad.clone() for k, p in m.named_parameters()}, ids)
+    torch.set_float32_matmul_precision("highest")
+    (l0, g0, i0), (l1, g1, i1) = res["highest"], res["high"]
+    assert abs(l1 - l0) <= 1e-4 * abs(l0), (l0, l1)
+    agree = float((i0 == i1).all(1).float().mean())
+    assert agree >= 0.99, agree
+    for k in g0:
+        if k.startswith("layers."):
+            # a codeword's gradient sums its assigned items: an id flip moves an item's whole
+            # contribution, so compare in norm (the flips are <= 1 % of the items)
+            assert (g1[k] - g0[k]).norm() <= 0.05 * g0[k].norm(), k
+        else:   # flipped items also change their encoder / decoder gradient paths
+            assert (g1[k] - g0[k]).norm() <= 3e-2 * g0[k].norm(), k
