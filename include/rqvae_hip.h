@@ -141,6 +141,22 @@ size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K);
 int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
                    int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream);
 
+/* General form of rq_gemm_bf16x3 for the fused MLP chain (modules/encoder.py:7-36 — Linear, SiLU,
+ * [Dropout], ..., Linear): an operand is fp32 (X_lo == NULL) or pre-split, two bf16 planes
+ * (X = hi, X_lo = lo) of the operand's shape; split operands need their contiguous axis and ld
+ * % 8 == 0. The epilogue turns the tile into:
+ *   0  C = A B^T                                                 (split-K allowed)
+ *   1  C = z = A B^T, and H = split(Dropout_p(SiLU(z)))          (a hidden layer's forward)
+ *   2  H = split(SiLU'(Z) * Dropout_p(A B^T)), C unused          (its pre-activation grad)
+ * H_hi / H_lo: bf16 planes (M, N) of row stride ldh; Z: (M, N) of stride ldc. The dropout mask is
+ * element e = m N + n of the same counter-based mask as rq_silu_dropout_fwd (seed). */
+int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                      void* workspace, size_t ws_bytes, void* stream);
+/* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
+int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
+
 /* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
  * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <math.h>
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4v __attribute__((ext_vector_type(4)));
@@ -94,6 +95,17 @@ __device__ __forceinline__ Keep4 keep4(uint64_t seed, uint64_t q, uint32_t thr) 
   r.k[2] = (uint32_t)b >= thr;
   r.k[3] = (uint32_t)(b >> 32) >= thr;
   return r;
+}
+// Element e of a tensor under the same mask: word (e & 1) of mix(e >> 1) (= keep4(seed, e / 4).k[e % 4]).
+__device__ __forceinline__ bool keep1(uint64_t seed, uint64_t e, uint32_t thr) {
+  return (uint32_t)(splitmix64(seed, e >> 1) >> (32 * (e & 1))) >= thr;
+}
+// SiLU and its gradient, ATen's formulas: silu(z) = z / (1 + exp(-z)),
+// silu'(z) g = g * s * (1 + z * (1 - s)), s = 1 / (1 + exp(-z)).
+__device__ __forceinline__ float silu_f(float z) { return z / (1.0f + expf(-z)); }
+__device__ __forceinline__ float silu_grad_f(float g, float z) {
+  const float s = 1.0f / (1.0f + expf(-z));
+  return g * s * (1.0f + z * (1.0f - s));
 }
 __device__ __forceinline__ float4 drop4(float4 v, uint64_t seed, uint64_t q, uint32_t thr, float scale) {
   if (thr == 0) return v;

@@ -271,67 +271,118 @@ __device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uin
 
 __device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
 
-// One operand's staging registers: 4 float4 per thread per stage (a 128 x 32 tile / 256 threads).
-template <bool KC>
+// One operand's staging registers (a 128 x 32 tile per stage, 256 threads). Operand formats:
+//   fp32  (SP = false): 4 float4 per thread, split into (hi, lo) bf16 while written to LDS;
+//   split (SP = true):  two bf16 planes (hi, lo) of the operand's shape, produced once upstream
+//                       (rq_split_bf16x3, or a GEMM epilogue): 2 + 2 16-byte chunks per thread,
+//                       copied to LDS as they are.
+template <bool KC, bool SP>
 struct XStage {
-  float4 v[4];
+  uint4 v[4];
   bool ok[4];
 
   // rows [r0, r0 + 128) of the operand (clamped to R - 1: they feed only outputs >= R, never
   // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time.
-  __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int r0, int R, int64_t kb,
-                                       int64_t k_lo, int64_t k_hi, int tid) {
-    if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8 (2 float4 each)
+  __device__ __forceinline__ void load(const void* __restrict__ Xv, const void* __restrict__ Xlv, int64_t ld, int r0,
+                                       int R, int64_t kb, int64_t k_lo, int64_t k_hi, int tid) {
+    if constexpr (!SP) {
+      const float* __restrict__ X = static_cast<const float*>(Xv);
+      if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8 (2 float4 each)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int rr = (tid >> 2) + 64 * (j >> 1);
-        const int64_t row = min(r0 + rr, R - 1);
-        const int64_t k = kb + (tid & 3) * 8 + 4 * (j & 1);
-        ok[j] = k < k_hi;
-        v[j] = *reinterpret_cast<const float4*>(X + row * ld + (ok[j] ? k : k_lo));
+        for (int j = 0; j < 4; ++j) {
+          const int rr = (tid >> 2) + 64 * (j >> 1);
+          const int64_t row = min(r0 + rr, R - 1);
+          const int64_t k = kb + (tid & 3) * 8 + 4 * (j & 1);
+          ok[j] = k < k_hi;
+          v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
+        }
+      } else {              // thread: 4 consecutive rows (tid % 32) * 4, k rows tid/32 + 8j
+        const int64_t col = min(r0 + 4 * (tid & 31), R - 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t k = kb + (tid >> 5) + 8 * j;
+          ok[j] = k < k_hi;
+          v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
+        }
       }
-    } else {              // thread: 4 consecutive rows (tid % 32) * 4, k rows tid/32 + 8j
-      const int64_t col = min(r0 + 4 * (tid & 31), R - 4);
+    } else {
+      const uint16_t* __restrict__ Xh = static_cast<const uint16_t*>(Xv);
+      const uint16_t* __restrict__ Xl = static_cast<const uint16_t*>(Xlv);
+      if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t k = kb + (tid >> 5) + 8 * j;
-        ok[j] = k < k_hi;
-        v[j] = *reinterpret_cast<const float4*>(X + (ok[j] ? k : k_lo) * ld + col);
+        for (int j = 0; j < 2; ++j) {
+          const int64_t row = min(r0 + (tid >> 2) + 64 * j, R - 1);
+          const int64_t k = kb + (tid & 3) * 8;
+          ok[j] = k < k_hi;
+          const int64_t o = row * ld + (ok[j] ? k : k_lo);
+          v[j] = *reinterpret_cast<const uint4*>(Xh + o);
+          v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
+        }
+      } else {              // thread: 8 consecutive rows (tid % 16) * 8, k rows tid/16 and tid/16 + 16
+        const int64_t col = min(r0 + 8 * (tid & 15), R - 8);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t k = kb + (tid >> 4) + 16 * j;
+          ok[j] = k < k_hi;
+          const int64_t o = (ok[j] ? k : k_lo) * ld + col;
+          v[j] = *reinterpret_cast<const uint4*>(Xh + o);
+          v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
+        }
       }
     }
   }
 
   __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, int tid) const {
-    float4 w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool k = ok[j];
-      w[j] = make_float4(k ? v[j].x : 0.f, k ? v[j].y : 0.f, k ? v[j].z : 0.f, k ? v[j].w : 0.f);
-    }
-    if constexpr (KC) {
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        const int rr = (tid >> 2) + 64 * c2, c = tid & 3;
-        const int off = rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4);
-        uint4 h, l;
-        split_bf16x2(w[2 * c2].x, w[2 * c2].y, h.x, l.x);
-        split_bf16x2(w[2 * c2].z, w[2 * c2].w, h.y, l.y);
-        split_bf16x2(w[2 * c2 + 1].x, w[2 * c2 + 1].y, h.z, l.z);
-        split_bf16x2(w[2 * c2 + 1].z, w[2 * c2 + 1].w, h.w, l.w);
-        *reinterpret_cast<uint4*>(hi_plane + off) = h;
-        *reinterpret_cast<uint4*>(lo_plane + off) = l;
-      }
-    } else {
-      const int m = 4 * (tid & 31);
+    if constexpr (!SP) {
+      float4 w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int kr = (tid >> 5) + 8 * j;
-        const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
-        uint2 h, l;
-        split_bf16x2(w[j].x, w[j].y, h.x, l.x);
-        split_bf16x2(w[j].z, w[j].w, h.y, l.y);
-        *reinterpret_cast<uint2*>(hi_plane + off) = h;
-        *reinterpret_cast<uint2*>(lo_plane + off) = l;
+        const bool k = ok[j];
+        const float4 f = __builtin_bit_cast(float4, v[j]);
+        w[j] = make_float4(k ? f.x : 0.f, k ? f.y : 0.f, k ? f.z : 0.f, k ? f.w : 0.f);
+      }
+      if constexpr (KC) {
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) {
+          const int rr = (tid >> 2) + 64 * c2, c = tid & 3;
+          const int off = rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4);
+          uint4 h, l;
+          split_bf16x2(w[2 * c2].x, w[2 * c2].y, h.x, l.x);
+          split_bf16x2(w[2 * c2].z, w[2 * c2].w, h.y, l.y);
+          split_bf16x2(w[2 * c2 + 1].x, w[2 * c2 + 1].y, h.z, l.z);
+          split_bf16x2(w[2 * c2 + 1].z, w[2 * c2 + 1].w, h.w, l.w);
+          *reinterpret_cast<uint4*>(hi_plane + off) = h;
+          *reinterpret_cast<uint4*>(lo_plane + off) = l;
+        }
+      } else {
+        const int m = 4 * (tid & 31);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kr = (tid >> 5) + 8 * j;
+          const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
+          uint2 h, l;
+          split_bf16x2(w[j].x, w[j].y, h.x, l.x);
+          split_bf16x2(w[j].z, w[j].w, h.y, l.y);
+          *reinterpret_cast<uint2*>(hi_plane + off) = h;
+          *reinterpret_cast<uint2*>(lo_plane + off) = l;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool k = ok[j];
+        const uint4 h = make_uint4(k ? v[j].x : 0u, k ? v[j].y : 0u, k ? v[j].z : 0u, k ? v[j].w : 0u);
+        const uint4 l = make_uint4(k ? v[2 + j].x : 0u, k ? v[2 + j].y : 0u, k ? v[2 + j].z : 0u, k ? v[2 + j].w : 0u);
+        int off;
+        if constexpr (KC) {
+          const int rr = (tid >> 2) + 64 * j, c = tid & 3;
+          off = rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4);
+        } else {
+          const int kr = (tid >> 4) + 16 * j;
+          off = 256 * kr + (((tid & 15) ^ col_swz(kr)) << 4);
+        }
+        *reinterpret_cast<uint4*>(hi_plane + off) = h;
+        *reinterpret_cast<uint4*>(lo_plane + off) = l;
       }
     }
   }
@@ -362,11 +413,43 @@ __device__ __forceinline__ bf16x8_t xfrag(const char* plane, int rb, int s, int 
   }
 }
 
-template <bool AKC, bool BKC>
+// Epilogues: what the accumulator tile becomes (all fp32 math; dropout mask = keep1(seed, m N + n),
+// the convention of the standalone dropout kernels, dropout.hip).
+enum X3Epi : int {
+  kEpiStore = 0,     // C = A B^T (fp32; split-K slabs when S > 1)
+  kEpiSiluFwd = 1,   // C = z = A B^T (fp32, kept for the backward); H = split(Dropout(SiLU(z)))
+  kEpiSiluBwd = 2,   // H = split(SiLU'(Z) * Dropout(A B^T)): the pre-activation grad of a hidden layer
+};
+
+struct X3Epilogue {
+  const float* Z;    // kEpiSiluBwd: pre-activations (ld = ldc)
+  uint16_t* Hh;      // split output planes (ld = ldh)
+  uint16_t* Hl;
+  int64_t ldh;
+  uint32_t thr;      // dropout threshold (0 = none) and scale
+  float scale;
+  uint64_t seed;
+};
+
+// Epilogue SiLU on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each) instead of
+// the IEEE expf + division of the standalone kernels (dropout.hip): the result is split to bf16
+// planes at ~2^-17 right after, so the last bits do not survive anyway, and the epilogue VALU drops
+// ~3x. s = sigmoid(z) = 1 / (1 + 2^(-z log2 e)).
+__device__ __forceinline__ float sigmoid_fast(float z) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
+}
+
+__device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo) {
+  const __bf16 h = (__bf16)v;
+  *hi = __builtin_bit_cast(uint16_t, h);
+  *lo = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));
+}
+
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false>
 __global__ void __launch_bounds__(256, 2)
-gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int M, int N,
-                   int64_t K, int tiles_n, int tiles, int S, int64_t chunk, int per, float* __restrict__ C,
-                   int64_t ldc) {
+gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
+                   const void* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S,
+                   int64_t chunk, int per, float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
   __shared__ __attribute__((aligned(16))) char lds[kXLds];
   const int bid = blockIdx.x;
   const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
@@ -378,8 +461,8 @@ gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
 
-  XStage<AKC> sa;
-  XStage<BKC> sb;
+  XStage<AKC, ASP> sa;
+  XStage<BKC, BSP> sb;
   floatx16 acc[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -390,8 +473,8 @@ gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
 
   auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
   const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
-  sa.load(A, lda, m0, M, k_lo, k_lo, k_hi, tid);
-  sb.load(B, ldb, n0, N, k_lo, k_lo, k_hi, tid);
+  sa.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
+  sb.load(B, Bl, ldb, n0, N, k_lo, k_lo, k_hi, tid);
   sa.store(plane(0, 0, 0), plane(0, 0, 1), tid);
   sb.store(plane(0, 1, 0), plane(0, 1, 1), tid);
   __syncthreads();
@@ -399,8 +482,8 @@ gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     const int buf = st & 1;
     if (st + 1 < nst) {   // next stage's loads in flight during this stage's MFMAs
       const int64_t kb = k_lo + (int64_t)(st + 1) * kXK;
-      sa.load(A, lda, m0, M, kb, k_lo, k_hi, tid);
-      sb.load(B, ldb, n0, N, kb, k_lo, k_hi, tid);
+      sa.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);
+      sb.load(B, Bl, ldb, n0, N, kb, k_lo, k_hi, tid);
     }
     const char* ah = plane(buf, 0, 0);
     const char* al = plane(buf, 0, 1);
@@ -420,9 +503,11 @@ gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_l[p], fb_h[q], acc[p][q], 0, 0, 0);
-          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_h[p], fb_l[q], acc[p][q], 0, 0, 0);
-          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_h[p], fb_h[q], acc[p][q], 0, 0, 0);
+          // transposed product D = B A^T (tile rows = n, columns = m): each lane then holds 4
+          // consecutive n of one row m per register quad, so the epilogue stores vectors
+          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);
         }
     }
     if (st + 1 < nst) {
@@ -432,20 +517,61 @@ gemm_bf16x3_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     __syncthreads();
   }
 
-  // C/D map of the 32x32 tile: row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column lane & 31.
+  // C/D map of D = B A^T: column (lane & 31) = m, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5) = n, so
+  // register quad g holds C[m][n .. n + 3], n = 8 g + 4 (lane >> 5) (+ tile offsets): 16-B fp32 /
+  // 8-B bf16 stores (N % 4 == 0).
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
   const int h = lane >> 5, c32 = lane & 31;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int n = n0 + wn * 64 + 32 * q + c32;
-    if (n >= N) continue;
+  for (int p = 0; p < 2; ++p) {
+    const int m = m0 + wm * 64 + 32 * p + c32;
+    if (m < M) {
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+      for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + 32 * p + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M) Cs[(int64_t)m * ldc + n] = acc[p][q][r];
-      }
+        for (int g = 0; g < 4; ++g) {
+          const int n = n0 + wn * 64 + 32 * q + 8 * g + 4 * h;
+          if (n >= N) continue;
+          const float4 v = make_float4(acc[p][q][4 * g], acc[p][q][4 * g + 1], acc[p][q][4 * g + 2], acc[p][q][4 * g + 3]);
+          if constexpr (EPI == kEpiStore) {
+            *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
+          } else {
+            const uint64_t e = (uint64_t)m * N + n;
+            float d[4] = {1.f, 1.f, 1.f, 1.f};   // dropout multipliers (0 or 1 / (1 - p))
+            if constexpr (DROP) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) d[j] = keep1(ep.seed, e + j, ep.thr) ? ep.scale : 0.f;
+            }
+            float4 o;
+            if constexpr (EPI == kEpiSiluFwd) {
+              *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = v;
+              o = make_float4(v.x * sigmoid_fast(v.x) * d[0], v.y * sigmoid_fast(v.y) * d[1],
+                              v.z * sigmoid_fast(v.z) * d[2], v.w * sigmoid_fast(v.w) * d[3]);
+            } else {   // silu'(z) g = g s (1 + z (1 - s)), g = Dropout(A B^T)
+              const float4 z = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
+              const float sx = sigmoid_fast(z.x), sy = sigmoid_fast(z.y), sz = sigmoid_fast(z.z),
+                          sw = sigmoid_fast(z.w);
+              o = make_float4(v.x * d[0] * sx * (1.f + z.x * (1.f - sx)), v.y * d[1] * sy * (1.f + z.y * (1.f - sy)),
+                              v.z * d[2] * sz * (1.f + z.z * (1.f - sz)), v.w * d[3] * sw * (1.f + z.w * (1.f - sw)));
+            }
+            uint2 hi, lo;
+            split_bf16x2(o.x, o.y, hi.x, lo.x);
+            split_bf16x2(o.z, o.w, hi.y, lo.y);
+            *reinterpret_cast<uint2*>(ep.Hh + (int64_t)m * ep.ldh + n) = hi;
+            *reinterpret_cast<uint2*>(ep.Hl + (int64_t)m * ep.ldh + n) = lo;
+          }
+        }
+    }
+  }
+}
+
+// Elementwise split (weights once per step; 4 elements per thread per iteration, any n).
+__global__ void __launch_bounds__(256) split_bf16x3_kernel(const float* __restrict__ x, int64_t n,
+                                                           uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u < n) split_store1(x[i + u], hi + i + u, lo + i + u);
   }
 }
 
@@ -454,13 +580,13 @@ struct X3Plan {
   int64_t chunk;
 };
 
-static X3Plan x3_plan(int64_t M, int64_t N, int64_t K) {
+static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
   X3Plan p;
   p.tiles_n = (int)((N + kXT - 1) / kXT);
   p.tiles = (int)((M + kXT - 1) / kXT) * p.tiles_n;
   // split K only when the output tiles cannot fill the chip (weight gradients)
   int64_t S = 1;
-  if (p.tiles < resident_slots() / 2 && (M * N) % 4 == 0) {   // the slab reduction reads float4
+  if (allow_split && p.tiles < resident_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
     S = resident_slots() / p.tiles;
     const int64_t max_s = (K + 4 * kXK - 1) / (4 * kXK);   // at least 4 stages per workgroup
     if (S > max_s) S = max_s;
@@ -526,50 +652,118 @@ size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) {
   return p.S > 1 ? (size_t)p.S * (size_t)(M * N) * sizeof(float) : 0;
 }
 
-int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
-                   int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream) {
-  RQ_CHECK_ARG(((A && B) || K == 0) && C && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30),
+int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                      void* workspace, size_t ws_bytes, void* stream) {
+  const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
+  RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
+                   epilogue <= 2,
                "rq_gemm_bf16x3: bad arguments");
-  RQ_CHECK_ARG((a_kcontig ? K % 4 == 0 : M % 4 == 0) && (b_kcontig ? K % 4 == 0 : N % 4 == 0) && lda % 4 == 0 &&
-                   ldb % 4 == 0,
-               "rq_gemm_bf16x3: the contiguous axis of each operand and the leading dims must be multiples of 4 "
-               "(float4 rows)");
-  RQ_CHECK_ARG(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && ldc >= N,
+  RQ_CHECK_ARG((epilogue == kEpiSiluBwd || C) && (epilogue == kEpiStore || (H_hi && H_lo && ldh >= N)) &&
+                   (epilogue != kEpiSiluBwd || Z),
+               "rq_gemm_bf16x3: epilogue %d needs %s", epilogue,
+               epilogue == kEpiSiluBwd ? "Z and H planes" : (epilogue ? "C and H planes" : "C"));
+  // float4 (fp32) / 8 x bf16 (split) vectors along each operand's contiguous axis
+  const int64_t va = asp ? 8 : 4, vb = bsp ? 8 : 4;
+  RQ_CHECK_ARG((a_kcontig ? K % va == 0 : M % va == 0) && (b_kcontig ? K % vb == 0 : N % vb == 0) && lda % va == 0 &&
+                   ldb % vb == 0,
+               "rq_gemm_bf16x3: the contiguous axis of each operand and its leading dim must be multiples of %d "
+               "(fp32) / 8 (split)", 4);
+  RQ_CHECK_ARG(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && (epilogue == kEpiSiluBwd || ldc >= N),
                "rq_gemm_bf16x3: leading dimension too small");
-  RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "rq_gemm_bf16x3: pointers must be 16-byte aligned");
+  RQ_CHECK_ARG(N % 4 == 0 && ldc % 4 == 0 && ldh % 4 == 0 && ((uintptr_t)C | (uintptr_t)Z) % 16 == 0 &&
+                   ((uintptr_t)H_hi | (uintptr_t)H_lo) % 8 == 0,
+               "rq_gemm_bf16x3: N and the output leading dims must be multiples of 4 (vector stores), outputs aligned");
+  RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)A_lo | (uintptr_t)B | (uintptr_t)B_lo) % 16 == 0,
+               "rq_gemm_bf16x3: operand pointers must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
+  X3Epilogue ep{Z, H_hi, H_lo, ldh, 0u, 1.f, seed};
+  dropout_params(p, &ep.thr, &ep.scale);
   if (K == 0) {
+    RQ_CHECK_ARG(epilogue == kEpiStore, "rq_gemm_bf16x3: K == 0 needs the plain epilogue");
     RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
     return 0;
   }
-  const X3Plan p = x3_plan(M, N, K);
+  const X3Plan pl = x3_plan(M, N, K, epilogue == kEpiStore);
   float* out = C;
-  if (p.S > 1) {
-    const size_t need = (size_t)p.S * (size_t)(M * N) * sizeof(float);
+  if (pl.S > 1) {
+    const size_t need = (size_t)pl.S * (size_t)(M * N) * sizeof(float);
     RQ_CHECK_ARG(workspace != nullptr && ws_bytes >= need && ldc == N,
                  "rq_gemm_bf16x3: split-K needs ldc == N and workspace %zu >= %zu bytes", ws_bytes, need);
     out = static_cast<float*>(workspace);
   }
-  const dim3 grid((unsigned)(p.per * 8)), block(256);
-  const int64_t ldo = p.S > 1 ? N : ldc;
-  if (a_kcontig && b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16x3_kernel<true, true>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
-                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
-  else if (a_kcontig)
-    hipLaunchKernelGGL((gemm_bf16x3_kernel<true, false>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
-                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
-  else if (b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16x3_kernel<false, true>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
-                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
-  else
-    hipLaunchKernelGGL((gemm_bf16x3_kernel<false, false>), grid, block, 0, s, A, lda, B, ldb, (int)M, (int)N, K,
-                       p.tiles_n, p.tiles, p.S, p.chunk, p.per, out, ldo);
+  const dim3 grid((unsigned)(pl.per * 8)), block(256);
+  const int64_t ldo = pl.S > 1 ? N : ldc;
+  const int code = (a_kcontig ? 16 : 0) | (asp ? 8 : 0) | (b_kcontig ? 4 : 0) | (bsp ? 2 : 0);
+#define RQ_X3D(AK, AS, BK, BS, EP, DR)                                                                               \
+  hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR>), grid, block, 0, s, A, A_lo, lda, B, B_lo, ldb,     \
+                     (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep)
+#define RQ_X3(AK, AS, BK, BS, EP)                                                                                    \
+  do {                                                                                                               \
+    if (EP != kEpiStore && ep.thr != 0)                                                                              \
+      RQ_X3D(AK, AS, BK, BS, EP, (EP != kEpiStore));                                                                 \
+    else                                                                                                             \
+      RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
+  } while (0)
+  bool launched = true;
+  if (epilogue == kEpiStore) {
+    switch (code) {
+      // every layout with fp32 operands (the generic entry point)
+      case 16 | 4: RQ_X3(true, false, true, false, kEpiStore); break;
+      case 16: RQ_X3(true, false, false, false, kEpiStore); break;
+      case 4: RQ_X3(false, false, true, false, kEpiStore); break;
+      case 0: RQ_X3(false, false, false, false, kEpiStore); break;
+      // fused MLP chain: forward of the last layer, data grads with split weights, weight grads
+      case 16 | 8 | 4 | 2: RQ_X3(true, true, true, true, kEpiStore); break;
+      case 16 | 4 | 2: RQ_X3(true, false, true, true, kEpiStore); break;
+      case 16 | 8 | 2: RQ_X3(true, true, false, true, kEpiStore); break;
+      case 16 | 2: RQ_X3(true, false, false, true, kEpiStore); break;
+      case 8 | 2: RQ_X3(false, true, false, true, kEpiStore); break;
+      case 8: RQ_X3(false, true, false, false, kEpiStore); break;
+      case 2: RQ_X3(false, false, false, true, kEpiStore); break;
+      default: launched = false;
+    }
+  } else if (epilogue == kEpiSiluFwd) {
+    switch (code) {
+      case 16 | 4 | 2: RQ_X3(true, false, true, true, kEpiSiluFwd); break;
+      case 16 | 8 | 4 | 2: RQ_X3(true, true, true, true, kEpiSiluFwd); break;
+      default: launched = false;
+    }
+  } else {
+    switch (code) {
+      case 16 | 2: RQ_X3(true, false, false, true, kEpiSiluBwd); break;
+      case 16 | 8 | 2: RQ_X3(true, true, false, true, kEpiSiluBwd); break;
+      default: launched = false;
+    }
+  }
+#undef RQ_X3
+#undef RQ_X3D
+  RQ_CHECK_ARG(launched, "rq_gemm_bf16x3: operand combination (a_kcontig %d, a_split %d, b_kcontig %d, b_split %d) "
+                         "not built for epilogue %d", a_kcontig, (int)asp, b_kcontig, (int)bsp, epilogue);
   RQ_LAUNCH_CHECK("gemm_bf16x3_kernel");
-  if (p.S > 1) {
+  if (pl.S > 1) {
     const int64_t n = M * N;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(256), 0, s, out, p.S, n, C);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(256), 0, s, out, pl.S, n, C);
     RQ_LAUNCH_CHECK("wgrad_reduce_kernel(gemm_bf16x3)");
   }
+  return 0;
+}
+
+int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
+                   int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream) {
+  return rq_gemm_bf16x3_ex(A, nullptr, lda, a_kcontig, B, nullptr, ldb, b_kcontig, M, N, K, C, ldc, kEpiStore, nullptr,
+                           nullptr, nullptr, 0, 0.f, 0, workspace, ws_bytes, stream);
+}
+
+// x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi): the split form the GEMM consumes.
+int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream) {
+  RQ_CHECK_ARG(n >= 0 && (n == 0 || (x && hi && lo)), "rq_split_bf16x3: bad arguments");
+  if (n == 0) return 0;
+  const int64_t blocks = (n + 1023) / 1024;
+  hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                     (hipStream_t)stream, x, n, hi, lo);
+  RQ_LAUNCH_CHECK("split_bf16x3_kernel");
   return 0;
 }
 

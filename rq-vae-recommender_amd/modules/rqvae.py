@@ -146,7 +146,7 @@ class RqVae(nn.Module):
         head = self.decoder.mlp
         if n == 0 and isinstance(head[-1], L2NormalizationLayer) and x.dtype == torch.float32:
             # decoder's final l2norm + ReconstructionLoss fused into one HIP row kernel (fwd + bwd)
-            reconstruction = hip_ops.l2norm_recon_loss(head[:-1](emb_sum), x)
+            reconstruction = hip_ops.l2norm_recon_loss(self.decoder.body(emb_sum), x)
         else:
             x_hat = self.decode(emb_sum)
             if n > 0:   # the reference's cat is a no-op for n == 0 (SURVEY A-10)

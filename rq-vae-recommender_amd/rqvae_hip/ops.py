@@ -4,10 +4,12 @@
   unique_count(ids, K)                       #distinct semantic-ID tuples (device scalar)
   padded_to_jagged_values(x, lengths, N)     jagged gather (+1-1 rounding) + offsets (fwd + VJP)
   varlen_attention(q, k, v, cu_q, cu_k, ...) jagged SDPA (fwd + deterministic VJP)
+  gemm_bf16x3 / gemm_x3 / mlp_chain          fp32 matmuls at 'high' precision (split-bf16 MFMA)
 
 All kernels run on torch's current HIP stream; tensors must be on the GPU (no CPU path).
 """
 import math
+from typing import NamedTuple
 
 import torch
 
@@ -210,6 +212,123 @@ def linear_dgrad_high(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 def linear_wgrad_high(g2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     """dW = g2^T x2 (O, I) at 'high' precision (split-K over the rows, fixed-order reduction)."""
     return gemm_bf16x3(g2, False, x2, False, g2.shape[1], x2.shape[1], g2.shape[0])
+
+
+class Split(NamedTuple):
+    """x = hi + lo: two bf16 planes of x's shape, the operand form the split-bf16 GEMM consumes
+    without converting (rq_split_bf16x3, or a GEMM epilogue that emits it)."""
+    hi: torch.Tensor
+    lo: torch.Tensor
+
+
+def split_bf16x3(x: torch.Tensor) -> Split:
+    require_gpu(x, what="split_bf16x3")
+    x = x.contiguous()
+    hi = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    lo = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    call("rq_split_bf16x3", ptr(x), x.numel(), ptr(hi), ptr(lo), stream_handle(x.device))
+    return Split(hi, lo)
+
+
+EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD = 0, 1, 2
+
+
+def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
+            Z: torch.Tensor = None, p: float = 0.0, seed: int = 0):
+    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex). a / b: fp32
+    tensors or Split. Returns C (EPI_STORE), (C, H) (EPI_SILU_FWD: C = z, H = split(Dropout(SiLU(z))))
+    or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split of shape (M, N)."""
+    def desc(t):
+        if isinstance(t, Split):
+            return t.hi, t.lo, t.hi.shape[-1], 1
+        t = t.contiguous()
+        return t, None, t.shape[-1], 0
+    ah, al, lda, asp = desc(a)
+    bh, bl, ldb, bsp = desc(b)
+    dev = ah.device
+    C = None if epilogue == EPI_SILU_BWD else torch.empty((M, N), device=dev, dtype=torch.float32)
+    H = None
+    if epilogue != EPI_STORE:
+        H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
+                  torch.empty((M, N), device=dev, dtype=torch.bfloat16))
+    nbytes = _lib.load().rq_gemm_bf16x3_workspace(M, N, K) if epilogue == EPI_STORE else 0
+    ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8) if nbytes else None
+    TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call,
+                 "rq_gemm_bf16x3_ex", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
+                 M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
+                 float(p), int(seed), ptr(ws), nbytes, stream_handle(dev))
+    if epilogue == EPI_STORE:
+        return C
+    return (C, H) if epilogue == EPI_SILU_FWD else H
+
+
+def mlp_fusable(x: torch.Tensor, weights) -> bool:
+    """The fused chain needs fp32 device tensors, split-operand widths (every dim % 8) and rows."""
+    return (x.is_cuda and x.dtype == torch.float32 and x.numel() > 0 and
+            all(w.dtype == torch.float32 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 for w in weights))
+
+
+class MLPFunction(torch.autograd.Function):
+    """The whole bias-free Linear -> SiLU -> [Dropout] -> ... -> Linear chain of modules/encoder.py:7-36
+    at 'high' matmul precision, as one autograd node. Each hidden layer is ONE GEMM launch whose
+    epilogue keeps z (for SiLU') and emits h = Dropout(SiLU(z)) already split into bf16 planes, so
+    the next layer's forward and this layer's weight grad read it without converting; backward
+    mirrors it (the data-grad GEMM's epilogue applies SiLU' and the dropout mask and emits the
+    split pre-activation grad). Weights are split once per call. Replaces eager torch's Linear +
+    SiLU + Dropout + mask kernels (forward) and their backward passes."""
+
+    @staticmethod
+    def forward(ctx, x, p: float, *weights):
+        n = len(weights)
+        I0 = weights[0].shape[1]
+        x2 = x.reshape(-1, I0).contiguous()
+        rows = x2.shape[0]
+        wsp = [split_bf16x3(w) for w in weights]
+        seeds = [next_seed() if p > 0 else 0 for _ in range(n - 1)]
+        a, zs, hs = x2, [], []
+        out = None
+        for i, w in enumerate(weights):
+            O, I = w.shape
+            if i < n - 1:
+                z, h = gemm_x3(a, True, wsp[i], True, rows, O, I, EPI_SILU_FWD, p=p, seed=seeds[i])
+                zs.append(z)
+                hs.append(h)
+                a = h
+            else:
+                out = gemm_x3(a, True, wsp[i], True, rows, O, I)
+        ctx.n, ctx.p, ctx.seeds, ctx.xshape = n, float(p), seeds, x.shape
+        ctx.save_for_backward(x2, *[t for s_ in wsp for t in s_], *zs, *[t for h in hs for t in h])
+        return out.view(*x.shape[:-1], weights[-1].shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        n, p = ctx.n, ctx.p
+        saved = ctx.saved_tensors
+        x2 = saved[0]
+        wsp = [Split(saved[1 + 2 * i], saved[2 + 2 * i]) for i in range(n)]
+        zs = list(saved[1 + 2 * n:1 + 2 * n + (n - 1)])
+        hb = 1 + 2 * n + (n - 1)
+        hs = [Split(saved[hb + 2 * i], saved[hb + 2 * i + 1]) for i in range(n - 1)]
+        rows = x2.shape[0]
+        gcur = g.reshape(rows, -1).contiguous()
+        dws = [None] * n
+        dx = None
+        for i in reversed(range(n)):
+            O, I = wsp[i].hi.shape
+            inp = x2 if i == 0 else hs[i - 1]
+            if ctx.needs_input_grad[2 + i]:
+                dws[i] = gemm_x3(gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
+            if i > 0:
+                gcur = gemm_x3(gcur, True, wsp[i], False, rows, I, O, EPI_SILU_BWD, Z=zs[i - 1], p=p,
+                               seed=ctx.seeds[i - 1])
+            elif ctx.needs_input_grad[0]:
+                dx = gemm_x3(gcur, True, wsp[0], False, rows, I, O).view(ctx.xshape)
+        return (dx, None, *dws)
+
+
+def mlp_chain(x: torch.Tensor, weights, p: float = 0.0) -> torch.Tensor:
+    """Fused Linear-SiLU-[Dropout]-...-Linear at 'high' precision (MLPFunction)."""
+    return MLPFunction.apply(x, float(p), *weights)
 
 
 class LinearFunction(torch.autograd.Function):

@@ -154,3 +154,129 @@ def test_rqvae_step_high_vs_highest(device):
             assert (g1[k] - g0[k]).norm() <= 0.05 * g0[k].norm(), k
         else:   # flipped items also change their encoder / decoder gradient paths
             assert (g1[k] - g0[k]).norm() <= 3e-2 * g0[k].norm(), k
+
+
+# ----------------------------------------------------------------- pre-split operands, fused epilogues
+SPLIT_COMBOS = [  # (a_kc, a_split, b_kc, b_split) built for the plain epilogue besides the fp32 ones
+    (True, True, True, True), (True, False, True, True), (True, True, False, True), (True, False, False, True),
+    (False, True, False, True), (False, True, False, False), (False, False, False, True)]
+
+
+def _split(t):
+    from rqvae_hip import ops
+    return ops.split_bf16x3(t)
+
+
+@pytest.mark.parametrize("combo", SPLIT_COMBOS)
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 136, 520), (64, 128, 4104), (8, 8, 8)])
+def test_gemm_x3_split_operands_exact_on_integers(device, combo, M, N, K):
+    from rqvae_hip import ops
+    a_kc, a_sp, b_kc, b_sp = combo
+    gen = torch.Generator(device=device).manual_seed(M + 3 * N + 7 * K)
+    a, b, A, B = _operands(M, N, K, a_kc, b_kc, gen, device, True)
+    C = ops.gemm_x3(_split(a) if a_sp else a, a_kc, _split(b) if b_sp else b, b_kc, M, N, K)
+    assert torch.equal(C.double(), A @ B.t())
+
+
+def test_split_bf16x3_roundtrip(device):
+    from rqvae_hip import ops
+    x = torch.randn(1000003, device=device)
+    s = ops.split_bf16x3(x)
+    hi = x.to(torch.bfloat16)
+    assert torch.equal(s.hi, hi)
+    assert torch.equal(s.lo, (x - hi.float()).to(torch.bfloat16))
+    rel = ((s.hi.float() + s.lo.float()) - x).abs() / x.abs().clamp_min(1e-30)
+    assert rel.max() <= 2.0 ** -16
+
+
+def _close_split(H, ref):
+    """hi + lo within the split's representation error (2^-18 relative) plus ~1 ulp of hardware
+    exp / rcp in the epilogue's sigmoid (1e-5 relative + 1e-6 of the max for the cancellation in
+    silu'); the dropout mask identical (same zeros)."""
+    h = H.hi.float() + H.lo.float()
+    assert torch.equal(h == 0, ref == 0)
+    # absolute slack scaled by the tensor: silu'(z) = s (1 + z (1 - s)) cancels near z = -1.28
+    tol = 1e-5 * ref.abs() + 1e-6 * ref.abs().max()
+    assert ((h - ref).abs() <= tol).all(), float(((h - ref).abs() / tol).max())
+
+
+@pytest.mark.parametrize("p", [0.0, 0.3])
+@pytest.mark.parametrize("a_split", [False, True])
+def test_gemm_x3_silu_epilogues_match_standalone_kernels(device, p, a_split):
+    """Epilogue 1 = GEMM + rq_silu_dropout_fwd, epilogue 2 = GEMM + rq_silu_dropout_bwd (same mask
+    convention): z exact on integer operands, H within the split / fast-sigmoid bound of the
+    standalone kernels' fp32 result, with the identical dropout mask."""
+    from rqvae_hip import ops
+    from rqvae_hip._lib import call, ptr, stream_handle
+    M, N, K = 1000, 264, 136
+    gen = torch.Generator(device=device).manual_seed(11)
+    x = torch.randint(-3, 4, (M, K), generator=gen, device=device).float() / 4
+    W = torch.randint(-3, 4, (N, K), generator=gen, device=device).float() / 8
+    seed = 1234567
+    a = _split(x) if a_split else x
+    z, H = ops.gemm_x3(a, True, _split(W), True, M, N, K, ops.EPI_SILU_FWD, p=p, seed=seed)
+    zref = (x.double() @ W.double().t()).float()
+    assert torch.equal(z, zref)
+    h_ref = torch.empty_like(z)
+    call("rq_silu_dropout_fwd", ptr(z), z.numel(), float(p), seed, ptr(h_ref), stream_handle(device))
+    _close_split(H, h_ref)
+    # backward epilogue: A = g (rows, N) k-contiguous, B(n=k_in, k=n) = W[n][k_in] (n-contiguous)
+    g = torch.randint(-3, 4, (M, N), generator=gen, device=device).float() / 4
+    W2 = torch.randint(-3, 4, (N, K), generator=gen, device=device).float() / 8
+    Zb = torch.randn(M, K, generator=gen, device=device)
+    Hb = ops.gemm_x3(_split(g) if a_split else g, True, _split(W2), False, M, K, N, ops.EPI_SILU_BWD, Z=Zb, p=p,
+                     seed=seed)
+    gh = (g.double() @ W2.double()).float()
+    gz_ref = torch.empty_like(Zb)
+    call("rq_silu_dropout_bwd", ptr(gh), ptr(Zb), Zb.numel(), float(p), seed, ptr(gz_ref), stream_handle(device))
+    _close_split(Hb, gz_ref)
+
+
+@pytest.mark.parametrize("dims", [[768, 512, 256, 128, 64], [64, 128, 256, 512, 768], [96, 64, 32, 16], [128, 1024, 128]])
+def test_mlp_chain_matches_fp64(device, dims):
+    """modules.encoder.MLP at 'high' (one fused MLPFunction node) vs the same MLP in fp64: output
+    and every gradient within the split-bf16 bound (1e-4 of the max)."""
+    from modules.encoder import MLP
+    torch.manual_seed(1)
+    mlp = MLP(dims[0], dims[1:-1], dims[-1]).to(device)
+    ref = MLP(dims[0], dims[1:-1], dims[-1]).to(device).double()
+    ref.load_state_dict({k: v.double() for k, v in mlp.state_dict().items()})
+    x = torch.randn(3000, dims[0], device=device, requires_grad=True)
+    xr = x.detach().double().requires_grad_(True)
+    torch.set_float32_matmul_precision("high")
+    assert mlp._fused_chain(x) is not None
+    y = mlp(x)
+    (y.sin().sum()).backward()
+    torch.set_float32_matmul_precision("highest")
+    yr = ref(xr)
+    (yr.sin().sum()).backward()
+
+    def close(a, b):
+        return (a.double() - b).abs().max() <= 1e-4 * b.abs().max() + 1e-7
+    assert close(y, yr)
+    assert close(x.grad, xr.grad)
+    for (k, p_), (_, pr) in zip(mlp.named_parameters(), ref.named_parameters()):
+        assert close(p_.grad, pr.grad), k
+
+
+def test_mlp_chain_dropout(device):
+    """Dropout inside the fused chain: train mode drops ~p of the hidden units (forward and the
+    matching backward mask), eval mode is deterministic and equals the p = 0 chain."""
+    from modules.encoder import MLP
+    torch.manual_seed(2)
+    mlp = MLP(128, [1024], 128, dropout=0.3).to(device)
+    x = torch.randn(4096, 128, device=device, requires_grad=True)
+    torch.set_float32_matmul_precision("high")
+    mlp.train()
+    y = mlp(x)
+    y.sum().backward()
+    assert torch.isfinite(y).all() and torch.isfinite(x.grad).all()
+    mlp.eval()
+    with torch.no_grad():
+        e1, e2 = mlp(x), mlp(x)
+    assert torch.equal(e1, e2)
+    torch.set_float32_matmul_precision("highest")
+    with torch.no_grad():
+        e3 = mlp(x)
+    assert (e1 - e3).abs().max() <= 1e-4 * e3.abs().max()
+    assert not torch.equal(y.detach(), e1)
