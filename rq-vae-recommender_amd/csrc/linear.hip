@@ -461,8 +461,6 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
 
-  XStage<AKC, ASP> sa;
-  XStage<BKC, BSP> sb;
   floatx16 acc[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -473,49 +471,58 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 
   auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
   const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
-  sa.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
-  sb.load(B, Bl, ldb, n0, N, k_lo, k_lo, k_hi, tid);
-  sa.store(plane(0, 0, 0), plane(0, 0, 1), tid);
-  sb.store(plane(0, 1, 0), plane(0, 1, 1), tid);
+  // Two register sets: stage st + 2 is loaded while stage st is multiplied and stage st + 1 (loaded
+  // one iteration earlier) is written to the other LDS buffer, so each load has two stages of
+  // MFMA work to land in (HBM latency under load is ~2-4k cycles, one stage ~1.5k).
+  XStage<AKC, ASP> sa0, sa1;
+  XStage<BKC, BSP> sb0, sb1;
+  sa0.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
+  sb0.load(B, Bl, ldb, n0, N, k_lo, k_lo, k_hi, tid);
+  sa1.load(A, Al, lda, m0, M, k_lo + (nst > 1 ? kXK : 0), k_lo, k_hi, tid);
+  sb1.load(B, Bl, ldb, n0, N, k_lo + (nst > 1 ? kXK : 0), k_lo, k_hi, tid);
+  sa0.store(plane(0, 0, 0), plane(0, 0, 1), tid);
+  sb0.store(plane(0, 1, 0), plane(0, 1, 1), tid);
   __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nst) {   // next stage's loads in flight during this stage's MFMAs
-      const int64_t kb = k_lo + (int64_t)(st + 1) * kXK;
-      sa.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);
-      sb.load(B, Bl, ldb, n0, N, kb, k_lo, k_hi, tid);
-    }
-    const char* ah = plane(buf, 0, 0);
-    const char* al = plane(buf, 0, 1);
-    const char* bh = plane(buf, 1, 0);
-    const char* bl = plane(buf, 1, 1);
-#pragma unroll
-    for (int ks = 0; ks < kXK / 16; ++ks) {
-      bf16x8_t fa_h[2], fa_l[2], fb_h[2], fb_l[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        fa_h[p] = xfrag<AKC>(ah, wm * 64 + 32 * p, ks, lane);
-        fa_l[p] = xfrag<AKC>(al, wm * 64 + 32 * p, ks, lane);
-        fb_h[p] = xfrag<BKC>(bh, wn * 64 + 32 * p, ks, lane);
-        fb_l[p] = xfrag<BKC>(bl, wn * 64 + 32 * p, ks, lane);
-      }
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          // transposed product D = B A^T (tile rows = n, columns = m): each lane then holds 4
-          // consecutive n of one row m per register quad, so the epilogue stores vectors
-          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);
-          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);
-          acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);
-        }
-    }
-    if (st + 1 < nst) {
-      sa.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);
-      sb.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
-    }
-    __syncthreads();
+
+#define RQ_X3_STAGE(ST, LA, LB, SA, SB)                                                                       \
+  {                                                                                                           \
+    const int st_ = (ST), buf = st_ & 1;                                                                      \
+    {  /* unconditional (past the end: the last stage again, an L2 hit) so vmcnt counts stay static */       \
+      const int64_t kb = k_lo + (int64_t)min(st_ + 2, nst - 1) * kXK;                                         \
+      LA.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);                                                        \
+      LB.load(B, Bl, ldb, n0, N, kb, k_lo, k_hi, tid);                                                        \
+    }                                                                                                         \
+    const char* ah = plane(buf, 0, 0);                                                                        \
+    const char* al = plane(buf, 0, 1);                                                                        \
+    const char* bh = plane(buf, 1, 0);                                                                        \
+    const char* bl = plane(buf, 1, 1);                                                                        \
+    _Pragma("unroll") for (int ks = 0; ks < kXK / 16; ++ks) {                                                 \
+      bf16x8_t fa_h[2], fa_l[2], fb_h[2], fb_l[2];                                                            \
+      _Pragma("unroll") for (int p = 0; p < 2; ++p) {                                                         \
+        fa_h[p] = xfrag<AKC>(ah, wm * 64 + 32 * p, ks, lane);                                                 \
+        fa_l[p] = xfrag<AKC>(al, wm * 64 + 32 * p, ks, lane);                                                 \
+        fb_h[p] = xfrag<BKC>(bh, wn * 64 + 32 * p, ks, lane);                                                 \
+        fb_l[p] = xfrag<BKC>(bl, wn * 64 + 32 * p, ks, lane);                                                 \
+      }                                                                                                       \
+      /* transposed product D = B A^T (tile rows = n, columns = m): each lane then holds 4 */                \
+      /* consecutive n of one row m per register quad, so the epilogue stores vectors */                     \
+      _Pragma("unroll") for (int p = 0; p < 2; ++p) _Pragma("unroll") for (int q = 0; q < 2; ++q) {          \
+        acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);            \
+        acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);            \
+        acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);            \
+      }                                                                                                       \
+    }                                                                                                         \
+    /* unconditional: past the last stage it writes a buffer nobody reads, and a conditional store */       \
+    /* would leave the set's loads possibly pending, so the compiler waits vmcnt(0) before reloading it */    \
+    SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                \
+    SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                \
+    __syncthreads();                                                                                          \
   }
+  for (int st = 0; st < nst; st += 2) {
+    RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)   // set 0 held stage st (already in LDS): reload it with st + 2
+    if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0)
+  }
+#undef RQ_X3_STAGE
 
   // C/D map of D = B A^T: column (lane & 31) = m, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5) = n, so
   // register quad g holds C[m][n .. n + 3], n = 8 g + 4 (lane >> 5) (+ tile offsets): 16-B fp32 /
