@@ -413,6 +413,35 @@ __device__ __forceinline__ bf16x8_t xfrag(const char* plane, int rb, int s, int 
   }
 }
 
+// 16x16x32 operand fragment (8 bf16: row rb + lane % 16, k = 8 (lane / 16) + 0..7 of the stage).
+template <bool KC>
+__device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane) {
+  if constexpr (KC) {
+    const int rr = rb + (lane & 15), c = lane >> 4;
+    return *reinterpret_cast<const bf16x8_t*>(plane + rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4));
+  } else {
+    // ds_read_b64_tr_b16 per 16-lane group G (k-rows 8G .. 8G + 7 in two 4-row blocks): lane
+    // 4q + p supplies the address of k-row q, rows 4p..4p+3, and receives row (lane % 16).
+    const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int m = rb + 4 * p;
+    s16x4_t t[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kr = 8 * G + 4 * u + q;
+      const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
+      t[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4_t*)(plane + off));
+    }
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    const s16x8_t r = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w};
+    return __builtin_bit_cast(bf16x8_t, r);
+  }
+}
+
+#ifndef RQ_X3_MFMA16
+#define RQ_X3_MFMA16 1   // 16x16x32 bf16 MFMA (4 x 4 tiles per wave); 0: 32x32x16 (2 x 2 tiles)
+#endif
+
 // Epilogues: what the accumulator tile becomes (all fp32 math; dropout mask = keep1(seed, m N + n),
 // the convention of the standalone dropout kernels, dropout.hip).
 enum X3Epi : int {
@@ -445,6 +474,42 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
   *lo = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));
 }
 
+// One LDS stage of MFMA work per wave. Transposed product D = B A^T (tile rows = n, columns = m):
+// each lane then holds consecutive n of one row m, so the epilogue stores vectors.
+#if RQ_X3_MFMA16
+#define RQ_X3_MMA                                                                                             \
+  {                                                                                                           \
+    bf16x8_t fa_h[4], fa_l[4], fb_h[4], fb_l[4];                                                              \
+    _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                                           \
+      fa_h[p] = xfrag16<AKC>(ah, wm * 64 + 16 * p, lane);                                                     \
+      fa_l[p] = xfrag16<AKC>(al, wm * 64 + 16 * p, lane);                                                     \
+      fb_h[p] = xfrag16<BKC>(bh, wn * 64 + 16 * p, lane);                                                     \
+      fb_l[p] = xfrag16<BKC>(bl, wn * 64 + 16 * p, lane);                                                     \
+    }                                                                                                         \
+    _Pragma("unroll") for (int p = 0; p < 4; ++p) _Pragma("unroll") for (int q = 0; q < 4; ++q) {            \
+      acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);              \
+      acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);              \
+      acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);              \
+    }                                                                                                         \
+  }
+#else
+#define RQ_X3_MMA                                                                                             \
+  _Pragma("unroll") for (int ks = 0; ks < kXK / 16; ++ks) {                                                   \
+    bf16x8_t fa_h[2], fa_l[2], fb_h[2], fb_l[2];                                                              \
+    _Pragma("unroll") for (int p = 0; p < 2; ++p) {                                                           \
+      fa_h[p] = xfrag<AKC>(ah, wm * 64 + 32 * p, ks, lane);                                                   \
+      fa_l[p] = xfrag<AKC>(al, wm * 64 + 32 * p, ks, lane);                                                   \
+      fb_h[p] = xfrag<BKC>(bh, wn * 64 + 32 * p, ks, lane);                                                   \
+      fb_l[p] = xfrag<BKC>(bl, wn * 64 + 32 * p, ks, lane);                                                   \
+    }                                                                                                         \
+    _Pragma("unroll") for (int p = 0; p < 2; ++p) _Pragma("unroll") for (int q = 0; q < 2; ++q) {            \
+      acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);              \
+      acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);              \
+      acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);              \
+    }                                                                                                         \
+  }
+#endif
+
 template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false>
 __global__ void __launch_bounds__(256, 2)
 gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
@@ -461,6 +526,13 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
 
+#if RQ_X3_MFMA16
+  floatx4v acc[4][4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+#else
   floatx16 acc[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -468,6 +540,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[p][q][r] = 0.f;
+#endif
 
   auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
   const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
@@ -496,22 +569,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
     const char* al = plane(buf, 0, 1);                                                                        \
     const char* bh = plane(buf, 1, 0);                                                                        \
     const char* bl = plane(buf, 1, 1);                                                                        \
-    _Pragma("unroll") for (int ks = 0; ks < kXK / 16; ++ks) {                                                 \
-      bf16x8_t fa_h[2], fa_l[2], fb_h[2], fb_l[2];                                                            \
-      _Pragma("unroll") for (int p = 0; p < 2; ++p) {                                                         \
-        fa_h[p] = xfrag<AKC>(ah, wm * 64 + 32 * p, ks, lane);                                                 \
-        fa_l[p] = xfrag<AKC>(al, wm * 64 + 32 * p, ks, lane);                                                 \
-        fb_h[p] = xfrag<BKC>(bh, wn * 64 + 32 * p, ks, lane);                                                 \
-        fb_l[p] = xfrag<BKC>(bl, wn * 64 + 32 * p, ks, lane);                                                 \
-      }                                                                                                       \
-      /* transposed product D = B A^T (tile rows = n, columns = m): each lane then holds 4 */                \
-      /* consecutive n of one row m per register quad, so the epilogue stores vectors */                     \
-      _Pragma("unroll") for (int p = 0; p < 2; ++p) _Pragma("unroll") for (int q = 0; q < 2; ++q) {          \
-        acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);            \
-        acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);            \
-        acc[p][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);            \
-      }                                                                                                       \
-    }                                                                                                         \
+    RQ_X3_MMA                                                                                                 \
     /* unconditional: past the last stage it writes a buffer nobody reads, and a conditional store */       \
     /* would leave the set's loads possibly pending, so the compiler waits vmcnt(0) before reloading it */    \
     SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                \
@@ -523,23 +581,38 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
     if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0)
   }
 #undef RQ_X3_STAGE
+#undef RQ_X3_MMA
 
-  // C/D map of D = B A^T: column (lane & 31) = m, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5) = n, so
-  // register quad g holds C[m][n .. n + 3], n = 8 g + 4 (lane >> 5) (+ tile offsets): 16-B fp32 /
-  // 8-B bf16 stores (N % 4 == 0).
+  // Each lane stores C[m][n .. n + 3] quads: 16-B fp32 / 8-B bf16 stores (N % 4 == 0).
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
-  const int h = lane >> 5, c32 = lane & 31;
+#if RQ_X3_MFMA16
+  // 16x16 C/D map of D = B A^T: column (lane & 15) = m, row 4 (lane >> 4) + j = n (j = register).
+  constexpr int kPM = 4, kPN = 4, kG = 1;
+#else
+  // 32x32 C/D map: column (lane & 31) = m, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5) = n: register
+  // quad g holds n = 8 g + 4 (lane >> 5) + 0..3.
+  constexpr int kPM = 2, kPN = 2, kG = 4;
+#endif
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int m = m0 + wm * 64 + 32 * p + c32;
+  for (int p = 0; p < kPM; ++p) {
+#if RQ_X3_MFMA16
+    const int m = m0 + wm * 64 + 16 * p + (lane & 15);
+#else
+    const int m = m0 + wm * 64 + 32 * p + (lane & 31);
+#endif
     if (m < M) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < kPN; ++q)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int n = n0 + wn * 64 + 32 * q + 8 * g + 4 * h;
-          if (n >= N) continue;
+        for (int g = 0; g < kG; ++g) {
+#if RQ_X3_MFMA16
+          const int n = n0 + wn * 64 + 16 * q + 4 * (lane >> 4);
+          const float4 v = make_float4(acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]);
+#else
+          const int n = n0 + wn * 64 + 32 * q + 8 * g + 4 * (lane >> 5);
           const float4 v = make_float4(acc[p][q][4 * g], acc[p][q][4 * g + 1], acc[p][q][4 * g + 2], acc[p][q][4 * g + 3]);
+#endif
+          if (n >= N) continue;
           if constexpr (EPI == kEpiStore) {
             *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
           } else {

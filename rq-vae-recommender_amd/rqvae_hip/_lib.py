@@ -93,7 +93,7 @@ def load(path: str = None):
 
 
 def call(name: str, *args):
-    rc = getattr(load(), name)(*args)
+    rc = getattr(_lib if _lib is not None else load(), name)(*args)
     if rc != 0:
         msg = load().rq_last_error().decode(errors="replace")
         raise RqHipError(f"{name} failed (rc={rc}): {msg}")
@@ -103,7 +103,21 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle(device=None):
+    """torch's current HIP stream of `device` (default: the current device) as a C pointer. Uses
+    the raw-stream query (no Stream object, no device-index normalisation): this runs once per
+    kernel launch, so the decoder step's ~140 launches make it a visible host cost."""
+    if _RAW_STREAM is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return ctypes.c_void_p(_RAW_STREAM(idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

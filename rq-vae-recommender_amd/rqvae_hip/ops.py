@@ -189,11 +189,14 @@ def gemm_bf16x3(a: torch.Tensor, a_kcontig: bool, b: torch.Tensor, b_kcontig: bo
     b = b.contiguous()
     lda, ldb = a.shape[1], b.shape[1]
     C = out if out is not None else torch.empty((M, N), device=a.device, dtype=torch.float32)
-    nbytes = _lib.load().rq_gemm_bf16x3_workspace(M, N, K)
+    nbytes = _x3_workspace(M, N, K)
     ws = torch.empty((nbytes,), device=a.device, dtype=torch.uint8) if nbytes else None
-    TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}", call, "rq_gemm_bf16x3", ptr(a), lda,
-                 int(a_kcontig), ptr(b), ldb, int(b_kcontig), M, N, K, ptr(C), N, ptr(ws), nbytes,
-                 stream_handle(a.device))
+    args = ("rq_gemm_bf16x3", ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), M, N, K, ptr(C), N, ptr(ws),
+            nbytes, stream_handle(a.device))
+    if TIMER.enabled:
+        TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}", call, *args)
+    else:
+        call(*args)
     return C
 
 
@@ -231,6 +234,16 @@ def split_bf16x3(x: torch.Tensor) -> Split:
 
 
 EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD = 0, 1, 2
+_X3_WS = {}
+
+
+def _x3_workspace(M: int, N: int, K: int) -> int:
+    """Split-K slab bytes of rq_gemm_bf16x3 for a shape (host-only plan, memoised per shape)."""
+    key = (M, N, K)
+    nb = _X3_WS.get(key)
+    if nb is None:
+        nb = _X3_WS[key] = int(_lib.load().rq_gemm_bf16x3_workspace(M, N, K))
+    return nb
 
 
 def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
@@ -251,12 +264,15 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     if epilogue != EPI_STORE:
         H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
-    nbytes = _lib.load().rq_gemm_bf16x3_workspace(M, N, K) if epilogue == EPI_STORE else 0
+    nbytes = _x3_workspace(M, N, K) if epilogue == EPI_STORE else 0
     ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8) if nbytes else None
-    TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call,
-                 "rq_gemm_bf16x3_ex", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
-                 M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
-                 float(p), int(seed), ptr(ws), nbytes, stream_handle(dev))
+    args = ("rq_gemm_bf16x3_ex", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
+            M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
+            float(p), int(seed), ptr(ws), nbytes, stream_handle(dev))
+    if TIMER.enabled:
+        TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call, *args)
+    else:
+        call(*args)
     if epilogue == EPI_STORE:
         return C
     return (C, H) if epilogue == EPI_SILU_FWD else H
@@ -343,8 +359,14 @@ class LinearFunction(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.high = matmul_high()
         O, I = weight.shape
+        ctx.wsp = None
         if ctx.high and x.numel() > 0:
-            y = linear_fwd_high(x.reshape(-1, I), weight)
+            x2 = x.reshape(-1, I)
+            if I % 8 == 0:   # split the weight once: forward and data grad read it without converting
+                ctx.wsp = split_bf16x3(weight)
+                y = gemm_x3(x2, True, ctx.wsp, True, x2.shape[0], O, I)
+            else:
+                y = linear_fwd_high(x2, weight)
             if bias is not None:
                 y += bias
             return y.view(*x.shape[:-1], O)
@@ -358,7 +380,11 @@ class LinearFunction(torch.autograd.Function):
         gx = dW = db = None
         high = ctx.high and g2.shape[0] > 0
         if ctx.needs_input_grad[0]:
-            gx = (linear_dgrad_high(g2, weight) if high else g2 @ weight).view(x.shape)
+            if high and ctx.wsp is not None:
+                gx = gemm_x3(g2, True, ctx.wsp, False, g2.shape[0], I, O).view(x.shape)
+            else:
+                gx = (linear_dgrad_high(g2, weight) if high else g2 @ weight).view(x.shape)
+        ctx.wsp = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             x2 = x.reshape(-1, I)
             if high:
