@@ -16,6 +16,7 @@ import torch
 from torch.utils.data import Dataset
 
 from data.schemas import SeqBatch, TokenizedSeqBatch
+from ops.jagged import register_row_counts
 
 
 class RecDataset(Enum):
@@ -129,6 +130,8 @@ def synthetic_tokenized_batch(B: int, max_items: int, sem_id_dim: int, K: int, s
     fut = g.integers(0, K, size=(B, sem_id_dim))
     fut[:, -1] = 0
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
-    return TokenizedSeqBatch(user_ids=t(g.integers(0, 10 ** 6, size=(B, 1))), sem_ids=t(sem), sem_ids_fut=t(fut),
-                             seq_mask=t(mask), token_type_ids=t(np.tile(np.arange(sem_id_dim), (B, max_items))),
-                             token_type_ids_fut=t(np.tile(np.arange(sem_id_dim), (B, 1))))
+    batch = TokenizedSeqBatch(user_ids=t(g.integers(0, 10 ** 6, size=(B, 1))), sem_ids=t(sem), sem_ids_fut=t(fut),
+                              seq_mask=t(mask), token_type_ids=t(np.tile(np.arange(sem_id_dim), (B, max_items))),
+                              token_type_ids_fut=t(np.tile(np.arange(sem_id_dim), (B, 1))))
+    register_row_counts(batch.seq_mask, mask.sum(axis=1))   # built on the host: lengths known, no sync later
+    return batch

@@ -23,7 +23,7 @@ from modules.embedding.id_embedder import Embedding, SemIdEmbedder, UserIdEmbedd
 from modules.normalize import RMSNorm
 from modules.transformer.model import TransformerEncoderDecoder
 from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
-from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged
+from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged, row_counts
 from rqvae_hip import gemm_tuning
 
 # As the reference (modules/model.py:27): fp32 matmuls at 'high' precision (split-bf16 GEMM on
@@ -87,7 +87,13 @@ class EncoderDecoderRetrievalModel(nn.Module):
         # one host sync (total); with tuned library GEMMs the row count is bucketed so that the
         # variable-length context presents a bounded set of GEMM shapes (rqvae_hip.gemm_tuning)
         bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
-        ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1], row_bucket=bucket)
+        host = row_counts(batch.seq_mask)   # registered by a CPU-side loader: no sync needed
+        if host is not None and host[3] == B:
+            ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1], total=host[0] + B,
+                                     known_max=min(host[2] + 1, ctx.shape[1]), known_min=min(host[1] + 1, ctx.shape[1]),
+                                     row_bucket=bucket)
+        else:
+            ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1], row_bucket=bucket)
         nf = fut.shape[1]                                                                # fixed length: no sync
         fut_lengths = torch.full((B,), nf, device=fut.device, dtype=torch.int64)
         fut_j = padded_to_jagged(fut.contiguous(), fut_lengths, nf, total=B * nf, known_max=nf)

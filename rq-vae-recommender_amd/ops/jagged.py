@@ -11,6 +11,8 @@ padded element once: copy or zero). Offsets are int64 (the reference stores them
 SURVEY A-1), and the NJT carries exact min/max sequence lengths, so downstream varlen
 attention never recomputes them.
 """
+import weakref
+
 import torch
 from torch import Tensor
 
@@ -65,8 +67,27 @@ def as_jagged(x) -> Jagged:
     return Jagged(x.values(), x.offsets(), int(mx), int(mn or 0))
 
 
+_HOST_ROWS = {}
+
+
+def register_row_counts(mask: Tensor, counts) -> None:
+    """Attach host-side per-row valid counts to a device mask tensor (a data loader that builds its
+    batches on the CPU knows them for free), so the jagged conversions of that batch need no
+    device -> host sync: the entry lives as long as the tensor."""
+    c = [int(v) for v in counts]
+    key = id(mask)
+    _HOST_ROWS[key] = (weakref.ref(mask), (sum(c), min(c), max(c), len(c)))
+    weakref.finalize(mask, _HOST_ROWS.pop, key, None)
+
+
+def row_counts(mask: Tensor):
+    """(sum, min, max, rows) of the counts registered for `mask`, or None."""
+    e = _HOST_ROWS.get(id(mask))
+    return e[1] if e is not None and e[0]() is mask else None
+
+
 def padded_to_jagged(x: Tensor, lengths: Tensor, max_len: int, total: int = None, add_one_sub_one: bool = True,
-                     known_max: int = None, row_bucket: int = None) -> Jagged:
+                     known_max: int = None, row_bucket: int = None, known_min: int = None) -> Jagged:
     """HIP padded -> jagged gather. `total` / `known_max` (host ints) skip the host sync when the
     caller already knows them (e.g. fixed-length decoder inputs). `row_bucket`: allocate the values
     with their row count rounded up to this multiple, tail rows zero (bounded set of GEMM shapes)."""
@@ -78,7 +99,8 @@ def padded_to_jagged(x: Tensor, lengths: Tensor, max_len: int, total: int = None
     if total is None:
         total, lmin, lmax = torch.stack([offsets[-1], lengths.clamp(0, n).min(), lengths.clamp(0, n).max()]).tolist()
     else:
-        lmin = lmax = known_max if known_max is not None else n
+        lmax = known_max if known_max is not None else n
+        lmin = known_min if known_min is not None else lmax
     alloc = int(total) if not row_bucket else (int(total) + row_bucket - 1) // row_bucket * row_bucket
     values = hip_ops.PaddedToJaggedValues.apply(x, offsets, int(total), add_one_sub_one, alloc)
     return Jagged(values, offsets, int(lmax), int(lmin), int(total))

@@ -26,11 +26,15 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
+        self.only = None      # optional set of name prefixes to record (others run untimed)
         self.events = {}
         self.bytes = {}
 
+    def wants(self, name: str) -> bool:
+        return self.enabled and (self.only is None or any(name.startswith(p) for p in self.only))
+
     def around(self, name, fn, *args):
-        if not self.enabled:
+        if not self.wants(name):
             return fn(*args)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
@@ -193,7 +197,7 @@ def gemm_bf16x3(a: torch.Tensor, a_kcontig: bool, b: torch.Tensor, b_kcontig: bo
     ws = torch.empty((nbytes,), device=a.device, dtype=torch.uint8) if nbytes else None
     args = ("rq_gemm_bf16x3", ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), M, N, K, ptr(C), N, ptr(ws),
             nbytes, stream_handle(a.device))
-    if TIMER.enabled:
+    if TIMER.wants("gemm_bf16x3"):
         TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}", call, *args)
     else:
         call(*args)
@@ -269,7 +273,7 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     args = ("rq_gemm_bf16x3_ex", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
             M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
             float(p), int(seed), ptr(ws), nbytes, stream_handle(dev))
-    if TIMER.enabled:
+    if TIMER.wants("gemm_bf16x3"):
         TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call, *args)
     else:
         call(*args)
@@ -655,7 +659,7 @@ class PaddedToJaggedValues(torch.autograd.Function):
             vals[total:].zero_()   # bucket tail rows (rqvae_hip.gemm_tuning)
         TIMER.around("jagged_from_padded", call, "jagged_from_padded", ptr(x), B, N, D, ptr(offsets), ptr(vals),
                      _DTYPES[x.dtype], int(add_one_sub_one), stream_handle(x.device))
-        if TIMER.enabled:
+        if TIMER.wants("jagged_from_padded"):
             TIMER.bytes.setdefault("jagged_from_padded", []).append(2 * total * D * x.element_size())
         ctx.save_for_backward(offsets)
         ctx.shape = (B, N, D)
@@ -669,7 +673,7 @@ class PaddedToJaggedValues(torch.autograd.Function):
         gx = torch.empty((B, N, D), device=g_vals.device, dtype=g_vals.dtype)
         TIMER.around("jagged_to_padded", call, "jagged_to_padded", ptr(g_vals), ptr(offsets), B, N, D, ptr(gx),
                      _DTYPES[g_vals.dtype], stream_handle(g_vals.device))
-        if TIMER.enabled:
+        if TIMER.wants("jagged_to_padded"):
             TIMER.bytes.setdefault("jagged_to_padded", []).append((g_vals.numel() + gx.numel()) * gx.element_size())
         return gx, None, None, None, None
 

@@ -63,7 +63,7 @@ def main():
     orig = J.padded_to_jagged
     cache = {}
 
-    def cached(x, lengths, max_len, total=None, add_one_sub_one=True, known_max=None, row_bucket=None):
+    def cached(x, lengths, max_len, total=None, add_one_sub_one=True, known_max=None, row_bucket=None, known_min=None):
         if total is None:
             key = ((it[0] - 1) % 4, lengths.shape[0], int(max_len))   # the batch being stepped
             if key not in cache:
@@ -71,7 +71,7 @@ def main():
                 cache[key] = (int(lengths.clamp(0, n).sum()), int(lengths.clamp(0, n).max()))
             total, known_max = cache[key]
         return orig(x, lengths, max_len, total=total, add_one_sub_one=add_one_sub_one, known_max=known_max,
-                    row_bucket=row_bucket)
+                    row_bucket=row_bucket, known_min=known_min)
     import modules.model as MM
     J.padded_to_jagged = cached
     MM.padded_to_jagged = cached
