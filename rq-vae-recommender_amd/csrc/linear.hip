@@ -438,6 +438,18 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
   }
 }
 
+#ifndef RQ_X3_DEPTH
+#define RQ_X3_DEPTH 2    // register stage sets in flight (2 or 3; 3 spills on the transposed-B variants)
+#endif
+
+#ifndef RQ_X3_MIN_STAGES
+#define RQ_X3_MIN_STAGES 4   // split-K: k-stages per workgroup at least (fewer slabs to reduce)
+#endif
+
+#ifndef RQ_X3_INTERLEAVE
+#define RQ_X3_INTERLEAVE 0   // 1: next-stage LDS writes between the MFMAs (measured 20 % slower)
+#endif
+
 #ifndef RQ_X3_MFMA16
 #define RQ_X3_MFMA16 1   // 16x16x32 bf16 MFMA (4 x 4 tiles per wave); 0: 32x32x16 (2 x 2 tiles)
 #endif
@@ -544,15 +556,23 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 
   auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
   const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
-  // Two register sets: stage st + 2 is loaded while stage st is multiplied and stage st + 1 (loaded
-  // one iteration earlier) is written to the other LDS buffer, so each load has two stages of
-  // MFMA work to land in (HBM latency under load is ~2-4k cycles, one stage ~1.5k).
+  // RQ_X3_DEPTH register stage sets: stage st + DEPTH is loaded while stage st is multiplied and
+  // stage st + 1 (loaded earlier) is written to the other LDS buffer, so each load has DEPTH stages
+  // of MFMA work to land in (HBM latency under load is ~2-4k cycles, one stage ~1.5k).
   XStage<AKC, ASP> sa0, sa1;
   XStage<BKC, BSP> sb0, sb1;
+#if RQ_X3_DEPTH == 3
+  XStage<AKC, ASP> sa2;
+  XStage<BKC, BSP> sb2;
+#endif
   sa0.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
   sb0.load(B, Bl, ldb, n0, N, k_lo, k_lo, k_hi, tid);
-  sa1.load(A, Al, lda, m0, M, k_lo + (nst > 1 ? kXK : 0), k_lo, k_hi, tid);
-  sb1.load(B, Bl, ldb, n0, N, k_lo + (nst > 1 ? kXK : 0), k_lo, k_hi, tid);
+  sa1.load(A, Al, lda, m0, M, k_lo + (int64_t)min(1, nst - 1) * kXK, k_lo, k_hi, tid);
+  sb1.load(B, Bl, ldb, n0, N, k_lo + (int64_t)min(1, nst - 1) * kXK, k_lo, k_hi, tid);
+#if RQ_X3_DEPTH == 3
+  sa2.load(A, Al, lda, m0, M, k_lo + (int64_t)min(2, nst - 1) * kXK, k_lo, k_hi, tid);
+  sb2.load(B, Bl, ldb, n0, N, k_lo + (int64_t)min(2, nst - 1) * kXK, k_lo, k_hi, tid);
+#endif
   sa0.store(plane(0, 0, 0), plane(0, 0, 1), tid);
   sb0.store(plane(0, 1, 0), plane(0, 1, 1), tid);
   __syncthreads();
@@ -561,7 +581,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   {                                                                                                           \
     const int st_ = (ST), buf = st_ & 1;                                                                      \
     {  /* unconditional (past the end: the last stage again, an L2 hit) so vmcnt counts stay static */       \
-      const int64_t kb = k_lo + (int64_t)min(st_ + 2, nst - 1) * kXK;                                         \
+      const int64_t kb = k_lo + (int64_t)min(st_ + RQ_X3_DEPTH, nst - 1) * kXK;                               \
       LA.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);                                                        \
       LB.load(B, Bl, ldb, n0, N, kb, k_lo, k_hi, tid);                                                        \
     }                                                                                                         \
@@ -569,18 +589,44 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
     const char* al = plane(buf, 0, 1);                                                                        \
     const char* bh = plane(buf, 1, 0);                                                                        \
     const char* bl = plane(buf, 1, 1);                                                                        \
-    RQ_X3_MMA                                                                                                 \
-    /* unconditional: past the last stage it writes a buffer nobody reads, and a conditional store */       \
-    /* would leave the set's loads possibly pending, so the compiler waits vmcnt(0) before reloading it */    \
-    SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                \
-    SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                \
+    RQ_X3_BODY(SA, SB)                                                                                        \
     __syncthreads();                                                                                          \
   }
+  // Stage body: the MFMAs on buffer buf and the write of the next stage's registers into buf ^ 1
+  // (free since the previous barrier; unconditional: past the last stage it writes a buffer nobody
+  // reads, and a conditional store would leave the set's loads possibly pending, so the compiler
+  // would wait vmcnt(0) before reloading it). RQ_X3_INTERLEAVE issues the write (its VALU and
+  // ds_writes) between the MFMAs instead of after them.
+#if RQ_X3_INTERLEAVE
+#define RQ_X3_BODY(SA, SB)                                                                                    \
+  SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
+  SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                  \
+  RQ_X3_MMA                                                                                                   \
+  _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);                                                        \
+  }
+#else
+#define RQ_X3_BODY(SA, SB)                                                                                    \
+  RQ_X3_MMA                                                                                                   \
+  SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
+  SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
+#endif
+#if RQ_X3_DEPTH == 3
+  for (int st = 0; st < nst; st += 3) {
+    RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)   // set j % 3 holds stage j: reload set (st % 3) with st + 3
+    if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2)
+    if (st + 2 < nst) RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0)
+  }
+#else
   for (int st = 0; st < nst; st += 2) {
     RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)   // set 0 held stage st (already in LDS): reload it with st + 2
     if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0)
   }
+#endif
 #undef RQ_X3_STAGE
+#undef RQ_X3_BODY
 #undef RQ_X3_MMA
 
   // Each lane stores C[m][n .. n + 3] quads: 16-B fp32 / 8-B bf16 stores (N % 4 == 0).
@@ -668,7 +714,7 @@ static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) 
   int64_t S = 1;
   if (allow_split && p.tiles < resident_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
     S = resident_slots() / p.tiles;
-    const int64_t max_s = (K + 4 * kXK - 1) / (4 * kXK);   // at least 4 stages per workgroup
+    const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
     if (S > max_s) S = max_s;
     if (S < 1) S = 1;
   }

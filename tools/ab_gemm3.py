@@ -4,7 +4,7 @@ entry point (a standalone .so of linear.hip + dropout.hip built with different m
 RQ-VAE MLP launch shapes (split operands / epilogues as the fused chain issues them). Interleaved
 rounds, HIP events.
 
-  python tools/ab_gemm3.py tools/_ab_x3_mfma32.so
+  python tools/ab_gemm3.py tools/_ab_x3_mfma32.so [dec]
 """
 import ctypes
 import json
@@ -29,6 +29,11 @@ CASES = [(65536, 512, 768, 1, 0, 1, 1, 1), (65536, 256, 512, 1, 1, 1, 1, 1), (65
          (65536, 128, 256, 1, 1, 1, 1, 1), (65536, 64, 128, 1, 1, 1, 1, 0)]
 
 
+# decoder weight grads (rows = bucketed context / future tokens of a 256-sequence batch)
+DEC_CASES = [(O, I, R, 0, 0, 0, 0, 0) for R in (12288, 20480) for (O, I) in ((512, 512), (1536, 512), (1024, 512),
+                                                                             (512, 1024))]
+
+
 def bind(lib):
     f = lib.rq_gemm_bf16x3_ex
     f.argtypes, f.restype = SIG, I
@@ -41,7 +46,8 @@ def main():
     dev = torch.device("cuda", 0)
     arms = {"new": bind(_lib.load()), "old": bind(ctypes.CDLL(os.path.abspath(sys.argv[1])))}
     tot = {a: 0.0 for a in arms}
-    for (M, N, K, akc, asp, bkc, bsp, epi) in CASES:
+    cases = DEC_CASES if len(sys.argv) > 2 and sys.argv[2] == "dec" else CASES
+    for (M, N, K, akc, asp, bkc, bsp, epi) in cases:
         g = torch.Generator(device=dev).manual_seed(M + N + K)
         a = torch.randn((M, K) if akc else (K, M), generator=g, device=dev)
         b = torch.randn((N, K) if bkc else (K, N), generator=g, device=dev) / K ** 0.5
