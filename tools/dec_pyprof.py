@@ -33,9 +33,16 @@ def main():
         opt.zero_grad(set_to_none=True)
         m(batches[i % 4]).loss.backward()
         opt.step()
+    torch.autograd.set_multithreading_enabled(False)   # backward on this thread: visible to cProfile
     for i in range(5):
         step(i)
     torch.cuda.synchronize()
+    import time
+    t0 = time.perf_counter()
+    for i in range(10):
+        step(i)
+    torch.cuda.synchronize()
+    print("ms/step (single-threaded autograd, no profiler):", (time.perf_counter() - t0) * 100)
     pr = cProfile.Profile()
     pr.enable()
     for i in range(10):
