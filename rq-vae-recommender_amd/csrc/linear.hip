@@ -280,29 +280,41 @@ template <bool KC, bool SP>
 struct XStage {
   uint4 v[4];
   bool ok[4];
+  bool full;   // every k of the stage < k_hi (all but a split's / the matrix's last stage): no masking
 
   // rows [r0, r0 + 128) of the operand (clamped to R - 1: they feed only outputs >= R, never
-  // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time.
+  // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time. The
+  // per-lane part of each address does not depend on the stage, so a full stage's load is a
+  // uniform base (X + kb) plus a loop-invariant lane offset.
   __device__ __forceinline__ void load(const void* __restrict__ Xv, const void* __restrict__ Xlv, int64_t ld, int r0,
                                        int R, int64_t kb, int64_t k_lo, int64_t k_hi, int tid) {
+    full = kb + kXK <= k_hi;
     if constexpr (!SP) {
       const float* __restrict__ X = static_cast<const float*>(Xv);
       if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8 (2 float4 each)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int rr = (tid >> 2) + 64 * (j >> 1);
-          const int64_t row = min(r0 + rr, R - 1);
-          const int64_t k = kb + (tid & 3) * 8 + 4 * (j & 1);
-          ok[j] = k < k_hi;
-          v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
+          const int64_t row = min(r0 + (tid >> 2) + 64 * (j >> 1), R - 1);
+          const int64_t lane = row * ld + (tid & 3) * 8 + 4 * (j & 1);
+          if (full) {
+            v[j] = *reinterpret_cast<const uint4*>(X + kb + lane);
+          } else {
+            const int64_t k = kb + (tid & 3) * 8 + 4 * (j & 1);
+            ok[j] = k < k_hi;
+            v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
+          }
         }
       } else {              // thread: 4 consecutive rows (tid % 32) * 4, k rows tid/32 + 8j
         const int64_t col = min(r0 + 4 * (tid & 31), R - 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int64_t k = kb + (tid >> 5) + 8 * j;
-          ok[j] = k < k_hi;
-          v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
+          if (full) {
+            v[j] = *reinterpret_cast<const uint4*>(X + kb * ld + ((tid >> 5) + 8 * j) * ld + col);
+          } else {
+            ok[j] = k < k_hi;
+            v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
+          }
         }
       }
     } else {
@@ -313,8 +325,13 @@ struct XStage {
         for (int j = 0; j < 2; ++j) {
           const int64_t row = min(r0 + (tid >> 2) + 64 * j, R - 1);
           const int64_t k = kb + (tid & 3) * 8;
-          ok[j] = k < k_hi;
-          const int64_t o = row * ld + (ok[j] ? k : k_lo);
+          int64_t o;
+          if (full) {
+            o = kb + row * ld + (tid & 3) * 8;
+          } else {
+            ok[j] = k < k_hi;
+            o = row * ld + (ok[j] ? k : k_lo);
+          }
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
         }
@@ -323,8 +340,13 @@ struct XStage {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int64_t k = kb + (tid >> 4) + 16 * j;
-          ok[j] = k < k_hi;
-          const int64_t o = (ok[j] ? k : k_lo) * ld + col;
+          int64_t o;
+          if (full) {
+            o = kb * ld + ((tid >> 4) + 16 * j) * ld + col;
+          } else {
+            ok[j] = k < k_hi;
+            o = (ok[j] ? k : k_lo) * ld + col;
+          }
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
         }
@@ -332,14 +354,20 @@ struct XStage {
     }
   }
 
+  __device__ __forceinline__ bool okj(int j) const { return full || ok[j]; }
+
   __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, int tid) const {
     if constexpr (!SP) {
       float4 w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bool k = ok[j];
         const float4 f = __builtin_bit_cast(float4, v[j]);
-        w[j] = make_float4(k ? f.x : 0.f, k ? f.y : 0.f, k ? f.z : 0.f, k ? f.w : 0.f);
+        if (full) {
+          w[j] = f;
+        } else {
+          const bool k = ok[j];
+          w[j] = make_float4(k ? f.x : 0.f, k ? f.y : 0.f, k ? f.z : 0.f, k ? f.w : 0.f);
+        }
       }
       if constexpr (KC) {
 #pragma unroll
@@ -370,9 +398,12 @@ struct XStage {
     } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const bool k = ok[j];
-        const uint4 h = make_uint4(k ? v[j].x : 0u, k ? v[j].y : 0u, k ? v[j].z : 0u, k ? v[j].w : 0u);
-        const uint4 l = make_uint4(k ? v[2 + j].x : 0u, k ? v[2 + j].y : 0u, k ? v[2 + j].z : 0u, k ? v[2 + j].w : 0u);
+        uint4 h = v[j], l = v[2 + j];
+        if (!full) {
+          const bool k = ok[j];
+          h = make_uint4(k ? h.x : 0u, k ? h.y : 0u, k ? h.z : 0u, k ? h.w : 0u);
+          l = make_uint4(k ? l.x : 0u, k ? l.y : 0u, k ? l.z : 0u, k ? l.w : 0u);
+        }
         int off;
         if constexpr (KC) {
           const int rr = (tid >> 2) + 64 * j, c = tid & 3;
