@@ -491,6 +491,7 @@ enum X3Epi : int {
   kEpiStore = 0,     // C = A B^T (fp32; split-K slabs when S > 1)
   kEpiSiluFwd = 1,   // C = z = A B^T (fp32, kept for the backward); H = split(Dropout(SiLU(z)))
   kEpiSiluBwd = 2,   // H = split(SiLU'(Z) * Dropout(A B^T)): the pre-activation grad of a hidden layer
+  kEpiAdd = 3,       // C = A B^T + Z (fp32; the residual add after an attention projection)
 };
 
 struct X3Epilogue {
@@ -692,6 +693,9 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
           if (n >= N) continue;
           if constexpr (EPI == kEpiStore) {
             *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
+          } else if constexpr (EPI == kEpiAdd) {
+            const float4 r = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
+            *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
           } else {
             const uint64_t e = (uint64_t)m * N + n;
             float d[4] = {1.f, 1.f, 1.f, 1.f};   // dropout multipliers (0 or 1 / (1 - p))
@@ -815,12 +819,14 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                       void* workspace, size_t ws_bytes, void* stream) {
   const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
   RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
-                   epilogue <= 2,
+                   epilogue <= 3,
                "rq_gemm_bf16x3: bad arguments");
-  RQ_CHECK_ARG((epilogue == kEpiSiluBwd || C) && (epilogue == kEpiStore || (H_hi && H_lo && ldh >= N)) &&
-                   (epilogue != kEpiSiluBwd || Z),
+  const bool needs_h = epilogue == kEpiSiluFwd || epilogue == kEpiSiluBwd;
+  RQ_CHECK_ARG((epilogue == kEpiSiluBwd || C) && (!needs_h || (H_hi && H_lo && ldh >= N)) &&
+                   ((epilogue != kEpiSiluBwd && epilogue != kEpiAdd) || Z),
                "rq_gemm_bf16x3: epilogue %d needs %s", epilogue,
-               epilogue == kEpiSiluBwd ? "Z and H planes" : (epilogue ? "C and H planes" : "C"));
+               epilogue == kEpiSiluBwd ? "Z and H planes"
+                                       : (epilogue == kEpiSiluFwd ? "C and H planes" : (epilogue ? "C and Z" : "C")));
   // float4 (fp32) / 8 x bf16 (split) vectors along each operand's contiguous axis
   const int64_t va = asp ? 8 : 4, vb = bsp ? 8 : 4;
   RQ_CHECK_ARG((a_kcontig ? K % va == 0 : M % va == 0) && (b_kcontig ? K % vb == 0 : N % vb == 0) && lda % va == 0 &&
@@ -858,8 +864,8 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                      (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep)
 #define RQ_X3(AK, AS, BK, BS, EP)                                                                                    \
   do {                                                                                                               \
-    if (EP != kEpiStore && ep.thr != 0)                                                                              \
-      RQ_X3D(AK, AS, BK, BS, EP, (EP != kEpiStore));                                                                 \
+    if ((EP == kEpiSiluFwd || EP == kEpiSiluBwd) && ep.thr != 0)                                                      \
+      RQ_X3D(AK, AS, BK, BS, EP, (EP == kEpiSiluFwd || EP == kEpiSiluBwd));                                         \
     else                                                                                                             \
       RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
   } while (0)
@@ -887,10 +893,15 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
       case 16 | 8 | 4 | 2: RQ_X3(true, true, true, true, kEpiSiluFwd); break;
       default: launched = false;
     }
-  } else {
+  } else if (epilogue == kEpiSiluBwd) {
     switch (code) {
       case 16 | 2: RQ_X3(true, false, false, true, kEpiSiluBwd); break;
       case 16 | 8 | 2: RQ_X3(true, true, false, true, kEpiSiluBwd); break;
+      default: launched = false;
+    }
+  } else {
+    switch (code) {
+      case 16 | 4 | 2: RQ_X3(true, false, true, true, kEpiAdd); break;   // Linear (split weight) + residual
       default: launched = false;
     }
   }

@@ -81,7 +81,10 @@ class MultiHeadAttention(nn.Module):
         return self._kv_cache
 
     def forward(self, x: AttentionInput, x_kv: Optional[AttentionInput] = None, padding_mask: Optional[Tensor] = None,
-                is_causal: Optional[bool] = True, jagged: bool = False, use_cache: bool = False) -> AttentionInput:
+                is_causal: Optional[bool] = True, jagged: bool = False, use_cache: bool = False,
+                residual: Optional[Tensor] = None) -> AttentionInput:
+        """`residual` (this build's extension, default None = the reference's contract): values
+        (T, d_out) added to the output projection inside its GEMM (out = proj(ctx) + residual)."""
         assert not self.cross_attn or x_kv is not None, "Found null x_kv in cross attn. layer"
         if not jagged:
             raise Exception("Unjagged attention currently not supported.")
@@ -97,5 +100,5 @@ class MultiHeadAttention(nn.Module):
             ctx = hip_ops.varlen_attention_packed(self.qkv(jx.values()), None, jx.offsets(), jx.offsets(),
                                                   self.num_heads, bool(is_causal), jx.max_len, jx.max_len,
                                                   rows_q=jx.rows, rows_k=jx.rows)
-        out = self.proj(ctx)
+        out = self.proj(ctx) if residual is None else hip_ops.linear_add(ctx, self.proj.weight, residual)
         return jx.with_values(out) if isinstance(x, Jagged) else _wrap_like(out, x)

@@ -69,11 +69,12 @@ class TransformerBlock(nn.Module):
     def _forward_jagged(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool) -> Jagged:
         use_cache = not self.training and self.enable_kv_cache
         xv = jx.values()
-        h = xv + self.attention(jx.with_values(self.attn_norm.forward_dropout(xv, self.do)), is_causal=is_causal,
-                                jagged=True, use_cache=use_cache).values()
+        # residual adds ride in the output-projection GEMMs' epilogue (h = x + MHA(..), h += CrossMHA(..))
+        h = self.attention(jx.with_values(self.attn_norm.forward_dropout(xv, self.do)), is_causal=is_causal,
+                           jagged=True, use_cache=use_cache, residual=xv).values()
         if self.do_cross_attn:
-            h = h + self.cross_attention(x=jx.with_values(self.cross_attn_norm.forward_dropout(xv, self.do)), x_kv=jkv,
-                                         is_causal=False, jagged=True, use_cache=use_cache).values()
+            h = self.cross_attention(x=jx.with_values(self.cross_attn_norm.forward_dropout(xv, self.do)), x_kv=jkv,
+                                     is_causal=False, jagged=True, use_cache=use_cache, residual=h).values()
         norm, mlp, drop = self.ff
         y = mlp(norm(h))
         if drop.training and drop.p > 0 and hip_ops.dropout_fusable(h) and hip_ops.dropout_fusable(y):

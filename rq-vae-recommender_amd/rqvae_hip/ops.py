@@ -237,7 +237,7 @@ def split_bf16x3(x: torch.Tensor) -> Split:
     return Split(hi, lo)
 
 
-EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD = 0, 1, 2
+EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD, EPI_ADD = 0, 1, 2, 3
 _X3_WS = {}
 
 
@@ -253,8 +253,9 @@ def _x3_workspace(M: int, N: int, K: int) -> int:
 def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
             Z: torch.Tensor = None, p: float = 0.0, seed: int = 0):
     """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex). a / b: fp32
-    tensors or Split. Returns C (EPI_STORE), (C, H) (EPI_SILU_FWD: C = z, H = split(Dropout(SiLU(z))))
-    or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split of shape (M, N)."""
+    tensors or Split. Returns C (EPI_STORE; EPI_ADD: A B^T + Z), (C, H) (EPI_SILU_FWD: C = z,
+    H = split(Dropout(SiLU(z)))) or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split
+    of shape (M, N)."""
     def desc(t):
         if isinstance(t, Split):
             return t.hi, t.lo, t.hi.shape[-1], 1
@@ -265,7 +266,7 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     dev = ah.device
     C = None if epilogue == EPI_SILU_BWD else torch.empty((M, N), device=dev, dtype=torch.float32)
     H = None
-    if epilogue != EPI_STORE:
+    if epilogue in (EPI_SILU_FWD, EPI_SILU_BWD):
         H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
     nbytes = _x3_workspace(M, N, K) if epilogue == EPI_STORE else 0
@@ -277,7 +278,7 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
         TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call, *args)
     else:
         call(*args)
-    if epilogue == EPI_STORE:
+    if epilogue in (EPI_STORE, EPI_ADD):
         return C
     return (C, H) if epilogue == EPI_SILU_FWD else H
 
@@ -400,6 +401,48 @@ class LinearFunction(torch.autograd.Function):
                 dW = g2.t() @ x2
                 db = g2.sum(0) if ctx.has_bias else None
         return gx, dW, db if ctx.has_bias else None
+
+
+class LinearAddFunction(torch.autograd.Function):
+    """y = x W^T + r (bias-free Linear followed by a residual add, e.g. the attention output
+    projection plus the block input, modules/transformer/model.py:75-78) as ONE split-bf16 GEMM
+    launch at 'high' precision (residual added in the epilogue); backward: dx = g W, dW = g^T x,
+    dr = g."""
+
+    @staticmethod
+    def forward(ctx, x, weight, r):
+        O, I = weight.shape
+        x2 = x.reshape(-1, I)
+        wsp = split_bf16x3(weight)
+        y = gemm_x3(x2, True, wsp, True, x2.shape[0], O, I, EPI_ADD, Z=r.reshape(-1, O).contiguous())
+        ctx.save_for_backward(x, weight)
+        ctx.wsp = wsp
+        return y.view(*x.shape[:-1], O)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        O, I = weight.shape
+        g2 = g.reshape(-1, O)
+        gx = dW = None
+        if ctx.needs_input_grad[0]:
+            gx = gemm_x3(g2, True, ctx.wsp, False, g2.shape[0], I, O).view(x.shape)
+        ctx.wsp = None
+        if ctx.needs_input_grad[1]:
+            dW = linear_wgrad_high(g2, x.reshape(-1, I))
+        return gx, dW, g if ctx.needs_input_grad[2] else None
+
+
+def linear_add(x: torch.Tensor, weight: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """x W^T + r: one fused launch at 'high' precision for fp32 device tensors with I % 8 == 0 and
+    O % 4 == 0 (else the Linear and the add run separately)."""
+    O, I = weight.shape
+    if (matmul_high() and x.is_cuda and x.dtype == torch.float32 and r.dtype == torch.float32 and
+            weight.dtype == torch.float32 and I % 8 == 0 and O % 4 == 0 and x.numel() > 0 and
+            r.shape == (*x.shape[:-1], O)):
+        return LinearAddFunction.apply(x, weight, r)
+    return LinearFunction.apply(x, weight, None) + r if wgrad_supported(weight) else \
+        torch.nn.functional.linear(x, weight) + r
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:

@@ -280,3 +280,29 @@ def test_mlp_chain_dropout(device):
         e3 = mlp(x)
     assert (e1 - e3).abs().max() <= 1e-4 * e3.abs().max()
     assert not torch.equal(y.detach(), e1)
+
+
+def test_linear_add_epilogue_matches_fp64(device):
+    """x W^T + r in one launch (residual in the epilogue) at 'high': output and the three gradients
+    within the split-bf16 bound of fp64; exact on small-integer operands."""
+    from rqvae_hip import ops
+    gen = torch.Generator(device=device).manual_seed(5)
+    xi = torch.randint(-4, 5, (1000, 512), generator=gen, device=device).float()
+    Wi = torch.randint(-4, 5, (256, 512), generator=gen, device=device).float()
+    ri = torch.randint(-4, 5, (1000, 256), generator=gen, device=device).float()
+    torch.set_float32_matmul_precision("high")
+    y = ops.linear_add(xi, Wi, ri)
+    assert torch.equal(y.double(), xi.double() @ Wi.double().t() + ri.double())
+    x = torch.randn(3, 700, 512, device=device, requires_grad=True)
+    W = (torch.randn(256, 512, device=device) / 512 ** 0.5).requires_grad_(True)
+    r = torch.randn(3, 700, 256, device=device, requires_grad=True)
+    y = ops.linear_add(x, W, r)
+    (y.sin().sum()).backward()
+    torch.set_float32_matmul_precision("highest")
+    xd, Wd, rd = (t.detach().double().requires_grad_(True) for t in (x, W, r))
+    yd = xd @ Wd.t() + rd
+    (yd.sin().sum()).backward()
+
+    def close(a, b):
+        return (a.double() - b).abs().max() <= 1e-4 * b.abs().max() + 1e-7
+    assert close(y, yd) and close(x.grad, xd.grad) and close(W.grad, Wd.grad) and close(r.grad, rd.grad)
