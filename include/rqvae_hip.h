@@ -156,6 +156,10 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                       void* workspace, size_t ws_bytes, void* stream);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
+/* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device
+ * pointers / element counts). */
+int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, uint16_t* const* hi,
+                          uint16_t* const* lo, void* stream);
 
 /* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).

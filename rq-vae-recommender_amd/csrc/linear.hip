@@ -736,6 +736,26 @@ __global__ void __launch_bounds__(256) split_bf16x3_kernel(const float* __restri
   }
 }
 
+// Several tensors at once (all weights of an MLP chain: one launch instead of one per weight).
+constexpr int kSplitMax = 16;
+struct SplitMulti {
+  const float* x[kSplitMax];
+  uint16_t* hi[kSplitMax];
+  uint16_t* lo[kSplitMax];
+  int64_t start[kSplitMax + 1];   // prefix sums of the element counts
+  int count;
+};
+
+__global__ void __launch_bounds__(256) split_bf16x3_multi_kernel(SplitMulti sm) {
+  const int64_t total = sm.start[sm.count];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int t = 0;
+    while (t + 1 < sm.count && i >= sm.start[t + 1]) ++t;
+    const int64_t j = i - sm.start[t];
+    split_store1(sm.x[t][j], sm.hi[t] + j, sm.lo[t] + j);
+  }
+}
+
 struct X3Plan {
   int tiles_n, tiles, S, per;
   int64_t chunk;
@@ -922,6 +942,28 @@ int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, i
                    int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream) {
   return rq_gemm_bf16x3_ex(A, nullptr, lda, a_kcontig, B, nullptr, ldb, b_kcontig, M, N, K, C, ldc, kEpiStore, nullptr,
                            nullptr, nullptr, 0, 0.f, 0, workspace, ws_bytes, stream);
+}
+
+int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, uint16_t* const* hi,
+                          uint16_t* const* lo, void* stream) {
+  RQ_CHECK_ARG(count >= 0 && count <= kSplitMax && (count == 0 || (x && n && hi && lo)),
+               "rq_split_bf16x3_multi: 0 <= count <= %d tensors", kSplitMax);
+  SplitMulti sm;
+  sm.count = count;
+  sm.start[0] = 0;
+  for (int t = 0; t < count; ++t) {
+    RQ_CHECK_ARG(n[t] >= 0 && (n[t] == 0 || (x[t] && hi[t] && lo[t])), "rq_split_bf16x3_multi: bad tensor %d", t);
+    sm.x[t] = x[t];
+    sm.hi[t] = hi[t];
+    sm.lo[t] = lo[t];
+    sm.start[t + 1] = sm.start[t] + n[t];
+  }
+  if (count == 0 || sm.start[count] == 0) return 0;
+  const int64_t blocks = (sm.start[count] + 255) / 256;
+  hipLaunchKernelGGL(split_bf16x3_multi_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0,
+                     (hipStream_t)stream, sm);
+  RQ_LAUNCH_CHECK("split_bf16x3_multi_kernel");
+  return 0;
 }
 
 // x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi): the split form the GEMM consumes.

@@ -96,6 +96,7 @@ class RqQuantizeFunction(torch.autograd.Function):
         ctx.save_for_backward(res, ids, cbs)
         ctx.mode, ctx.beta = int(mode), float(beta)
         ctx.mark_non_differentiable(ids)
+        ctx.set_materialize_grads(False)   # unused outputs arrive as None = NULL (no (L,B,D) zero fills)
         return emb, res, ids, ql, es
 
     @staticmethod
@@ -237,6 +238,23 @@ def split_bf16x3(x: torch.Tensor) -> Split:
     return Split(hi, lo)
 
 
+def split_bf16x3_many(xs) -> list:
+    """split_bf16x3 of up to 16 tensors in one launch (rq_split_bf16x3_multi)."""
+    import ctypes
+    xs = [x.contiguous() for x in xs]
+    if not xs:
+        return []
+    require_gpu(*xs, what="split_bf16x3_many")
+    assert len(xs) <= 16
+    out = [Split(torch.empty(x.shape, device=x.device, dtype=torch.bfloat16),
+                 torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)) for x in xs]
+    n = len(xs)
+    P = ctypes.c_void_p * n
+    call("rq_split_bf16x3_multi", n, P(*[x.data_ptr() for x in xs]), (ctypes.c_int64 * n)(*[x.numel() for x in xs]),
+         P(*[o.hi.data_ptr() for o in out]), P(*[o.lo.data_ptr() for o in out]), stream_handle(xs[0].device))
+    return out
+
+
 EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD, EPI_ADD = 0, 1, 2, 3
 _X3_WS = {}
 
@@ -304,7 +322,7 @@ class MLPFunction(torch.autograd.Function):
         I0 = weights[0].shape[1]
         x2 = x.reshape(-1, I0).contiguous()
         rows = x2.shape[0]
-        wsp = [split_bf16x3(w) for w in weights]
+        wsp = split_bf16x3_many(weights) if len(weights) <= 16 else [split_bf16x3(w) for w in weights]
         seeds = [next_seed() if p > 0 else 0 for _ in range(n - 1)]
         a, zs, hs = x2, [], []
         out = None
@@ -662,16 +680,24 @@ class LossMeansFunction(torch.autograd.Function):
         out = torch.empty((3,), device=recon.device, dtype=torch.float32)
         call("rq_loss_means", ptr(recon), ptr(qloss), recon.numel(), ptr(out), stream_handle(recon.device))
         ctx.B = recon.numel()
+        ctx.set_materialize_grads(False)   # the logged means usually get no gradient
         return out[0], out[1], out[2]
 
     @staticmethod
     def backward(ctx, g0, g1, g2):
-        z = torch.zeros((), device=g0.device if g0 is not None else g1.device)
-        g0 = z if g0 is None else g0
-        g1 = z if g1 is None else g1
-        g2 = z if g2 is None else g2
         B = ctx.B
-        return ((g0 + g1) / B).expand(B), ((g0 + g2) / B).expand(B)
+
+        def tot(a, b):
+            if a is None:
+                return b
+            return a if b is None else a + b
+        gr, gq = tot(g0, g1), tot(g0, g2)
+        if gr is None and gq is None:
+            return None, None
+        if gr is gq:   # only the total loss has a gradient: one scale for both inputs
+            gr = gq = (gr / B).expand(B)
+            return gr, gq
+        return (None if gr is None else (gr / B).expand(B)), (None if gq is None else (gq / B).expand(B))
 
 
 def loss_means(recon, qloss):

@@ -306,3 +306,12 @@ def test_linear_add_epilogue_matches_fp64(device):
     def close(a, b):
         return (a.double() - b).abs().max() <= 1e-4 * b.abs().max() + 1e-7
     assert close(y, yd) and close(x.grad, xd.grad) and close(W.grad, Wd.grad) and close(r.grad, rd.grad)
+
+
+def test_split_many_matches_single(device):
+    from rqvae_hip import ops
+    xs = [torch.randn(*s, device=device) for s in ((512, 768), (3,), (256, 512), (1, 7))]
+    many = ops.split_bf16x3_many(xs)
+    for x, m in zip(xs, many):
+        one = ops.split_bf16x3(x)
+        assert torch.equal(m.hi, one.hi) and torch.equal(m.lo, one.lo)
