@@ -239,22 +239,27 @@ __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict
 
 // Row L2 norms: out[r] = sqrt(sum_d x[r][d]^2), one wave per row (the RqVae embs_norm statistic,
 // modules/rqvae.py:155: emb.norm(dim=-1) over (L, B, D) embeddings in one pass).
+// One row per group of G lanes (G = D / 4 rounded up to a power of two, <= 64): at D = 64 a wave
+// covers 4 rows with every lane loading a float4 (one row per wave left 3/4 of the lanes idle).
+template <int G>
 __global__ void __launch_bounds__(256) row_norm_kernel(const float* __restrict__ x, int64_t rows, int D,
                                                        float* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const float* p = x + r * D;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t r = (int64_t)blockIdx.x * (256 / G) + (threadIdx.x / G);
+  const bool ok = r < rows;
+  const float* p = x + (ok ? r : 0) * D;
   float s = 0.f;
-  for (int c = lane * 4; c < D; c += 256) {
-    const float4 v = *reinterpret_cast<const float4*>(p + c);
-    s = __builtin_fmaf(v.x, v.x, s);
-    s = __builtin_fmaf(v.y, v.y, s);
-    s = __builtin_fmaf(v.z, v.z, s);
-    s = __builtin_fmaf(v.w, v.w, s);
+  if (ok) {
+    for (int c = lane * 4; c < D; c += 4 * G) {
+      const float4 v = *reinterpret_cast<const float4*>(p + c);
+      s = __builtin_fmaf(v.x, v.x, s);
+      s = __builtin_fmaf(v.y, v.y, s);
+      s = __builtin_fmaf(v.z, v.z, s);
+      s = __builtin_fmaf(v.w, v.w, s);
+    }
   }
-  s = group_sum<64>(s);
-  if (lane == 0) out[r] = sqrtf(s);
+  s = group_sum<G>(s);
+  if (ok && lane == 0) out[r] = sqrtf(s);
 }
 
 // The three scalar losses of RqVae.forward (modules/rqvae.py:151-162) in one pass over (B,) vectors:
@@ -266,8 +271,31 @@ __global__ void __launch_bounds__(1024) loss_means_kernel(const float* __restric
   __shared__ float red[3][1024];
   const int t = threadIdx.x;
   float a = 0.f, b = 0.f, c = 0.f;
-  for (int64_t i = t; i < B; i += 1024) {
-    const float r = recon[i], q = ql[i];
+  // fixed order: thread t sums float4 groups t, t + 1024, ... (4 loads in flight), then the tail
+  const int64_t n4 = B / 4;
+  int64_t i = t;
+  for (; i + 3 * 1024 < n4; i += 4 * 1024) {
+    float4 r[4], q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      r[u] = reinterpret_cast<const float4*>(recon)[i + u * 1024];
+      q[u] = reinterpret_cast<const float4*>(ql)[i + u * 1024];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a += (r[u].x + q[u].x) + (r[u].y + q[u].y) + (r[u].z + q[u].z) + (r[u].w + q[u].w);
+      b += r[u].x + r[u].y + r[u].z + r[u].w;
+      c += q[u].x + q[u].y + q[u].z + q[u].w;
+    }
+  }
+  for (; i < n4; i += 1024) {
+    const float4 r = reinterpret_cast<const float4*>(recon)[i], q = reinterpret_cast<const float4*>(ql)[i];
+    a += (r.x + q.x) + (r.y + q.y) + (r.z + q.z) + (r.w + q.w);
+    b += r.x + r.y + r.z + r.w;
+    c += q.x + q.y + q.z + q.w;
+  }
+  if (t < B - n4 * 4) {
+    const float r = recon[n4 * 4 + t], q = ql[n4 * 4 + t];
     a += r + q;
     b += r;
     c += q;
@@ -329,14 +357,22 @@ int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stre
   RQ_CHECK_ARG(rows >= 0 && D > 0 && D % 4 == 0, "rq_row_norms: need D %% 4 == 0");
   if (rows == 0) return 0;
   RQ_CHECK_ARG(x && out, "rq_row_norms: null pointer");
-  hipLaunchKernelGGL(row_norm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, rows,
-                     (int)D, out);
+  int g = 1;
+  while (g < 64 && 4 * g < D) g <<= 1;
+  const dim3 grid((unsigned)((rows + 256 / g - 1) / (256 / g)));
+  hipStream_t st = (hipStream_t)stream;
+  switch (g) {
+#define RN_CASE(G) case G: hipLaunchKernelGGL((row_norm_kernel<G>), grid, dim3(256), 0, st, x, rows, (int)D, out); break;
+    RN_CASE(1) RN_CASE(2) RN_CASE(4) RN_CASE(8) RN_CASE(16) RN_CASE(32) RN_CASE(64)
+#undef RN_CASE
+  }
   RQ_LAUNCH_CHECK("rq_row_norms");
   return 0;
 }
 
 int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out, void* stream) {
   RQ_CHECK_ARG(B > 0 && recon && qloss && out, "rq_loss_means: bad arguments");
+  RQ_CHECK_ARG(((uintptr_t)recon | (uintptr_t)qloss) % 16 == 0, "rq_loss_means: inputs must be 16-byte aligned");
   hipLaunchKernelGGL(loss_means_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, recon, qloss, B, out);
   RQ_LAUNCH_CHECK("rq_loss_means");
   return 0;
