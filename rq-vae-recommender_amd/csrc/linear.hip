@@ -473,6 +473,10 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #define RQ_X3_DEPTH 2    // register stage sets in flight (2 or 3; 3 spills on the transposed-B variants)
 #endif
 
+#ifndef RQ_X3_MAX_SPLIT
+#define RQ_X3_MAX_SPLIT 64   // split-K: at most this many k chunks
+#endif
+
 #ifndef RQ_X3_MIN_STAGES
 #define RQ_X3_MIN_STAGES 4   // split-K: k-stages per workgroup at least (fewer slabs to reduce)
 #endif
@@ -771,6 +775,7 @@ static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) 
     S = resident_slots() / p.tiles;
     const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
     if (S > max_s) S = max_s;
+    if (S > RQ_X3_MAX_SPLIT) S = RQ_X3_MAX_SPLIT;   // slab traffic of the reduction grows with S
     if (S < 1) S = 1;
   }
   int64_t chunk = (K + S - 1) / S;

@@ -1,0 +1,28 @@
+"""Row-norm and loss-mean kernels of RqVae.forward's statistics (rq_row_norms, rq_loss_means) on
+every lane grouping (D/4 lanes per row) and ragged lengths (vector body + scalar tail)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rows,D", [(196608, 64), (1000, 32), (7, 4), (513, 96), (300, 768), (5, 1028)])
+def test_row_norms(device, rows, D):
+    from rqvae_hip import ops
+    x = torch.randn(rows, D, device=device, generator=torch.Generator(device=device).manual_seed(rows + D))
+    got = ops.row_norms(x)
+    ref = x.double().norm(dim=1)
+    assert ((got.double() - ref).abs() <= 2e-6 * ref + 1e-7).all()
+
+
+@pytest.mark.parametrize("B", [65536, 65537, 3, 1, 4097])
+def test_loss_means(device, B):
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(B)
+    r = torch.rand(B, device=device, generator=g)
+    q = torch.rand(B, device=device, generator=g)
+    loss, rm, qm = ops.loss_means(r, q)
+    for got, ref in ((loss, (r.double() + q.double()).mean()), (rm, r.double().mean()), (qm, q.double().mean())):
+        assert abs(float(got) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-7
+    again = ops.loss_means(r, q)
+    assert all(torch.equal(a, b) for a, b in zip((loss, rm, qm), again)), "fixed-order reduction"
