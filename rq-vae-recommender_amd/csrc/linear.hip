@@ -473,6 +473,15 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #define RQ_X3_DEPTH 2    // register stage sets in flight (2 or 3; 3 spills on the transposed-B variants)
 #endif
 
+#ifndef RQ_X3_SETPRIO
+#define RQ_X3_SETPRIO 0   // 1: s_setprio(1) around each stage's MFMA cluster (guide T5; measured -1 %)
+#endif
+#if RQ_X3_SETPRIO
+#define RQ_X3_PRIO(P) __builtin_amdgcn_s_setprio(P);
+#else
+#define RQ_X3_PRIO(P)
+#endif
+
 #ifndef RQ_X3_MAX_SPLIT
 #define RQ_X3_MAX_SPLIT 64   // split-K: at most this many k chunks
 #endif
@@ -645,7 +654,9 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   }
 #else
 #define RQ_X3_BODY(SA, SB)                                                                                    \
+  RQ_X3_PRIO(1)                                                                                               \
   RQ_X3_MMA                                                                                                   \
+  RQ_X3_PRIO(0)                                                                                               \
   SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
   SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
 #endif
