@@ -222,7 +222,10 @@ def main():
     B = args.batch
 
     model = build_model(device)
-    buckets = dp.GradBuckets(model.parameters())
+    # grads become ready decoder -> codebooks -> encoder: the first bucket's all-reduce overlaps the
+    # encoder MLP backward
+    buckets = dp.GradBuckets([list(model.decoder.parameters()) + list(model.layers.parameters()),
+                              list(model.encoder.parameters())])
     buckets.broadcast_params()
     try:
         opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"], fused=True)

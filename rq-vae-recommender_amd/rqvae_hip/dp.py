@@ -66,30 +66,37 @@ def shard_range(global_batch: int, rank_: int, world_: int):
 class GradBuckets:
     """Flat gradient buffers + bucketed async all-reduce for a module's parameters."""
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 32 << 20, average: bool = True,
-                 overlap: bool = True):
-        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+    def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, overlap: bool = True):
+        """`params`: an iterable of parameters (buckets follow reverse registration order, ~ the order
+        grads become ready), or a list of parameter groups given in the order their grads become
+        ready (each group gets its own buckets, so an early group's all-reduce overlaps the rest of
+        the backward — e.g. [decoder + codebooks, encoder] for the RQ-VAE)."""
+        params = list(params)
+        grouped = bool(params) and isinstance(params[0], (list, tuple))
+        groups = [list(g) for g in params] if grouped else [list(reversed(params))]
+        seen = set()
+        groups = [[p for p in g if p.requires_grad and not (id(p) in seen or seen.add(id(p)))] for g in groups]
+        self.params: List[torch.nn.Parameter] = [p for g in groups for p in g]
         self.average = average
         self.active = world() > 1   # single process: no flat views (AccumulateGrad steals, no add_)
         self.overlap = overlap and world() > 1
         self.buckets = []
         self._handles = []
         self._pending = {}
-        by_dtype = {}
-        for p in (self.params if self.active else []):
-            by_dtype.setdefault((p.dtype, p.device), []).append(p)
-        for (dt, dev), ps in by_dtype.items():
-            # reverse registration order ~= order grads become ready in backward
-            ps = list(reversed(ps))
-            cur, cur_bytes = [], 0
-            for p in ps:
-                cur.append(p)
-                cur_bytes += p.numel() * p.element_size()
-                if cur_bytes >= bucket_bytes:
+        for g in (groups if self.active else []):
+            by_dtype = {}
+            for p in g:
+                by_dtype.setdefault((p.dtype, p.device), []).append(p)
+            for (dt, dev), ps in by_dtype.items():
+                cur, cur_bytes = [], 0
+                for p in ps:
+                    cur.append(p)
+                    cur_bytes += p.numel() * p.element_size()
+                    if cur_bytes >= bucket_bytes:
+                        self._make_bucket(cur, dt, dev)
+                        cur, cur_bytes = [], 0
+                if cur:
                     self._make_bucket(cur, dt, dev)
-                    cur, cur_bytes = [], 0
-            if cur:
-                self._make_bucket(cur, dt, dev)
         if self.overlap:
             for bi, b in enumerate(self.buckets):
                 for p in b["params"]:

@@ -38,14 +38,18 @@ def _loss(model, x):
     return ((model(x) - 0.1) ** 2).sum(-1).mean()
 
 
-def _worker(rank, world, port, gb, bucket_bytes, q):
+def _worker(rank, world, port, gb, bucket_bytes, q, grouped=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
         r, w, _ = dp.init_from_env(backend="gloo")
         torch.manual_seed(100 + rank)          # different init per rank: broadcast must fix it
         model = _Net()
-        buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
+        if grouped:   # parameter groups in grad-ready order (the bench's RQ-VAE layout)
+            ps = list(model.parameters())
+            buckets = dp.GradBuckets([ps[len(ps) // 2:][::-1], ps[:len(ps) // 2][::-1]], bucket_bytes=bucket_bytes)
+        else:
+            buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
         buckets.broadcast_params()
         g = torch.Generator().manual_seed(7)
         x = torch.randn(gb, 24, generator=g)
@@ -64,12 +68,13 @@ def _worker(rank, world, port, gb, bucket_bytes, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,gb,bucket_bytes", [(2, 64, 1 << 20), (3, 63, 2048)])
-def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes):
+@pytest.mark.parametrize("world,gb,bucket_bytes,grouped", [(2, 64, 1 << 20, False), (3, 63, 2048, False),
+                                                          (2, 64, 1 << 20, True)])
+def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, grouped):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, gb, bucket_bytes, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, gb, bucket_bytes, q, grouped)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda t: t[0])
