@@ -80,7 +80,10 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
                 model(SeqBatch(None, None, None, items[: min(20000, n_items)], None, None), 0.2)
         for layer in model.layers:
             layer.kmeans_initted = True
-    buckets = dp.GradBuckets(model.parameters())
+    # grads become ready decoder -> codebooks -> encoder: the first bucket's all-reduce overlaps the
+    # encoder backward
+    buckets = dp.GradBuckets([list(model.decoder.parameters()) + list(model.layers.parameters()),
+                              list(model.encoder.parameters())])
     buckets.broadcast_params()
 
     gen = torch.Generator(device=device).manual_seed(seed + 17)   # same stream on every rank
