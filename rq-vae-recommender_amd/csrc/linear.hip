@@ -252,8 +252,13 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
+#ifndef RQ_X3_BK16
+#define RQ_X3_BK16 0   // 1: 16-deep k stages (32 KiB LDS, 3 workgroups/CU, 32x32x16 MFMA)
+#endif
 constexpr int kXT = 128;                       // output tile (m and n)
-constexpr int kXK = 32;                        // k per LDS stage
+constexpr int kXK = RQ_X3_BK16 ? 16 : 32;      // k per LDS stage
+constexpr int kXCPR = kXK / 8;                 // 16-byte bf16 chunks per row of the row image
+constexpr int kXWG = RQ_X3_BK16 ? 3 : 2;       // resident workgroups per CU
 constexpr int kXPlane = kXT * kXK * 2;         // bytes of one bf16 plane (8 KiB)
 constexpr int kXOp = 2 * kXPlane;              // hi + lo planes of one operand
 constexpr int kXBuf = 2 * kXOp;                // A + B
@@ -270,6 +275,10 @@ __device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uin
 }
 
 __device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+// Row image: row rr of 2 kXK bytes, 16-B chunk c stored at c ^ row_swz(rr) (conflict-free for 16
+// consecutive rows at one chunk, and for the staging writes).
+__device__ __forceinline__ int row_swz(int rr) { return kXCPR == 4 ? ((rr >> 2) & 3) : ((rr >> 3) & 1); }
+__device__ __forceinline__ int row_off(int rr, int c) { return rr * (2 * kXK) + ((c ^ row_swz(rr)) << 4); }
 
 // One operand's staging registers (a 128 x 32 tile per stage, 256 threads). Operand formats:
 //   fp32  (SP = false): 4 float4 per thread, split into (hi, lo) bf16 while written to LDS;
@@ -291,15 +300,15 @@ struct XStage {
     full = kb + kXK <= k_hi;
     if constexpr (!SP) {
       const float* __restrict__ X = static_cast<const float*>(Xv);
-      if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8 (2 float4 each)
+      if constexpr (KC) {   // thread: chunk tid % CPR of rows tid / CPR (+ 256 / CPR), 2 float4 per chunk
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t row = min(r0 + (tid >> 2) + 64 * (j >> 1), R - 1);
-          const int64_t lane = row * ld + (tid & 3) * 8 + 4 * (j & 1);
+        for (int j = 0; j < kXK / 8; ++j) {
+          const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * (j >> 1), R - 1);
+          const int64_t lane = row * ld + (tid % kXCPR) * 8 + 4 * (j & 1);
           if (full) {
             v[j] = *reinterpret_cast<const uint4*>(X + kb + lane);
           } else {
-            const int64_t k = kb + (tid & 3) * 8 + 4 * (j & 1);
+            const int64_t k = kb + (tid % kXCPR) * 8 + 4 * (j & 1);
             ok[j] = k < k_hi;
             v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
           }
@@ -307,7 +316,7 @@ struct XStage {
       } else {              // thread: 4 consecutive rows (tid % 32) * 4, k rows tid/32 + 8j
         const int64_t col = min(r0 + 4 * (tid & 31), R - 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < kXK / 8; ++j) {
           const int64_t k = kb + (tid >> 5) + 8 * j;
           if (full) {
             v[j] = *reinterpret_cast<const uint4*>(X + kb * ld + ((tid >> 5) + 8 * j) * ld + col);
@@ -320,14 +329,14 @@ struct XStage {
     } else {
       const uint16_t* __restrict__ Xh = static_cast<const uint16_t*>(Xv);
       const uint16_t* __restrict__ Xl = static_cast<const uint16_t*>(Xlv);
-      if constexpr (KC) {   // thread: rows tid/4 and tid/4 + 64, k chunk (tid % 4) * 8
+      if constexpr (KC) {   // thread: chunk tid % CPR of rows tid / CPR (+ 256 / CPR)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int64_t row = min(r0 + (tid >> 2) + 64 * j, R - 1);
-          const int64_t k = kb + (tid & 3) * 8;
+        for (int j = 0; j < kXK / 16; ++j) {
+          const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * j, R - 1);
+          const int64_t k = kb + (tid % kXCPR) * 8;
           int64_t o;
           if (full) {
-            o = kb + row * ld + (tid & 3) * 8;
+            o = kb + row * ld + (tid % kXCPR) * 8;
           } else {
             ok[j] = k < k_hi;
             o = row * ld + (ok[j] ? k : k_lo);
@@ -338,7 +347,7 @@ struct XStage {
       } else {              // thread: 8 consecutive rows (tid % 16) * 8, k rows tid/16 and tid/16 + 16
         const int64_t col = min(r0 + 8 * (tid & 15), R - 8);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < kXK / 16; ++j) {
           const int64_t k = kb + (tid >> 4) + 16 * j;
           int64_t o;
           if (full) {
@@ -360,7 +369,7 @@ struct XStage {
     if constexpr (!SP) {
       float4 w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < kXK / 8; ++j) {
         const float4 f = __builtin_bit_cast(float4, v[j]);
         if (full) {
           w[j] = f;
@@ -371,9 +380,9 @@ struct XStage {
       }
       if constexpr (KC) {
 #pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2) {
-          const int rr = (tid >> 2) + 64 * c2, c = tid & 3;
-          const int off = rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4);
+        for (int c2 = 0; c2 < kXK / 16; ++c2) {
+          const int rr = (tid / kXCPR) + (256 / kXCPR) * c2, c = tid % kXCPR;
+          const int off = row_off(rr, c);
           uint4 h, l;
           split_bf16x2(w[2 * c2].x, w[2 * c2].y, h.x, l.x);
           split_bf16x2(w[2 * c2].z, w[2 * c2].w, h.y, l.y);
@@ -385,7 +394,7 @@ struct XStage {
       } else {
         const int m = 4 * (tid & 31);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < kXK / 8; ++j) {
           const int kr = (tid >> 5) + 8 * j;
           const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
           uint2 h, l;
@@ -397,7 +406,7 @@ struct XStage {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < kXK / 16; ++j) {
         uint4 h = v[j], l = v[2 + j];
         if (!full) {
           const bool k = ok[j];
@@ -406,8 +415,8 @@ struct XStage {
         }
         int off;
         if constexpr (KC) {
-          const int rr = (tid >> 2) + 64 * j, c = tid & 3;
-          off = rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4);
+          const int rr = (tid / kXCPR) + (256 / kXCPR) * j, c = tid % kXCPR;
+          off = row_off(rr, c);
         } else {
           const int kr = (tid >> 4) + 16 * j;
           off = 256 * kr + (((tid & 15) ^ col_swz(kr)) << 4);
@@ -424,7 +433,7 @@ template <bool KC>
 __device__ __forceinline__ bf16x8_t xfrag(const char* plane, int rb, int s, int lane) {
   if constexpr (KC) {
     const int rr = rb + (lane & 31), c = 2 * s + (lane >> 5);
-    return *reinterpret_cast<const bf16x8_t*>(plane + rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4));
+    return *reinterpret_cast<const bf16x8_t*>(plane + row_off(rr, c));
   } else {
     // ds_read_b64_tr_b16: 16-lane group G reads a 4 (k) x 16 (row) block; lane 4q + p supplies
     // the address of k-row q, rows 4p..4p+3, and receives row (lane % 16) of all 4 k-rows.
@@ -449,7 +458,7 @@ template <bool KC>
 __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane) {
   if constexpr (KC) {
     const int rr = rb + (lane & 15), c = lane >> 4;
-    return *reinterpret_cast<const bf16x8_t*>(plane + rr * 64 + ((c ^ ((rr >> 2) & 3)) << 4));
+    return *reinterpret_cast<const bf16x8_t*>(plane + row_off(rr, c));
   } else {
     // ds_read_b64_tr_b16 per 16-lane group G (k-rows 8G .. 8G + 7 in two 4-row blocks): lane
     // 4q + p supplies the address of k-row q, rows 4p..4p+3, and receives row (lane % 16).
@@ -495,8 +504,9 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #endif
 
 #ifndef RQ_X3_MFMA16
-#define RQ_X3_MFMA16 1   // 16x16x32 bf16 MFMA (4 x 4 tiles per wave); 0: 32x32x16 (2 x 2 tiles)
+#define RQ_X3_MFMA16 (RQ_X3_BK16 ? 0 : 1)   // 16x16x32 bf16 MFMA (4 x 4 tiles per wave); 0: 32x32x16 (2 x 2)
 #endif
+static_assert(!(RQ_X3_MFMA16 && RQ_X3_BK16), "16x16x32 MFMA needs 32-deep k stages");
 
 // Epilogues: what the accumulator tile becomes (all fp32 math; dropout mask = keep1(seed, m N + n),
 // the convention of the standalone dropout kernels, dropout.hip).
@@ -568,7 +578,7 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
 #endif
 
 template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, kXWG)
 gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
                    const void* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S,
                    int64_t chunk, int per, float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
@@ -776,14 +786,16 @@ struct X3Plan {
   int64_t chunk;
 };
 
+static int x3_slots() { return resident_slots() / 2 * kXWG; }
+
 static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
   X3Plan p;
   p.tiles_n = (int)((N + kXT - 1) / kXT);
   p.tiles = (int)((M + kXT - 1) / kXT) * p.tiles_n;
   // split K only when the output tiles cannot fill the chip (weight gradients)
   int64_t S = 1;
-  if (allow_split && p.tiles < resident_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
-    S = resident_slots() / p.tiles;
+  if (allow_split && p.tiles < x3_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
+    S = x3_slots() / p.tiles;
     const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
     if (S > max_s) S = max_s;
     if (S > RQ_X3_MAX_SPLIT) S = RQ_X3_MAX_SPLIT;   // slab traffic of the reduction grows with S
