@@ -315,3 +315,34 @@ def test_split_many_matches_single(device):
     for x, m in zip(xs, many):
         one = ops.split_bf16x3(x)
         assert torch.equal(m.hi, one.hi) and torch.equal(m.lo, one.lo)
+
+
+def test_mlp_chain_dropout_masks_match_composition(device):
+    """Train-mode fused chain == the same chain composed from the standalone kernels with the SAME
+    dropout keys (the fused chain draws one key per hidden layer from ops.next_seed): z = A W^T on
+    the split GEMM, h = rq_silu_dropout_fwd(z, p, key); forward within the split / fast-sigmoid
+    bound, identical dropout zeros."""
+    from modules.encoder import MLP
+    from rqvae_hip import ops
+    from rqvae_hip._lib import call, ptr, stream_handle
+    torch.manual_seed(11)
+    mlp = MLP(128, [256, 512], 64, dropout=0.25).to(device).train()
+    x = torch.randn(3000, 128, device=device)
+    torch.set_float32_matmul_precision("high")
+    ops.next_seed()                      # bind the key counter to the current torch seed
+    n0 = ops._SEED["n"]
+    y = mlp(x)
+    ops._SEED["n"] = n0                  # replay the two keys the fused chain drew
+    keys = [ops.next_seed() for _ in range(2)]
+    ws = [m.weight for m in mlp.mlp if isinstance(m, torch.nn.Linear)]
+    a = x
+    for i, w in enumerate(ws):
+        z = ops.gemm_x3(a, True, ops.split_bf16x3(w.detach()), True, a.shape[0], w.shape[0], w.shape[1])
+        if i < len(ws) - 1:
+            h = torch.empty_like(z)
+            call("rq_silu_dropout_fwd", ptr(z), z.numel(), 0.25, keys[i], ptr(h), stream_handle(device))
+            a = h
+        else:
+            a = z
+    torch.set_float32_matmul_precision("highest")
+    assert (y - a).abs().max() <= 1e-4 * a.abs().max()
