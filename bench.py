@@ -205,6 +205,7 @@ def cpu_baseline(budget_s, B=2048):
 def main():
     args = parse()
     from rqvae_hip import dp, ops
+    from rqvae_hip import optim as hip_optim
     from data.schemas import SeqBatch
     rk, ws, lr = dp.init_from_env()
     if not torch.cuda.is_available():
@@ -227,10 +228,7 @@ def main():
     buckets = dp.GradBuckets([list(model.decoder.parameters()) + list(model.layers.parameters()),
                               list(model.encoder.parameters())])
     buckets.broadcast_params()
-    try:
-        opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"], fused=True)
-    except (RuntimeError, TypeError):
-        opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"], foreach=True)
+    opt = hip_optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"])   # one launch per step
     gen = torch.Generator(device=device).manual_seed(1000 + rk)
     pool = [make_items(B, CFG["input_dim"], gen, device) for _ in range(4)]   # resident in HBM
     it = [0]
@@ -445,6 +443,7 @@ def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
     weak scaling), gradients all-reduced by GradBuckets (RCCL), fused AdamW. HIP jagged conversion,
     varlen attention and fused dropout kernels. Tokens/s = context tokens of all ranks / max time."""
     from rqvae_hip import dp, ops
+    from rqvae_hip import optim as hip_optim
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel
     torch.manual_seed(3)
@@ -454,7 +453,7 @@ def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
                                      max_pos=DEC["max_items"] * DEC["sem_id_dim"]).to(device).train()
     buckets = dp.GradBuckets(m.parameters())
     buckets.broadcast_params()
-    opt = torch.optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"], fused=True)
+    opt = hip_optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"])
     batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + 97 * rk + i,
                                          device) for i in range(4)]
     ctx_tokens = [int(b.seq_mask.sum()) + DEC["B"] for b in batches]

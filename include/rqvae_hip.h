@@ -212,6 +212,17 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, float* delta,
                     void* stream);
 
+/* AdamW step (torch.optim.AdamW as stepped by train_rqvae.py:168-172 / train_decoder.py:203) over
+ * every fp32 parameter of a group, one launch per 64 tensors. segs: HOST array of nseg records of 5
+ * int64 {p, g, exp_avg, exp_avg_sq (device pointers), n}; it is copied into the kernel arguments, so
+ * the call needs no device-side table and is graph-capturable. Per element (rq_adamw_chunk_elems()
+ * elements per workgroup):
+ *   p -= lr*wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= (lr/bc1) m / (sqrt(v)/bc2_sqrt + eps).
+ * bias_correction1 = 1 - b1^step, bias_correction2_sqrt = sqrt(1 - b2^step) (caller-computed). */
+int rq_adamw_step(const int64_t* segs, int64_t nseg, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, float bias_correction1, float bias_correction2_sqrt, void* stream);
+size_t rq_adamw_chunk_elems(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,8 @@ _SIGS = {
                          _I64, _P], _I),
     "varlen_attn_bwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
                          _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _P], _I),
+    "rq_adamw_step": ([_P, _I64, _F, _F, _F, _F, _F, _F, _F, _P], _I),
+    "rq_adamw_chunk_elems": ([], _SZ),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

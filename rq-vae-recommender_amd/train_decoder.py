@@ -23,6 +23,7 @@ from modules.scheduler.inv_sqrt import InverseSquareRootScheduler
 from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
+from rqvae_hip import optim as hip_optim
 
 
 @gin.configurable
@@ -68,7 +69,7 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
                                          sem_id_dim=tokenizer.sem_ids_dim,
                                          max_pos=train_ds.max_seq_len * tokenizer.sem_ids_dim,
                                          jagged_mode=model_jagged_mode).to(device)
-    opt = torch.optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay, fused=True)
+    opt = hip_optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay)
     sched = InverseSquareRootScheduler(optimizer=opt, warmup_steps=10000)
     start_iter = 0
     if pretrained_decoder_path is not None:

@@ -27,6 +27,7 @@ from modules.rqvae import RqVae
 from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
+from rqvae_hip import optim as hip_optim
 
 
 @gin.configurable
@@ -60,7 +61,7 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
                   codebook_size=vae_codebook_size, codebook_kmeans_init=use_kmeans_init and pretrained_rqvae_path is None,
                   codebook_normalize=vae_codebook_normalize, codebook_sim_vq=vae_sim_vq, codebook_mode=vae_codebook_mode,
                   n_layers=vae_n_layers, n_cat_features=vae_n_cat_feats, commitment_weight=commitment_weight).to(device)
-    opt = torch.optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay, fused=True)
+    opt = hip_optim.AdamW(model.parameters(), lr=learning_rate, weight_decay=weight_decay)
     start_iter = 0
     if pretrained_rqvae_path is not None:
         state = torch.load(pretrained_rqvae_path, map_location=device, weights_only=True)
