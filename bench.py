@@ -49,6 +49,15 @@ HBM_PEAK_GBS = 8000.0
 CFG = dict(input_dim=768, hidden=[512, 256, 128], D=64, K=256, L=3, lr=1e-4, wd=0.01, beta=0.25)
 
 
+def make_adamw(params, lr, wd):
+    """The HIP multi-tensor AdamW (one launch per step); RQVAE_TORCH_ADAMW=1 selects torch's fused AdamW
+    (A/B switch for tools/gpu_check.sh)."""
+    if os.environ.get("RQVAE_TORCH_ADAMW") == "1":
+        return torch.optim.AdamW(params, lr=lr, weight_decay=wd, fused=True)
+    from rqvae_hip import optim as hip_optim
+    return hip_optim.AdamW(params, lr=lr, weight_decay=wd)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,7 +214,6 @@ def cpu_baseline(budget_s, B=2048):
 def main():
     args = parse()
     from rqvae_hip import dp, ops
-    from rqvae_hip import optim as hip_optim
     from data.schemas import SeqBatch
     rk, ws, lr = dp.init_from_env()
     if not torch.cuda.is_available():
@@ -228,7 +236,7 @@ def main():
     buckets = dp.GradBuckets([list(model.decoder.parameters()) + list(model.layers.parameters()),
                               list(model.encoder.parameters())])
     buckets.broadcast_params()
-    opt = hip_optim.AdamW(model.parameters(), lr=CFG["lr"], weight_decay=CFG["wd"])   # one launch per step
+    opt = make_adamw(model.parameters(), CFG["lr"], CFG["wd"])
     gen = torch.Generator(device=device).manual_seed(1000 + rk)
     pool = [make_items(B, CFG["input_dim"], gen, device) for _ in range(4)]   # resident in HBM
     it = [0]
@@ -443,7 +451,6 @@ def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
     weak scaling), gradients all-reduced by GradBuckets (RCCL), fused AdamW. HIP jagged conversion,
     varlen attention and fused dropout kernels. Tokens/s = context tokens of all ranks / max time."""
     from rqvae_hip import dp, ops
-    from rqvae_hip import optim as hip_optim
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel
     torch.manual_seed(3)
@@ -453,7 +460,7 @@ def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
                                      max_pos=DEC["max_items"] * DEC["sem_id_dim"]).to(device).train()
     buckets = dp.GradBuckets(m.parameters())
     buckets.broadcast_params()
-    opt = hip_optim.AdamW(m.parameters(), lr=DEC["lr"], weight_decay=DEC["wd"])
+    opt = make_adamw(m.parameters(), DEC["lr"], DEC["wd"])
     batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + 97 * rk + i,
                                          device) for i in range(4)]
     ctx_tokens = [int(b.seq_mask.sum()) + DEC["B"] for b in batches]

@@ -18,6 +18,14 @@ import torch
 from ._lib import RqHipError, call, load, require_gpu, stream_handle
 
 
+def _check(p):
+    require_gpu(p, p.grad, what="AdamW")
+    if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+        raise RqHipError("rqvae_hip.optim.AdamW: fp32 parameters and grads only")
+    if p.grad.is_sparse or not (p.is_contiguous() and p.grad.is_contiguous()):
+        raise RqHipError("rqvae_hip.optim.AdamW: dense contiguous parameters and grads only")
+
+
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
                  maximize=False, **unused):
@@ -40,6 +48,8 @@ class AdamW(torch.optim.Optimizer):
         hit = self._tables.get(slot)
         if hit is not None and hit[0] == key:
             return hit[1]
+        for p, _ in live:   # validated whenever a pointer changes (a new grad tensor included)
+            _check(p)
         table = (ctypes.c_int64 * (5 * len(key)))(*[v for row in key for v in row])
         self._tables[slot] = (key, table)
         return table
@@ -51,27 +61,23 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for gi, group in enumerate(self.param_groups):
-            live = []
-            for p in group["params"]:
-                if p.grad is None or p.numel() == 0:
-                    continue
-                require_gpu(p, p.grad, what="AdamW")
-                if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
-                    raise RqHipError("rqvae_hip.optim.AdamW: fp32 parameters and grads only")
-                if p.grad.is_sparse or not (p.is_contiguous() and p.grad.is_contiguous()):
-                    raise RqHipError("rqvae_hip.optim.AdamW: dense contiguous parameters and grads only")
+            live = [p for p in group["params"] if p.grad is not None and p.numel() > 0]
+            if not live:
+                continue
+            states = []
+            for p in live:
                 st = self.state[p]
                 if len(st) == 0:
+                    _check(p)
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                live.append((p, st))
-            if not live:
-                continue
+                states.append(st)
+            steps = [st["step"] for st in states]
+            torch._foreach_add_(steps, 1)   # one host op for the group's step counters (as torch's AdamW)
             by_step = {}   # torch keeps a step count per parameter: one launch per distinct count
-            for p, st in live:
-                by_step.setdefault(float(st["step"]), []).append((p, st))
+            for p, st, t in zip(live, states, steps):
+                by_step.setdefault(t.item(), []).append((p, st))
             b1, b2 = group["betas"]
             for k, (step, members) in enumerate(sorted(by_step.items())):
                 bc1 = 1.0 - b1 ** step

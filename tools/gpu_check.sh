@@ -79,6 +79,11 @@ for s in $steps; do
       run prof_wgrad 200 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o wgrad -- \
         python3 "$R/tools/bench_kernels.py" --wgrad --rounds 3 > "$O/prof_wgrad.log" 2>&1
       cd "$R" ;;
+    abopt)   # same box, alternating: HIP multi-tensor AdamW (A) vs torch fused AdamW (B)
+      for k in 1 2; do
+        run abopt_A$k 200 python -u "$R/bench.py" --no-cpu-baseline --no-pmc > "$O/abopt_A$k.json" 2> "$O/abopt.err"
+        RQVAE_TORCH_ADAMW=1 run abopt_B$k 200 python -u "$R/bench.py" --no-cpu-baseline --no-pmc > "$O/abopt_B$k.json" 2>> "$O/abopt.err"
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
