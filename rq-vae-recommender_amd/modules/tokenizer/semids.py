@@ -3,7 +3,9 @@
 
 MI355X path:
   * corpus ids: the frozen RqVae's eval-mode fused quantize kernel over the whole corpus in large
-    device batches (the reference walks 512-item batches);
+    device batches (the reference walks 512-item batches); with `shard=True` under data
+    parallelism each rank quantizes its contiguous slice and the ids are all-gathered,
+    the dedup column is then computed on the gathered corpus (identical on every rank);
   * dedup column (`semids.py:84-99`: for each item, the number of EARLIER items with the same
     L-tuple): one stable device sort of packed tuple keys + a segmented rank, O(N log N) instead
     of the reference's O(N^2) all-pairs comparison — identical values;
@@ -23,6 +25,7 @@ from torch import Tensor
 from data.schemas import SeqBatch, TokenizedSeqBatch
 from modules.rqvae import RqVae
 from modules.utils import eval_mode
+from rqvae_hip import dp
 
 BATCH_SIZE = 16
 CORPUS_BATCH = 65536
@@ -85,15 +88,20 @@ class SemanticIdTokenizer(nn.Module):
 
     @torch.no_grad()
     @eval_mode
-    def precompute_corpus_ids(self, movie_dataset) -> Tensor:
+    def precompute_corpus_ids(self, movie_dataset, shard: bool = False) -> Tensor:
+        """(N, L+1) corpus ids (semids.py:74-101). `shard=True` (a collective: every rank must call
+        it) splits the quantization over the data-parallel ranks and all-gathers the ids."""
         dev = self.rq_vae.device
         n = len(movie_dataset)
+        lo, hi = dp.shard_range(n, dp.rank(), dp.world()) if shard else (0, n)
         chunks = []
-        for a in range(0, n, CORPUS_BATCH):
-            batch = movie_dataset[list(range(a, min(n, a + CORPUS_BATCH)))]
+        for a in range(lo, hi, CORPUS_BATCH):
+            batch = movie_dataset[list(range(a, min(hi, a + CORPUS_BATCH)))]
             x = batch.x.to(dev, non_blocking=True)
             chunks.append(self.rq_vae.get_semantic_ids(x).sem_ids)
-        ids = torch.cat(chunks, 0)
+        ids = torch.cat(chunks, 0) if chunks else torch.zeros((0, self.n_layers), dtype=torch.int64, device=dev)
+        if shard:
+            ids = dp.all_gather_rows(ids, n)
         self.cached_ids = torch.cat([ids, dedup_rank(ids).unsqueeze(1)], 1)
         self._prefix_index = {}
         return self.cached_ids

@@ -6,17 +6,27 @@ train_decoder.py:171-173,196) and fixes its defects (SURVEY §5, Appendix A-5..A
     ranks iterating the same un-sharded generator;
   * parameters (incl. k-means-initialised codebooks) are broadcast from rank 0 once, after init;
   * gradients live in ONE flat fp32 buffer per dtype ("gradient-as-bucket-view"), so the
-    exchange is a few large all-reduces with no pack/unpack copies; parameters that never
-    receive a gradient (e.g. `tte_fut`, `ffn_norm`) are simply excluded from the buckets;
+    exchange is a few large all-reduces with no pack/unpack copies;
+  * parameters that receive no gradient on ANY rank in the first step (the decoder's `tte_fut`
+    and `ffn_norm`, SURVEY A-7) are found once (one small all-reduce of a usage mask at the first
+    `synchronize`) and from then on keep `grad = None` after every exchange, exactly as with one
+    process (AdamW skips them; 1-rank and N-rank checkpoints stay identical);
   * buckets are all-reduced asynchronously as soon as backward has produced all their grads
     (post-accumulate-grad hooks), overlapping the RCCL ring with the rest of backward; the
-    optimizer step waits on the handles. Average = sum / world.
+    optimizer step waits on the handles. Average = sum / world;
+  * gradient accumulation: backward passes run inside `no_sync()` except the last micro-batch
+    (like DDP), so the exchange starts once, on the accumulated gradients.
+Loss normalisation for unequal shards (`shard_range` with a remainder, token-balanced decoder
+shards from `balanced_partition`): each rank scales its shard-mean loss by
+`shard_weight(n_local, n_global)` = n_local * world / n_global, so the averaged gradient is the
+gradient of the GLOBAL-batch mean (the reference's mean over B, model.py:261, rqvae.py:150).
 Bucket size: 32 MiB by default — large enough that each ring step is link-bandwidth-bound on
 the 7 point-to-point xGMI links, small enough to start overlapping early in backward.
 Works with the gloo backend on CPU for tests.
 """
+import contextlib
 import os
-from typing import Iterable, List, Optional
+from typing import Iterable, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -63,6 +73,43 @@ def shard_range(global_batch: int, rank_: int, world_: int):
     return start, start + base + (1 if rank_ < rem else 0)
 
 
+def shard_weight(n_local: int, n_global: int) -> float:
+    """Factor on a rank's shard-MEAN loss that makes the world-averaged gradient equal the gradient
+    of the global-batch mean: n_local * world / n_global (1.0 for equal shards)."""
+    return float(n_local) * world() / float(n_global) if n_global > 0 else 0.0
+
+
+def balanced_partition(costs: Sequence[int], world_: int) -> List[List[int]]:
+    """Split items with the given costs (e.g. context tokens per sequence) into `world_` bins of
+    near-equal total cost (longest-first greedy: each item goes to the currently lightest bin; ties
+    to the lower rank). Deterministic, host-only; every rank computes the same partition. Bins keep
+    their items in ascending index order. Used for token-balanced decoder shards."""
+    order = sorted(range(len(costs)), key=lambda i: (-int(costs[i]), i))
+    load = [0] * world_
+    bins: List[List[int]] = [[] for _ in range(world_)]
+    for i in order:
+        r = min(range(world_), key=lambda k: (load[k], k))
+        bins[r].append(i)
+        load[r] += int(costs[i])
+    return [sorted(b) for b in bins]
+
+
+def all_gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
+    """Concatenate the per-rank row blocks of a tensor sharded by `shard_range(n_total, r, world)`
+    (rank order) on every rank: one all_gather of equal-size padded blocks, no host sync beyond
+    the collective."""
+    ws = world()
+    if ws == 1:
+        return local
+    spans = [shard_range(n_total, r, ws) for r in range(ws)]
+    width = max(b - a for a, b in spans)
+    pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(ws)]
+    dist.all_gather(parts, pad)
+    return torch.cat([p[:b - a] for p, (a, b) in zip(parts, spans)], 0)
+
+
 class GradBuckets:
     """Flat gradient buffers + bucketed async all-reduce for a module's parameters."""
 
@@ -83,6 +130,8 @@ class GradBuckets:
         self.buckets = []
         self._handles = []
         self._pending = {}
+        self._sync = True          # False inside no_sync(): hooks record usage but launch nothing
+        self._unused = None        # ids of params unused on every rank (decided at the first sync)
         for g in (groups if self.active else []):
             by_dtype = {}
             for p in g:
@@ -112,20 +161,36 @@ class GradBuckets:
             p.grad = v          # grads accumulate in place into the flat buffer
             views.append(v)
             off += p.numel()
-        self.buckets.append(dict(params=ps, flat=flat, views=views, ready=0, used=set()))
+        self.buckets.append(dict(params=ps, flat=flat, views=views, ready=0, used=set(), expect=len(ps)))
 
     def _make_hook(self, bi):
         def hook(p):
             b = self.buckets[bi]
+            if self._unused is not None and id(p) in self._unused:
+                raise RuntimeError("GradBuckets: a parameter that received no gradient on any rank in the first "
+                                   "step got one later; its gradient would not be exchanged (build the buckets "
+                                   "without it, or make it take part in the first step)")
             b["used"].add(id(p))
-            if len(b["used"]) == len(b["params"]):
+            if self._sync and len(b["used"]) == b["expect"]:
                 self._launch(bi)
         return hook
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside accumulate into the flat buffers without starting the exchange
+        (all micro-batches but the last of a gradient-accumulation step)."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
 
     def _launch(self, bi):
         if bi in self._pending:
             return
         b = self.buckets[bi]
+        if b["expect"] == 0:   # every parameter of the bucket is unused on every rank
+            return
         self._pending[bi] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, async_op=True)
 
     def zero_grad(self):
@@ -133,10 +198,13 @@ class GradBuckets:
             for p in self.params:
                 p.grad = None
             return
+        unused = self._unused or ()
         for b in self.buckets:
             b["flat"].zero_()
             b["used"].clear()
             for p, v in zip(b["params"], b["views"]):
+                if id(p) in unused:
+                    continue
                 if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                     p.grad = v
         self._pending = {}
@@ -154,6 +222,27 @@ class GradBuckets:
             if self.average:
                 self.buckets[bi]["flat"].div_(ws)
         self._pending = {}
+        if self._unused is None:
+            self._find_unused()
+        for p in self.params:
+            if id(p) in self._unused:
+                p.grad = None
+
+    def _find_unused(self):
+        """Once, at the first exchange: parameters whose grad hook fired on no rank. They are
+        structurally unused (the decoder's tte_fut / ffn_norm): from now on their grad stays None,
+        and a bucket launches as soon as its USED parameters are ready."""
+        dev = self.buckets[0]["flat"].device if self.buckets else torch.device("cpu")
+        used = torch.tensor([float(id(p) in b["used"]) for b in self.buckets for p in b["params"]], device=dev)
+        dist.all_reduce(used, op=dist.ReduceOp.MAX)
+        flags = used.cpu().tolist()
+        self._unused, k = set(), 0
+        for b in self.buckets:
+            for p in b["params"]:
+                if flags[k] == 0.0:
+                    self._unused.add(id(p))
+                k += 1
+            b["expect"] = sum(1 for p in b["params"] if id(p) not in self._unused)
 
     def broadcast_params(self, src: int = 0):
         if world() == 1:

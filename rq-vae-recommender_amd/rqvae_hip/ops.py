@@ -12,6 +12,7 @@ import math
 from typing import NamedTuple
 
 import torch
+import torch.distributed as _dist
 
 from . import _lib
 from ._lib import RqHipError, call, ptr, stream_handle, require_gpu
@@ -521,14 +522,18 @@ _SEED = {"base": None, "n": 0}
 
 
 def next_seed() -> int:
-    """Key of the next dropout mask: a counter under torch.initial_seed(), so torch.manual_seed makes
-    the masks reproducible (the generator is counter-based; masks are never stored). Host-only: no
-    device sync. A hipGraph capture freezes the key of each captured call."""
+    """Key of the next dropout mask: a counter under torch.initial_seed(), mixed with the
+    data-parallel rank so ranks that share a seed draw independent masks on their different shards
+    (torch.manual_seed still makes every rank's masks reproducible; the generator is counter-based
+    and masks are never stored). Host-only: no device sync. A hipGraph capture freezes the key of
+    each captured call."""
     base = torch.initial_seed()
     if _SEED["base"] != base:
         _SEED["base"], _SEED["n"] = base, 0
     _SEED["n"] += 1
-    return (base * 0x9E3779B97F4A7C15 + _SEED["n"] * 0xD1B54A32D192ED03) & 0x7FFFFFFFFFFFFFFF   # fits int64
+    rank = _dist.get_rank() if _dist.is_available() and _dist.is_initialized() else 0
+    return (base * 0x9E3779B97F4A7C15 + _SEED["n"] * 0xD1B54A32D192ED03 +
+            rank * 0x94D049BB133111EB) & 0x7FFFFFFFFFFFFFFF   # fits int64
 
 
 def dropout_fusable(t: torch.Tensor) -> bool:

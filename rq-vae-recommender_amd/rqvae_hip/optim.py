@@ -38,7 +38,26 @@ class AdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                                       amsgrad=False, maximize=False))
         self._tables = {}
+        self._checked = {}
         load()   # fail loudly here if the HIP library is missing
+
+    @staticmethod
+    def _check_group(group):
+        if group.get("amsgrad", False) or group.get("maximize", False):
+            raise RqHipError("rqvae_hip.optim.AdamW: amsgrad / maximize are not supported")
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.AdamW state (e.g. a reference checkpoint's "optimizer", train_rqvae.py:110-112):
+        groups asking for amsgrad / maximize are rejected, and every `step` counter is kept as a CPU
+        float32 tensor (a checkpoint loaded with map_location=<gpu> would otherwise make each step read
+        it back with a blocking device sync)."""
+        for g in state_dict.get("param_groups", []):
+            self._check_group(g)
+        super().load_state_dict(state_dict)
+        for st in self.state.values():
+            if "step" in st:
+                st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32)
+        self._tables, self._checked = {}, {}
 
     def _table(self, slot, live):
         """Host (ctypes) segment table {p, g, exp_avg, exp_avg_sq, n} per tensor, rebuilt only when a
@@ -48,8 +67,6 @@ class AdamW(torch.optim.Optimizer):
         hit = self._tables.get(slot)
         if hit is not None and hit[0] == key:
             return hit[1]
-        for p, _ in live:   # validated whenever a pointer changes (a new grad tensor included)
-            _check(p)
         table = (ctypes.c_int64 * (5 * len(key)))(*[v for row in key for v in row])
         self._tables[slot] = (key, table)
         return table
@@ -61,14 +78,20 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for gi, group in enumerate(self.param_groups):
+            self._check_group(group)
             live = [p for p in group["params"] if p.grad is not None and p.numel() > 0]
             if not live:
                 continue
+            # validate BEFORE any state changes, whenever a tensor changed since the last check
+            key = tuple((p.data_ptr(), p.grad.data_ptr()) for p in live)
+            if self._checked.get(gi) != key:
+                for p in live:
+                    _check(p)
+                self._checked[gi] = key
             states = []
             for p in live:
                 st = self.state[p]
                 if len(st) == 0:
-                    _check(p)
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)

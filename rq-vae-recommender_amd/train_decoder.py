@@ -1,13 +1,18 @@
 """Decoder (generative retrieval) training entry point — drop-in for reference train_decoder.py
 (same gin-configurable `train(...)` signature; `python train_decoder.py configs/decoder_amazon.gin`).
 
-MI355X path: frozen RQ-VAE tokenizer (fused eval quantize + device dedup), decoder on the HIP jagged
-conversion + varlen attention kernels, one process per GPU with rqvae_hip.dp (disjoint shards of
-each global batch, bucketed RCCL all-reduce overlapped with backward, loss averaged over ranks).
+MI355X path: frozen RQ-VAE tokenizer (fused eval quantize + device dedup; corpus quantization
+sharded over the ranks and all-gathered), decoder on the HIP jagged conversion + varlen attention
+kernels, one process per GPU with rqvae_hip.dp: each global batch is split into TOKEN-BALANCED
+shards (dp.balanced_partition over context lengths, so ranks finish together), each rank scales its
+shard-mean loss by n_local * world / n_global (dp.shard_weight) so the averaged gradient is the
+gradient of the reference's global-batch mean (model.py:261), bucketed RCCL all-reduce overlapped
+with backward, no_sync() for all but the last micro-batch of an accumulation step.
 The reference rejects non-AMAZON datasets and its ML-32M gin binds a non-existent parameter
 (SURVEY A-8); this entry accepts every RecDataset (the ML-32M config still fails on
 `train.attn_dropout`, exactly like gin). Checkpoints: plain state dicts with "scheduler".
 """
+import contextlib
 import json
 import os
 import time
@@ -24,6 +29,16 @@ from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
 from rqvae_hip import optim as hip_optim
+
+
+def token_balanced_shard(seq_mask: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """Indices (host int64) of this rank's sequences of a host-side global batch: the batch is split
+    into `world` bins of near-equal context-token counts (dp.balanced_partition over
+    seq_mask.sum(1)); every rank computes the same partition, no communication."""
+    if world == 1:
+        return torch.arange(seq_mask.shape[0])
+    costs = seq_mask.sum(1).tolist()
+    return torch.tensor(dp.balanced_partition(costs, world)[rank], dtype=torch.int64)
 
 
 @gin.configurable
@@ -49,7 +64,6 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     train_ds = SeqData(root=dataset_folder, dataset=dataset, is_train=True, subsample=train_data_subsample,
                        data_path=data_path, seed=seed)
     global_batch = batch_size if split_batches else batch_size * world
-    lo, hi = dp.shard_range(global_batch, rank, world)
     g = torch.Generator().manual_seed(seed + 5)
     loader = cycle(DataLoader(train_ds, batch_size=global_batch, shuffle=True, generator=g))
 
@@ -57,7 +71,7 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
                                     codebook_size=vae_codebook_size, n_layers=vae_n_layers, n_cat_feats=vae_n_cat_feats,
                                     rqvae_weights_path=pretrained_rqvae_path,
                                     rqvae_codebook_normalize=vae_codebook_normalize, rqvae_sim_vq=vae_sim_vq).to(device)
-    corpus_ids = tokenizer.precompute_corpus_ids(item_ds)   # not DDP-wrapped (reference A-7)
+    corpus_ids = tokenizer.precompute_corpus_ids(item_ds, shard=True)   # not DDP-wrapped (reference A-7)
     top = int(corpus_ids.max())
     if top >= vae_codebook_size:   # would index past the SemIdEmbedder table on the device
         raise ValueError(f"semantic id / dedup value {top} >= codebook size {vae_codebook_size}: the tokenizer's "
@@ -86,14 +100,20 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
         model.train()
         buckets.zero_grad()
         total = 0.0
-        for _ in range(gradient_accumulate_every):
+        for micro in range(gradient_accumulate_every):
             data = next(loader)
-            data = batch_to(type(data)(*[v[lo:hi] for v in data]), device)
+            n_glob = data.seq_mask.shape[0]   # the loader's last batch of an epoch may be short
+            mine = token_balanced_shard(data.seq_mask, rank, world)
+            if len(mine) == 0:   # fewer sequences than ranks: this rank contributes zero gradient
+                continue
+            data = batch_to(type(data)(*[v[mine] for v in data]), device)
             out = model(tokenizer(data))
-            # mean over the GLOBAL batch: the average of equal-size shard means (ranks average grads)
-            loss = out.loss / gradient_accumulate_every
-            loss.backward()
-            total = total + loss.detach()
+            # this rank's shard mean -> share of the GLOBAL-batch mean (unequal, token-balanced shards)
+            loss = out.loss * (dp.shard_weight(len(mine), n_glob) / gradient_accumulate_every)
+            last = micro == gradient_accumulate_every - 1
+            with (contextlib.nullcontext() if last else buckets.no_sync()):
+                loss.backward()
+            total = total + out.loss.detach() / gradient_accumulate_every
         buckets.synchronize()
         opt.step()
         sched.step()

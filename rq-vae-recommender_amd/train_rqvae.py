@@ -11,6 +11,7 @@ Differences from the reference loop (train_rqvae.py:24-250), all on the MI355X p
   * the loop runs `iterations + 1` times like the reference (SURVEY A-4).
 Data: `data.processed.ItemData` (seeded synthetic corpus unless `data_path` names a feature file).
 """
+import contextlib
 import json
 import os
 import time
@@ -28,6 +29,14 @@ from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
 from rqvae_hip import optim as hip_optim
+
+
+def sample_batch_indices(gen: torch.Generator, n_items: int, global_batch: int, device) -> torch.Tensor:
+    """Item indices of one GLOBAL batch (every rank draws the same stream and keeps its own slice).
+    The reference samples without replacement per epoch (BatchSampler(RandomSampler), train_rqvae.py:68);
+    here i.i.d. draws on the device (no host round trip per step). Module-level so a test can
+    substitute the reference's recorded batch order."""
+    return torch.randint(0, n_items, (global_batch,), generator=gen, device=device)
 
 
 @gin.configurable
@@ -55,6 +64,7 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
     n_items = items.shape[0]
     global_batch = batch_size if split_batches else batch_size * world
     lo, hi = dp.shard_range(global_batch, rank, world)
+    w_shard = dp.shard_weight(hi - lo, global_batch)
 
     torch.manual_seed(seed)
     model = RqVae(input_dim=vae_input_dim, embed_dim=vae_embed_dim, hidden_dims=vae_hidden_dims,
@@ -94,12 +104,15 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
         model.train()
         buckets.zero_grad()
         total = 0.0
-        for _ in range(gradient_accumulate_every):
-            idx = torch.randint(0, n_items, (global_batch,), generator=gen, device=device)[lo:hi]
+        for micro in range(gradient_accumulate_every):
+            idx = sample_batch_indices(gen, n_items, global_batch, device)[lo:hi]
             out = model(SeqBatch(None, None, None, items[idx], None, None), gumbel_t=0.2)
-            loss = out.loss / gradient_accumulate_every
-            loss.backward()
-            total = total + loss.detach()
+            # shard mean -> global-batch mean under unequal shards (dp.shard_weight), / micro-batches
+            loss = out.loss * (w_shard / gradient_accumulate_every)
+            last = micro == gradient_accumulate_every - 1
+            with (contextlib.nullcontext() if last else buckets.no_sync()):
+                loss.backward()
+            total = total + out.loss.detach() / gradient_accumulate_every
         buckets.synchronize()
         opt.step()
         hist.append(torch.stack([total, out.reconstruction_loss.detach(), out.rqvae_loss.detach(),

@@ -71,3 +71,39 @@ def named_param(name: str, shape, seed: int) -> np.ndarray:
         return (1.0 + g.uniform(-0.1, 0.1, size=shape)).astype(np.float32)
     b = 1.0 / np.sqrt(shape[-1])
     return g.uniform(-b, b, size=shape).astype(np.float32)
+
+
+def gumbel_noise(shape, seed: int, eps: float = 1e-20) -> np.ndarray:
+    """Gumbel(0, 1) noise as the reference draws it (distributions/gumbel.py:8-11:
+    -log(-log(U + eps) + eps), U ~ U[0, 1)) but from a seeded PCG64 stream, so a fixture can inject
+    the same noise into the reference and into this build."""
+    u = rng(seed).random(shape, dtype=np.float32)
+    e = np.float32(eps)
+    return (-np.log(-np.log(u + e) + e)).astype(np.float32)
+
+
+def topn_multinomial(probs, num_samples, replacement=False, *, generator=None, out=None):
+    """Deterministic stand-in for torch.multinomial in generation fixtures (reference
+    modules/model.py:178): the num_samples most probable classes, highest first, ties to the lower
+    class index. Patched identically into the reference and into this build."""
+    import torch
+    return torch.sort(probs, dim=-1, descending=True, stable=True).indices[..., :num_samples]
+
+
+def prefix_verifier(prefix):
+    """Deterministic inference_verifier_fn for generation fixtures (stands in for
+    SemanticIdTokenizer.exists_prefix): a prefix is valid unless sum(ids) % 7 == 3."""
+    return (prefix.sum(-1) % 7) != 3
+
+
+def batch_permutation(n: int, seed: int, epoch: int) -> np.ndarray:
+    """Index order of one epoch of the deterministic sampler used by the training-trace fixture."""
+    return rng(seed * 1000 + epoch).permutation(n).astype(np.int64)
+
+
+def synthetic_item_corpus(n: int, seed: int, eval_fraction: float = 0.05):
+    """(train, eval, all) item features of the build's synthetic ItemData (data/processed.py):
+    unit-norm 768-d rows from PCG64(seed), train/eval split from PCG64(seed + 1)."""
+    x = items(n, 768, seed)
+    is_train = rng(seed + 1).random(n) >= eval_fraction
+    return x[is_train], x[~is_train], x

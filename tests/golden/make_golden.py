@@ -4,7 +4,7 @@
 Test infrastructure only; run in the build container (never on the GPU box, where
 /root/reference does not exist):
 
-    python tests/golden/make_golden.py [/root/reference]
+    python tests/golden/make_golden.py [/root/reference] [fixture names ... (default: all)]
 
 The reference is imported as-is from its own tree; nothing is copied. Modules the
 reference imports but this image lacks (gin, swanlab, polars, sentence_transformers,
@@ -28,13 +28,19 @@ os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
 sys.dont_write_bytecode = True
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+REF = next((a for a in sys.argv[1:] if os.path.isdir(a)), "/root/reference")
 sys.path.insert(0, HERE)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import gen_inputs as gi  # noqa: E402
+
+
+try:   # before the stubs: accelerate probes find_spec("swanlab"), which a stub without a spec breaks
+    import accelerate  # noqa: E402,F401  (train_rqvae.py:7; only the training-trace fixture needs it)
+except ImportError:  # pragma: no cover
+    pass
 
 
 # --------------------------------------------------------------------------- stubs
@@ -70,7 +76,7 @@ _tg.io = _stub("torch_geometric.io", fs=None)
 
 sys.path.insert(0, REF)
 
-from modules.quantize import Quantize, QuantizeForwardMode  # noqa: E402
+from modules.quantize import Quantize, QuantizeForwardMode, QuantizeDistance  # noqa: E402
 from modules.rqvae import RqVae  # noqa: E402
 from modules.model import EncoderDecoderRetrievalModel  # noqa: E402
 from modules.tokenizer.semids import SemanticIdTokenizer  # noqa: E402
@@ -78,6 +84,8 @@ from data.schemas import SeqBatch, TokenizedSeqBatch  # noqa: E402
 from ops.triton.jagged import padded_to_jagged_tensor  # noqa: E402
 from init.kmeans import Kmeans  # noqa: E402
 import modules.transformer.attention as ref_attention  # noqa: E402
+import distributions.gumbel as ref_gumbel  # noqa: E402
+import modules.quantize as ref_quantize  # noqa: E402
 
 torch.set_num_threads(min(8, os.cpu_count() or 1))
 F32 = np.float32
@@ -260,9 +268,11 @@ class _DenseLoopSDPA:
         return torch.nested.nested_tensor_from_jagged(vals, q.offsets()).transpose(1, 2)
 
 
-def tokenized_batch(B, n_max, L1, K, seed):
+def tokenized_batch(B, n_max, L1, K, seed, full_first=False):
     g = gi.rng(seed)
     n_items = g.integers(1, n_max + 1, size=B)
+    if full_first:   # the config's longest context: n_max items -> n_max * L1 + 1 tokens
+        n_items[0] = n_max
     N = n_max * L1
     sem = g.integers(0, K, size=(B, N)).astype(np.int64)
     mask = np.zeros((B, N), bool)
@@ -277,7 +287,7 @@ def tokenized_batch(B, n_max, L1, K, seed):
                 token_type_ids=tt, token_type_ids_fut=tt_fut)
 
 
-def decoder_fixture(tag, E, A, H, n_layers, K, L1, B, n_max, seed):
+def decoder_fixture(tag, E, A, H, n_layers, K, L1, B, n_max, seed, full_first=False):
     ref_attention.F = _DenseLoopSDPA()
     torch.manual_seed(seed)
     model = EncoderDecoderRetrievalModel(embedding_dim=E, attn_dim=A, dropout=0.0, num_heads=H,
@@ -290,12 +300,12 @@ def decoder_fixture(tag, E, A, H, n_layers, K, L1, B, n_max, seed):
         for name, p in model.named_parameters():
             p.copy_(torch.from_numpy(gi.named_param(name, p.shape, seed)))
     model.train()
-    tb = tokenized_batch(B, n_max, L1, K, seed + 1)
+    tb = tokenized_batch(B, n_max, L1, K, seed + 1, full_first)
     batch = TokenizedSeqBatch(**{k: torch.from_numpy(v) for k, v in tb.items()})
     o = model(batch)
     o.loss.backward()
     out = dict(E=E, A=A, H=H, n_layers=n_layers, K=K, L1=L1, B=B, n_max=n_max, seed=seed,
-               sdpa_substitute=1, loss=npf(o.loss), logits=npf(o.logits), loss_d=npf(o.loss_d), **tb)
+               full_first=int(full_first), sdpa_substitute=1, loss=npf(o.loss), logits=npf(o.logits), loss_d=npf(o.loss_d), **tb)
     for name, p in model.named_parameters():
         if p.grad is None:
             continue
@@ -357,14 +367,249 @@ def kmeans_fixture():
          centroids=npf(km.centroids), assignment=km.assignment.numpy().astype(np.int64))
 
 
+# ------------------------------------------------------------- quantize variants (a4)
+def quantize_variants_fixture(B=128, D=64, K=256, seed=404, T=0.2):
+    """Gumbel-softmax (the reference's default mode, quantize.py:124-129 with noise injected through
+    a patched distributions.gumbel.sample_gumbel), COSINE distance (:113-117), sim_vq (out_proj
+    Linear, :64-67) and codebook_normalize (L2-normalised codebook, :68-70) at ML-32M dims."""
+    x_np, cb_np = gi.quantize_case(B, D, K, seed)
+    g = gi.rng(seed + 1)
+    g_emb = g.standard_normal((B, D), dtype=F32)
+    g_loss = g.random(B, dtype=F32)
+    noise = gi.gumbel_noise((B, K), seed + 2)
+    proj_w = gi.linear_weight(D, D, seed + 3)
+    out = dict(B=B, D=D, K=K, seed=seed, T=F32(T), x=x_np, codebook=cb_np, g_emb=g_emb, g_loss=g_loss,
+               noise_checksum=gi.checksum(noise), proj_w=proj_w)
+    variants = {   # name: (forward_mode, distance, sim_vq, codebook_normalize, training)
+        "gumbel": (QuantizeForwardMode.GUMBEL_SOFTMAX, QuantizeDistance.L2, False, False, True),
+        "gumbel_eval": (QuantizeForwardMode.GUMBEL_SOFTMAX, QuantizeDistance.L2, False, False, False),
+        "cosine_rotation": (QuantizeForwardMode.ROTATION_TRICK, QuantizeDistance.COSINE, False, False, True),
+        "cosine_eval": (QuantizeForwardMode.ROTATION_TRICK, QuantizeDistance.COSINE, False, False, False),
+        "simvq_rotation": (QuantizeForwardMode.ROTATION_TRICK, QuantizeDistance.L2, True, False, True),
+        "cbnorm_ste": (QuantizeForwardMode.STE, QuantizeDistance.L2, False, True, True),
+        "simvq_gumbel": (QuantizeForwardMode.GUMBEL_SOFTMAX, QuantizeDistance.L2, True, False, True),
+    }
+    orig = ref_gumbel.sample_gumbel
+    ref_gumbel.sample_gumbel = lambda shape, device, eps=1e-20: torch.from_numpy(noise.copy()).reshape(shape)
+    try:
+        for name, (fm, dm, sim, cbn, training) in variants.items():
+            q = Quantize(D, K, do_kmeans_init=False, codebook_normalize=cbn, sim_vq=sim, forward_mode=fm,
+                         distance_mode=dm)
+            with torch.no_grad():
+                q.embedding.weight.copy_(torch.from_numpy(cb_np))
+                if sim:
+                    q.out_proj[0].weight.copy_(torch.from_numpy(proj_w))
+            q.train(training)
+            x = torch.from_numpy(x_np.copy()).requires_grad_(True)
+            o = q(x, temperature=T)
+            ((o.embeddings * torch.from_numpy(g_emb)).sum() + (o.loss * torch.from_numpy(g_loss)).sum()).backward()
+            out.update({f"{name}_ids": o.ids.numpy().astype(np.int64), f"{name}_emb": npf(o.embeddings),
+                        f"{name}_loss": npf(o.loss), f"{name}_grad_x": npf(x.grad),
+                        f"{name}_grad_cb": npf(q.embedding.weight.grad)})
+            if sim:
+                out[f"{name}_grad_proj"] = npf(q.out_proj[0].weight.grad)
+    finally:
+        ref_gumbel.sample_gumbel = orig
+    out["variants"] = np.array(list(variants))
+    save("quantize_variants.npz", **out)
+
+
+# ------------------------------------------------------------------ generation (f3)
+def generation_fixture(E=32, A=64, H=4, n_layers=4, K=256, L1=4, B=3, n_max=5, seed=41):
+    """EncoderDecoderRetrievalModel.generate_next_sem_id (modules/model.py:149-245) with
+    torch.multinomial replaced by a deterministic top-n (gi.topn_multinomial) and a deterministic
+    prefix verifier (gi.prefix_verifier) — the same patches the GPU test applies to this build."""
+    ref_attention.F = _DenseLoopSDPA()
+    model = EncoderDecoderRetrievalModel(embedding_dim=E, attn_dim=A, dropout=0.3, num_heads=H, n_layers=n_layers,
+                                         num_embeddings=K, sem_id_dim=L1, inference_verifier_fn=gi.prefix_verifier,
+                                         max_pos=n_max * L1, jagged_mode=True)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            v = gi.named_param(name, p.shape, seed)
+            if name == "out_proj.weight":
+                v = v * 4.0     # well-separated candidate probabilities
+            p.copy_(torch.from_numpy(v))
+    tb = tokenized_batch(B, n_max, L1, K, seed + 1)
+    batch = TokenizedSeqBatch(**{k: torch.from_numpy(v) for k, v in tb.items()})
+    model.enable_generation = True
+    orig = torch.multinomial
+    torch.multinomial = gi.topn_multinomial
+    try:
+        for top_k in (True, False):
+            g = model.generate_next_sem_id(batch, temperature=1, top_k=top_k)
+            tag = "topk" if top_k else "greedy"
+            tb[f"{tag}_sem_ids"] = g.sem_ids.numpy().astype(np.int64)
+            tb[f"{tag}_log_probas"] = npf(g.log_probas)
+    finally:
+        torch.multinomial = orig
+    save("generation.npz", E=E, A=A, H=H, n_layers=n_layers, K=K, L1=L1, B=B, n_max=n_max, seed=seed,
+         out_proj_scale=F32(4.0), sdpa_substitute=1, **tb)
+
+
+# ------------------------------------------------------------ checkpoints (f4)
+def checkpoint_fixture(seed=11, steps=3, lr=5e-4, wd=0.01):
+    """A checkpoint in the reference's train_rqvae.py:209-221 layout {"iter", "model", "optimizer"}
+    (tensors / plain containers only, so it loads with weights_only=True; the reference's
+    model_config pickles the module itself, SURVEY A-13) written by the reference RqVae + torch AdamW
+    after `steps` steps, plus the reference's NEXT step from it (loss, updated parameters). Also the
+    reference's state-dict key/shape manifests of RqVae and EncoderDecoderRetrievalModel."""
+    inp, hidden, D, K, L = 96, [64, 32], 16, 32, 3
+    model = RqVae(input_dim=inp, embed_dim=D, hidden_dims=hidden, codebook_size=K, codebook_kmeans_init=False,
+                  codebook_mode=QuantizeForwardMode.ROTATION_TRICK, n_layers=L, n_cat_features=0)
+    z = np.load(os.path.join(HERE, "rqvae_small.npz"))
+    model.load_state_dict(rqvae_state((inp, hidden, D), list(z["codebooks"]), seed))
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=wd)
+
+    def step(i):
+        x = torch.from_numpy(gi.items(64, inp, 700 + i))
+        opt.zero_grad()
+        o = model(SeqBatch(None, None, None, x, None, None), gumbel_t=0.2)
+        o.loss.backward()
+        opt.step()
+        return float(o.loss)
+    for i in range(steps):
+        step(i)
+    torch.save({"iter": steps - 1, "model": model.state_dict(), "optimizer": opt.state_dict()},
+               os.path.join(HERE, "ckpt_rqvae_small.pt"))
+    print("wrote ckpt_rqvae_small.pt")
+    loss = step(steps)
+    out = {"next_loss": np.float64(loss), "iter": steps - 1, "lr": lr, "wd": wd, "seed": seed}
+    for name, p in model.named_parameters():
+        out["next__" + name] = npf(p)
+    for name, t in RqVae(input_dim=768, embed_dim=32, hidden_dims=[512, 256, 128], codebook_size=256,
+                         codebook_kmeans_init=False, n_layers=3, n_cat_features=0).state_dict().items():
+        out["rqvae_keys__" + name] = np.array(t.shape, np.int64)
+    dec = EncoderDecoderRetrievalModel(embedding_dim=128, attn_dim=512, dropout=0.3, num_heads=8, n_layers=8,
+                                       num_embeddings=256, sem_id_dim=4, inference_verifier_fn=None, max_pos=80)
+    for name, t in dec.state_dict().items():
+        out["decoder_keys__" + name] = np.array(t.shape, np.int64)
+    out["decoder_n_params"] = np.int64(sum(p.numel() for p in dec.parameters()))
+    save("checkpoint.npz", **out)
+
+
+# ----------------------------------------------------------- C1 loss trace (train_rqvae.train)
+def train_trace_fixture(iterations=24, batch_size=64, seed=0, np_seed=2024, sampler_seed=5, w_seed=13):
+    """A (iterations+1)-step run of the reference's own train_rqvae.train() at configs/rqvae_amazon.gin
+    dims (768 -> [512,256,128] -> 32, K=256, L=3, ROTATION_TRICK, AdamW 1e-4 / 0.01, k-means init on
+    the first min(20000, N) items), on the build's seeded synthetic Amazon-sized corpus. Patched into
+    the reference module: ItemData (synthetic corpus), RandomSampler (seeded permutation per epoch,
+    gi.batch_permutation), RqVae (numpy-seeded MLP weights after construction, per-step loss
+    recording), np.random.seed(np_seed) for the k-means init draws. Records the batch indices, the
+    post-k-means codebooks and the per-step losses."""
+    import train_rqvae as tr
+    from torch.utils.data import Sampler
+    x_train, x_eval, x_all = gi.synthetic_item_corpus(12101, seed)
+
+    class _Items:
+        def __init__(self, *a, train_test_split="all", **k):
+            self.x = torch.from_numpy({"train": x_train, "eval": x_eval}.get(train_test_split, x_all))
+
+        def __len__(self):
+            return self.x.shape[0]
+
+        def __getitem__(self, idx):
+            item_ids = torch.tensor(idx).unsqueeze(0) if not isinstance(idx, torch.Tensor) else idx
+            neg = -torch.ones_like(item_ids.squeeze(0))
+            return SeqBatch(user_ids=neg, ids=item_ids, ids_fut=neg, x=self.x[idx, :768], x_fut=neg,
+                            seq_mask=torch.ones_like(item_ids, dtype=torch.bool))
+
+    class _Sampler(Sampler):
+        epochs = {}
+
+        def __init__(self, ds):
+            self.n = len(ds)
+            self.key = id(ds)
+
+        def __len__(self):
+            return self.n
+
+        def __iter__(self):
+            e = _Sampler.epochs.get(self.key, 0)
+            _Sampler.epochs[self.key] = e + 1
+            return iter(gi.batch_permutation(self.n, sampler_seed, e).tolist())
+
+    record = {"loss": [], "rl": [], "vl": [], "pu": [], "idx": []}
+    kmeans_cbs = []
+    orig_init = ref_quantize.kmeans_init_
+
+    def kmeans_rec(tensor, x):
+        orig_init(tensor, x)
+        kmeans_cbs.append(tensor.detach().numpy().copy())
+
+    class _RqVae(RqVae):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            enc = gi.mlp_weights([self.input_dim] + list(self.hidden_dims) + [self.embed_dim], w_seed)
+            dec = gi.mlp_weights([self.embed_dim] + list(self.hidden_dims)[::-1] + [self.input_dim], w_seed + 1)
+            with torch.no_grad():
+                for j, w in enumerate(enc):
+                    self.encoder.mlp[2 * j].weight.copy_(torch.from_numpy(w))
+                for j, w in enumerate(dec):
+                    self.decoder.mlp[2 * j].weight.copy_(torch.from_numpy(w))
+
+        def forward(self, batch, gumbel_t):
+            o = super().forward(batch, gumbel_t)
+            if self.training and batch.x.shape[0] == batch_size:
+                record["loss"].append(float(o.loss))
+                record["rl"].append(float(o.reconstruction_loss))
+                record["vl"].append(float(o.rqvae_loss))
+                record["pu"].append(float(o.p_unique_ids))
+                record["idx"].append(batch.ids.numpy().astype(np.int64).copy())
+            return o
+
+    saved = (tr.ItemData, tr.RandomSampler, tr.RqVae, ref_quantize.kmeans_init_, torch.save)
+    tr.ItemData, tr.RandomSampler, tr.RqVae, ref_quantize.kmeans_init_ = _Items, _Sampler, _RqVae, kmeans_rec
+    torch.save = lambda *a, **k: None   # the end-of-run checkpoint pickles the (local) model class
+    cwd = os.getcwd()
+    import tempfile
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            os.chdir(d)
+            np.random.seed(np_seed)
+            torch.manual_seed(0)
+            tr.train(iterations=iterations, batch_size=batch_size, learning_rate=1e-4, weight_decay=0.01,
+                     vae_input_dim=768, vae_embed_dim=32, vae_hidden_dims=[512, 256, 128], vae_codebook_size=256,
+                     vae_n_layers=3, vae_n_cat_feats=0, vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK,
+                     commitment_weight=0.25, use_kmeans_init=True, do_eval=True, save_dir_root=d + "/",
+                     eval_every=10 ** 9, save_model_every=10 ** 9)
+    finally:
+        os.chdir(cwd)
+        tr.ItemData, tr.RandomSampler, tr.RqVae, ref_quantize.kmeans_init_, torch.save = saved
+    assert len(record["loss"]) == iterations + 1, len(record["loss"])
+    save("train_trace_amazon.npz", iterations=iterations, batch_size=batch_size, seed=seed, np_seed=np_seed,
+         sampler_seed=sampler_seed, w_seed=w_seed, lr=1e-4, wd=0.01, n_train=x_train.shape[0],
+         kmeans_codebooks=np.stack(kmeans_cbs), batch_idx=np.stack(record["idx"]),
+         loss=np.array(record["loss"]), reconstruction_loss=np.array(record["rl"]),
+         rqvae_loss=np.array(record["vl"]), p_unique_ids=np.array(record["pu"]))
+
+
+FIXTURES = {
+    "quantize_amazon": lambda: quantize_fixture("amazon", B=256, D=32, K=256, seed=101, store_inputs=True),
+    "quantize_ml32m": lambda: quantize_fixture("ml32m", B=256, D=64, K=256, seed=202, store_inputs=True),
+    "quantize_synth": lambda: quantize_fixture("synth", B=24, D=1024, K=2048, seed=303, store_inputs=False,
+                                               modes=("rotation", "eval")),
+    "rqvae_small": lambda: rqvae_fixture("small", inp=96, hidden=[64, 32], D=16, K=32, L=3, B=128, seed=11,
+                                         store_grads_full=True),
+    "rqvae_ml32m": lambda: rqvae_fixture("ml32m", inp=768, hidden=[512, 256, 128], D=64, K=256, L=3, B=64, seed=12,
+                                         store_grads_full=False),
+    "jagged": jagged_fixture,
+    "decoder_small": lambda: decoder_fixture("small", E=32, A=64, H=4, n_layers=4, K=16, L1=4, B=6, n_max=5, seed=21),
+    # configs[3] (decoder_ml32m.gin: A=384, H=6, 8 layers, E=128): one sequence of 200 items = 801 ctx tokens
+    "decoder_dm": lambda: decoder_fixture("dm", E=128, A=384, H=6, n_layers=8, K=256, L1=4, B=3, n_max=200, seed=22,
+                                          full_first=True),
+    # configs[4] jagged half (DA dims, L=4 -> 5 tokens per item, K=2048): one sequence of 256 items = 1281 tokens
+    "decoder_c5": lambda: decoder_fixture("c5", E=128, A=512, H=8, n_layers=8, K=2048, L1=5, B=2, n_max=256, seed=23,
+                                          full_first=True),
+    "tokenizer": tokenizer_fixture,
+    "kmeans": kmeans_fixture,
+    "quantize_variants": quantize_variants_fixture,
+    "generation": generation_fixture,
+    "checkpoint": checkpoint_fixture,
+    "train_trace": train_trace_fixture,
+}
+
+
 if __name__ == "__main__":
-    quantize_fixture("amazon", B=256, D=32, K=256, seed=101, store_inputs=True)
-    quantize_fixture("ml32m", B=256, D=64, K=256, seed=202, store_inputs=True)
-    quantize_fixture("synth", B=24, D=1024, K=2048, seed=303, store_inputs=False, modes=("rotation", "eval"))
-    rqvae_fixture("small", inp=96, hidden=[64, 32], D=16, K=32, L=3, B=128, seed=11, store_grads_full=True)
-    rqvae_fixture("ml32m", inp=768, hidden=[512, 256, 128], D=64, K=256, L=3, B=64, seed=12,
-                  store_grads_full=False)
-    jagged_fixture()
-    decoder_fixture("small", E=32, A=64, H=4, n_layers=4, K=16, L1=4, B=6, n_max=5, seed=21)
-    tokenizer_fixture()
-    kmeans_fixture()
+    names = [a for a in sys.argv[1:] if a in FIXTURES] or list(FIXTURES)
+    for n in names:
+        FIXTURES[n]()

@@ -2,11 +2,16 @@
 
 Checks: disjoint sharding of a global batch; rank-0 parameter broadcast; bucketed async
 all-reduce (gradient-as-bucket-view, post-accumulate hooks) reproduces the single-process
-gradient of the global-batch mean loss; parameters that receive no gradient are tolerated.
+gradient of the GLOBAL-batch mean loss — with equal shards, unequal shards (remainder rows,
+dp.shard_weight), token-balanced variable-length shards (dp.balanced_partition) and gradient
+accumulation (no_sync on all but the last micro-batch); parameters unused on every rank keep
+grad None exactly as with one process, so AdamW steps give identical parameters at 1 and N ranks;
+corpus all-gather (dp.all_gather_rows).
 """
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -35,76 +40,148 @@ class _Net(torch.nn.Module):
 
 
 def _loss(model, x):
+    """Per-row loss, mean over the rows (the reference's mean over the batch)."""
     return ((model(x) - 0.1) ** 2).sum(-1).mean()
 
 
-def _worker(rank, world, port, gb, bucket_bytes, q, grouped=False):
+def _seq_loss(model, x, lengths):
+    """Variable-length 'sequences' (rows of x grouped by lengths): per-sequence sum over its tokens,
+    mean over the sequences — the decoder's CE summed over positions and averaged over B."""
+    per_tok = ((model(x) - 0.1) ** 2).sum(-1)
+    off = np.concatenate([[0], np.cumsum(lengths)])
+    per_seq = torch.stack([per_tok[off[i]:off[i + 1]].sum() for i in range(len(lengths))])
+    return per_seq.mean()
+
+
+def _data(gb):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(gb, 24, generator=g)
+    lengths = torch.randint(1, 9, (gb,), generator=g).tolist()
+    toks = torch.randn(sum(lengths), 24, generator=g)
+    return x, lengths, toks
+
+
+def _seq_slice(toks, lengths, idx):
+    off = np.concatenate([[0], np.cumsum(lengths)])
+    rows = torch.cat([toks[off[i]:off[i + 1]] for i in idx])
+    return rows, [lengths[i] for i in idx]
+
+
+def _worker(rank, world, port, gb, bucket_bytes, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
         r, w, _ = dp.init_from_env(backend="gloo")
         torch.manual_seed(100 + rank)          # different init per rank: broadcast must fix it
         model = _Net()
-        if grouped:   # parameter groups in grad-ready order (the bench's RQ-VAE layout)
+        if mode == "grouped":   # parameter groups in grad-ready order (the bench's RQ-VAE layout)
             ps = list(model.parameters())
             buckets = dp.GradBuckets([ps[len(ps) // 2:][::-1], ps[:len(ps) // 2][::-1]], bucket_bytes=bucket_bytes)
         else:
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
         buckets.broadcast_params()
-        g = torch.Generator().manual_seed(7)
-        x = torch.randn(gb, 24, generator=g)
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
+        x, lengths, toks = _data(gb)
         a, b = dp.shard_range(gb, r, w)
+        mine = dp.balanced_partition(lengths, w)[r]
         for _ in range(2):                     # two steps: zero_grad must reset the flat buffers
             buckets.zero_grad()
-            _loss(model, x[a:b]).backward()
+            if mode == "accum":                # two micro-batches: the global batch, then its reverse
+                for micro, xb in enumerate((x[a:b], x.flip(0)[a:b])):
+                    loss = _loss(model, xb) * dp.shard_weight(b - a, gb) / 2
+                    if micro == 0:
+                        with buckets.no_sync():
+                            loss.backward()
+                        assert not buckets._pending, "no_sync must not start the exchange"
+                    else:
+                        loss.backward()
+            elif mode == "tokens":             # token-balanced shards of variable-length sequences
+                rows, lens = _seq_slice(toks, lengths, mine)
+                (_seq_loss(model, rows, lens) * dp.shard_weight(len(mine), gb)).backward()
+            else:
+                (_loss(model, x[a:b]) * dp.shard_weight(b - a, gb)).backward()
             buckets.synchronize()
+            grads = {n: (None if p.grad is None else p.grad.detach().numpy().copy()) for n, p in model.named_parameters()}
+            opt.step()
         # numpy copies: tensors sent through a torch.multiprocessing queue are shared-memory handles
         # that die with this process (the parent may read after we exit)
-        grads = {n: p.grad.detach().numpy().copy() for n, p in model.named_parameters()}
         params = {n: p.detach().numpy().copy() for n, p in model.named_parameters()}
-        q.put((r, (a, b), params, grads, len(buckets.buckets)))
+        q.put((r, (a, b), params, grads, len(buckets.buckets), mine))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,gb,bucket_bytes,grouped", [(2, 64, 1 << 20, False), (3, 63, 2048, False),
-                                                          (2, 64, 1 << 20, True)])
-def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, grouped):
+def _run(world, gb, bucket_bytes, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, gb, bucket_bytes, q, grouped)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, gb, bucket_bytes, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # shards: disjoint, cover the global batch
-    spans = [r[1] for r in res]
-    assert spans[0][0] == 0 and spans[-1][1] == gb and all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
-    # params identical on all ranks (rank-0 broadcast)
-    res = [(r[0], r[1], {n: torch.from_numpy(v) for n, v in r[2].items()},
-            {n: torch.from_numpy(v) for n, v in r[3].items()}, r[4]) for r in res]
-    for r in res[1:]:
-        for n in r[2]:
-            assert torch.equal(r[2][n], res[0][2][n])
+    return res
+
+
+def _single_process(state0, gb, mode, world):
+    """Same two steps in one process: params after the first step + grads of the second step."""
+    model = _Net()
+    model.load_state_dict(state0)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
+    x, lengths, toks = _data(gb)
+    grads = None
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        if mode == "accum":
+            ((_loss(model, x) + _loss(model, x.flip(0))) / 2).backward()
+        elif mode == "tokens":
+            _seq_loss(model, toks, lengths).backward()
+        else:
+            _loss(model, x).backward()
+        grads = {n: p.grad for n, p in model.named_parameters()}
+        opt.step()
+    return model, grads
+
+
+@pytest.mark.parametrize("world,gb,bucket_bytes,mode", [
+    (2, 64, 1 << 20, "plain"),      # equal shards
+    (3, 64, 2048, "plain"),         # unequal shards (22/21/21), several buckets
+    (2, 63, 1 << 20, "grouped"),    # unequal shards, grouped buckets
+    (2, 64, 1 << 20, "accum"),      # gradient accumulation with no_sync
+    (3, 61, 4096, "tokens"),        # token-balanced variable-length shards (unequal sequence counts)
+])
+def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode):
+    res = _run(world, gb, bucket_bytes, mode)
+    if mode != "tokens":   # contiguous shards: disjoint, cover the global batch
+        spans = [r[1] for r in res]
+        assert spans[0][0] == 0 and spans[-1][1] == gb and all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    else:                  # token-balanced shards: a partition of the sequences
+        allidx = sorted(i for r in res for i in r[5])
+        assert allidx == list(range(gb))
     if bucket_bytes == 2048:
         assert res[0][4] > 1, "expected several buckets"
-    # reference: single process, same params, mean over the shard means (equal shards when gb % world == 0)
-    model = _Net()
-    model.load_state_dict(res[0][2])
-    g = torch.Generator().manual_seed(7)
-    x = torch.randn(gb, 24, generator=g)
-    total = sum(_loss(model, x[a:b]) for a, b in spans) / world
-    total.backward()
+    # rank-0 broadcast + identical updates: parameters identical on all ranks after 2 AdamW steps
+    for r in res[1:]:
+        for n in r[2]:
+            assert np.array_equal(r[2][n], res[0][2][n]), n
+    # single process from the same initial parameters (rank 0's init after broadcast = seed 100)
+    torch.manual_seed(100)
+    state0 = _Net().state_dict()
+    model, grads = _single_process(state0, gb, mode, world)
     for n, p in model.named_parameters():
         got = res[0][3][n]
-        ref = p.grad if p.grad is not None else torch.zeros_like(p)
-        assert torch.allclose(got, ref, rtol=1e-5, atol=1e-7), n
+        ref = grads[n]
+        if ref is None:   # unused everywhere: grad None at N ranks as at 1 (AdamW skips it)
+            assert got is None, n
+            continue
+        assert torch.allclose(torch.from_numpy(got), ref, rtol=2e-5, atol=1e-7), n
         for r in res[1:]:
-            assert torch.equal(r[3][n], got)
+            assert np.array_equal(r[3][n], got)
+        assert np.allclose(res[0][2][n], p.detach().numpy(), rtol=1e-5, atol=1e-6), f"params {n}"
+    assert np.array_equal(res[0][2]["unused.weight"], model.unused.weight.detach().numpy())
 
 
 def test_shard_range_partitions():
@@ -115,3 +192,45 @@ def test_shard_range_partitions():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_balanced_partition_properties():
+    g = np.random.Generator(np.random.PCG64(3))
+    for B, w, hi in [(256, 8, 81), (64, 8, 801), (7, 3, 10), (3, 4, 5), (1000, 2, 1281)]:
+        costs = (4 * g.integers(1, hi // 4 + 1, size=B) + 1).tolist()
+        bins = dp.balanced_partition(costs, w)
+        assert sorted(i for b in bins for i in b) == list(range(B))
+        assert all(b == sorted(b) for b in bins)
+        loads = [sum(costs[i] for i in b) for b in bins]
+        # longest-first greedy: the spread is at most the largest single cost
+        assert max(loads) - min(loads) <= max(costs)
+        assert bins == dp.balanced_partition(costs, w)   # deterministic
+
+
+def _gather_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        dp.init_from_env(backend="gloo")
+        a, b = dp.shard_range(n, rank, world)
+        full = torch.arange(n * 3, dtype=torch.int64).view(n, 3) * 7 % 101
+        got = dp.all_gather_rows(full[a:b].clone(), n)
+        q.put((rank, bool(torch.equal(got, full))))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 11), (3, 64), (3, 2)])
+def test_all_gather_rows(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)

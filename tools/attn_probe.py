@@ -3,6 +3,7 @@
 
   Amazon:  B=256 sequences, ctx len 4*U{2..20}+1 (<= 81), H=8, hd=64 (attn_dim 512)
   ML-32M:  B=64 sequences,  ctx len 4*U{2..200}+1 (<= 801), H=6, hd=64 (attn_dim 384)
+  C5:      B=64 sequences,  ctx len 5*U{2..256}+1 (<= 1281), H=8, hd=64 (DA dims, L=4)
 """
 import json
 import os
@@ -27,9 +28,9 @@ def t(fn, iters=20):
     return a.elapsed_time(b) / iters
 
 
-def case(name, B, H, hd, max_items, dev):
+def case(name, B, H, hd, max_items, dev, L1=4):
     g = np.random.Generator(np.random.PCG64(7))
-    lens = 4 * g.integers(2, max_items + 1, size=B) + 1
+    lens = L1 * g.integers(2, max_items + 1, size=B) + 1
     cu = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).to(dev)
     T = int(lens.sum())
     A = H * hd
@@ -55,6 +56,7 @@ def main():
         print(json.dumps(dict(lib=sys.argv[1])))
     case("amazon", 256, 8, 64, 20, dev)
     case("ml32m", 64, 6, 64, 200, dev)
+    case("c5", 64, 8, 64, 256, dev, L1=5)
 
 
 if __name__ == "__main__":
