@@ -352,8 +352,9 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 }
 
 static bool attn_args_ok(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k) {
+  // max_q / max_k bound the grid's x extent and every in-kernel int index (row * stride fits int64)
   return B >= 0 && B <= 65535 && H >= 1 && H <= 65535 && (hd == 16 || hd == 32 || hd == 64 || hd == 128) && max_q >= 0 &&
-         max_k >= 0;
+         max_k >= 0 && max_q <= (1 << 24) && max_k <= (1 << 24);
 }
 
 }  // namespace rqhip

@@ -125,10 +125,13 @@ def test_linear_high_precision_matches_fp64(device, bias):
 
 
 def test_rqvae_step_high_vs_highest(device):
-    """The RQ-VAE train step (ML-32M dims) at 'high' (split-bf16 MLP matmuls) against the same step
-    at 'highest': loss within 1e-4 relative, MLP gradients within 3 % in norm (dominated by the items whose ids flip), codebook
-    gradients within 5 % in norm, and the semantic ids of >= 99 % of the items identical (near-ties may flip under a 2^-17 perturbation,
-    as they do between TF32 and fp32 in the reference)."""
+    """The RQ-VAE train step (ML-32M dims, 4096 items) at 'high' (split-bf16 MLP matmuls) against the
+    same step at 'highest', under the margin contract: the 'high' encoder output differs from the
+    exact one by ~2^-17 relative, which can move an argmin only where the top-2 distance gap is
+    tiny. So: semantic ids identical on every item whose exact-path top-2 relative gap exceeds 1e-4
+    at every level (fp64 distances of the 'highest' residuals); the loss within 1e-5 relative; and
+    every MLP / codebook gradient within 1e-3 relative in norm plus the share of the items whose ids
+    flipped (a flipped item moves its whole contribution)."""
     import bench
     from data.schemas import SeqBatch
     m = bench.build_model(device)
@@ -140,20 +143,25 @@ def test_rqvae_step_high_vs_highest(device):
         out = m(SeqBatch(None, None, None, x, None, None), gumbel_t=0.2)
         out.loss.backward()
         with torch.no_grad():
-            ids = m.get_semantic_ids(x).sem_ids
-        res[prec] = (float(out.loss), {k: p.grad.clone() for k, p in m.named_parameters()}, ids)
+            sem = m.get_semantic_ids(x)
+        res[prec] = (float(out.loss), {k: p.grad.clone() for k, p in m.named_parameters()}, sem.sem_ids,
+                     sem.residuals)
     torch.set_float32_matmul_precision("highest")
-    (l0, g0, i0), (l1, g1, i1) = res["highest"], res["high"]
-    assert abs(l1 - l0) <= 1e-4 * abs(l0), (l0, l1)
-    agree = float((i0 == i1).all(1).float().mean())
-    assert agree >= 0.99, agree
+    (l0, g0, i0, r0), (l1, g1, i1, _) = res["highest"], res["high"]
+    safe = torch.ones(x.shape[0], dtype=torch.bool, device=device)
+    for l, layer in enumerate(m.layers):
+        r = r0[:, :, l].double()
+        c = layer.embedding.weight.detach().double()
+        d = (r * r).sum(1, keepdim=True) + (c * c).sum(1)[None] - 2 * r @ c.T
+        top2 = d.topk(2, dim=1, largest=False).values
+        safe &= (top2[:, 1] - top2[:, 0]) > 1e-4 * top2[:, 0].abs()
+    assert safe.float().mean() > 0.95
+    assert torch.equal(i0[safe], i1[safe]), "ids differ on margin-safe items"
+    flipped = float((i0 != i1).any(1).float().mean())
+    assert abs(l1 - l0) <= 1e-5 * abs(l0), (l0, l1)
     for k in g0:
-        if k.startswith("layers."):
-            # a codeword's gradient sums its assigned items: an id flip moves an item's whole
-            # contribution, so compare in norm (the flips are <= 1 % of the items)
-            assert (g1[k] - g0[k]).norm() <= 0.05 * g0[k].norm(), k
-        else:   # flipped items also change their encoder / decoder gradient paths
-            assert (g1[k] - g0[k]).norm() <= 3e-2 * g0[k].norm(), k
+        # a codeword row sums ~N/K items, so n flips move its norm by ~sqrt(n / N), not n / N
+        assert (g1[k] - g0[k]).norm() <= (1e-3 + 2 * flipped ** 0.5) * g0[k].norm(), (k, flipped)
 
 
 # ----------------------------------------------------------------- pre-split operands, fused epilogues

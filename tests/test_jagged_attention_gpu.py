@@ -70,6 +70,10 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (9, 5, 5, 8, 64, True, True),        # decoder causal self-attention (DA)
     (6, 5, 81, 8, 64, False, False),     # cross-attention (DA)
     (3, 300, 300, 6, 64, False, True),   # long context (DM-like)
+    (2, 801, 801, 6, 64, False, True),   # DM longest context (200 items x 4 + 1)
+    (2, 1281, 1281, 8, 64, False, True), # C5 longest context (256 items x 5 + 1)
+    (3, 6, 1281, 8, 64, False, False),   # C5 cross-attention: L+2 future queries x 1281 keys
+    (2, 6, 6, 8, 64, True, True),        # C5 decoder causal self-attention
     (4, 70, 70, 4, 32, True, True),
     (2, 40, 90, 2, 128, False, False),
     (5, 30, 30, 4, 16, True, True),      # small head dim (decoder fixtures: A=64, H=4)
