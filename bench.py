@@ -18,14 +18,20 @@ Matmul precision follows the reference: it sets torch.set_float32_matmul_precisi
 import (modules/rqvae.py:19), so the MLP matmuls run on the split-bf16 GEMM (rq_gemm_bf16x3);
 the same step at 'highest' (exact fp32) is reported beside it (exact_fp32_highest).
 
+The timed region carries no instrumentation; kernel statistics come from an untimed pass of 5 more
+steps of the same loop with HIP events on the launching stream.
 roofline: the dominant kernel — the split-bf16 GEMM at its largest-time launch shape (fp32-matmul
-FLOPs 2MNK / mean device time, peak = bf16 dense MFMA / 3 products) — measured with HIP events on
-the launching stream inside the timed region; roofline_quantize: the fused quantize forward
+FLOPs 2MNK / mean device time, peak = bf16 dense MFMA / 3 products); roofline_quantize: the fused quantize forward
 (rq_quantize_fwd), algorithmic FLOPs 2*K*D*L per item, peak = fp32 MFMA 157.3
 TFLOP/s. traffic: HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 +
 WRITE_SIZE, child processes running the same kernel at the same shape, N=1 only) next to the
 algorithmic bytes. cpu_baseline: the pinned numpy oracle
 of the same train step (oracle/rqvae.py) on a bounded sample, timed on this host.
+
+decoder_amazon (configs[2]) / decoder_ml32m (configs[3], 8 and 64 sequences per GPU): decoder train
+steps replayed from one hipGraph per context row bucket (eager ms beside it), context tokens/s over
+all ranks, a roofline over the step's algorithmic FLOPs, attention / jagged kernel statistics from an
+untimed eager pass, and the pinned torch-CPU decoder oracle (oracle/decoder.py) as its cpu_baseline.
 """
 import argparse
 import json
@@ -71,6 +77,8 @@ def parse():
     ap.add_argument("--no-tunable", action="store_true", help="library GEMMs on their default heuristic")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
+    ap.add_argument("--no-graph", action="store_true", help="decoder steps eager instead of hipGraph replays")
+    ap.add_argument("--no-dm", action="store_true", help="skip the ML-32M decoder lines")
     return ap.parse_args()
 
 
@@ -108,7 +116,7 @@ def time_region(fn, steps, warmup, sync_all):
 
 
 def gemm_launch_stats(timer, steps=1):
-    """Split-bf16 GEMM launches recorded in the timed region (ops.TIMER keys
+    """Split-bf16 GEMM launches recorded in the kernel-statistics pass (ops.TIMER keys
     'gemm_bf16x3:MxNxK:<a_kc><b_kc>'): the shape with the largest total device time, its mean
     launch time, fp32-matmul TFLOP/s (2MNK / time) and algorithmic bytes (fp32 A, B in, C out),
     plus the aggregate over every GEMM launch of the step."""
@@ -183,7 +191,7 @@ def cpu_baseline(budget_s, B=2048):
         threadpool_limits, threadpool_info = None, None
     from oracle import rqvae as R
     import gen_inputs as gi  # tests/golden (seeded synthetic inputs)
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = cpu_threads()
     ctx = threadpool_limits(limits=threads) if threadpool_limits else None
     try:
         D, K, L, inp, hid = CFG["D"], CFG["K"], CFG["L"], CFG["input_dim"], CFG["hidden"]
@@ -206,7 +214,7 @@ def cpu_baseline(budget_s, B=2048):
     finally:
         if ctx is not None:
             ctx.__exit__(None, None, None)
-    return dict(value=round(n * B / dt, 1), unit="items/s", cores=threads, kind="port",
+    return dict(value=round(n * B / dt, 1), unit="items/s", cores=threads, kind="port", cpu_model=cpu_model(),
                 sample=f"{n} numpy-oracle RqVae train steps (fwd+bwd+AdamW) at B={B}, ML-32M dims, "
                        f"{dt:.1f} s on {threads} host threads")
 
@@ -224,7 +232,8 @@ def main():
         from rqvae_hip import gemm_tuning
         gemm_tuning.enable()
     if args.decoder_only:
-        print(json.dumps({"decoder_amazon": measure_decoder(torch.device("cuda", lr), ws, rk)}), flush=True)
+        print(json.dumps({"decoder_amazon": measure_decoder(torch.device("cuda", lr), ws, rk, graphs=not args.no_graph,
+                                                            stats=False)}), flush=True)
         return
     device = torch.device("cuda", lr)
     torch.cuda.set_device(device)
@@ -260,22 +269,26 @@ def main():
     for _ in range(args.warmup):
         step()
     sync_all()
-    ops.TIMER.reset()
-    ops.TIMER.enabled = True
-    t0 = time.perf_counter()
+    t0 = time.perf_counter()            # timed region: no kernel events (they are taken in a separate pass)
     for _ in range(args.steps):
         last = step()
     sync_all()
     elapsed = time.perf_counter() - t0
-    ops.TIMER.enabled = False
     if ws > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
-    q_ms, q_n = ops.TIMER.mean_ms("rq_quantize_fwd")
-    gemm = gemm_launch_stats(ops.TIMER, args.steps)
     loss = float(last.loss.detach())
     del last
+    # kernel statistics from an untimed pass of the same step (HIP events on the launching stream)
+    ops.TIMER.reset()
+    ops.TIMER.enabled = True
+    for _ in range(5):
+        step()
+    sync_all()
+    ops.TIMER.enabled = False
+    q_ms, q_n = ops.TIMER.mean_ms("rq_quantize_fwd")
+    gemm = gemm_launch_stats(ops.TIMER, 5)
     exact = None
     if not args.no_extras and ws == 1 and torch.get_float32_matmul_precision() != "highest":
         # the same step with exact-fp32 matmuls ('highest': library fp32 GEMMs + split-K wgrad kernel)
@@ -288,7 +301,18 @@ def main():
         exact = {"ms_per_step": round(dt / 10 * 1e3, 3), "items_per_s": round(B * 10 / dt, 1)}
 
     # decoder-train tokens/s (BASELINE metric, second half): data parallel over the same ranks
-    dec = None if args.no_decoder else measure_decoder(device, ws, rk)
+    dec = dec_dm = None
+    if not args.no_decoder:
+        dec = measure_decoder(device, ws, rk, DEC, graphs=not args.no_graph,
+                              cpu_seconds=0.0 if args.no_cpu_baseline else 8.0)
+        if ws == 1 and not args.no_extras and not args.no_graph:
+            eager = measure_decoder(device, ws, rk, DEC, steps=10, warmup=3, graphs=False, stats=False)
+            dec["eager_ms_per_step"] = eager["ms_per_step"]
+        if not args.no_dm:
+            dec_dm = {}
+            for b in (8, 64):   # the config's global 64 split over 8 ranks, and 64 per rank (throughput)
+                dec_dm[f"per_gpu_batch_{b}"] = measure_decoder(device, ws, rk, DEC_DM, B=b, steps=10, warmup=3,
+                                                               graphs=not args.no_graph, stats=(b == 64))
     extras = {}
     if not args.no_extras and rk == 0 and ws == 1:
         extras = measure_extras(model, device, pool[0])
@@ -359,6 +383,8 @@ def main():
         line["exact_fp32_highest"] = exact
     if dec is not None:
         line["decoder_amazon"] = dec
+    if dec_dm is not None:
+        line["decoder_ml32m"] = dec_dm
     line.update(extras)
     if not args.no_cpu_baseline and ws == 1:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -442,36 +468,129 @@ def measure_quantize_synthetic(device, B=16384, D=1024, K=2048, L=4):
             "achieved_TFLOPs": round(tf, 2), "frac_fp32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
-DEC = dict(B=256, max_items=20, E=128, A=512, H=8, layers=8, K=256, sem_id_dim=4, dropout=0.3, lr=3e-4, wd=0.035)
+# decoder configs: configs[2] (decoder_amazon.gin) and configs[3] (decoder_ml32m.gin; its lr / wd are
+# train_decoder.train's defaults, its dropout the default dropout_p 0.1 — the gin's attn_dropout binds
+# nothing, SURVEY A-8)
+DEC = dict(name="amazon", B=256, max_items=20, E=128, A=512, H=8, layers=8, F=1024, K=256, sem_id_dim=4, dropout=0.3,
+           lr=3e-4, wd=0.035)
+DEC_DM = dict(name="ml32m", B=64, max_items=200, E=128, A=384, H=6, layers=8, F=1024, K=256, sem_id_dim=4,
+              dropout=0.1, lr=1e-3, wd=0.01)
 
 
-def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
-    """BASELINE configs[2] (decoder_amazon.gin dims, dropout 0.3), data parallel over the ranks: each
-    rank trains on its own synthetic tokenized batches (n_items ~ U{2..20}, 256 sequences per rank,
-    weak scaling), gradients all-reduced by GradBuckets (RCCL), fused AdamW. HIP jagged conversion,
-    varlen attention and fused dropout kernels. Tokens/s = context tokens of all ranks / max time."""
-    from rqvae_hip import dp, ops
+def decoder_flops(cfg, ctx_lens):
+    """Algorithmic FLOPs of one decoder train step (step = 3 x forward) for a batch with
+    context lengths `ctx_lens` (tokens incl. the user token): (dense projections / MLPs / output
+    layer, attention score + value products)."""
+    E, A, F, K = cfg["E"], cfg["A"], cfg["F"], cfg["K"]
+    Le = Ld = cfg["layers"] // 2
+    nf = cfg["sem_id_dim"] + 1                        # bos + the L+1 future sem-id tokens
+    n = np.asarray(ctx_lens, np.float64)
+    B = len(n)
+    dense = n.sum() * (2 * E * A + Le * (8 * A * A + 4 * A * F) + Ld * 4 * A * A) + \
+        B * nf * (2 * E * A + Ld * (12 * A * A + 4 * A * F) + 2 * A * K)
+    attn = Le * 4 * A * (n * n).sum() + Ld * 4 * A * nf * n.sum() + Ld * 4 * A * nf * nf * B
+    return 3.0 * dense, 3.0 * attn
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """Threads for the CPU baselines: the process's affinity cores, capped at the one-GPU box's CPU
+    share (16; os.cpu_count() there reports the whole host)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def decoder_cpu_baseline(cfg, budget_s, B=16, seed=60):
+    """The pinned CPU restatement of the decoder train step (oracle/decoder.py: eager torch on the
+    host, forward + autograd backward + torch AdamW) on a bounded subset of `B` sequences of the
+    same config, same length law; context tokens / s."""
+    from oracle import decoder as Dm
+    from modules.model import EncoderDecoderRetrievalModel
+    th = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(th)
+    try:
+        import gen_inputs as gi
+        m = EncoderDecoderRetrievalModel(embedding_dim=cfg["E"], attn_dim=cfg["A"], dropout=cfg["dropout"],
+                                         num_heads=cfg["H"], n_layers=cfg["layers"], num_embeddings=cfg["K"],
+                                         sem_id_dim=cfg["sem_id_dim"], inference_verifier_fn=None,
+                                         max_pos=cfg["max_items"] * cfg["sem_id_dim"])
+        P = {n: torch.from_numpy(gi.named_param(n, p.shape, seed)).requires_grad_(True) for n, p in m.named_parameters()}
+        del m
+        opt = torch.optim.AdamW(list(P.values()), lr=cfg["lr"], weight_decay=cfg["wd"])
+        from data.processed import synthetic_tokenized_batch
+        b = synthetic_tokenized_batch(B, cfg["max_items"], cfg["sem_id_dim"], cfg["K"], seed, torch.device("cpu"))
+        batch = dict(b._asdict())
+        toks = int(b.seq_mask.sum()) + B
+
+        def step():
+            opt.zero_grad()
+            loss, _, _ = Dm.decoder_forward(P, batch, cfg["K"], cfg["sem_id_dim"], cfg["H"], cfg["layers"],
+                                            dropout=cfg["dropout"])
+            loss.backward()
+            opt.step()
+        step()
+        n, t0 = 0, time.perf_counter()
+        while True:
+            step()
+            n += 1
+            if time.perf_counter() - t0 >= budget_s or n >= 50:
+                break
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return dict(value=round(n * toks / dt, 1), unit="ctx_tokens/s", cores=th, kind="port", cpu_model=cpu_model(),
+                sample=f"{n} oracle decoder train steps (oracle/decoder.py: torch-CPU fwd + bwd + AdamW) on {B} "
+                       f"sequences ({toks} ctx tokens/step) of the {cfg['name']} config, {dt:.1f} s, {th} threads")
+
+
+def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, graphs=True, stats=True,
+                    cpu_seconds=0.0):
+    """Decoder train steps/s and context tokens/s, data parallel over the ranks: each rank trains on
+    its own synthetic tokenized batches (n_items ~ U{2..max_items}, B sequences per rank, weak
+    scaling), gradients all-reduced by GradBuckets (RCCL), HIP AdamW. `graphs`: forward + backward
+    replayed from one hipGraph per context row bucket (rqvae_hip.graph.GraphedSteps); else eager.
+    Tokens/s = context tokens of all ranks / max time. `stats`: an untimed eager pass with kernel
+    events on the jagged and attention launches (their own throughput / roofline fractions)."""
+    from rqvae_hip import dp, gemm_tuning, ops
+    from rqvae_hip.graph import GraphedSteps
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel
+    from ops.jagged import copy_row_counts
+    B = B or cfg["B"]
     torch.manual_seed(3)
-    m = EncoderDecoderRetrievalModel(embedding_dim=DEC["E"], attn_dim=DEC["A"], dropout=DEC["dropout"],
-                                     num_heads=DEC["H"], n_layers=DEC["layers"], num_embeddings=DEC["K"],
-                                     sem_id_dim=DEC["sem_id_dim"], inference_verifier_fn=None,
-                                     max_pos=DEC["max_items"] * DEC["sem_id_dim"]).to(device).train()
-    buckets = dp.GradBuckets(m.parameters())
+    m = EncoderDecoderRetrievalModel(embedding_dim=cfg["E"], attn_dim=cfg["A"], dropout=cfg["dropout"],
+                                     num_heads=cfg["H"], n_layers=cfg["layers"], num_embeddings=cfg["K"],
+                                     sem_id_dim=cfg["sem_id_dim"], inference_verifier_fn=None,
+                                     max_pos=cfg["max_items"] * cfg["sem_id_dim"]).to(device).train()
+    buckets = dp.GradBuckets(m.parameters(), overlap=not graphs, flat_views=graphs)
     buckets.broadcast_params()
-    opt = make_adamw(m.parameters(), DEC["lr"], DEC["wd"])
-    batches = [synthetic_tokenized_batch(DEC["B"], DEC["max_items"], DEC["sem_id_dim"], DEC["K"], 50 + 97 * rk + i,
-                                         device) for i in range(4)]
-    ctx_tokens = [int(b.seq_mask.sum()) + DEC["B"] for b in batches]
+    opt = make_adamw(m.parameters(), cfg["lr"], cfg["wd"])
+    batches = [synthetic_tokenized_batch(B, cfg["max_items"], cfg["sem_id_dim"], cfg["K"], 50 + 97 * rk + i, device)
+               for i in range(4)]
+    ctx_lens = [(b.seq_mask.sum(1) + 1).cpu().tolist() for b in batches]   # host copies, before timing
+    ctx_tokens = [int(sum(c)) for c in ctx_lens]
+    bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
+    gs = GraphedSteps(lambda b: m(b).loss, lambda b: m.context_rows(b, bucket), buckets,
+                      prepare=lambda static, b: copy_row_counts(static.seq_mask, b.seq_mask)) if graphs else None
     it = [0]
 
     def step():
         b = batches[it[0] % len(batches)]
         it[0] += 1
-        buckets.zero_grad()
-        o = m(b)
-        o.loss.backward()
+        if gs is not None:
+            gs(b)
+        else:
+            buckets.zero_grad()
+            m(b).loss.backward()
         buckets.synchronize()
         opt.step()
 
@@ -483,31 +602,84 @@ def measure_decoder(device, ws=1, rk=0, steps=20, warmup=5):
     for _ in range(warmup):
         step()
     sync_all()
-    ops.TIMER.reset()
-    ops.TIMER.only = {"jagged_"}   # the decoder step is host-bound: time only the jagged kernels it reports
-    ops.TIMER.enabled = True
     it[0] = 0
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     sync_all()
     dt = time.perf_counter() - t0
-    ops.TIMER.enabled = False
-    ops.TIMER.only = None
     toks = sum(ctx_tokens[i % len(batches)] for i in range(steps))
-    tot = torch.tensor([dt, float(toks)], device=device, dtype=torch.float64)
+    dense = attn = 0.0
+    for i in range(steps):
+        d_, a_ = decoder_flops(cfg, ctx_lens[i % len(batches)])
+        dense, attn = dense + d_, attn + a_
+    tot = torch.tensor([dt, float(toks), dense, attn], device=device, dtype=torch.float64)
     if ws > 1:
         mx = tot[:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dt, toks = float(mx), float(tot[1])
-    fut = ws * steps * DEC["B"] * (DEC["sem_id_dim"] + 1)
-    return {"ctx_tokens_per_s": round(toks / dt, 1), "ctx_plus_fut_tokens_per_s": round((toks + fut) / dt, 1),
-            "ms_per_step": round(dt / steps * 1e3, 3), "per_gpu_batch": DEC["B"], "n_gpus": ws,
-            "parallelism": f"dp{ws}", "scaling": "weak",
-            "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
-            "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
-            "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}
+        dt, toks, dense, attn = float(mx), float(tot[1]), float(tot[2]), float(tot[3])
+    ms = dt / steps * 1e3
+    fut = ws * steps * B * (cfg["sem_id_dim"] + 1)
+    # roofline: dense matmuls on the split-bf16 GEMM (ceiling bf16 peak / 3), attention on fp32 MFMA
+    gemm_peak, attn_peak = BF16_MFMA_PEAK_TFLOPS / 3, FP32_MFMA_PEAK_TFLOPS
+    t_min = (dense / (gemm_peak * 1e12) + attn / (attn_peak * 1e12)) / ws
+    out = {"config": f"decoder_{cfg['name']} (A={cfg['A']}, H={cfg['H']}, {cfg['layers']} layers, max "
+                     f"{cfg['max_items']} items -> ctx <= {cfg['max_items'] * cfg['sem_id_dim'] + 1})",
+           "ctx_tokens_per_s": round(toks / dt, 1), "ctx_plus_fut_tokens_per_s": round((toks + fut) / dt, 1),
+           "ms_per_step": round(ms, 3), "per_gpu_batch": B, "n_gpus": ws, "parallelism": f"dp{ws}",
+           "scaling": "weak", "step_mode": "hipgraph per row bucket" if graphs else "eager",
+           "graphs_captured": len(gs.graphs) if gs is not None else 0,
+           "roofline": {"bound": "mfma", "achieved": round((dense + attn) / dt / 1e12, 2),
+                        "peak": round(gemm_peak, 1), "unit": "TFLOP/s",
+                        "frac": round((dense + attn) / dt / 1e12 / gemm_peak, 4),
+                        "frac_of_step_roofline": round(t_min / dt, 4) if dt > 0 else None,
+                        "flops_per_step_per_gpu": round((dense + attn) / steps / ws),
+                        "attention_flops_share": round(attn / (dense + attn), 4),
+                        "note": "algorithmic FLOPs (SURVEY 8d, step = 3 x forward); peak = split-bf16 GEMM ceiling "
+                                "(2.5 PF / 3); frac_of_step_roofline = (dense / 833 TF + attention / 157.3 TF) / step time"}}
+    if stats and rk == 0:
+        out["kernels"] = decoder_kernel_stats(m, buckets, batches[0], ctx_lens[0], cfg)
+    if cpu_seconds > 0 and rk == 0 and ws == 1:
+        out["cpu_baseline"] = decoder_cpu_baseline(cfg, cpu_seconds)
+    return out
+
+
+def decoder_kernel_stats(m, buckets, batch, ctx_lens, cfg, reps=3):
+    """Untimed eager passes with HIP events on the attention and jagged launches of one step: device
+    time per step, TFLOP/s vs the fp32 MFMA peak (attention: algorithmic 4 A n^2-type products, the
+    backward counted as 2 x forward) and GB/s of the jagged conversions."""
+    from rqvae_hip import ops
+    n = np.asarray(ctx_lens, np.float64)
+    A, nf, Le, Ld, Bn = cfg["A"], cfg["sem_id_dim"] + 1, cfg["layers"] // 2, cfg["layers"] // 2, len(ctx_lens)
+    attn_fwd = Le * 4 * A * (n * n).sum() + Ld * 4 * A * nf * n.sum() + Ld * 4 * A * nf * nf * Bn
+    for _ in range(2):
+        buckets.zero_grad()
+        m(batch).loss.backward()
+    torch.cuda.synchronize()
+    ops.TIMER.reset()
+    ops.TIMER.only = {"jagged_", "varlen_attn"}
+    ops.TIMER.enabled = True
+    for _ in range(reps):
+        buckets.zero_grad()
+        m(batch).loss.backward()
+    torch.cuda.synchronize()
+    ops.TIMER.enabled = False
+    ops.TIMER.only = None
+    fwd_ms, nf_ = ops.TIMER.mean_ms("varlen_attn_fwd")
+    bwd_ms, nb_ = ops.TIMER.mean_ms("varlen_attn_bwd")
+    f_step, b_step = fwd_ms * nf_ / reps, bwd_ms * nb_ / reps
+    res = {"attention": {"launches_per_step": {"fwd": nf_ // reps, "bwd": nb_ // reps},
+                         "fwd_ms_per_step": round(f_step, 4), "bwd_ms_per_step": round(b_step, 4),
+                         "fwd_TFLOPs": round(attn_fwd / (f_step * 1e-3) / 1e12, 2),
+                         "bwd_TFLOPs": round(2 * attn_fwd / (b_step * 1e-3) / 1e12, 2),
+                         "frac_fp32_peak": round(3 * attn_fwd / ((f_step + b_step) * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "note": "algorithmic attention FLOPs per step (fwd 4 A sum_b n_q n_k over the 12 "
+                                 "calls; bwd = 2 x fwd) / device time of the varlen_attn launches"},
+           "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
+           "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
+           "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}
+    return res
 
 
 if __name__ == "__main__":

@@ -117,6 +117,15 @@ int rq_silu_dropout_bwd(const float* g, const float* z, int64_t n, float p, uint
 int rq_dropout_add_fwd(const float* h, const float* y, int64_t n, float p, uint64_t seed, float* out, void* stream);
 int rq_dropout_bwd(const float* g, int64_t n, float p, uint64_t seed, float* gy, void* stream);
 
+/* Dropout epoch: a device-side word mixed into every mask key of the functions above and of
+ * rq_gemm_bf16x3_ex (key = seed + epoch * C). 0 by default (keys = the host seeds). A train step
+ * captured into a hipGraph ends with rq_seed_epoch_advance, so every replay draws fresh masks while
+ * the forward and backward of one step share the epoch (replaces the per-step host RNG state that
+ * torch.compile's cudagraphs trees manage for the reference's nn.Dropout, modules/model.py:247).
+ * Both are stream-ordered kernel launches (capturable). */
+int rq_seed_epoch_advance(void* stream);
+int rq_seed_epoch_set(uint64_t value, void* stream);
+
 /* Weight / bias gradient of a Linear layer over a large batch: dW (O,I) = g^T x, db (O,) = sum_b g
  * (or NULL). g: (Bn, O) rows of stride ldg, x: (Bn, I) rows of stride ldx, fp32, O, I, ld % 4 == 0,
  * 16-byte aligned. Replaces torch autograd's grad_weight = grad_out^T @ input for the nn.Linear
@@ -188,11 +197,16 @@ int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out,
  * jagged_offsets: offsets (B+1) int64 = [0, cumsum(clamp(lengths, 0, N))]   (jagged.py:30-33)
  * jagged_from_padded: values[offsets[b]+t] = x[b,t] (+1-1 rounding when add_one_sub_one, as
  *   `target + 1 - 1` at jagged.py:65), x (B,N,D) contiguous            (jagged.py:11-66,92-125)
+ * jagged_from_padded_rows: the same into a values buffer of alloc_rows (>= offsets[B]) rows whose tail
+ *   rows [offsets[B], alloc_rows) are zero-filled on the device (a row-bucketed allocation: the
+ *   caller never needs the valid total on the host, so the call is graph-capturable per bucket)
  * jagged_to_padded: x = zeros(B,N,D); x[b,t] = values[offsets[b]+t] for t < len_b (jagged.py:69-77)
- * B <= 65535 per call. */
+ * B < 65535 per call. */
 int jagged_offsets(const int64_t* lengths, int64_t B, int64_t N, int64_t* offsets, void* stream);
 int jagged_from_padded(const void* x, int64_t B, int64_t N, int64_t D, const int64_t* offsets, void* values, int dtype,
                        int add_one_sub_one, void* stream);
+int jagged_from_padded_rows(const void* x, int64_t B, int64_t N, int64_t D, const int64_t* offsets, void* values,
+                            int64_t alloc_rows, int dtype, int add_one_sub_one, void* stream);
 int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int64_t N, int64_t D, void* x, int dtype,
                      void* stream);
 
@@ -201,16 +215,18 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
  *   q[t][h][d] at q + t*sq + h*hd + d (likewise k, v, out, dout, dq, dk, dv with their strides);
  *   cu_q, cu_k (B+1) int64 offsets; max_q / max_k >= the longest segment (grid bound);
  *   lse (H, Tq) fp32 log-sum-exp per query (written by fwd, read by bwd). hd in {16, 32, 64, 128}.
+ *   Tq / Tk: ALLOCATED rows of the q-side / kv-side buffers (>= cu_q[B] / cu_k[B]); rows past the
+ *   last sequence get zero out / dq / dk / dv (written by the kernels: graph-capturable per bucket).
  * Backward is deterministic (no atomics): dq per query block (also writes delta (H, Tq) = rowsum(dO*O),
- * caller-provided scratch), then dk/dv per key block. */
+ * caller-provided scratch), then dk/dv per key block. B < 65535. */
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream);
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
-                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, float* delta,
-                    void* stream);
+                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
+                    float* delta, void* stream);
 
 /* AdamW step (torch.optim.AdamW as stepped by train_rqvae.py:168-172 / train_decoder.py:203) over
  * every fp32 parameter of a group, one launch per 64 tensors. segs: HOST array of nseg records of 5

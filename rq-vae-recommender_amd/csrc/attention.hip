@@ -1,4 +1,4 @@
-// Varlen (jagged) multi-head attention, forward + backward, fp32 on v_mfma_f32_32x32x2_f32.
+// Varlen (jagged) multi-head attention, forward + backward, exact fp32 on v_mfma_f32_16x16x4_f32.
 //
 // Reference: modules/transformer/attention.py:113-124 (Attend.jagged_forward) —
 // F.scaled_dot_product_attention on NJT q/k/v (B, H, j, hd), dropout 0 (:177), scale
@@ -8,320 +8,598 @@
 //
 // Layout: packed token-major rows. q[t][h][d] at q + t*sq + h*HD + d (sq = row stride, so the
 // (T, 3A) qkv projection is consumed in place); cu_q / cu_k int64 (B+1) NJT offsets;
-// out (Tq, H*HD) rows with stride so; lse (H, Tq) = m + log(l) per query (saved for bwd).
+// out (Tq, H*HD) rows with stride so; lse (H, Tq) = m + log(l) per query (natural log, saved
+// for the backward). Tq / Tk are the ALLOCATED row counts of the q-side / kv-side buffers: rows
+// past cu_q[B] / cu_k[B] (a row-bucketed tail) get zero outputs and zero gradients, written by an
+// extra grid slice, so no host-side valid row count is needed (graph-capturable).
 //
-// Orientation trick: every score tile is computed TRANSPOSED (keys on the MFMA row axis,
-// queries on lanes) in the forward and dQ passes, so a query's running max / sum / output
-// live in ONE lane pair (lane j and j+32) — the online softmax needs a single lane swap per
-// tile, no LDS round trip. The dK/dV pass puts keys on lanes the same way. P / dS feed the
-// next MFMA straight from the accumulator registers (register t of the 32x32 tile is the
-// k-slice of MFMA step t with key index (t&3)+8(t>>2)+4*(lane>>5)).
+// Tiling (CDNA4, wave64). The unit is a 16 x 16 tile of the 16x16x4 fp32 MFMA, so a ragged
+// sequence pads to a multiple of 16 rows (not 32): at the decoder's Amazon contexts
+// (4*U{2..20}+1 <= 81 tokens, mean ~45) 73 % of the MFMA work is useful instead of 56 %.
+// Each wave owns 16 query rows (forward / dQ) or 16 key rows (dK/dV) for one (sequence, head);
+// a workgroup of NW waves shares 32- or 64-row K/V (or Q/dO) chunks staged through LDS (row stride
+// HD+4 floats: conflict-free 16-B row reads and 4-B column reads). The wave's own 16 rows stay
+// in registers as the MFMA B operand for the whole key (query) loop.
+//
+// Orientation: score tiles are computed TRANSPOSED in the forward and dQ passes (S^T = K Q^T:
+// keys on the accumulator rows, queries on the lanes), so each lane's 4 accumulator registers
+// are 4 keys of ONE query and P^T / dS^T feed the next MFMA (O^T += V^T P^T, dQ^T += K^T dS^T)
+// straight from the accumulators (key order 4*(lane>>4)+i matches the B operand k index). The
+// dK/dV pass computes S = Q K^T (queries on rows, keys on lanes) for the same reason. A query's
+// running max needs a 4-lane reduction per staged key chunk (not per tile); its running sum stays
+// per lane until the end. exp via v_exp_f32 on log2e-prescaled scores.
 // Backward = two launches (dQ per query block, which also stores delta = rowsum(dO*O); then
-// dK,dV per key block) with recomputed P: no atomics, bitwise deterministic.
+// dK, dV per key block) with recomputed P: no atomics, bitwise deterministic.
 #include "common.h"
 
 #include <math.h>
 
-#ifndef RQ_ATTN_ONE_WAVE_MAX
-#define RQ_ATTN_ONE_WAVE_MAX 96   // longest sequence served by one-wave workgroups
+#include <algorithm>
+
+// Build switches (A/B-measured on MI355X, tools/attn_ab.sh, profiles/r02/attn_ab.txt): register
+// prefetch of the next staged chunk (off: +33-64 VGPRs cost more occupancy than the overlap gains),
+// and the number of 16-row tiles whose S / dP chains the backward passes interleave (2: 4 would
+// drop the dK/dV pass to one wave per SIMD). The Makefile builds this file with
+// -mllvm -amdgpu-mfma-vgpr-form (accumulators in VGPRs: no accvgpr moves around the softmax).
+#ifndef RQ_ATTN_PREFETCH
+#define RQ_ATTN_PREFETCH 0
+#endif
+#ifndef RQ_ATTN_BWD_GROUP
+#define RQ_ATTN_BWD_GROUP 2
 #endif
 
 namespace rqhip {
 
-__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Head dims below 32 use 32-wide LDS rows / output tiles whose extra columns stay zero.
-template <int HD>
-struct Pad {
-  static constexpr int P = HD < 32 ? 32 : HD;   // padded width
-  static constexpr int LD = P + 4;              // LDS row stride (floats)
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+// rows of K/V (or Q/dO) staged per LDS round: 64 for 4-wave workgroups, 32 for narrower ones (LDS per
+// workgroup 2 x CH x (HD+4) x 4 B: 34.8 KB / 17.4 KB at HD = 64, i.e. 4 / 9 workgroups per CU)
+template <int NW>
+struct Chunk {
+  static constexpr int CH = NW >= 4 ? 64 : 32;
+  static constexpr int T = CH / 16;   // 16-row tiles per chunk
 };
 
-// Zero the padding columns [HD, P) of a [32][LD] LDS image once per kernel.
-template <int HD, int NT>
-__device__ __forceinline__ void zero_pad32(float* dst, int tid) {
-  constexpr int P = Pad<HD>::P, LD = Pad<HD>::LD;
-  if constexpr (P > HD) {
-    for (int f = tid; f < 32 * (P - HD); f += NT) dst[(f / (P - HD)) * LD + HD + f % (P - HD)] = 0.f;
-  }
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int HD>
-__device__ __forceinline__ void load_half_row(const float* p, bool valid, float (&f)[HD / 2]) {
+// Register-staged chunk copy: CH rows x HD floats of a strided row source, global -> registers
+// (load) and registers -> LDS [CH][HD+4] (store), so the NEXT chunk's global loads are in flight
+// while the current chunk is multiplied. Rows >= n are zero.
+template <int HD, int NT, int CH>
+struct RowStage {
+  static constexpr int F4 = HD / 4, PER = (CH * F4 + NT - 1) / NT;
+  float4 r[PER];
+  __device__ __forceinline__ void load(const float* __restrict__ src, int64_t stride, int row0, int n, int tid) {
 #pragma unroll
-  for (int s = 0; s < HD / 2; s += 4) {
-    float4 v = valid ? *reinterpret_cast<const float4*>(p + s) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < PER; ++i) {
+      const int f = tid + i * NT;
+      const int row = f / F4, c = (f % F4) * 4;
+      r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < CH * F4 && row0 + row < n) r[i] = *reinterpret_cast<const float4*>(src + (int64_t)(row0 + row) * stride + c);
+    }
+  }
+  __device__ __forceinline__ void store(float* dst, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int f = tid + i * NT;
+      if (f < CH * F4) *reinterpret_cast<float4*>(dst + (f / F4) * (HD + 4) + (f % F4) * 4) = r[i];
+    }
+  }
+};
+
+// This lane's HD/4 consecutive elements of a row (lane group g = lane >> 4 holds d in [g*HD/4, (g+1)*HD/4)).
+template <int HD>
+__device__ __forceinline__ void load_frag(const float* p, bool valid, float (&f)[HD / 4]) {
+#pragma unroll
+  for (int s = 0; s < HD / 4; s += 4) {
+    const float4 v = valid ? *reinterpret_cast<const float4*>(p + s) : make_float4(0.f, 0.f, 0.f, 0.f);
     f[s] = v.x; f[s + 1] = v.y; f[s + 2] = v.z; f[s + 3] = v.w;
   }
 }
 
-// Stage 32 rows x HD of a strided row source into LDS [32][HD+4]; rows >= n are zero.
-template <int HD, int NT>
-__device__ __forceinline__ void stage32(float* dst, const float* src, int64_t stride, int row0, int n, int tid) {
-  constexpr int F4 = HD / 4, LD = Pad<HD>::LD;
-  for (int f = tid; f < 32 * F4; f += NT) {
-    const int r = f / F4, c = (f % F4) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row0 + r < n) v = *reinterpret_cast<const float4*>(src + (int64_t)(row0 + r) * stride + c);
-    *reinterpret_cast<float4*>(dst + r * LD + c) = v;
+// acc[t][row = tile row (lane&15)][col = lane&15] += LDS rows (A operand: NTT consecutive 16-row tiles of a
+// row-major [.][HD+4] image) x frag (B operand: this lane's HD/4 elements of the shared dimension).
+// The NTT tile products are independent MFMA chains, interleaved so the 16x16x4's 40-cycle
+// dependent latency hides behind the other chains' 32-cycle issues.
+template <int HD, int NTT>
+__device__ __forceinline__ void tiles_x_frag(const float* rows, const float (&frag)[HD / 4], int lane, f32x4 (&acc)[NTT]) {
+  constexpr int LD = HD + 4;
+  const float* ap = rows + (lane & 15) * LD + (lane >> 4) * (HD / 4);
+#pragma unroll
+  for (int s = 0; s < HD / 4; s += 4) {
+    float4 a[NTT];
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) a[t] = *reinterpret_cast<const float4*>(ap + t * 16 * LD + s);
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) acc[t] = mfma4(a[t].x, frag[s], acc[t]);
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) acc[t] = mfma4(a[t].y, frag[s + 1], acc[t]);
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) acc[t] = mfma4(a[t].z, frag[s + 2], acc[t]);
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) acc[t] = mfma4(a[t].w, frag[s + 3], acc[t]);
   }
 }
 
-// acc += Mat[rows i][HD] (LDS, A operand, row = lane&31) x frag (B operand, registers)
-template <int HD>
-__device__ __forceinline__ floatx16 mfma_rows_x_frag(const float* Ms, const float (&frag)[HD / 2], int lane, floatx16 acc) {
-  const float* ap = Ms + (lane & 31) * Pad<HD>::LD + (lane >> 5) * (HD / 2);
+// Two such products over the same tiles (S and dP in the backward passes): 2 x NTT chains.
+template <int HD, int NTT>
+__device__ __forceinline__ void tiles_x_frag2(const float* rows_a, const float (&fa)[HD / 4], const float* rows_b,
+                                              const float (&fb)[HD / 4], int lane, f32x4 (&acc_a)[NTT],
+                                              f32x4 (&acc_b)[NTT]) {
+  constexpr int LD = HD + 4;
+  const int off = (lane & 15) * LD + (lane >> 4) * (HD / 4);
 #pragma unroll
-  for (int s = 0; s < HD / 2; s += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(ap + s);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, frag[s], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, frag[s + 1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, frag[s + 2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, frag[s + 3], acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-// acc[tile] (rows d, cols lane) += Ms^T[d][t-row] * w[t] over the 32 rows of Ms (LDS [32][LD]).
-template <int HD>
-__device__ __forceinline__ void mfma_colsT_x_regs(const float* Ms, const floatx16& w, int lane,
-                                                  floatx16 (&acc)[Pad<HD>::P / 32]) {
-  const int h = lane >> 5, c = lane & 31;
+  for (int s = 0; s < HD / 4; s += 4) {
+    float4 a[NTT], b[NTT];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const float* row = Ms + crow(t, h) * Pad<HD>::LD + c;
-#pragma unroll
-    for (int tl = 0; tl < Pad<HD>::P / 32; ++tl)
-      acc[tl] = __builtin_amdgcn_mfma_f32_32x32x2f32(row[tl * 32], w[t], acc[tl], 0, 0, 0);
-  }
-}
-
-// Write rows-d accumulators for one row (lane) as float4 runs: d = 32 tl + 8 g + 4 h + 0..3.
-template <int HD>
-__device__ __forceinline__ void store_dT(float* rowp, const floatx16 (&acc)[Pad<HD>::P / 32], float mul, int h) {
-#pragma unroll
-  for (int tl = 0; tl < Pad<HD>::P / 32; ++tl)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = tl * 32 + 8 * g + 4 * h;
-      if (d < HD)
-        *reinterpret_cast<float4*>(rowp + d) =
-            make_float4(acc[tl][4 * g] * mul, acc[tl][4 * g + 1] * mul, acc[tl][4 * g + 2] * mul, acc[tl][4 * g + 3] * mul);
+    for (int t = 0; t < NTT; ++t) {
+      a[t] = *reinterpret_cast<const float4*>(rows_a + off + t * 16 * LD + s);
+      b[t] = *reinterpret_cast<const float4*>(rows_b + off + t * 16 * LD + s);
     }
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) { acc_a[t] = mfma4(a[t].x, fa[s], acc_a[t]); acc_b[t] = mfma4(b[t].x, fb[s], acc_b[t]); }
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) { acc_a[t] = mfma4(a[t].y, fa[s + 1], acc_a[t]); acc_b[t] = mfma4(b[t].y, fb[s + 1], acc_b[t]); }
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) { acc_a[t] = mfma4(a[t].z, fa[s + 2], acc_a[t]); acc_b[t] = mfma4(b[t].z, fb[s + 2], acc_b[t]); }
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) { acc_a[t] = mfma4(a[t].w, fa[s + 3], acc_a[t]); acc_b[t] = mfma4(b[t].w, fb[s + 3], acc_b[t]); }
+  }
+}
+
+// acc[dt] (rows d = 16 dt + (lane&15) of the transposed product, cols = lane&15 of w) +=
+// M^T[d][t] * w[t] over the 16 rows t of the LDS tile M (row-major [.][HD+4]) whose order
+// 4*(lane>>4)+i matches the accumulator layout of w (register i).
+template <int HD>
+__device__ __forceinline__ void colsT_x_acc(const float* tile, const f32x4& w, int lane, f32x4 (&acc)[HD / 16]) {
+  const float* base = tile + 4 * (lane >> 4) * (HD + 4) + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma4(base[i * (HD + 4) + dt * 16], w[i], acc[dt]);
+  }
+}
+
+// Store the transposed accumulators of one row (this lane's column): d = 16 dt + 4 (lane>>4) + 0..3.
+template <int HD>
+__device__ __forceinline__ void store_rowT(float* rowp, const f32x4 (&acc)[HD / 16], float mul, int lane) {
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+    *reinterpret_cast<float4*>(rowp + dt * 16 + 4 * (lane >> 4)) =
+        make_float4(acc[dt][0] * mul, acc[dt][1] * mul, acc[dt][2] * mul, acc[dt][3] * mul);
+}
+
+// Zero rows [r0, r1) of one head's HD columns of a row-major buffer (grid-stride over the x extent):
+// the extra grid slice z == nseq clears a row-bucketed buffer's tail past the last sequence, so a
+// caller never needs the valid row count on the host (graph-capturable).
+template <int HD, int NT>
+__device__ __forceinline__ void zero_rows(float* base, int64_t stride, int64_t r0, int64_t r1, int hh, int tid) {
+  constexpr int F4 = HD / 4;
+  const int64_t n = (r1 - r0) * F4;
+  for (int64_t f = (int64_t)blockIdx.x * NT + tid; f < n; f += (int64_t)gridDim.x * NT)
+    *reinterpret_cast<float4*>(base + (r0 + f / F4) * stride + hh * HD + (f % F4) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Calls f.template run<NTT, MASK>() for a chunk of `nt` 16-row tiles: every tile unmasked when the
+// chunk is interior (all NTL tiles present, every row valid, no causal diagonal), else masked.
+template <int NTL, typename F>
+__device__ __forceinline__ void dispatch_tiles(int nt, bool interior, F& f) {
+  if (nt <= 0) return;
+  if (interior && nt == NTL) { f.template run<NTL, false>(); return; }
+  if (nt == 1) { f.template run<1, true>(); return; }
+  if constexpr (NTL >= 3) {
+    if (nt == 2) { f.template run<2, true>(); return; }
+    if (nt == 3) { f.template run<3, true>(); return; }
+  }
+  f.template run<NTL, true>();
 }
 
 // ---------------------------------------------------------------------------------------- fwd
+template <int HD>
+struct FwdChunk {
+  const float* K_s;
+  const float* V_s;
+  const float* qf;
+  int lane, kc, lk, qi, causal;
+  float sl2;
+  float* m;
+  float* l;
+  f32x4* o;
+  template <int NTT, bool MASK>
+  __device__ __forceinline__ void run() {
+    constexpr int LD = HD + 4;
+    const int g = lane >> 4;
+    f32x4 s[NTT];
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    tiles_x_frag<HD, NTT>(K_s, *reinterpret_cast<const float(*)[HD / 4]>(qf), lane, s);   // S^T: rows = keys
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NTT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (MASK) {
+          const int key = kc + t * 16 + 4 * g + i;
+          if (!(key < lk && (!causal || key <= qi))) s[t][i] = -INFINITY;
+        }
+        mt = fmaxf(mt, s[t][i]);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(*m, mt * sl2);         // running max in log2 units (sl2 > 0 keeps the order)
+    const bool none = MASK && mn == -INFINITY;    // every key so far masked (causal padding lanes)
+    const float alpha = none ? 1.f : exp2_fast(*m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[t][i] = none ? 0.f : exp2_fast(__builtin_fmaf(s[t][i], sl2, -mn));
+        ls += s[t][i];
+      }
+    *l = *l * alpha + ls;                         // per-lane partial sum (alpha is uniform per query)
+    *m = mn;
+    f32x4(&oa)[HD / 16] = *reinterpret_cast<f32x4(*)[HD / 16]>(o);
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) oa[dt] *= alpha;
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) colsT_x_acc<HD>(V_s + t * 16 * LD, s[t], lane, oa);   // O^T += V^T P^T
+  }
+};
+
 template <int HD, int NW>
 __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restrict__ q, int64_t sq, const float* __restrict__ k,
                                                         int64_t sk, const float* __restrict__ v, int64_t sv,
                                                         const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
                                                         int causal, float scale, float* __restrict__ out, int64_t so,
                                                         float* __restrict__ lse, int64_t Tq) {
-  constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
-  __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD];
+  constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
   float* K_s = smem;
-  float* V_s = smem + 32 * LD;
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  zero_pad32<HD, 64 * NW>(K_s, tid);
-  zero_pad32<HD, 64 * NW>(V_s, tid);
+  float* V_s = smem + CH * LD;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
+    zero_rows<HD, 64 * NW>(out, so, cu_q[b], Tq, hh, tid);
+    return;
+  }
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int qbase = blockIdx.x * 32 * NW;
-  if (qbase >= lq) return;
-  const int qi = qbase + wave * 32 + (lane & 31);
-  const bool qv = qi < lq;
-  float qf[HD / 2];
-  load_half_row<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + h * (HD / 2), qv, qf);
-  floatx16 o[NTL];
+  const int qwg = blockIdx.x * 16 * NW;
+  if (qwg >= lq) return;                      // uniform over the workgroup
+  const int qb = qwg + wave * 16, qi = qb + (lane & 15);
+  const bool wave_on = qb < lq, qv = qi < lq;
+  float qf[HD / 4];
+  load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+  f32x4 o[DT];
 #pragma unroll
-  for (int tl = 0; tl < NTL; ++tl)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[tl][r] = 0.f;
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
-  const int kend = causal ? min(lk, qbase + 32 * NW) : lk;
-  for (int kt = 0; kt < kend; kt += 32) {
-    __syncthreads();
-    stage32<HD, 64 * NW>(K_s, k + k0 * sk + hh * HD, sk, kt, lk, tid);
-    stage32<HD, 64 * NW>(V_s, v + k0 * sv + hh * HD, sv, kt, lk, tid);
-    __syncthreads();
-    floatx16 s;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = 0.f;
-    s = mfma_rows_x_frag<HD>(K_s, qf, lane, s);   // S^T: rows = keys, cols = queries
-    float mt = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kt + crow(r, h);
-      const bool ok = key < lk && (!causal || key <= qi);
-      s[r] = ok ? s[r] * scale : -INFINITY;
-      mt = fmaxf(mt, s[r]);
-    }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = (mn == -INFINITY) ? 1.f : expf(m - mn);
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[r] = (s[r] == -INFINITY) ? 0.f : expf(s[r] - mn);
-      ls += s[r];
-    }
-    ls += __shfl_xor(ls, 32, 64);
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int tl = 0; tl < NTL; ++tl)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[tl][r] *= alpha;
-    mfma_colsT_x_regs<HD>(V_s, s, lane, o);        // O^T += V^T P^T
+  const int kend = causal ? min(lk, qwg + 16 * NW) : lk;   // workgroup's last key (staging loop)
+  const int kend_w = causal ? min(lk, qb + 16) : lk;        // this wave's last key
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  RowStage<HD, 64 * NW, CH> stk, stv;
+  if (RQ_ATTN_PREFETCH && kend > 0) {
+    stk.load(kb_, sk, 0, lk, tid);
+    stv.load(vb_, sv, 0, lk, tid);
   }
+  FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, lk, qi, causal, scale * kLog2e, &m, &l, o};
+  for (int kc = 0; kc < kend; kc += CH) {
+    if (!RQ_ATTN_PREFETCH) {
+      stk.load(kb_, sk, kc, lk, tid);
+      stv.load(vb_, sv, kc, lk, tid);
+    }
+    __syncthreads();                          // the previous chunk's LDS reads are done
+    stk.store(K_s, tid);
+    stv.store(V_s, tid);
+    __syncthreads();
+    if (RQ_ATTN_PREFETCH && kc + CH < kend) {   // next chunk's loads fly while this one is multiplied
+      stk.load(kb_, sk, kc + CH, lk, tid);
+      stv.load(vb_, sv, kc + CH, lk, tid);
+    }
+    const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend_w - kc + 15) >> 4) : 0);
+    fc.kc = kc;
+    dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fc);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
   if (!qv) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  store_dT<HD>(out + (q0 + qi) * so + hh * HD, o, inv, h);
-  if (h == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? m + logf(l) : 0.f;
-}
-
-// ------------------------------------------------------------------------------- bwd: dK, dV
-template <int HD, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
-    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
-    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
-    const float* __restrict__ lse, const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q,
-    const int64_t* __restrict__ cu_k, int causal, float scale, float* __restrict__ dk, int64_t sdk,
-    float* __restrict__ dv, int64_t sdv) {
-  constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
-  __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD + 64];
-  float* Q_s = smem;
-  float* O_s = smem + 32 * LD;   // dO tile
-  float* lse_s = O_s + 32 * LD;
-  float* dl_s = lse_s + 32;
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  zero_pad32<HD, 64 * NW>(Q_s, tid);
-  zero_pad32<HD, 64 * NW>(O_s, tid);
-  const int64_t q0 = cu_q[b], k0 = cu_k[b];
-  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int kbase = blockIdx.x * 32 * NW;
-  if (kbase >= lk) return;
-  const int kj = kbase + wave * 32 + (lane & 31);
-  const bool kv = kj < lk;
-  float kf[HD / 2], vf[HD / 2];
-  load_half_row<HD>(k + (k0 + (kv ? kj : 0)) * sk + hh * HD + h * (HD / 2), kv, kf);
-  load_half_row<HD>(v + (k0 + (kv ? kj : 0)) * sv + hh * HD + h * (HD / 2), kv, vf);
-  floatx16 dka[NTL], dva[NTL];
-#pragma unroll
-  for (int tl = 0; tl < NTL; ++tl)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dka[tl][r] = 0.f; dva[tl][r] = 0.f; }
-  const int qstart = causal ? (kbase / 32) * 32 : 0;
-  for (int qt = qstart; qt < lq; qt += 32) {
-    __syncthreads();
-    stage32<HD, 64 * NW>(Q_s, q + q0 * sq + hh * HD, sq, qt, lq, tid);
-    stage32<HD, 64 * NW>(O_s, dout + q0 * sdo + hh * HD, sdo, qt, lq, tid);
-    if (tid < 32) {   // delta_q = sum_d dO*O (written by the dQ pass) and lse for the 32 queries
-      const int qq = qt + tid;
-      const bool ok = qq < lq;
-      dl_s[tid] = ok ? delta[(int64_t)hh * Tq + q0 + qq] : 0.f;
-      lse_s[tid] = ok ? lse[(int64_t)hh * Tq + q0 + qq] : 0.f;
-    }
-    __syncthreads();
-    floatx16 s, dp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-    s = mfma_rows_x_frag<HD>(Q_s, kf, lane, s);    // S: rows = queries, cols = keys
-    dp = mfma_rows_x_frag<HD>(O_s, vf, lane, dp);  // dP = dO V^T
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qr = crow(r, h), qq = qt + qr;
-      const bool ok = kv && qq < lq && (!causal || kj <= qq);
-      const float p = ok ? expf(s[r] * scale - lse_s[qr]) : 0.f;
-      s[r] = p;
-      dp[r] = p * (dp[r] - dl_s[qr]);
-    }
-    mfma_colsT_x_regs<HD>(O_s, s, lane, dva);   // dV^T += dO^T P
-    mfma_colsT_x_regs<HD>(Q_s, dp, lane, dka);  // dK^T += Q^T dS
-  }
-  if (!kv) return;
-  store_dT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, h);
-  store_dT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, h);
+  store_rowT<HD>(out + (q0 + qi) * so + hh * HD, o, inv, lane);
+  if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (m + log2f(l)) * kLn2 : 0.f;
 }
 
 // ------------------------------------------------------------------------------------ bwd: dQ
+template <int HD>
+struct DqChunk {
+  const float* K_s;
+  const float* V_s;
+  const float* qf;
+  const float* dof;
+  int lane, kc, lk, qi, causal;
+  float sl2, lse2, delta;
+  f32x4* acc;
+  template <int NTT, bool MASK>
+  __device__ __forceinline__ void run() { groups<NTT, MASK>(0); }
+  template <int N, bool MASK>   // tiles [tb, tb + N) in groups of RQ_ATTN_BWD_GROUP
+  __device__ __forceinline__ void groups(int tb) {
+    constexpr int NG = N < RQ_ATTN_BWD_GROUP ? N : RQ_ATTN_BWD_GROUP;
+    group<NG, MASK>(tb);
+    if constexpr (N > NG) groups<N - NG, MASK>(tb + NG);
+  }
+  template <int NG, bool MASK>
+  __device__ __forceinline__ void group(int tb) {
+    constexpr int LD = HD + 4;
+    const int g = lane >> 4;
+    f32x4 s[NG], dp[NG];
+#pragma unroll
+    for (int t = 0; t < NG; ++t) { s[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    tiles_x_frag2<HD, NG>(K_s + tb * 16 * LD, *reinterpret_cast<const float(*)[HD / 4]>(qf), V_s + tb * 16 * LD,
+                          *reinterpret_cast<const float(*)[HD / 4]>(dof), lane, s, dp);   // S^T, dP^T = V dO^T
+#pragma unroll
+    for (int t = 0; t < NG; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float p = exp2_fast(__builtin_fmaf(s[t][i], sl2, -lse2));
+        if constexpr (MASK) {
+          const int key = kc + (tb + t) * 16 + 4 * g + i;
+          if (!(key < lk && (!causal || key <= qi))) p = 0.f;
+        }
+        s[t][i] = p * (dp[t][i] - delta);       // dS^T
+      }
+    f32x4(&aa)[HD / 16] = *reinterpret_cast<f32x4(*)[HD / 16]>(acc);
+#pragma unroll
+    for (int t = 0; t < NG; ++t) colsT_x_acc<HD>(K_s + (tb + t) * 16 * LD, s[t], lane, aa);   // dQ^T += K^T dS^T
+  }
+};
+
 template <int HD, int NW>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ delta_out) {
-  constexpr int LD = Pad<HD>::LD, NTL = Pad<HD>::P / 32;
-  __shared__ __attribute__((aligned(16))) float smem[2 * 32 * LD];
+  constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
   float* K_s = smem;
-  float* V_s = smem + 32 * LD;
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-  zero_pad32<HD, 64 * NW>(K_s, tid);
-  zero_pad32<HD, 64 * NW>(V_s, tid);
+  float* V_s = smem + CH * LD;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {              // tail slice: dQ rows past the last sequence
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
+    return;
+  }
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int qbase = blockIdx.x * 32 * NW;
-  if (qbase >= lq) return;
-  const int qi = qbase + wave * 32 + (lane & 31);
-  const bool qv = qi < lq;
+  const int qwg = blockIdx.x * 16 * NW;
+  if (qwg >= lq) return;
+  const int qb = qwg + wave * 16, qi = qb + (lane & 15);
+  const bool wave_on = qb < lq, qv = qi < lq;
   const int64_t qrow = q0 + (qv ? qi : 0);
-  float qf[HD / 2], dof[HD / 2];
-  load_half_row<HD>(q + qrow * sq + hh * HD + h * (HD / 2), qv, qf);
-  load_half_row<HD>(dout + qrow * sdo + hh * HD + h * (HD / 2), qv, dof);
+  float qf[HD / 4], dof[HD / 4];
+  load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv, qf);
+  load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv, dof);
   float delta = 0.f;
   {
-    const float* orow = out + qrow * so + hh * HD + h * (HD / 2);
-    if (qv)
-      for (int d = 0; d < HD / 2; ++d) delta += dof[d] * orow[d];
+    float of[HD / 4];
+    load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+    delta += __shfl_xor(delta, 16, 64);
     delta += __shfl_xor(delta, 32, 64);
-    if (qv && h == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;   // reused by the dK/dV pass
+    if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;   // reused by the dK/dV pass
   }
-  const float lq_lse = qv ? lse[(int64_t)hh * Tq + qrow] : 0.f;
-  floatx16 dqa[NTL];
+  f32x4 acc[DT];
 #pragma unroll
-  for (int tl = 0; tl < NTL; ++tl)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dqa[tl][r] = 0.f;
-  const int kend = causal ? min(lk, qbase + 32 * NW) : lk;
-  for (int kt = 0; kt < kend; kt += 32) {
-    __syncthreads();
-    stage32<HD, 64 * NW>(K_s, k + k0 * sk + hh * HD, sk, kt, lk, tid);
-    stage32<HD, 64 * NW>(V_s, v + k0 * sv + hh * HD, sv, kt, lk, tid);
-    __syncthreads();
-    floatx16 s, dp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-    s = mfma_rows_x_frag<HD>(K_s, qf, lane, s);    // S^T
-    dp = mfma_rows_x_frag<HD>(V_s, dof, lane, dp); // dP^T = V dO^T
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kt + crow(r, h);
-      const bool ok = qv && key < lk && (!causal || key <= qi);
-      const float p = ok ? expf(s[r] * scale - lq_lse) : 0.f;
-      s[r] = p * (dp[r] - delta);   // dS^T
+  for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kend = causal ? min(lk, qwg + 16 * NW) : lk;
+  const int kend_w = causal ? min(lk, qb + 16) : lk;
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  RowStage<HD, 64 * NW, CH> stk, stv;
+  if (RQ_ATTN_PREFETCH && kend > 0) {
+    stk.load(kb_, sk, 0, lk, tid);
+    stv.load(vb_, sv, 0, lk, tid);
+  }
+  DqChunk<HD> fc{K_s, V_s, qf, dof, lane, 0, lk, qi, causal, scale * kLog2e,
+                 qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f, delta, acc};
+  for (int kc = 0; kc < kend; kc += CH) {
+    if (!RQ_ATTN_PREFETCH) {
+      stk.load(kb_, sk, kc, lk, tid);
+      stv.load(vb_, sv, kc, lk, tid);
     }
-    mfma_colsT_x_regs<HD>(K_s, s, lane, dqa);     // dQ^T += K^T dS^T
+    __syncthreads();
+    stk.store(K_s, tid);
+    stv.store(V_s, tid);
+    __syncthreads();
+    if (RQ_ATTN_PREFETCH && kc + CH < kend) {
+      stk.load(kb_, sk, kc + CH, lk, tid);
+      stv.load(vb_, sv, kc + CH, lk, tid);
+    }
+    const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend_w - kc + 15) >> 4) : 0);
+    fc.kc = kc;
+    dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fc);
   }
   if (!qv) return;
-  store_dT<HD>(dq + (q0 + qi) * sdq + hh * HD, dqa, scale, h);
+  store_rowT<HD>(dq + (q0 + qi) * sdq + hh * HD, acc, scale, lane);
 }
 
-// Short sequences (<= 96 rows, e.g. Amazon contexts of <= 81 tokens) run one wave (32 rows) per
-// workgroup so no wave idles on a padded 32-row half; longer ones share each staged K/V (Q/dO)
-// tile between two waves.
+// ------------------------------------------------------------------------------- bwd: dK, dV
+template <int HD>
+struct DkdvChunk {
+  const float* Q_s;
+  const float* O_s;
+  const float* lse_s;
+  const float* dl_s;
+  const float* kf;
+  const float* vf;
+  int lane, qc, t0, lq, kj, causal;
+  float sl2;
+  f32x4* dka;
+  f32x4* dva;
+  template <int NTT, bool MASK>
+  __device__ __forceinline__ void run() { groups<NTT, MASK>(t0); }
+  template <int N, bool MASK>   // tiles [tb, tb + N) in groups of RQ_ATTN_BWD_GROUP
+  __device__ __forceinline__ void groups(int tb) {
+    constexpr int NG = N < RQ_ATTN_BWD_GROUP ? N : RQ_ATTN_BWD_GROUP;
+    group<NG, MASK>(tb);
+    if constexpr (N > NG) groups<N - NG, MASK>(tb + NG);
+  }
+  template <int NG, bool MASK>
+  __device__ __forceinline__ void group(int tb) {
+    constexpr int LD = HD + 4;
+    const int g = lane >> 4;
+    const float* Qt = Q_s + tb * 16 * LD;
+    const float* Ot = O_s + tb * 16 * LD;
+    f32x4 s[NG], dp[NG];
+#pragma unroll
+    for (int t = 0; t < NG; ++t) { s[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    tiles_x_frag2<HD, NG>(Qt, *reinterpret_cast<const float(*)[HD / 4]>(kf), Ot,
+                          *reinterpret_cast<const float(*)[HD / 4]>(vf), lane, s, dp);   // S, dP = dO V^T
+#pragma unroll
+    for (int t = 0; t < NG; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = (tb + t) * 16 + 4 * g + i;
+        float p = exp2_fast(__builtin_fmaf(s[t][i], sl2, -lse_s[qr]));
+        if constexpr (MASK) {
+          const int qq = qc + qr;
+          if (!(qq < lq && (!causal || kj <= qq))) p = 0.f;
+        }
+        s[t][i] = p;
+        dp[t][i] = p * (dp[t][i] - dl_s[qr]);   // dS
+      }
+    f32x4(&dk_)[HD / 16] = *reinterpret_cast<f32x4(*)[HD / 16]>(dka);
+    f32x4(&dv_)[HD / 16] = *reinterpret_cast<f32x4(*)[HD / 16]>(dva);
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+      colsT_x_acc<HD>(Ot + t * 16 * LD, s[t], lane, dv_);    // dV^T += dO^T P
+      colsT_x_acc<HD>(Qt + t * 16 * LD, dp[t], lane, dk_);   // dK^T += Q^T dS
+    }
+  }
+};
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
+    const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dk, int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk) {
+  constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD + 2 * CH];
+  float* Q_s = smem;
+  float* O_s = smem + CH * LD;   // dO tile
+  float* lse_s = O_s + CH * LD;
+  float* dl_s = lse_s + CH;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {              // tail slice: dK / dV rows past the last sequence
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[b], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[b], Tk, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  const int kwg = blockIdx.x * 16 * NW;
+  if (kwg >= lk) return;
+  const int kb = kwg + wave * 16, kj = kb + (lane & 15);
+  const bool wave_on = kb < lk, kv = kj < lk;
+  const int64_t krow = k0 + (kv ? kj : 0);
+  float kf[HD / 4], vf[HD / 4];
+  load_frag<HD>(k + krow * sk + hh * HD + g * (HD / 4), kv, kf);
+  load_frag<HD>(v + krow * sv + hh * HD + g * (HD / 4), kv, vf);
+  f32x4 dka[DT], dva[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  // causal (key <= query): query chunks that end before this workgroup's first key contribute nothing
+  const int qstart = causal ? (kwg / CH) * CH : 0;
+  const float* qb_ = q + q0 * sq + hh * HD;
+  const float* ob_ = dout + q0 * sdo + hh * HD;
+  const float* lse_h = lse + (int64_t)hh * Tq + q0;
+  const float* dl_h = delta + (int64_t)hh * Tq + q0;
+  RowStage<HD, 64 * NW, CH> stq, sto;
+  float lse_r = 0.f, dl_r = 0.f;              // thread tid < CH stages the chunk's row tid
+  auto load_chunk = [&](int qc) {
+    stq.load(qb_, sq, qc, lq, tid);
+    sto.load(ob_, sdo, qc, lq, tid);
+    const bool ok = tid < CH && qc + tid < lq;
+    lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
+    dl_r = ok ? dl_h[qc + tid] : 0.f;
+  };
+  if (RQ_ATTN_PREFETCH && qstart < lq) load_chunk(qstart);
+  DkdvChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, lane, 0, 0, lq, kj, causal, scale * kLog2e, dka, dva};
+  for (int qc = qstart; qc < lq; qc += CH) {
+    if (!RQ_ATTN_PREFETCH) load_chunk(qc);
+    __syncthreads();
+    stq.store(Q_s, tid);
+    sto.store(O_s, tid);
+    if (tid < CH) {
+      lse_s[tid] = lse_r;
+      dl_s[tid] = dl_r;
+    }
+    __syncthreads();
+    if (RQ_ATTN_PREFETCH && qc + CH < lq) load_chunk(qc + CH);
+    const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);   // tiles wholly before the keys
+    const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (lq - qc + 15) >> 4) - t0 : 0);
+    fc.qc = qc;
+    fc.t0 = t0;
+    dispatch_tiles<NTL>(nt, !causal && qc + CH <= lq, fc);
+  }
+  if (!kv) return;
+  store_rowT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, lane);
+  store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
+}
+
+// Waves per workgroup by the longest row count: 16 rows per wave; short sequences (the Amazon
+// decoder's contexts <= 81 tokens, its 5-6 future tokens) use narrow workgroups so few waves idle
+// on padding, long ones (ML-32M <= 801, C5 <= 1281) share each staged 64-row chunk between 4 waves.
+static int waves_for(int64_t rows) { return rows <= 16 ? 1 : (rows <= 96 ? 2 : 4); }
+
+template <int HD, int NW>
+static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
+                   int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal, float scale,
+                   float* out, int64_t so, float* lse, int64_t Tq) {
+  dim3 g((unsigned)std::max<int64_t>(1, (max_q + 16 * NW - 1) / (16 * NW)), (unsigned)H, (unsigned)B + 1);   // + tail slice
+  hipLaunchKernelGGL((attn_fwd_kernel<HD, NW>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
+                     so, lse, Tq);
+}
+
 template <int HD>
 static void launch_fwd(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
                        float scale, float* out, int64_t so, float* lse, int64_t Tq) {
-  if (max_q <= RQ_ATTN_ONE_WAVE_MAX) {
-    dim3 g((unsigned)((max_q + 31) / 32), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
-                       so, lse, Tq);
-  } else {
-    dim3 g((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, 2>), g, dim3(128), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
-                       so, lse, Tq);
+  switch (waves_for(max_q)) {
+    case 1: fwd_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+    case 2: fwd_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+    default: fwd_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
   }
+}
+
+template <int HD, int NW>
+static void dq_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
+                  int64_t sk, const float* v, int64_t sv, const float* out, int64_t so, const float* dout, int64_t sdo,
+                  const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck, int causal, float scale, float* dq,
+                  int64_t sdq, float* delta) {
+  dim3 g((unsigned)std::max<int64_t>(1, (max_q + 16 * NW - 1) / (16 * NW)), (unsigned)H, (unsigned)B + 1);   // + tail slice
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, NW>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
+                     Tq, cq, ck, causal, scale, dq, sdq, delta);
+}
+
+template <int HD, int NW>
+static void dkdv_nw(int64_t B, int64_t H, int64_t max_k, hipStream_t st, const float* q, int64_t sq, const float* k,
+                    int64_t sk, const float* v, int64_t sv, const float* dout, int64_t sdo, const float* lse,
+                    const float* delta, int64_t Tq, const int64_t* cq, const int64_t* ck, int causal, float scale,
+                    float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk) {
+  dim3 g((unsigned)std::max<int64_t>(1, (max_k + 16 * NW - 1) / (16 * NW)), (unsigned)H, (unsigned)B + 1);   // + tail slice
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, NW>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta,
+                     Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk);
 }
 
 template <int HD>
@@ -329,31 +607,23 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                        const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
                        const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck,
                        int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv,
-                       float* delta) {
-  // dQ pass first: it also writes delta_q = dO.O, which the dK/dV pass reads per query tile
-  if (max_q <= RQ_ATTN_ONE_WAVE_MAX) {
-    dim3 gq((unsigned)((max_q + 31) / 32), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 1>), gq, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
-                       Tq, cq, ck, causal, scale, dq, sdq, delta);
-  } else {
-    dim3 gq((unsigned)((max_q + 63) / 64), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, 2>), gq, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse,
-                       Tq, cq, ck, causal, scale, dq, sdq, delta);
+                       int64_t Tk, float* delta) {
+  // dQ pass first: it also writes delta_q = dO.O, which the dK/dV pass reads per query chunk
+  switch (waves_for(max_q)) {
+    case 1: dq_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
+    case 2: dq_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
+    default: dq_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
   }
-  if (max_k <= RQ_ATTN_ONE_WAVE_MAX) {
-    dim3 gk((unsigned)((max_k + 31) / 32), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 1>), gk, dim3(64), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
-                       lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
-  } else {
-    dim3 gk((unsigned)((max_k + 63) / 64), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, 2>), gk, dim3(128), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo,
-                       lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv);
+  switch (waves_for(max_k)) {
+    case 1: dkdv_nw<HD, 1>(B, H, max_k, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk); break;
+    case 2: dkdv_nw<HD, 2>(B, H, max_k, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk); break;
+    default: dkdv_nw<HD, 4>(B, H, max_k, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk); break;
   }
 }
 
 static bool attn_args_ok(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k) {
   // max_q / max_k bound the grid's x extent and every in-kernel int index (row * stride fits int64)
-  return B >= 0 && B <= 65535 && H >= 1 && H <= 65535 && (hd == 16 || hd == 32 || hd == 64 || hd == 128) && max_q >= 0 &&
+  return B >= 0 && B < 65535 && H >= 1 && H <= 65535 && (hd == 16 || hd == 32 || hd == 64 || hd == 128) && max_q >= 0 &&
          max_k >= 0 && max_q <= (1 << 24) && max_k <= (1 << 24);
 }
 
@@ -367,9 +637,9 @@ int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
   RQ_CHECK_ARG(q && k && v && cu_q && cu_k && out && lse, "varlen_attn_fwd: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<=65535)");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
-  if (B == 0 || max_q == 0) return 0;
+  if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
     case 16: launch_fwd<16>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
@@ -384,21 +654,21 @@ int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
-                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, float* delta,
-                    void* stream) {
+                    float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
+                    float* delta, void* stream) {
   RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv && delta,
                "varlen_attn_bwd: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd: bad shape (hd must be 16/32/64/128, B<=65535)");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd: bad shape (hd must be 16/32/64/128, B<65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0 && sdo % 4 == 0 && sdq % 4 == 0 &&
                    sdk % 4 == 0 && sdv % 4 == 0,
                "varlen_attn_bwd: row strides must be x4");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
-    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
-    case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
-    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
-    case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, delta); break;
+    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
+    case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
+    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
+    case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_bwd");
   return 0;

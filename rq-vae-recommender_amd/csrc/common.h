@@ -82,6 +82,16 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t c) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+// Dropout epoch: a device word mixed into every mask key. Eager callers leave it at 0 (keys =
+// the host seeds); a captured (hipGraph) train step advances it once per replay
+// (rq_seed_epoch_advance, captured at the end of the step), so each replay draws fresh masks while
+// the forward and backward of one step see the same epoch. One copy per translation unit (no
+// relocatable device code): dropout.hip / rowwise.hip / linear.hip each export its address and
+// rq_seed_epoch_advance / rq_seed_epoch_set update all of them.
+static __device__ uint64_t rq_seed_epoch = 0;
+__device__ __forceinline__ uint64_t epoch_seed(uint64_t seed) {
+  return seed + rq_seed_epoch * 0xD6E8FEB86659FD93ull;
+}
 // thr / scale of nn.Dropout(p) for the kernels below (dropout.hip).
 void dropout_params(float p, uint32_t* thr, float* scale);
 struct Keep4 {

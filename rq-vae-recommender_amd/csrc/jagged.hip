@@ -55,11 +55,22 @@ __device__ __forceinline__ float p1m1(float v) {
   return t - 1.0f;
 }
 
-// Grid: (ceil(N*D/VEC / 256), B). Each thread moves VEC contiguous elements of one row.
+// Grid: (ceil(N*D/VEC / 256), B [+1]). Each thread moves VEC contiguous elements of one row. With
+// alloc_rows >= 0 the extra grid row y == B zero-fills the values rows [offsets[B], alloc_rows) (a
+// row-bucketed buffer's tail, so callers never need the valid row count on the host).
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) jagged_gather_kernel(const T* __restrict__ x, const int64_t* __restrict__ off,
-                                                             int64_t N, int64_t D, T* __restrict__ values, int p1m1_on) {
+                                                             int64_t N, int64_t D, T* __restrict__ values, int p1m1_on,
+                                                             int64_t nseq, int64_t alloc_rows) {
   const int64_t b = blockIdx.y;
+  if (b == nseq) {   // tail rows of the allocation
+    const int64_t e0 = off[nseq] * D, e1 = alloc_rows * D;
+    for (int64_t e = e0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC; e < e1; e += (int64_t)gridDim.x * 256 * VEC) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) values[e + k] = T(0.0f);
+    }
+    return;
+  }
   const int64_t o0 = off[b], len = off[b + 1] - o0;
   const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
   if (idx >= len * D) return;   // rows past len_b are never read (ragged tail)
@@ -107,13 +118,16 @@ __global__ void __launch_bounds__(256) jagged_scatter_kernel(const T* __restrict
 
 template <typename T>
 static int launch_gather(const void* x, const int64_t* off, int64_t B, int64_t N, int64_t D, void* values, int p1,
-                         hipStream_t s) {
+                         int64_t alloc_rows, hipStream_t s) {
+  const unsigned gy = (unsigned)(alloc_rows >= 0 ? B + 1 : B);
   if (sizeof(T) == 4 && D % 4 == 0) {
-    dim3 g((unsigned)((N * D / 4 + 255) / 256), (unsigned)B);
-    hipLaunchKernelGGL((jagged_gather_kernel<T, 4>), g, dim3(256), 0, s, (const T*)x, off, N, D, (T*)values, p1);
+    dim3 g((unsigned)((N * D / 4 + 255) / 256), gy);
+    hipLaunchKernelGGL((jagged_gather_kernel<T, 4>), g, dim3(256), 0, s, (const T*)x, off, N, D, (T*)values, p1, B,
+                       alloc_rows);
   } else {
-    dim3 g((unsigned)((N * D + 255) / 256), (unsigned)B);
-    hipLaunchKernelGGL((jagged_gather_kernel<T, 1>), g, dim3(256), 0, s, (const T*)x, off, N, D, (T*)values, p1);
+    dim3 g((unsigned)((N * D + 255) / 256), gy);
+    hipLaunchKernelGGL((jagged_gather_kernel<T, 1>), g, dim3(256), 0, s, (const T*)x, off, N, D, (T*)values, p1, B,
+                       alloc_rows);
   }
   return 0;
 }
@@ -144,20 +158,27 @@ int jagged_offsets(const int64_t* lengths, int64_t B, int64_t N, int64_t* offset
   return 0;
 }
 
-int jagged_from_padded(const void* x, int64_t B, int64_t N, int64_t D, const int64_t* offsets, void* values, int dtype,
-                       int add_one_sub_one, void* stream) {
+int jagged_from_padded_rows(const void* x, int64_t B, int64_t N, int64_t D, const int64_t* offsets, void* values,
+                            int64_t alloc_rows, int dtype, int add_one_sub_one, void* stream) {
   RQ_CHECK_ARG(x && offsets && values, "jagged_from_padded: null pointer");
-  RQ_CHECK_ARG(B >= 0 && B <= 65535 && N >= 0 && D > 0, "jagged_from_padded: bad shape (B <= 65535 per call)");
-  if (B == 0 || N == 0) return 0;
+  RQ_CHECK_ARG(B >= 0 && B < 65535 && N >= 0 && D > 0, "jagged_from_padded: bad shape (B < 65535 per call)");
+  if (B == 0 || (N == 0 && alloc_rows < 0)) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const int64_t n = N > 0 ? N : 1;   // N == 0 with a tail: one grid column zero-fills it
   switch (dtype) {
-    case kF32: launch_gather<float>(x, offsets, B, N, D, values, add_one_sub_one, s); break;
-    case kBF16: launch_gather<__hip_bfloat16>(x, offsets, B, N, D, values, add_one_sub_one, s); break;
-    case kF16: launch_gather<__half>(x, offsets, B, N, D, values, add_one_sub_one, s); break;
+    case kF32: launch_gather<float>(x, offsets, B, n, D, values, add_one_sub_one, alloc_rows, s); break;
+    case kBF16: launch_gather<__hip_bfloat16>(x, offsets, B, n, D, values, add_one_sub_one, alloc_rows, s); break;
+    case kF16: launch_gather<__half>(x, offsets, B, n, D, values, add_one_sub_one, alloc_rows, s); break;
     default: RQ_CHECK_ARG(false, "jagged_from_padded: dtype %d unsupported", dtype);
   }
   RQ_LAUNCH_CHECK("jagged_from_padded");
   return 0;
+}
+
+int jagged_from_padded(const void* x, int64_t B, int64_t N, int64_t D, const int64_t* offsets, void* values, int dtype,
+                       int add_one_sub_one, void* stream) {
+  if (N == 0) return (x && offsets && values) ? 0 : jagged_from_padded_rows(x, B, N, D, offsets, values, -1, dtype, 0, stream);
+  return jagged_from_padded_rows(x, B, N, D, offsets, values, -1, dtype, add_one_sub_one, stream);
 }
 
 int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int64_t N, int64_t D, void* x, int dtype,

@@ -582,6 +582,7 @@ __global__ void __launch_bounds__(256, kXWG)
 gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
                    const void* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S,
                    int64_t chunk, int per, float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
+  ep.seed = epoch_seed(ep.seed);
   __shared__ __attribute__((aligned(16))) char lds[kXLds];
   const int bid = blockIdx.x;
   const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
@@ -1004,5 +1005,7 @@ int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void*
   RQ_LAUNCH_CHECK("split_bf16x3_kernel");
   return 0;
 }
+
+int rq_seed_epoch_addr_linear(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }
 
 }  // extern "C"

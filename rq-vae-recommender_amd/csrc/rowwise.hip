@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restric
                                                           int64_t B, int D, float eps, uint32_t thr, float dscale,
                                                           uint64_t seed, float* __restrict__ y,
                                                           float* __restrict__ rstd) {
+  seed = epoch_seed(seed);
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
@@ -136,6 +137,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
                                                           const float* __restrict__ rstd, const float* __restrict__ gy,
                                                           int64_t B, int D, uint32_t thr, float dscale, uint64_t seed,
                                                           float* __restrict__ gx, float* __restrict__ gw_part) {
+  seed = epoch_seed(seed);
   __shared__ float4 part[4][VPL * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float4 wv[VPL], gwa[VPL];
@@ -443,5 +445,7 @@ int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const floa
                    float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream) {
   return rq_rmsnorm_dropout_bwd(x, w, rstd, gy, B, D, 0.f, 0, gx, gw, workspace, ws_bytes, stream);
 }
+
+int rq_seed_epoch_addr_rowwise(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }
 
 }  // extern "C"

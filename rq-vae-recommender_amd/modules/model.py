@@ -73,6 +73,15 @@ class EncoderDecoderRetrievalModel(nn.Module):
         self.in_proj_context = Linear(embedding_dim, attn_dim, bias=False)
         self.out_proj = Linear(attn_dim, num_embeddings, bias=False)
 
+    @staticmethod
+    def context_rows(batch: TokenizedSeqBatch, bucket=None) -> int:
+        """Allocated rows of the jagged context: valid tokens (user token + sequence) rounded up to
+        `bucket`. Host-known counts (ops.jagged.register_row_counts) avoid the device sync."""
+        B = batch.seq_mask.shape[0]
+        host = row_counts(batch.seq_mask)
+        total = host[0] + B if host is not None and host[3] == B else int(batch.seq_mask.sum()) + B
+        return total if not bucket else (total + bucket - 1) // bucket * bucket
+
     def _predict(self, batch: TokenizedSeqBatch):
         user_emb = self.user_id_embedder(batch.user_ids)                  # (B, 1, E)
         sem = self.sem_id_embedder(batch)
@@ -84,16 +93,16 @@ class EncoderDecoderRetrievalModel(nn.Module):
         if fut_emb is not None:
             fut = torch.cat([fut, fut_emb + self.tte(batch.token_type_ids_fut)], dim=1)
         ctx_lengths = batch.seq_mask.sum(axis=1) + 1
-        # one host sync (total); with tuned library GEMMs the row count is bucketed so that the
-        # variable-length context presents a bounded set of GEMM shapes (rqvae_hip.gemm_tuning)
+        # the context's valid row total is data-dependent; a CPU-side loader registers it with the
+        # mask (no device sync). The values buffer is allocated at the total rounded up to the GEMM
+        # row bucket (bounded GEMM shapes; rqvae_hip.gemm_tuning); the gather and attention kernels
+        # keep the tail rows zero on the device, and attention is launched over the padded width,
+        # so nothing in the step depends on the exact total on the host: a step captured for one
+        # bucket (rqvae_hip.graph.GraphedSteps) replays for every batch of that bucket.
         bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
-        host = row_counts(batch.seq_mask)   # registered by a CPU-side loader: no sync needed
-        if host is not None and host[3] == B:
-            ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1], total=host[0] + B,
-                                     known_max=min(host[2] + 1, ctx.shape[1]), known_min=min(host[1] + 1, ctx.shape[1]),
-                                     row_bucket=bucket)
-        else:
-            ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, ctx.shape[1], row_bucket=bucket)
+        alloc = self.context_rows(batch, bucket)
+        Nc = ctx.shape[1]
+        ctx_j = padded_to_jagged(ctx.contiguous(), ctx_lengths, Nc, alloc_rows=alloc, known_max=Nc)
         nf = fut.shape[1]                                                                # fixed length: no sync
         fut_lengths = torch.full((B,), nf, device=fut.device, dtype=torch.int64)
         fut_j = padded_to_jagged(fut.contiguous(), fut_lengths, nf, total=B * nf, known_max=nf)

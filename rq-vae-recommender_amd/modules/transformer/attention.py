@@ -95,10 +95,9 @@ class MultiHeadAttention(nn.Module):
             jkv = as_jagged(x_kv)
             ctx = hip_ops.varlen_attention_packed(self.q(jx.values()), self.kv(jkv.values()), jx.offsets(),
                                                   jkv.offsets(), self.num_heads, bool(is_causal), jx.max_len,
-                                                  jkv.max_len, rows_q=jx.rows, rows_k=jkv.rows)
+                                                  jkv.max_len)
         else:
             ctx = hip_ops.varlen_attention_packed(self.qkv(jx.values()), None, jx.offsets(), jx.offsets(),
-                                                  self.num_heads, bool(is_causal), jx.max_len, jx.max_len,
-                                                  rows_q=jx.rows, rows_k=jx.rows)
+                                                  self.num_heads, bool(is_causal), jx.max_len, jx.max_len)
         out = self.proj(ctx) if residual is None else hip_ops.linear_add(ctx, self.proj.weight, residual)
         return jx.with_values(out) if isinstance(x, Jagged) else _wrap_like(out, x)

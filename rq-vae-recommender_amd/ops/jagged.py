@@ -34,9 +34,10 @@ class Jagged:
 
     def __init__(self, values: Tensor, offsets: Tensor, max_len: int, min_len: int = 0, rows: int = None):
         self._values, self._offsets, self.max_len, self.min_len = values, offsets, int(max_len), int(min_len)
-        # valid rows (= offsets[-1]); values may carry zero tail rows past it (row bucketing, see
-        # rqvae_hip.gemm_tuning), which every row-wise op carries along and attention ignores
-        self.rows = int(values.shape[0]) if rows is None else int(rows)
+        # valid rows (= offsets[-1]) when known on the host, else None; values may carry zero tail
+        # rows past it (row bucketing, see rqvae_hip.gemm_tuning), which every row-wise op carries
+        # along and the attention / gather kernels keep zero on the device
+        self.rows = None if rows is None else int(rows)
 
     def values(self) -> Tensor:
         return self._values
@@ -47,9 +48,13 @@ class Jagged:
     def with_values(self, values: Tensor) -> "Jagged":
         return Jagged(values, self._offsets, self.max_len, self.min_len, self.rows)
 
+    def valid_rows(self) -> int:
+        """offsets[-1] (a device -> host sync when the caller did not know it)."""
+        return self.rows if self.rows is not None else int(self._offsets[-1])
+
     def to_nested(self):
-        return torch.nested.nested_tensor_from_jagged(self._values[:self.rows], self._offsets, min_seqlen=self.min_len,
-                                                      max_seqlen=self.max_len)
+        return torch.nested.nested_tensor_from_jagged(self._values[:self.valid_rows()], self._offsets,
+                                                      min_seqlen=self.min_len, max_seqlen=self.max_len)
 
     @property
     def shape(self):
@@ -64,7 +69,7 @@ def as_jagged(x) -> Jagged:
     mn = getattr(x, "_maybe_min_seqlen", None)
     if mx is None:
         mx = x._get_max_seqlen()
-    return Jagged(x.values(), x.offsets(), int(mx), int(mn or 0))
+    return Jagged(x.values(), x.offsets(), int(mx), int(mn or 0), int(x.values().shape[0]))
 
 
 _HOST_ROWS = {}
@@ -80,6 +85,16 @@ def register_row_counts(mask: Tensor, counts) -> None:
     weakref.finalize(mask, _HOST_ROWS.pop, key, None)
 
 
+def copy_row_counts(dst: Tensor, src: Tensor) -> None:
+    """Give `dst` the host-side row counts registered for `src` (e.g. a captured step's static
+    input mask takes over the counts of the batch it is captured with)."""
+    e = _HOST_ROWS.get(id(src))
+    if e is not None and e[0]() is src:
+        key = id(dst)
+        _HOST_ROWS[key] = (weakref.ref(dst), e[1])
+        weakref.finalize(dst, _HOST_ROWS.pop, key, None)
+
+
 def row_counts(mask: Tensor):
     """(sum, min, max, rows) of the counts registered for `mask`, or None."""
     e = _HOST_ROWS.get(id(mask))
@@ -87,23 +102,31 @@ def row_counts(mask: Tensor):
 
 
 def padded_to_jagged(x: Tensor, lengths: Tensor, max_len: int, total: int = None, add_one_sub_one: bool = True,
-                     known_max: int = None, row_bucket: int = None, known_min: int = None) -> Jagged:
+                     known_max: int = None, row_bucket: int = None, known_min: int = None,
+                     alloc_rows: int = None) -> Jagged:
     """HIP padded -> jagged gather. `total` / `known_max` (host ints) skip the host sync when the
     caller already knows them (e.g. fixed-length decoder inputs). `row_bucket`: allocate the values
-    with their row count rounded up to this multiple, tail rows zero (bounded set of GEMM shapes)."""
+    with their row count rounded up to this multiple (bounded set of GEMM shapes). `alloc_rows`: the
+    allocation itself (>= the valid total; graph-captured steps pass the bucket and never the exact
+    total). Rows past the valid total are zero-filled by the kernel on the device."""
     assert x.dim() == 3 and x.is_contiguous()
     hip_ops.require_gpu(x, lengths, what="padded_to_jagged")
     B, N, _ = x.shape
     n = min(int(max_len), N)
     offsets = hip_ops.jagged_offsets(lengths, n)
-    if total is None:
-        total, lmin, lmax = torch.stack([offsets[-1], lengths.clamp(0, n).min(), lengths.clamp(0, n).max()]).tolist()
-    else:
+    if alloc_rows is not None:
         lmax = known_max if known_max is not None else n
-        lmin = known_min if known_min is not None else lmax
-    alloc = int(total) if not row_bucket else (int(total) + row_bucket - 1) // row_bucket * row_bucket
-    values = hip_ops.PaddedToJaggedValues.apply(x, offsets, int(total), add_one_sub_one, alloc)
-    return Jagged(values, offsets, int(lmax), int(lmin), int(total))
+        lmin = known_min if known_min is not None else 0
+        alloc = int(alloc_rows)
+    else:
+        if total is None:
+            total, lmin, lmax = torch.stack([offsets[-1], lengths.clamp(0, n).min(), lengths.clamp(0, n).max()]).tolist()
+        else:
+            lmax = known_max if known_max is not None else n
+            lmin = known_min if known_min is not None else lmax
+        alloc = int(total) if not row_bucket else (int(total) + row_bucket - 1) // row_bucket * row_bucket
+    values = hip_ops.PaddedToJaggedValues.apply(x, offsets, alloc, add_one_sub_one, total)
+    return Jagged(values, offsets, int(lmax), int(lmin), None if total is None else int(total))
 
 
 def padded_to_jagged_tensor(x: Tensor, lengths: Tensor, max_len: int):

@@ -58,11 +58,14 @@ _SIGS = {
     "rq_l2norm_recon_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P], _I),
     "jagged_offsets": ([_P, _I64, _I64, _P, _P], _I),
     "jagged_from_padded": ([_P, _I64, _I64, _I64, _P, _P, _I, _I, _P], _I),
+    "jagged_from_padded_rows": ([_P, _I64, _I64, _I64, _P, _P, _I64, _I, _I, _P], _I),
     "jagged_to_padded": ([_P, _P, _I64, _I64, _I64, _P, _I, _P], _I),
     "varlen_attn_fwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
                          _I64, _P], _I),
     "varlen_attn_bwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
-                         _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _P], _I),
+                         _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I),
+    "rq_seed_epoch_advance": ([_P], _I),
+    "rq_seed_epoch_set": ([_U64, _P], _I),
     "rq_adamw_step": ([_P, _I64, _F, _F, _F, _F, _F, _F, _F, _P], _I),
     "rq_adamw_chunk_elems": ([], _SZ),
 }

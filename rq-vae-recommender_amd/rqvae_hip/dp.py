@@ -113,11 +113,16 @@ def all_gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
 class GradBuckets:
     """Flat gradient buffers + bucketed async all-reduce for a module's parameters."""
 
-    def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, overlap: bool = True):
+    def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, overlap: bool = True,
+                 flat_views: bool = False):
         """`params`: an iterable of parameters (buckets follow reverse registration order, ~ the order
         grads become ready), or a list of parameter groups given in the order their grads become
         ready (each group gets its own buckets, so an early group's all-reduce overlaps the rest of
-        the backward — e.g. [decoder + codebooks, encoder] for the RQ-VAE)."""
+        the backward — e.g. [decoder + codebooks, encoder] for the RQ-VAE).
+        `overlap=False`: the exchange starts in `synchronize()` only (hooks just record which
+        parameters took part) — required when the backward is replayed from a captured hipGraph.
+        `flat_views=True`: gradients live in the flat buffers even with one process, so they sit
+        at fixed addresses that several captured graphs can share."""
         params = list(params)
         grouped = bool(params) and isinstance(params[0], (list, tuple))
         groups = [list(g) for g in params] if grouped else [list(reversed(params))]
@@ -125,7 +130,8 @@ class GradBuckets:
         groups = [[p for p in g if p.requires_grad and not (id(p) in seen or seen.add(id(p)))] for g in groups]
         self.params: List[torch.nn.Parameter] = [p for g in groups for p in g]
         self.average = average
-        self.active = world() > 1   # single process: no flat views (AccumulateGrad steals, no add_)
+        # single process without flat_views: no flat views (AccumulateGrad steals, no add_)
+        self.active = world() > 1 or flat_views
         self.overlap = overlap and world() > 1
         self.buckets = []
         self._handles = []
@@ -146,10 +152,9 @@ class GradBuckets:
                         cur, cur_bytes = [], 0
                 if cur:
                     self._make_bucket(cur, dt, dev)
-        if self.overlap:
-            for bi, b in enumerate(self.buckets):
-                for p in b["params"]:
-                    p.register_post_accumulate_grad_hook(self._make_hook(bi))
+        for bi, b in enumerate(self.buckets):   # usage tracking (+ overlapped launches when overlap)
+            for p in b["params"]:
+                p.register_post_accumulate_grad_hook(self._make_hook(bi))
 
     def _make_bucket(self, ps, dt, dev):
         n = sum(p.numel() for p in ps)
@@ -171,7 +176,7 @@ class GradBuckets:
                                    "step got one later; its gradient would not be exchanged (build the buckets "
                                    "without it, or make it take part in the first step)")
             b["used"].add(id(p))
-            if self._sync and len(b["used"]) == b["expect"]:
+            if self.overlap and self._sync and len(b["used"]) == b["expect"]:
                 self._launch(bi)
         return hook
 
@@ -213,34 +218,37 @@ class GradBuckets:
         """Finish the exchange (launch buckets whose hooks did not all fire — params unused this
         step contribute zeros — then wait) and average."""
         ws = world()
-        if ws == 1:
+        if not self.active:
             return
-        for bi in range(len(self.buckets)):
-            self._launch(bi)
-        for bi, h in sorted(self._pending.items()):
-            h.wait()
-            if self.average:
-                self.buckets[bi]["flat"].div_(ws)
+        if ws > 1:
+            for bi in range(len(self.buckets)):
+                self._launch(bi)
+            for bi, h in sorted(self._pending.items()):
+                h.wait()
+                if self.average:
+                    self.buckets[bi]["flat"].div_(ws)
         self._pending = {}
         if self._unused is None:
             self._find_unused()
-        for p in self.params:
-            if id(p) in self._unused:
-                p.grad = None
+        for p in self._unused_params:
+            p.grad = None
 
     def _find_unused(self):
         """Once, at the first exchange: parameters whose grad hook fired on no rank. They are
         structurally unused (the decoder's tte_fut / ffn_norm): from now on their grad stays None,
         and a bucket launches as soon as its USED parameters are ready."""
-        dev = self.buckets[0]["flat"].device if self.buckets else torch.device("cpu")
-        used = torch.tensor([float(id(p) in b["used"]) for b in self.buckets for p in b["params"]], device=dev)
-        dist.all_reduce(used, op=dist.ReduceOp.MAX)
-        flags = used.cpu().tolist()
-        self._unused, k = set(), 0
+        flags = [float(id(p) in b["used"]) for b in self.buckets for p in b["params"]]
+        if world() > 1:
+            dev = self.buckets[0]["flat"].device if self.buckets else torch.device("cpu")
+            used = torch.tensor(flags, device=dev)
+            dist.all_reduce(used, op=dist.ReduceOp.MAX)
+            flags = used.cpu().tolist()
+        self._unused, self._unused_params, k = set(), [], 0
         for b in self.buckets:
             for p in b["params"]:
                 if flags[k] == 0.0:
                     self._unused.add(id(p))
+                    self._unused_params.append(p)
                 k += 1
             b["expect"] = sum(1 for p in b["params"] if id(p) not in self._unused)
 

@@ -536,6 +536,17 @@ def next_seed() -> int:
             rank * 0x94D049BB133111EB) & 0x7FFFFFFFFFFFFFFF   # fits int64
 
 
+def seed_epoch_advance(device=None) -> None:
+    """Advance the device-side dropout epoch (mixed into every mask key, csrc/common.h) on the current
+    stream: a captured train step ends with this call, so every replay draws fresh masks."""
+    call("rq_seed_epoch_advance", stream_handle(device))
+
+
+def seed_epoch_set(value: int, device=None) -> None:
+    """Set the device-side dropout epoch (0 = eager keys)."""
+    call("rq_seed_epoch_set", int(value), stream_handle(device))
+
+
 def dropout_fusable(t: torch.Tensor) -> bool:
     return t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
 
@@ -720,21 +731,22 @@ def jagged_offsets(lengths: torch.Tensor, N: int) -> torch.Tensor:
 
 
 class PaddedToJaggedValues(torch.autograd.Function):
-    """values (T, D) of the NJT built by ops/triton/jagged.py:11-66; backward = :69-77."""
+    """values (T, D) of the NJT built by ops/triton/jagged.py:11-66; backward = :69-77. `alloc` rows
+    are allocated (>= the valid total offsets[B]); the kernel zero-fills the rows past offsets[B] on
+    the device, so the valid total never has to be known on the host. `total` (optional, host int)
+    only labels the kernel timer's algorithmic bytes."""
 
     @staticmethod
-    def forward(ctx, x, offsets, total: int, add_one_sub_one: bool, alloc: int = None):
+    def forward(ctx, x, offsets, alloc: int, add_one_sub_one: bool, total: int = None):
         require_gpu(x, offsets, what="padded_to_jagged")
         assert x.dim() == 3 and x.is_contiguous()
         B, N, D = x.shape
-        alloc = total if alloc is None else alloc
-        vals = torch.empty((alloc, D), device=x.device, dtype=x.dtype)
-        if alloc > total:
-            vals[total:].zero_()   # bucket tail rows (rqvae_hip.gemm_tuning)
-        TIMER.around("jagged_from_padded", call, "jagged_from_padded", ptr(x), B, N, D, ptr(offsets), ptr(vals),
-                     _DTYPES[x.dtype], int(add_one_sub_one), stream_handle(x.device))
+        vals = torch.empty((int(alloc), D), device=x.device, dtype=x.dtype)
+        TIMER.around("jagged_from_padded", call, "jagged_from_padded_rows", ptr(x), B, N, D, ptr(offsets), ptr(vals),
+                     int(alloc), _DTYPES[x.dtype], int(add_one_sub_one), stream_handle(x.device))
         if TIMER.wants("jagged_from_padded"):
-            TIMER.bytes.setdefault("jagged_from_padded", []).append(2 * total * D * x.element_size())
+            TIMER.bytes.setdefault("jagged_from_padded", []).append(2 * (alloc if total is None else total) * D *
+                                                                    x.element_size())
         ctx.save_for_backward(offsets)
         ctx.shape = (B, N, D)
         return vals
@@ -809,8 +821,8 @@ class VarlenAttentionFunction(torch.autograd.Function):
         delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
         call("varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
              out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
-             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), ptr(delta),
-             stream_handle(q.device))
+             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), k.shape[0],
+             ptr(delta), stream_handle(q.device))
         return dq, dk, dv, None, None, None, None, None, None, None
 
 
@@ -818,11 +830,12 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
     """Varlen attention on the packed projection outputs: self-attention reads q/k/v as the three
     column blocks of qkv (T, 3A); cross-attention reads q (Tq, A) and k/v as the two column blocks
     of kv (Tk, 2A). The backward writes dq/dk/dv straight into one gradient buffer per projection
-    output (row-strided), so autograd never concatenates the three chunk gradients."""
+    output (row-strided), so autograd never concatenates the three chunk gradients. Buffers may
+    carry zero tail rows past the last sequence (row bucketing): the kernels write zero outputs
+    and gradients there themselves."""
 
     @staticmethod
-    def forward(ctx, qsrc, kvsrc, cu_q, cu_k, num_heads: int, causal: bool, max_q: int, max_k: int, scale: float,
-                rows_q: int = None, rows_k: int = None):
+    def forward(ctx, qsrc, kvsrc, cu_q, cu_k, num_heads: int, causal: bool, max_q: int, max_k: int, scale: float):
         require_gpu(qsrc, cu_q, cu_k, what="varlen_attention")
         self_attn = kvsrc is None
         A = qsrc.shape[1] // 3 if self_attn else qsrc.shape[1]
@@ -838,20 +851,14 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        call("varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
-             B, num_heads, hd, int(max_q), int(max_k), int(causal), float(scale), ptr(out), out.stride(0), ptr(lse), Tq,
-             stream_handle(q.device))
-        # rows past the valid count (row-bucket tail) are never written by the kernels: keep them 0
-        rows_q = Tq if rows_q is None else int(rows_q)
-        rows_k = src_kv.shape[0] if rows_k is None else int(rows_k)
-        if rows_q < Tq:
-            out[rows_q:].zero_()
+        TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+                     v.stride(0), ptr(cu_q), ptr(cu_k), B, num_heads, hd, int(max_q), int(max_k), int(causal),
+                     float(scale), ptr(out), out.stride(0), ptr(lse), Tq, stream_handle(q.device))
         if self_attn:
             ctx.save_for_backward(qsrc, out, lse, cu_q, cu_k)
         else:
             ctx.save_for_backward(qsrc, kvsrc, out, lse, cu_q, cu_k)
         ctx.cfg = (self_attn, A, num_heads, bool(causal), int(max_q), int(max_k), float(scale))
-        ctx.rows = (rows_q, rows_k)
         return out
 
     @staticmethod
@@ -872,27 +879,20 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         Tq = q.shape[0]
         B = cu_q.shape[0] - 1
         delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
-        call("varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-             out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
-             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), ptr(delta),
-             stream_handle(q.device))
-        rows_q, rows_k = ctx.rows
-        if rows_q < gq_src.shape[0]:
-            gq_src[rows_q:].zero_()
-        if not self_attn and rows_k < gkv_src.shape[0]:
-            gkv_src[rows_k:].zero_()
-        return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None, None, None
+        TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+                     v.stride(0), ptr(out), out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q),
+                     ptr(cu_k), B, H, A // H, max_q, max_k, int(causal), scale, ptr(dq), dq.stride(0), ptr(dk),
+                     dk.stride(0), ptr(dv), dv.stride(0), k.shape[0], ptr(delta), stream_handle(q.device))
+        return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None
 
 
-def varlen_attention_packed(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None, rows_q=None,
-                            rows_k=None):
+def varlen_attention_packed(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):
     """qsrc = qkv (T, 3A) with kvsrc None (self-attention), or q (Tq, A) with kv (Tk, 2A) (cross).
-    rows_q / rows_k: valid row counts when the buffers carry zero tail rows (row bucketing)."""
+    Rows past the last sequence (bucket tail) come out zero in the output and the gradients."""
     A = qsrc.shape[1] // 3 if kvsrc is None else qsrc.shape[1]
     if scale is None:
         scale = 1.0 / math.sqrt(A // num_heads)
-    return PackedVarlenAttentionFunction.apply(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale, rows_q,
-                                               rows_k)
+    return PackedVarlenAttentionFunction.apply(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale)
 
 
 def varlen_attention(q, k, v, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):

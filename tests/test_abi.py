@@ -32,7 +32,7 @@ def test_library_exports_declared_symbols():
     assert not missing, missing
     assert set(_declared()) == set(_lib.EXPORTED_SYMBOLS)
     typed = _lib.load()
-    assert typed.rq_abi_version() == 1
+    assert typed.rq_abi_version() == 2
     # argument checks run on the host and never touch the device
     rc = typed.rq_quantize_fwd(None, 4, 48, None, None, 8, 1, 3, 0.25, None, None, None, None, None, None)
     assert rc == -22 and b"null pointer" in typed.rq_last_error()

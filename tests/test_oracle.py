@@ -135,3 +135,37 @@ def test_attention_oracle_self_consistent():
             fm = (A.attn_fwd(q, k, v, cu, cu, causal)[0] * do).sum()
             arr[idx] += eps
             assert (fp - fm) / (2 * eps) == pytest.approx(grad[idx], rel=1e-5, abs=1e-8)
+
+
+@pytest.mark.parametrize("tag", ["small", "dm"])
+def test_decoder_oracle_vs_reference(golden, tag):
+    """oracle/decoder.py (padded + masks, plain torch CPU) against the reference's own decoder fixture:
+    loss, logits, per-position loss and the parameter gradients."""
+    import torch
+    from oracle import decoder as Dm
+    z = golden(f"decoder_{tag}")
+    E, A, H, nl, K, L1, n_max, seed = (int(z[k]) for k in ("E", "A", "H", "n_layers", "K", "L1", "n_max", "seed"))
+    names = [k[len("grad__"):].replace("__norm", "") for k in z if k.startswith("grad__") and not k.endswith("__row0")]
+    shapes = {n: (z["grad__" + n].shape if "grad__" + n in z else None) for n in names}
+    # parameter shapes: small tensors are stored whole; the rest from the module layout
+    from modules.model import EncoderDecoderRetrievalModel
+    m = EncoderDecoderRetrievalModel(embedding_dim=E, attn_dim=A, dropout=0.0, num_heads=H, n_layers=nl,
+                                     num_embeddings=K, sem_id_dim=L1, inference_verifier_fn=None, max_pos=n_max * L1)
+    P = {n: torch.from_numpy(gi.named_param(n, p.shape, seed)).requires_grad_(True) for n, p in m.named_parameters()}
+    keys = ("user_ids", "sem_ids", "sem_ids_fut", "seq_mask", "token_type_ids", "token_type_ids_fut")
+    batch = {k: torch.from_numpy(z[k]) for k in keys}
+    loss, logits, loss_d = Dm.decoder_forward(P, batch, K, L1, H, nl, dropout=0.0)
+    loss.backward()
+    assert float(loss) == pytest.approx(float(z["loss"]), rel=2e-6)
+    assert np.abs(logits.detach().numpy() - z["logits"]).max() <= 2e-6 * np.abs(z["logits"]).max()
+    assert np.allclose(loss_d.detach().numpy(), z["loss_d"], rtol=1e-5, atol=1e-7)
+    checked = 0
+    for n in names:
+        g = P[n].grad
+        if "grad__" + n in z:
+            ref = z["grad__" + n]
+            assert np.abs(g.numpy() - ref).max() <= 2e-5 * np.abs(ref).max() + 1e-7, n
+        else:
+            assert g.double().norm().item() == pytest.approx(float(z["grad__" + n + "__norm"]), rel=2e-5), n
+        checked += 1
+    assert checked == len(names) and shapes
