@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     ap.add_argument("--no-graph", action="store_true", help="decoder steps eager instead of hipGraph replays")
     ap.add_argument("--no-dm", action="store_true", help="skip the ML-32M decoder lines")
+    ap.add_argument("--dm-batch", type=int, default=0, help="with --decoder-only: the ML-32M config at this batch")
     return ap.parse_args()
 
 
@@ -231,9 +232,11 @@ def main():
         # solution per shape; shapes missing from the shipped table are tuned in the warmup
         from rqvae_hip import gemm_tuning
         gemm_tuning.enable()
-    if args.decoder_only:
-        print(json.dumps({"decoder_amazon": measure_decoder(torch.device("cuda", lr), ws, rk, graphs=not args.no_graph,
-                                                            stats=False)}), flush=True)
+    if args.decoder_only:   # profile helper: one decoder config (amazon, or ml32m with --dm-batch)
+        cfg, b = (DEC_DM, args.dm_batch) if args.dm_batch else (DEC, None)
+        print(json.dumps({f"decoder_{cfg['name']}": measure_decoder(torch.device("cuda", lr), ws, rk, cfg, B=b,
+                                                                     graphs=not args.no_graph, stats=False)}),
+              flush=True)
         return
     device = torch.device("cuda", lr)
     torch.cuda.set_device(device)

@@ -163,6 +163,15 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
                       void* workspace, size_t ws_bytes, void* stream);
+
+/* Which kernel rq_gemm_bf16x3_ex runs for a call: 1 = the wide 256 x 256-tile kernel (both operands
+ * split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile kernel; *splits (optional) = its split-K
+ * factor. -1 for an empty shape. Host-only. */
+int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_split, int a_kcontig, int b_kcontig,
+                          int epilogue, int* splits);
+/* Enable (1) / disable (0) the wide kernel for this process (default: on unless RQ_X3W=0 is set);
+ * returns the previous setting. For A/B measurements and kernel-vs-kernel tests. */
+int rq_gemm_x3w_enable(int enable);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
 /* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device

@@ -535,6 +535,42 @@ __device__ __forceinline__ float sigmoid_fast(float z) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
 }
 
+// Epilogue of one lane quad C[m][n .. n + 3] = v (fp32 accumulator values); Cs = the split-K slab
+// (kEpiStore) or C itself.
+template <int EPI, bool DROP>
+__device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, float* __restrict__ C,
+                                        float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
+  if constexpr (EPI == kEpiStore) {
+    *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
+  } else if constexpr (EPI == kEpiAdd) {
+    const float4 r = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
+    *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+  } else {
+    const uint64_t e = (uint64_t)m * N + n;
+    float d[4] = {1.f, 1.f, 1.f, 1.f};   // dropout multipliers (0 or 1 / (1 - p))
+    if constexpr (DROP) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = keep1(ep.seed, e + j, ep.thr) ? ep.scale : 0.f;
+    }
+    float4 o;
+    if constexpr (EPI == kEpiSiluFwd) {
+      *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = v;
+      o = make_float4(v.x * sigmoid_fast(v.x) * d[0], v.y * sigmoid_fast(v.y) * d[1], v.z * sigmoid_fast(v.z) * d[2],
+                      v.w * sigmoid_fast(v.w) * d[3]);
+    } else {   // silu'(z) g = g s (1 + z (1 - s)), g = Dropout(A B^T)
+      const float4 z = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
+      const float sx = sigmoid_fast(z.x), sy = sigmoid_fast(z.y), sz = sigmoid_fast(z.z), sw = sigmoid_fast(z.w);
+      o = make_float4(v.x * d[0] * sx * (1.f + z.x * (1.f - sx)), v.y * d[1] * sy * (1.f + z.y * (1.f - sy)),
+                      v.z * d[2] * sz * (1.f + z.z * (1.f - sz)), v.w * d[3] * sw * (1.f + z.w * (1.f - sw)));
+    }
+    uint2 hi, lo;
+    split_bf16x2(o.x, o.y, hi.x, lo.x);
+    split_bf16x2(o.z, o.w, hi.y, lo.y);
+    *reinterpret_cast<uint2*>(ep.Hh + (int64_t)m * ep.ldh + n) = hi;
+    *reinterpret_cast<uint2*>(ep.Hl + (int64_t)m * ep.ldh + n) = lo;
+  }
+}
+
 __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo) {
   const __bf16 h = (__bf16)v;
   *hi = __builtin_bit_cast(uint16_t, h);
@@ -717,40 +753,285 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
           const float4 v = make_float4(acc[p][q][4 * g], acc[p][q][4 * g + 1], acc[p][q][4 * g + 2], acc[p][q][4 * g + 3]);
 #endif
           if (n >= N) continue;
-          if constexpr (EPI == kEpiStore) {
-            *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
-          } else if constexpr (EPI == kEpiAdd) {
-            const float4 r = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
-            *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
-          } else {
-            const uint64_t e = (uint64_t)m * N + n;
-            float d[4] = {1.f, 1.f, 1.f, 1.f};   // dropout multipliers (0 or 1 / (1 - p))
-            if constexpr (DROP) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) d[j] = keep1(ep.seed, e + j, ep.thr) ? ep.scale : 0.f;
-            }
-            float4 o;
-            if constexpr (EPI == kEpiSiluFwd) {
-              *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = v;
-              o = make_float4(v.x * sigmoid_fast(v.x) * d[0], v.y * sigmoid_fast(v.y) * d[1],
-                              v.z * sigmoid_fast(v.z) * d[2], v.w * sigmoid_fast(v.w) * d[3]);
-            } else {   // silu'(z) g = g s (1 + z (1 - s)), g = Dropout(A B^T)
-              const float4 z = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
-              const float sx = sigmoid_fast(z.x), sy = sigmoid_fast(z.y), sz = sigmoid_fast(z.z),
-                          sw = sigmoid_fast(z.w);
-              o = make_float4(v.x * d[0] * sx * (1.f + z.x * (1.f - sx)), v.y * d[1] * sy * (1.f + z.y * (1.f - sy)),
-                              v.z * d[2] * sz * (1.f + z.z * (1.f - sz)), v.w * d[3] * sw * (1.f + z.w * (1.f - sw)));
-            }
-            uint2 hi, lo;
-            split_bf16x2(o.x, o.y, hi.x, lo.x);
-            split_bf16x2(o.z, o.w, hi.y, lo.y);
-            *reinterpret_cast<uint2*>(ep.Hh + (int64_t)m * ep.ldh + n) = hi;
-            *reinterpret_cast<uint2*>(ep.Hl + (int64_t)m * ep.ldh + n) = lo;
-          }
+          x3_epi4<EPI, DROP>(v, m, n, N, C, Cs, ldc, ep);
         }
     }
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Wide split-bf16 GEMM ("x3w"): 256 x 256 output tile per workgroup, 8 waves (2 along m x 4
+// along n, 128 x 64 outputs each), both operands already split into bf16 planes. The operand tile
+// of one 32-deep k step is four "halves" (A rows 0-127 / 128-255, B rows 0-127 / 128-255), each a
+// hi and a lo plane of 8 KiB: a row image for a k-contiguous operand (64-B rows, 16-B chunk c of
+// row r at c ^ ((r >> 2) & 2): conflict-free for the 16x16x32 fragment's ds_read_b128 lane
+// groups), else the column image of gemm_bf16x3_kernel read by ds_read_b64_tr_b16. A (the
+// streamed activation: HBM / Infinity-Cache misses) has THREE k-step slots, B (the weights, L2
+// hits) two: 3 x 32 + 2 x 32 KiB = 160 KiB, the whole LDS, one workgroup per CU.
+//
+// Staging is LDS-DMA (global_load_lds_dwordx4: no VGPR round trip; the images' XOR swizzles go on
+// the per-lane SOURCE address, the LDS side stays lane-linear: wave w fills bytes [1 KiB w,
+// 1 KiB (w + 1)) of every half-plane). A k step is four phases, one per C quadrant of the wave
+// (A half h x B half g), in the order (0,0) (0,1) (1,1) (1,0); reads: A0 + B0 (phase 0), B1 (1),
+// A1 (2), none (3: B0 kept in registers). Phase p of step t issues, 2 DMA instructions per wave
+// each, B0 (t + 1), B1 (t + 1), A0 (t + 2), A1 (t + 2): A lands 5-7 phases after issue, B in 4,
+// and since vmcnt retires in issue order, B issued after A never waits on A's misses early. The
+// only waits are a counted vmcnt(6) (three halves left in flight) at the end of phases 3 and 0;
+// phase 2's A1 was retired by phase 0's. Never vmcnt(0) inside the loop. The two wave groups
+// (waves 0-3 / 4-7: one of each per SIMD) run staggered by one barrier with two barriers per
+// phase, so on every SIMD one wave issues its LDS reads and DMAs while the other runs its 24
+// MFMAs. Ordering rules:
+//  * RAW: data read in phase f is retired (each wave's own vmcnt) before the barrier that ends
+//    the interval BEFORE either group's read interval of phase f: group 0 waits at the end of its
+//    MFMA interval of phase f - 1, group 1 (one interval behind) at the end of its read interval;
+//  * WAR: a DMA overwrites a slot last read >= 3 phases earlier (A: step t - 1's copy; B: step
+//    t - 1's), those reads retired by lgkmcnt(0) before their phase's MFMAs.
+// Per k step and wave: 24 ds_read_b128 / tr reads, 8 DMA instructions, 96 MFMAs (16x16x32 bf16).
+// The accumulation order over k equals gemm_bf16x3_kernel's (same 32-deep steps, same product
+// order), so for the same split the two kernels agree bitwise.
+// ---------------------------------------------------------------------------------------------
+#ifndef RQ_X3W_STAGGER
+#define RQ_X3W_STAGGER 1   // 0: both wave groups in lock-step (A/B switch)
+#endif
+#ifndef RQ_X3W_EPI_LDS
+#define RQ_X3W_EPI_LDS 1   // epilogue through LDS in whole rows (0: straight from the accumulators)
+#endif
+#ifndef RQ_X3W_DIAG
+#define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs (wrong results)
+#endif
+#ifndef RQ_X3W_PRIO
+#define RQ_X3W_PRIO 1      // s_setprio(1) around each MFMA cluster (keeps hipcc from moving it)
+#endif
+constexpr int kWT2 = 256;          // output tile (m and n)
+constexpr int kWH = 8192;          // one half-plane: 128 rows x 32 k bf16
+constexpr int kWStep = 4 * kWH;    // one operand's k step: 2 halves x 2 planes
+constexpr int kWB0 = 3 * kWStep;   // B's slots follow A's three
+constexpr int kWLds = 5 * kWStep;  // 160 KiB
+
+__device__ __forceinline__ void glds16(const uint16_t* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+__device__ __forceinline__ int wrow_swz(int r) { return (r >> 2) & 2; }
+
+// Element offset (from the k step's base) of the 16 bytes lane `lane` of wave `wave` DMAs into its
+// slot of a half-plane image whose first row (m or n) is r0.
+template <bool KC>
+__device__ __forceinline__ int64_t x3w_src(int64_t ld, int r0, int R, int wave, int lane) {
+  if constexpr (KC) {   // row image: 16 rows x 4 chunks per 1 KiB; position c holds k-chunk c ^ swz
+    const int row = 16 * wave + (lane >> 2);
+    const int kc = (lane & 3) ^ wrow_swz(row);
+    return (int64_t)min(r0 + row, R - 1) * ld + 8 * kc;
+  } else {              // column image: 4 k-rows x 16 chunks per 1 KiB; position c holds m-chunk c ^ col_swz
+    const int kr = 4 * wave + (lane >> 4);
+    const int mc = (lane & 15) ^ col_swz(kr);
+    return (int64_t)kr * ld + min(r0 + 8 * mc, R - 8);
+  }
+}
+
+// 16x16x32 operand fragment of a wide-kernel half-plane (row rb + lane % 16, k = 8 (lane / 16) + 0..7).
+template <bool KC>
+__device__ __forceinline__ bf16x8_t wfrag16(const char* plane, int rb, int lane) {
+  if constexpr (KC) {
+    const int rr = rb + (lane & 15), c = lane >> 4;
+    return *reinterpret_cast<const bf16x8_t*>(plane + rr * 64 + ((c ^ wrow_swz(rr)) << 4));
+  } else {
+    return xfrag16<false>(plane, rb, lane);
+  }
+}
+
+#define RQ_W_BAR() __builtin_amdgcn_s_barrier()
+#define RQ_W_VM6() asm volatile("s_waitcnt vmcnt(6)" ::: "memory")
+#define RQ_W_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+template <bool AKC, bool BKC, int EPI, bool DROP>
+__global__ void __launch_bounds__(512, 1)
+gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al, int64_t lda,
+                const uint16_t* __restrict__ Bh, const uint16_t* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K,
+                int tiles_n, int tiles, int64_t chunk, float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
+  ep.seed = epoch_seed(ep.seed);
+  __shared__ __attribute__((aligned(16))) char lds[kWLds];   // the kernel's only LDS object (DMA waits)
+  // bijective XCD-major remap: consecutive work items (same A rows, same k chunk) share an L2
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xq = nwg >> 3, xr = nwg & 7, xcd = bid & 7;
+  const int lw = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (bid >> 3);
+  const int s = lw / tiles, t = lw - s * tiles;
+  const int m0 = (t / tiles_n) * kWT2, n0 = (t % tiles_n) * kWT2;
+  const int64_t k_lo = (int64_t)s * chunk;
+  const int64_t k_hi = k_lo + chunk < K ? k_lo + chunk : K;
+  const int nk = (int)((k_hi - k_lo) >> 5);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool g1 = RQ_X3W_STAGGER && wr != 0;
+
+  const int64_t da = AKC ? 32 : 32 * lda, db = BKC ? 32 : 32 * ldb;
+  const int64_t ka = AKC ? k_lo : k_lo * lda, kb = BKC ? k_lo : k_lo * ldb;
+  const int64_t oa0 = ka + x3w_src<AKC>(lda, m0, M, wave, lane), oa1 = ka + x3w_src<AKC>(lda, m0 + 128, M, wave, lane);
+  const int64_t ob0 = kb + x3w_src<BKC>(ldb, n0, N, wave, lane), ob1 = kb + x3w_src<BKC>(ldb, n0 + 128, N, wave, lane);
+  char* const wl = lds + 1024 * wave;
+  // A half h of k step `step` into A slot `slot`; B half g of step `step` into B parity step & 1.
+  // Steps past the end are clamped (the last step again, into a slot nobody reads), so every wave
+  // issues the same DMA count in every phase and the vmcnt counts stay static.
+  auto issue_a = [&](int h, int step, int slot) {
+    if (RQ_X3W_DIAG == 1) return;   // diagnostic build: no operand loads (wrong results)
+    const int64_t o = (h == 0 ? oa0 : oa1) + (int64_t)(step < nk ? step : nk - 1) * da;
+    char* dst = wl + slot * kWStep + h * 2 * kWH;
+    glds16(Ah + o, dst);
+    glds16(Al + o, dst + kWH);
+  };
+  auto issue_b = [&](int g, int step) {
+    if (RQ_X3W_DIAG == 1) return;
+    const int64_t o = (g == 0 ? ob0 : ob1) + (int64_t)(step < nk ? step : nk - 1) * db;
+    char* dst = wl + kWB0 + (step & 1) * kWStep + g * 2 * kWH;
+    glds16(Bh + o, dst);
+    glds16(Bl + o, dst + kWH);
+  };
+  auto aplane = [&](int slot, int h, int pl) -> const char* { return lds + slot * kWStep + (h * 2 + pl) * kWH; };
+  auto bplane = [&](int par, int g, int pl) -> const char* {
+    return lds + kWB0 + par * kWStep + (g * 2 + pl) * kWH;
+  };
+
+  floatx4v acc[2][2][4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[h][g][i][j] = floatx4v{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t fah[4], fal[4], fb0h[2], fb0l[2], fb1h[2], fb1l[2];
+
+#define RQ_W_READ_A(SLOT, H)                                                                   \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                              \
+    fah[i] = wfrag16<AKC>(aplane(SLOT, H, 0), wr * 64 + 16 * i, lane);                         \
+    fal[i] = wfrag16<AKC>(aplane(SLOT, H, 1), wr * 64 + 16 * i, lane);                         \
+  }
+#define RQ_W_READ_B(PAR, G, BH, BL)                                                            \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                              \
+    BH[j] = wfrag16<BKC>(bplane(PAR, G, 0), wc * 32 + 16 * j, lane);                           \
+    BL[j] = wfrag16<BKC>(bplane(PAR, G, 1), wc * 32 + 16 * j, lane);                           \
+  }
+#define RQ_W_MMA(H, G, BH, BL)                                                                 \
+  if (RQ_X3W_DIAG != 2) {                                                                      \
+  if (RQ_X3W_PRIO) __builtin_amdgcn_s_setprio(1);                                              \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) { \
+    floatx4v& c_ = acc[H][G][i][j];                                                            \
+    c_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BH[j], fal[i], c_, 0, 0, 0);                  \
+    c_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BL[j], fah[i], c_, 0, 0, 0);                  \
+    c_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BH[j], fah[i], c_, 0, 0, 0);                  \
+  }                                                                                            \
+  if (RQ_X3W_PRIO) __builtin_amdgcn_s_setprio(0);                                              \
+  }
+
+  // prologue, in the steady state's issue order (A of steps 0 and 1, B of step 0); phase 0 of
+  // step 0 needs A0 (0) and B0 (0): B1 (0), A0 (1), A1 (1) may stay in flight
+  issue_a(0, 0, 0);
+  issue_a(1, 0, 0);
+  issue_b(0, 0);
+  issue_b(1, 0);
+  issue_a(0, 1, 1);
+  issue_a(1, 1, 1);
+  RQ_W_VM6();
+  RQ_W_BAR();
+  if (g1) RQ_W_BAR();   // group 1 runs one barrier behind
+  int slot = 0;         // A slot of step st (st % 3); step st + 2 goes to (st + 2) % 3
+  for (int st = 0; st < nk; ++st) {
+    const int par = st & 1, slot2 = slot == 0 ? 2 : slot - 1;
+    // phase 0: quadrant (A0, B0)
+    RQ_W_READ_A(slot, 0)
+    RQ_W_READ_B(par, 0, fb0h, fb0l)
+    issue_b(0, st + 1);
+    if (g1) RQ_W_VM6();   // B1 (and A1) of this step, for phases 1 and 2
+    RQ_W_BAR();
+    RQ_W_LGKM0();
+    RQ_W_MMA(0, 0, fb0h, fb0l)
+    if (!g1) RQ_W_VM6();
+    RQ_W_BAR();
+    // phase 1: (A0, B1)
+    RQ_W_READ_B(par, 1, fb1h, fb1l)
+    issue_b(1, st + 1);
+    RQ_W_BAR();
+    RQ_W_LGKM0();
+    RQ_W_MMA(0, 1, fb1h, fb1l)
+    RQ_W_BAR();
+    // phase 2: (A1, B1)
+    RQ_W_READ_A(slot, 1)
+    issue_a(0, st + 2, slot2);
+    RQ_W_BAR();
+    RQ_W_LGKM0();
+    RQ_W_MMA(1, 1, fb1h, fb1l)
+    RQ_W_BAR();
+    // phase 3: (A1, B0) from registers
+    issue_a(1, st + 2, slot2);
+    if (g1) RQ_W_VM6();   // A0 and B0 of the next step, for its phase 0
+    RQ_W_BAR();
+    RQ_W_MMA(1, 0, fb0h, fb0l)
+    if (!g1) RQ_W_VM6();
+    RQ_W_BAR();
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+#undef RQ_W_READ_A
+#undef RQ_W_READ_B
+#undef RQ_W_MMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!g1) RQ_W_BAR();   // balance group 1's extra barrier
+
+  float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
+#if RQ_X3W_EPI_LDS
+  // Epilogue through LDS, one 128-row half of the tile at a time (128 KiB): the waves scatter their
+  // accumulator quads into a [128][256] fp32 image (16-B chunk c of row r at c ^ (r & 15): the
+  // 16 rows of a quad store and the 16 chunks of a row read hit distinct bank groups), then each
+  // wave runs the epilogue on 16 whole rows, one 1 KiB row segment per instruction (coalesced
+  // stores / Z reads instead of 64-B pieces of 16 rows).
+  __syncthreads();   // every wave's DMAs retired (vmcnt(0) above) and its reads done: LDS is free
+  float* const img = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = wr * 64 + 16 * i + (lane & 15);
+          const int c = 32 * g + 8 * wc + 4 * j + (lane >> 4);
+          *reinterpret_cast<floatx4v*>(img + r * 256 + 4 * (c ^ (r & 15))) = acc[h][g][i][j];
+        }
+    __syncthreads();
+    const int n = n0 + 4 * lane;
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      const int r = wave * 16 + q, m = m0 + 128 * h + r;
+      const floatx4v a = *reinterpret_cast<const floatx4v*>(img + r * 256 + 4 * (lane ^ (r & 15)));
+      if (m < M && n < N) x3_epi4<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), m, n, N, C, Cs, ldc, ep);
+    }
+    __syncthreads();
+  }
+#else
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + 128 * h + wr * 64 + 16 * i + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = n0 + 128 * g + wc * 32 + 16 * j + 4 * (lane >> 4);
+          if (n >= N) continue;
+          const floatx4v a = acc[h][g][i][j];
+          x3_epi4<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), m, n, N, C, Cs, ldc, ep);
+        }
+    }
+#endif
+}
+#undef RQ_W_BAR
+#undef RQ_W_VM6
+#undef RQ_W_LGKM0
 
 // Elementwise split (weights once per step; 4 elements per thread per iteration, any n).
 __global__ void __launch_bounds__(256) split_bf16x3_kernel(const float* __restrict__ x, int64_t n,
@@ -811,6 +1092,57 @@ static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) 
   return p;
 }
 
+#ifndef RQ_X3W_MIN_STEPS
+#define RQ_X3W_MIN_STEPS 8   // split-K of the wide kernel: k steps per workgroup at least
+#endif
+
+// RQ_X3W=0 in the environment (or rq_gemm_x3w_enable(0)) disables the wide kernel: A/B runs and
+// kernel-vs-kernel tests in one build.
+static int g_x3w = -1;
+static bool x3w_enabled() {
+  if (g_x3w < 0) {
+    const char* e = getenv("RQ_X3W");
+    g_x3w = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_x3w == 1;
+}
+
+// Plan of the wide kernel, or false when the 128-tile kernel serves the shape better: k steps
+// must be whole (K % 32), padding of a partial 256-row tile must stay small (R % 256 == 0 or
+// R >= 2048), and the launch must cover at least a quarter of the CUs (split-K when allowed).
+static bool x3w_plan(int64_t M, int64_t N, int64_t K, bool allow_split, X3Plan* p) {
+  if (!x3w_enabled() || K % 32 != 0 || K <= 0) return false;
+  auto fits = [](int64_t R) { return R % kWT2 == 0 || R >= 2048; };
+  if (!fits(M) || !fits(N)) return false;
+  const int cus = resident_slots() / 2;
+  p->tiles_n = (int)((N + kWT2 - 1) / kWT2);
+  p->tiles = (int)((M + kWT2 - 1) / kWT2) * p->tiles_n;
+  int64_t S = 1;
+  if (allow_split && p->tiles < cus / 2 && (M * N) % 4 == 0) {
+    S = cus / p->tiles;
+    const int64_t max_s = K / (32 * RQ_X3W_MIN_STEPS);
+    if (S > max_s) S = max_s;
+    if (S > RQ_X3_MAX_SPLIT) S = RQ_X3_MAX_SPLIT;
+    if (S < 1) S = 1;
+  }
+  int64_t chunk = (K + S - 1) / S;
+  chunk = (chunk + 31) / 32 * 32;
+  p->chunk = chunk;
+  p->S = (int)((K + chunk - 1) / chunk);
+  p->per = 0;
+  return (int64_t)p->tiles * p->S >= cus / 4;
+}
+
+// The wide kernel runs when both operands are split planes, the (layout, epilogue) pair is
+// instantiated (every layout for the plain store; the fused MLP chain's layouts otherwise) and the
+// shape plans (x3w_plan).
+static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool a_kc, bool b_kc, int epilogue,
+                       X3Plan* p) {
+  const bool combo = epilogue == kEpiStore || (epilogue == kEpiSiluFwd && a_kc && b_kc) ||
+                     (epilogue == kEpiSiluBwd && a_kc && !b_kc) || (epilogue == kEpiAdd && a_kc && b_kc);
+  return asp && bsp && combo && x3w_plan(M, N, K, epilogue == kEpiStore, p);
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -858,8 +1190,12 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
 
 size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
+  // the larger of the two kernels' split-K slabs (which one runs depends on the operand formats)
   const X3Plan p = x3_plan(M, N, K);
-  return p.S > 1 ? (size_t)p.S * (size_t)(M * N) * sizeof(float) : 0;
+  X3Plan pw;
+  int S = p.S;
+  if (x3w_plan(M, N, K, true, &pw) && pw.S > S) S = pw.S;
+  return S > 1 ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
 }
 
 int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
@@ -897,7 +1233,10 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
     RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
     return 0;
   }
-  const X3Plan pl = x3_plan(M, N, K, epilogue == kEpiStore);
+  X3Plan pl = x3_plan(M, N, K, epilogue == kEpiStore);
+  X3Plan pw;
+  const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, &pw);
+  if (wide) pl = pw;
   float* out = C;
   if (pl.S > 1) {
     const size_t need = (size_t)pl.S * (size_t)(M * N) * sizeof(float);
@@ -919,7 +1258,33 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
       RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
   } while (0)
   bool launched = true;
-  if (epilogue == kEpiStore) {
+  if (wide) {
+    const uint16_t *ah = static_cast<const uint16_t*>(A), *al = static_cast<const uint16_t*>(A_lo);
+    const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
+    const dim3 wgrid((unsigned)(pl.tiles * pl.S)), wblock(512);
+#define RQ_X3W(AK, BK, EP, DR)                                                                                        \
+  hipLaunchKernelGGL((gemm_x3w_kernel<AK, BK, EP, DR>), wgrid, wblock, 0, s, ah, al, lda, bh, bl, ldb, (int)M, (int)N, \
+                     K, pl.tiles_n, pl.tiles, pl.chunk, out, ldo, ep)
+    const bool drop = ep.thr != 0;
+    const int kc = (a_kcontig ? 2 : 0) | (b_kcontig ? 1 : 0);
+    if (epilogue == kEpiStore) {
+      switch (kc) {
+        case 3: RQ_X3W(true, true, kEpiStore, false); break;
+        case 2: RQ_X3W(true, false, kEpiStore, false); break;
+        case 1: RQ_X3W(false, true, kEpiStore, false); break;
+        default: RQ_X3W(false, false, kEpiStore, false); break;
+      }
+    } else if (epilogue == kEpiSiluFwd && kc == 3) {
+      if (drop) RQ_X3W(true, true, kEpiSiluFwd, true); else RQ_X3W(true, true, kEpiSiluFwd, false);
+    } else if (epilogue == kEpiSiluBwd && kc == 2) {
+      if (drop) RQ_X3W(true, false, kEpiSiluBwd, true); else RQ_X3W(true, false, kEpiSiluBwd, false);
+    } else if (epilogue == kEpiAdd && kc == 3) {
+      RQ_X3W(true, true, kEpiAdd, false);
+    } else {
+      launched = false;
+    }
+#undef RQ_X3W
+  } else if (epilogue == kEpiStore) {
     switch (code) {
       // every layout with fp32 operands (the generic entry point)
       case 16 | 4: RQ_X3(true, false, true, false, kEpiStore); break;
@@ -965,6 +1330,21 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
     RQ_LAUNCH_CHECK("wgrad_reduce_kernel(gemm_bf16x3)");
   }
   return 0;
+}
+
+int rq_gemm_x3w_enable(int enable) {
+  const int prev = x3w_enabled() ? 1 : 0;
+  g_x3w = enable ? 1 : 0;
+  return prev;
+}
+
+int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_split, int a_kcontig, int b_kcontig,
+                          int epilogue, int* splits) {
+  if (M <= 0 || N <= 0 || K <= 0) return -1;
+  X3Plan pw;
+  const bool wide = x3w_choose(M, N, K, a_split, b_split, a_kcontig, b_kcontig, epilogue, &pw);
+  if (splits) *splits = wide ? pw.S : x3_plan(M, N, K, epilogue == kEpiStore).S;
+  return wide ? 1 : 0;
 }
 
 int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,

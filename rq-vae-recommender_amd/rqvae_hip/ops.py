@@ -302,6 +302,22 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     return (C, H) if epilogue == EPI_SILU_FWD else H
 
 
+def gemm_x3_choice(M: int, N: int, K: int, a_split: bool, b_split: bool, a_kcontig: bool, b_kcontig: bool,
+                   epilogue: int = EPI_STORE):
+    """(kernel, splits) rq_gemm_bf16x3_ex picks for a call: kernel 'wide' (256 x 256 tiles, LDS-DMA,
+    both operands split) or 'x3' (128 x 128 tiles); host-only."""
+    import ctypes
+    s = ctypes.c_int(0)
+    k = _lib.load().rq_gemm_bf16x3_choice(M, N, K, int(a_split), int(b_split), int(a_kcontig), int(b_kcontig),
+                                          int(epilogue), ctypes.byref(s))
+    return ("wide" if k == 1 else "x3"), int(s.value)
+
+
+def gemm_x3w_enable(enable: bool) -> bool:
+    """Turn the wide split-bf16 GEMM kernel on / off for this process; returns the previous state."""
+    return bool(_lib.load().rq_gemm_x3w_enable(int(enable)))
+
+
 def mlp_fusable(x: torch.Tensor, weights) -> bool:
     """The fused chain needs fp32 device tensors, split-operand widths (every dim % 8) and rows."""
     return (x.is_cuda and x.dtype == torch.float32 and x.numel() > 0 and
