@@ -166,7 +166,8 @@ class GradBuckets:
             p.grad = v          # grads accumulate in place into the flat buffer
             views.append(v)
             off += p.numel()
-        self.buckets.append(dict(params=ps, flat=flat, views=views, ready=0, used=set(), expect=len(ps)))
+        self.buckets.append(dict(params=ps, flat=flat, views=views, ready=0, used=set(), fired=set(),
+                                 expect=len(ps)))
 
     def _make_hook(self, bi):
         def hook(p):
@@ -176,7 +177,12 @@ class GradBuckets:
                                    "step got one later; its gradient would not be exchanged (build the buckets "
                                    "without it, or make it take part in the first step)")
             b["used"].add(id(p))
-            if self.overlap and self._sync and len(b["used"]) == b["expect"]:
+            if not self._sync:
+                return
+            # count this pass's grads only: after no_sync micro-batches `used` is already full, and a
+            # launch on the first hook of the last micro-batch would reduce partial gradients
+            b["fired"].add(id(p))
+            if self.overlap and len(b["fired"]) == b["expect"]:
                 self._launch(bi)
         return hook
 
@@ -189,6 +195,8 @@ class GradBuckets:
             yield
         finally:
             self._sync = prev
+            for b in self.buckets:
+                b["fired"].clear()
 
     def _launch(self, bi):
         if bi in self._pending:
@@ -207,6 +215,7 @@ class GradBuckets:
         for b in self.buckets:
             b["flat"].zero_()
             b["used"].clear()
+            b["fired"].clear()
             for p, v in zip(b["params"], b["views"]):
                 if id(p) in unused:
                     continue
