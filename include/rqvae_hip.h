@@ -194,6 +194,10 @@ int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, 
                         void* stream);
 int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
                         int64_t C, float* g_pre, void* stream);
+/* The same gradient emitted as split-bf16 planes (g = hi + lo, rq_split_bf16x3's form): the input of the
+ * decoder MLP's last data-grad / weight-grad GEMMs at matmul precision 'high'. */
+int rq_l2norm_recon_bwd_split(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
+                              int64_t C, uint16_t* g_hi, uint16_t* g_lo, void* stream);
 
 /* RqVae.forward statistics (modules/rqvae.py:151-162):
  *   rq_row_norms   out[r] = |x_r|_2 for rows (rows, D), D % 4 == 0 — embs_norm = emb.norm(dim=-1)

@@ -54,6 +54,29 @@ __device__ __forceinline__ float group_sum(float v) {
 
 __device__ __forceinline__ int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// Split-bf16 operand form of the 'high' matmul path (linear.hip): (a, b) -> packed bf16 (hi) and
+// packed bf16 of the exact remainders (lo), round-to-nearest-even.
+__device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const f32x2_t v = {a, b};
+  const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+  const f32x2_t hf = {__builtin_bit_cast(float, hb << 16), __builtin_bit_cast(float, hb & 0xffff0000u)};
+  const f32x2_t r = v - hf;
+  hi = hb;
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
+}
+
+// 4 consecutive fp32 values -> their hi / lo bf16 planes (8-B stores each).
+__device__ __forceinline__ void split_store4(const float4 o, uint16_t* hi, uint16_t* lo) {
+  uint2 h, l;
+  split_bf16x2(o.x, o.y, h.x, l.x);
+  split_bf16x2(o.z, o.w, h.y, l.y);
+  *reinterpret_cast<uint2*>(hi) = h;
+  *reinterpret_cast<uint2*>(lo) = l;
+}
+
 // Correctly rounded a / b (bitwise the IEEE quotient) for a divisor shared by many numerators:
 // y = 1.0f / b is computed once with the IEEE division, then q0 = RN(a*y) is within an ulp of
 // a/b and one fma correction returns RN(a/b) (Markstein's theorem) whenever the residual

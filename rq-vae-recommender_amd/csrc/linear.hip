@@ -247,10 +247,8 @@ static WgradPlan wgrad_plan(int64_t Bn, int64_t O, int64_t I) {
 // Both images come from coalesced float4 loads in the operand's HBM layout.
 // ---------------------------------------------------------------------------------------------
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 #ifndef RQ_X3_BK16
 #define RQ_X3_BK16 0   // 1: 16-deep k stages (32 KiB LDS, 3 workgroups/CU, 32x32x16 MFMA)
@@ -263,16 +261,6 @@ constexpr int kXPlane = kXT * kXK * 2;         // bytes of one bf16 plane (8 KiB
 constexpr int kXOp = 2 * kXPlane;              // hi + lo planes of one operand
 constexpr int kXBuf = 2 * kXOp;                // A + B
 constexpr int kXLds = 2 * kXBuf;               // double buffer: 64 KiB
-
-// (a, b) -> packed bf16 (hi) and packed bf16 of the exact remainders (lo), round-to-nearest-even.
-__device__ __forceinline__ void split_bf16x2(float a, float b, uint32_t& hi, uint32_t& lo) {
-  const f32x2_t v = {a, b};
-  const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
-  const f32x2_t hf = {__builtin_bit_cast(float, hb << 16), __builtin_bit_cast(float, hb & 0xffff0000u)};
-  const f32x2_t r = v - hf;
-  hi = hb;
-  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
-}
 
 __device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
 // Row image: row rr of 2 kXK bytes, 16-B chunk c stored at c ^ row_swz(rr) (conflict-free for 16

@@ -8,6 +8,8 @@
 //   fwd: n_b = max(|pre_b|, 1e-12); y = pre_b / n_b; recon_b = sum (y - x_b)^2; saves n_b
 //   bwd: g_y = 2 g_b (y - x_b); g_pre = (g_y - y (g_y . y)) / n_b   (|pre_b| > eps)
 //                                g_pre = g_y / eps                  (clamped rows)
+//        written fp32, or (rq_l2norm_recon_bwd_split) as the split-bf16 planes the next data-grad /
+//        weight-grad GEMMs of the 'high' path consume directly (same bytes as fp32).
 #include "common.h"
 
 namespace rqhip {
@@ -48,11 +50,12 @@ __global__ void __launch_bounds__(256) l2norm_recon_fwd_kernel(const float* __re
   }
 }
 
-template <int VPL>
+template <int VPL, bool SPLIT>
 __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __restrict__ pre, const float* __restrict__ x,
                                                                 const float* __restrict__ nrm,
                                                                 const float* __restrict__ g_recon, int64_t B, int C,
-                                                                float* __restrict__ g_pre) {
+                                                                float* __restrict__ g_pre, uint16_t* __restrict__ g_hi,
+                                                                uint16_t* __restrict__ g_lo) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= B) return;
@@ -86,7 +89,10 @@ __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __re
       o = make_float4((gy[v].x - yv[v].x * dot) / n, (gy[v].y - yv[v].y * dot) / n, (gy[v].z - yv[v].z * dot) / n,
                       (gy[v].w - yv[v].w * dot) / n);
     }
-    *reinterpret_cast<float4*>(g_pre + r * C + c) = o;
+    if constexpr (SPLIT)
+      split_store4(o, g_hi + r * C + c, g_lo + r * C + c);
+    else
+      *reinterpret_cast<float4*>(g_pre + r * C + c) = o;
   }
 }
 
@@ -337,22 +343,43 @@ int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, 
   return 0;
 }
 
-int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
-                        int64_t C, float* g_pre, void* stream) {
-  RQ_CHECK_ARG(pre && x && norms && g_recon && g_pre, "rq_l2norm_recon_bwd: null pointer");
+static int l2norm_recon_bwd_launch(const float* pre, const float* x, const float* norms, const float* g_recon,
+                                   int64_t B, int64_t C, float* g_pre, uint16_t* g_hi, uint16_t* g_lo, void* stream) {
   RQ_CHECK_ARG(B >= 0 && C > 0 && C % 4 == 0 && C <= 4096, "rq_l2norm_recon_bwd: need C %% 4 == 0, C <= 4096");
   if (B == 0) return 0;
   dim3 g((unsigned)((B + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
   const int vpl = (int)((C + 255) / 256);
+  const bool sp = g_hi != nullptr;
   switch (vpl) {
-#define L2R_CASE(V) case V: hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, g_pre); break;
+#define L2R_CASE(V)                                                                                                 \
+  case V:                                                                                                           \
+    if (sp)                                                                                                         \
+      hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, true>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, \
+                         g_pre, g_hi, g_lo);                                                                        \
+    else                                                                                                            \
+      hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, false>), g, dim3(256), 0, s, pre, x, norms, g_recon, B,        \
+                         (int)C, g_pre, g_hi, g_lo);                                                                \
+    break;
     L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE(5) L2R_CASE(6) L2R_CASE(7) L2R_CASE(8)
     L2R_CASE(9) L2R_CASE(10) L2R_CASE(11) L2R_CASE(12) L2R_CASE(13) L2R_CASE(14) L2R_CASE(15) L2R_CASE(16)
 #undef L2R_CASE
   }
   RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd");
   return 0;
+}
+
+int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
+                        int64_t C, float* g_pre, void* stream) {
+  RQ_CHECK_ARG(pre && x && norms && g_recon && g_pre, "rq_l2norm_recon_bwd: null pointer");
+  return l2norm_recon_bwd_launch(pre, x, norms, g_recon, B, C, g_pre, nullptr, nullptr, stream);
+}
+
+int rq_l2norm_recon_bwd_split(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
+                              int64_t C, uint16_t* g_hi, uint16_t* g_lo, void* stream) {
+  RQ_CHECK_ARG(pre && x && norms && g_recon && g_hi && g_lo, "rq_l2norm_recon_bwd_split: null pointer");
+  RQ_CHECK_ARG(((uintptr_t)g_hi | (uintptr_t)g_lo) % 8 == 0, "rq_l2norm_recon_bwd_split: planes must be 8-byte aligned");
+  return l2norm_recon_bwd_launch(pre, x, norms, g_recon, B, C, nullptr, g_hi, g_lo, stream);
 }
 
 int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream) {

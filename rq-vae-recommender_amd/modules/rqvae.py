@@ -145,8 +145,14 @@ class RqVae(nn.Module):
         n = self.n_cat_feats
         head = self.decoder.mlp
         if n == 0 and isinstance(head[-1], L2NormalizationLayer) and x.dtype == torch.float32:
-            # decoder's final l2norm + ReconstructionLoss fused into one HIP row kernel (fwd + bwd)
-            reconstruction = hip_ops.l2norm_recon_loss(self.decoder.body(emb_sum), x)
+            fused = self.decoder._fused_chain(emb_sum)
+            if fused is not None and x.shape[-1] % 4 == 0:
+                # 'high': the decoder MLP chain + l2norm + ReconstructionLoss as one node whose
+                # backward hands the split output gradient straight to the chain's GEMMs
+                reconstruction = hip_ops.mlp_l2norm_recon(emb_sum, x, fused[0], fused[1])
+            else:
+                # decoder's final l2norm + ReconstructionLoss fused into one HIP row kernel (fwd + bwd)
+                reconstruction = hip_ops.l2norm_recon_loss(self.decoder.body(emb_sum), x)
         else:
             x_hat = self.decode(emb_sum)
             if n > 0:   # the reference's cat is a no-op for n == 0 (SURVEY A-10)

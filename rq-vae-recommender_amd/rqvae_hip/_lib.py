@@ -58,6 +58,7 @@ _SIGS = {
     "rq_row_norms": ([_P, _I64, _I64, _P, _P], _I),
     "rq_loss_means": ([_P, _P, _I64, _P, _P], _I),
     "rq_l2norm_recon_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P], _I),
+    "rq_l2norm_recon_bwd_split": ([_P, _P, _P, _P, _I64, _I64, _P, _P, _P], _I),
     "jagged_offsets": ([_P, _I64, _I64, _P, _P], _I),
     "jagged_from_padded": ([_P, _I64, _I64, _I64, _P, _P, _I, _I, _P], _I),
     "jagged_from_padded_rows": ([_P, _I64, _I64, _I64, _P, _P, _I64, _I, _I, _P], _I),

@@ -324,67 +324,149 @@ def mlp_fusable(x: torch.Tensor, weights) -> bool:
             all(w.dtype == torch.float32 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 for w in weights))
 
 
+def _presplit_input(rows: int, weights, n_layers: int) -> bool:
+    """Split the fp32 chain input once up front when that moves the first layer's forward (and its
+    weight grad, which reads the same operand) onto the wide LDS-DMA kernel, which takes split
+    operands only: at the RQ-VAE batch the split (one HBM pass) costs less than the 128-tile kernel's
+    on-the-fly conversion loses (ML-32M encoder layer 0: 235 -> ~150 us forward, 178 -> ~145 us wgrad)."""
+    O, I = weights[0].shape
+    epi = EPI_SILU_FWD if n_layers > 1 else EPI_STORE
+    return gemm_x3_choice(rows, O, I, True, True, True, True, epi)[0] == "wide"
+
+
+def _mlp_forward(a, wsp, rows: int, p: float, seeds):
+    """The chain's forward GEMMs from input a (fp32 or Split): (out fp32, zs, hs)."""
+    n = len(wsp)
+    zs, hs = [], []
+    out = None
+    for i, w in enumerate(wsp):
+        O, I = w.hi.shape
+        if i < n - 1:
+            z, h = gemm_x3(a, True, w, True, rows, O, I, EPI_SILU_FWD, p=p, seed=seeds[i])
+            zs.append(z)
+            hs.append(h)
+            a = h
+        else:
+            out = gemm_x3(a, True, w, True, rows, O, I)
+    return out, zs, hs
+
+
+def _mlp_backward(gcur, x_in, wsp, zs, hs, rows: int, p: float, seeds, need_w, need_x: bool):
+    """The chain's backward from the output grad gcur (fp32 or Split): (dx fp32 or None, [dW])."""
+    n = len(wsp)
+    dws = [None] * n
+    dx = None
+    for i in reversed(range(n)):
+        O, I = wsp[i].hi.shape
+        inp = x_in if i == 0 else hs[i - 1]
+        if need_w[i]:
+            dws[i] = gemm_x3(gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
+        if i > 0:
+            gcur = gemm_x3(gcur, True, wsp[i], False, rows, I, O, EPI_SILU_BWD, Z=zs[i - 1], p=p, seed=seeds[i - 1])
+        elif need_x:
+            dx = gemm_x3(gcur, True, wsp[0], False, rows, I, O)
+    return dx, dws
+
+
+def _mlp_save(ctx, x_in, wsp, zs, hs):
+    xs = list(x_in) if isinstance(x_in, Split) else [x_in]
+    ctx.x_split = isinstance(x_in, Split)
+    return [*xs, *[t for s_ in wsp for t in s_], *zs, *[t for h in hs for t in h]]
+
+
+def _mlp_load(ctx, n: int, saved):
+    k = 2 if ctx.x_split else 1
+    x_in = Split(saved[0], saved[1]) if ctx.x_split else saved[0]
+    wsp = [Split(saved[k + 2 * i], saved[k + 1 + 2 * i]) for i in range(n)]
+    zs = list(saved[k + 2 * n:k + 2 * n + (n - 1)])
+    hb = k + 2 * n + (n - 1)
+    hs = [Split(saved[hb + 2 * i], saved[hb + 2 * i + 1]) for i in range(n - 1)]
+    return x_in, wsp, zs, hs, hb + 2 * (n - 1)
+
+
+def _mlp_prologue(x, p: float, weights):
+    n = len(weights)
+    x2 = x.reshape(-1, weights[0].shape[1]).contiguous()
+    rows = x2.shape[0]
+    wsp = split_bf16x3_many(weights) if len(weights) <= 16 else [split_bf16x3(w) for w in weights]
+    seeds = [next_seed() if p > 0 else 0 for _ in range(n - 1)]
+    x_in = split_bf16x3(x2) if _presplit_input(rows, weights, n) else x2
+    return x_in, rows, wsp, seeds
+
+
 class MLPFunction(torch.autograd.Function):
     """The whole bias-free Linear -> SiLU -> [Dropout] -> ... -> Linear chain of modules/encoder.py:7-36
     at 'high' matmul precision, as one autograd node. Each hidden layer is ONE GEMM launch whose
     epilogue keeps z (for SiLU') and emits h = Dropout(SiLU(z)) already split into bf16 planes, so
     the next layer's forward and this layer's weight grad read it without converting; backward
     mirrors it (the data-grad GEMM's epilogue applies SiLU' and the dropout mask and emits the
-    split pre-activation grad). Weights are split once per call. Replaces eager torch's Linear +
-    SiLU + Dropout + mask kernels (forward) and their backward passes."""
+    split pre-activation grad). Weights are split once per call; a large fp32 input is split once
+    too (_presplit_input). Replaces eager torch's Linear + SiLU + Dropout + mask kernels (forward)
+    and their backward passes."""
 
     @staticmethod
     def forward(ctx, x, p: float, *weights):
-        n = len(weights)
-        I0 = weights[0].shape[1]
-        x2 = x.reshape(-1, I0).contiguous()
-        rows = x2.shape[0]
-        wsp = split_bf16x3_many(weights) if len(weights) <= 16 else [split_bf16x3(w) for w in weights]
-        seeds = [next_seed() if p > 0 else 0 for _ in range(n - 1)]
-        a, zs, hs = x2, [], []
-        out = None
-        for i, w in enumerate(weights):
-            O, I = w.shape
-            if i < n - 1:
-                z, h = gemm_x3(a, True, wsp[i], True, rows, O, I, EPI_SILU_FWD, p=p, seed=seeds[i])
-                zs.append(z)
-                hs.append(h)
-                a = h
-            else:
-                out = gemm_x3(a, True, wsp[i], True, rows, O, I)
-        ctx.n, ctx.p, ctx.seeds, ctx.xshape = n, float(p), seeds, x.shape
-        ctx.save_for_backward(x2, *[t for s_ in wsp for t in s_], *zs, *[t for h in hs for t in h])
+        x_in, rows, wsp, seeds = _mlp_prologue(x, p, weights)
+        out, zs, hs = _mlp_forward(x_in, wsp, rows, p, seeds)
+        ctx.n, ctx.p, ctx.seeds, ctx.xshape = len(weights), float(p), seeds, x.shape
+        ctx.save_for_backward(*_mlp_save(ctx, x_in, wsp, zs, hs))
         return out.view(*x.shape[:-1], weights[-1].shape[0])
 
     @staticmethod
     def backward(ctx, g):
-        n, p = ctx.n, ctx.p
-        saved = ctx.saved_tensors
-        x2 = saved[0]
-        wsp = [Split(saved[1 + 2 * i], saved[2 + 2 * i]) for i in range(n)]
-        zs = list(saved[1 + 2 * n:1 + 2 * n + (n - 1)])
-        hb = 1 + 2 * n + (n - 1)
-        hs = [Split(saved[hb + 2 * i], saved[hb + 2 * i + 1]) for i in range(n - 1)]
-        rows = x2.shape[0]
+        x_in, wsp, zs, hs, _ = _mlp_load(ctx, ctx.n, ctx.saved_tensors)
+        rows = (x_in.hi if ctx.x_split else x_in).shape[0]
         gcur = g.reshape(rows, -1).contiguous()
-        dws = [None] * n
-        dx = None
-        for i in reversed(range(n)):
-            O, I = wsp[i].hi.shape
-            inp = x2 if i == 0 else hs[i - 1]
-            if ctx.needs_input_grad[2 + i]:
-                dws[i] = gemm_x3(gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
-            if i > 0:
-                gcur = gemm_x3(gcur, True, wsp[i], False, rows, I, O, EPI_SILU_BWD, Z=zs[i - 1], p=p,
-                               seed=ctx.seeds[i - 1])
-            elif ctx.needs_input_grad[0]:
-                dx = gemm_x3(gcur, True, wsp[0], False, rows, I, O).view(ctx.xshape)
-        return (dx, None, *dws)
+        dx, dws = _mlp_backward(gcur, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[2:],
+                                ctx.needs_input_grad[0])
+        return (None if dx is None else dx.view(ctx.xshape), None, *dws)
 
 
 def mlp_chain(x: torch.Tensor, weights, p: float = 0.0) -> torch.Tensor:
     """Fused Linear-SiLU-[Dropout]-...-Linear at 'high' precision (MLPFunction)."""
     return MLPFunction.apply(x, float(p), *weights)
+
+
+class MLPL2ReconFunction(torch.autograd.Function):
+    """The RqVae decoder (modules/rqvae.py:145-148: MLP chain ending in l2norm, modules/encoder.py:34)
+    fused with ReconstructionLoss (modules/loss.py:5-10): recon_b = |l2norm(MLP(e)_b) - x_b|^2 at
+    'high' matmul precision. Same as MLPFunction followed by L2NormReconFunction, except that the
+    row kernel's backward emits the output gradient already split (rq_l2norm_recon_bwd_split), so the
+    chain's last data-grad and weight-grad GEMMs take split operands (the wide kernel) without a
+    conversion pass. Gradients w.r.t. e and the weights (x is data)."""
+
+    @staticmethod
+    def forward(ctx, e, x, p: float, *weights):
+        x_in, rows, wsp, seeds = _mlp_prologue(e, p, weights)
+        pre, zs, hs = _mlp_forward(x_in, wsp, rows, p, seeds)
+        x2 = x.reshape(rows, -1).contiguous()
+        C = pre.shape[1]
+        recon = torch.empty((rows,), device=pre.device, dtype=torch.float32)
+        norms = torch.empty((rows,), device=pre.device, dtype=torch.float32)
+        call("rq_l2norm_recon_fwd", ptr(pre), ptr(x2), rows, C, ptr(recon), ptr(norms), stream_handle(pre.device))
+        ctx.n, ctx.p, ctx.seeds, ctx.eshape = len(weights), float(p), seeds, e.shape
+        ctx.save_for_backward(*_mlp_save(ctx, x_in, wsp, zs, hs), pre, x2, norms)
+        return recon.view(e.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, g_recon):
+        x_in, wsp, zs, hs, k = _mlp_load(ctx, ctx.n, ctx.saved_tensors)
+        pre, x2, norms = ctx.saved_tensors[k:k + 3]
+        rows, C = pre.shape
+        g = Split(torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16),
+                  torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16))
+        call("rq_l2norm_recon_bwd_split", ptr(pre), ptr(x2), ptr(norms), ptr(g_recon.contiguous()), rows, C, ptr(g.hi),
+             ptr(g.lo), stream_handle(pre.device))
+        de, dws = _mlp_backward(g, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[3:],
+                                ctx.needs_input_grad[0])
+        return (None if de is None else de.view(ctx.eshape), None, None, *dws)
+
+
+def mlp_l2norm_recon(e: torch.Tensor, x: torch.Tensor, weights, p: float = 0.0) -> torch.Tensor:
+    """recon_b = |l2norm(MLP(e)_b) - x_b|^2 (MLPL2ReconFunction); fp32 device tensors, split-operand
+    widths (mlp_fusable), x of the chain's output width."""
+    require_gpu(e, x, what="mlp_l2norm_recon")
+    return MLPL2ReconFunction.apply(e, x, float(p), *weights)
 
 
 class LinearFunction(torch.autograd.Function):
