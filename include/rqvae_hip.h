@@ -154,7 +154,8 @@ int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, i
  * [Dropout], ..., Linear): an operand is fp32 (X_lo == NULL) or pre-split, two bf16 planes
  * (X = hi, X_lo = lo) of the operand's shape; split operands need their contiguous axis and ld
  * % 8 == 0. The epilogue turns the tile into:
- *   0  C = A B^T                                                 (split-K allowed)
+ *   0  C = A B^T
+ *   3  C = A B^T + Z                                             (a residual add after a projection)
  *   1  C = z = A B^T, and H = split(Dropout_p(SiLU(z)))          (a hidden layer's forward)
  *   2  H = split(SiLU'(Z) * Dropout_p(A B^T)), C unused          (its pre-activation grad)
  * H_hi / H_lo: bf16 planes (M, N) of row stride ldh; Z: (M, N) of stride ldc. The dropout mask is
@@ -163,6 +164,17 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
                       void* workspace, size_t ws_bytes, void* stream);
+/* rq_gemm_bf16x3_ex with split-K for every epilogue and accumulation. When the output tiles cannot
+ * fill the GPU (e.g. the decoder's 1,280 future-token rows), K is split for any epilogue: the partials
+ * go to the workspace and a fixed-order reduction applies the epilogue (deterministic). accumulate = 1
+ * (plain epilogue only): C += A B^T — a weight gradient added straight into an existing .grad buffer
+ * (replaces autograd's AccumulateGrad add into data-parallel flat gradient buckets). Slab calls need
+ * ldc == N and workspace >= rq_gemm_bf16x3_workspace2(M, N, K, accumulate) bytes. */
+size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate);
+int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                       int accumulate, void* workspace, size_t ws_bytes, void* stream);
 
 /* Which kernel rq_gemm_bf16x3_ex runs for a call: 1 = the wide 256 x 256-tile kernel (both operands
  * split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile kernel; *splits (optional) = its split-K

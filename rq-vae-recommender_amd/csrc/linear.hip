@@ -484,7 +484,7 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #endif
 
 #ifndef RQ_X3_MIN_STAGES
-#define RQ_X3_MIN_STAGES 4   // split-K: k-stages per workgroup at least (fewer slabs to reduce)
+#define RQ_X3_MIN_STAGES 2   // split-K: k-stages per workgroup at least (fewer slabs to reduce)
 #endif
 
 #ifndef RQ_X3_INTERLEAVE
@@ -1021,13 +1021,71 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 #undef RQ_W_VM6
 #undef RQ_W_LGKM0
 
-// Elementwise split (weights once per step; 4 elements per thread per iteration, any n).
+// Split-K slab reduction with the GEMM's epilogue: element j of the (M, N) output (ldc == N) is the
+// fixed-order sum over s of P[s][j] (wave w sums s = w, w + 4, ...; the four wave partials are added
+// in wave order: deterministic, no atomics), then (ACC) plus the current C[j], then the epilogue of
+// x3_epi4 at (m, n) = (j / N, j % N). Lets every epilogue — SiLU fwd / bwd with dropout, residual
+// add, accumulation into an existing gradient — use split-K when the output tiles cannot fill the
+// chip (the decoder's 1,280 future-token rows: 40 tiles of 128 x 128).
+template <int EPI, bool DROP, bool ACC>
+__global__ void __launch_bounds__(256) x3_reduce_kernel(const float* __restrict__ P, int S, int64_t n, int N,
+                                                        float* __restrict__ C, X3Epilogue ep) {
+  ep.seed = epoch_seed(ep.seed);
+  __shared__ float4 part[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t j = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const bool ok = j < n;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    int s = wave;
+    for (; s + 12 < S; s += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+    }
+    for (; s < S; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  part[wave][lane] = a;
+  __syncthreads();
+  if (wave == 0 && ok) {
+    float4 r = part[0][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 v = part[w][lane];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    if constexpr (ACC) {
+      const float4 c = *reinterpret_cast<const float4*>(C + j);
+      r = make_float4(c.x + r.x, c.y + r.y, c.z + r.z, c.w + r.w);
+    }
+    x3_epi4<EPI, DROP>(r, (int)(j / N), (int)(j % N), N, C, C, N, ep);
+  }
+}
+
+// Elementwise split (weights once per step, a large chain input once per step). HBM-bound: 4 B
+// read + 2 x 2 B written per element. VEC: float4 loads and 8-B plane stores, 2 float4 in flight
+// per thread per iteration (n % 4 == 0, 16-B aligned x, 8-B aligned planes); else scalar.
+template <bool VEC>
 __global__ void __launch_bounds__(256) split_bf16x3_kernel(const float* __restrict__ x, int64_t n,
                                                            uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * 1024) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i + u < n) split_store1(x[i + u], hi + i + u, lo + i + u);
+  if constexpr (VEC) {
+    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+      const float4 a = reinterpret_cast<const float4*>(x)[i];
+      const float4 b = reinterpret_cast<const float4*>(x)[i + stride];
+      split_store4(a, hi + 4 * i, lo + 4 * i);
+      split_store4(b, hi + 4 * (i + stride), lo + 4 * (i + stride));
+    }
+    if (i < n4) split_store4(reinterpret_cast<const float4*>(x)[i], hi + 4 * i, lo + 4 * i);
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+      split_store1(x[i], hi + i, lo + i);
   }
 }
 
@@ -1058,6 +1116,17 @@ struct X3Plan {
 
 static int x3_slots() { return resident_slots() / 2 * kXWG; }
 
+#ifndef RQ_X3_SLAB_MB
+#define RQ_X3_SLAB_MB 64   // split-K: slab bytes (S x M x N fp32) allowed beyond RQ_X3_MAX_SPLIT slabs
+#endif
+// Split-K count cap: RQ_X3_MAX_SPLIT slabs, or more while the slabs stay within RQ_X3_SLAB_MB — the
+// small weight grads (e.g. 128 x 64 over 65,536 rows: one output tile) need hundreds of k chunks to
+// cover the chip, and their slabs are tiny.
+static int64_t x3_split_cap(int64_t M, int64_t N) {
+  const int64_t by_bytes = ((int64_t)RQ_X3_SLAB_MB << 20) / (4 * M * N);
+  return by_bytes > RQ_X3_MAX_SPLIT ? by_bytes : RQ_X3_MAX_SPLIT;
+}
+
 static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
   X3Plan p;
   p.tiles_n = (int)((N + kXT - 1) / kXT);
@@ -1068,7 +1137,7 @@ static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) 
     S = x3_slots() / p.tiles;
     const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
     if (S > max_s) S = max_s;
-    if (S > RQ_X3_MAX_SPLIT) S = RQ_X3_MAX_SPLIT;   // slab traffic of the reduction grows with S
+    if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);   // slab traffic of the reduction grows with S
     if (S < 1) S = 1;
   }
   int64_t chunk = (K + S - 1) / S;
@@ -1110,7 +1179,7 @@ static bool x3w_plan(int64_t M, int64_t N, int64_t K, bool allow_split, X3Plan* 
     S = cus / p->tiles;
     const int64_t max_s = K / (32 * RQ_X3W_MIN_STEPS);
     if (S > max_s) S = max_s;
-    if (S > RQ_X3_MAX_SPLIT) S = RQ_X3_MAX_SPLIT;
+    if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);
     if (S < 1) S = 1;
   }
   int64_t chunk = (K + S - 1) / S;
@@ -1128,7 +1197,7 @@ static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool
                        X3Plan* p) {
   const bool combo = epilogue == kEpiStore || (epilogue == kEpiSiluFwd && a_kc && b_kc) ||
                      (epilogue == kEpiSiluBwd && a_kc && !b_kc) || (epilogue == kEpiAdd && a_kc && b_kc);
-  return asp && bsp && combo && x3w_plan(M, N, K, epilogue == kEpiStore, p);
+  return asp && bsp && combo && x3w_plan(M, N, K, true, p);
 }
 
 }  // namespace rqhip
@@ -1176,20 +1245,29 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
 }
 
 
-size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) {
+// Slab bytes of a call: split-K slabs (S > 1), or one slab for an accumulating call (C += A B^T runs
+// through the slab reduction even unsplit).
+static size_t x3_workspace_bytes(int64_t M, int64_t N, int64_t K, bool accumulate) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   // the larger of the two kernels' split-K slabs (which one runs depends on the operand formats)
   const X3Plan p = x3_plan(M, N, K);
   X3Plan pw;
   int S = p.S;
   if (x3w_plan(M, N, K, true, &pw) && pw.S > S) S = pw.S;
-  return S > 1 ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
+  if (accumulate && S < 1) S = 1;
+  return (S > 1 || accumulate) ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
 }
 
-int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                      void* workspace, size_t ws_bytes, void* stream) {
+size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) { return x3_workspace_bytes(M, N, K, false); }
+
+size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate) {
+  return x3_workspace_bytes(M, N, K, accumulate != 0);
+}
+
+int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                       int accumulate, void* workspace, size_t ws_bytes, void* stream) {
   const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
   RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
                    epilogue <= 3,
@@ -1216,22 +1294,27 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
   hipStream_t s = (hipStream_t)stream;
   X3Epilogue ep{Z, H_hi, H_lo, ldh, 0u, 1.f, seed};
   dropout_params(p, &ep.thr, &ep.scale);
+  RQ_CHECK_ARG(!accumulate || epilogue == kEpiStore, "rq_gemm_bf16x3: accumulate needs the plain epilogue");
   if (K == 0) {
     RQ_CHECK_ARG(epilogue == kEpiStore, "rq_gemm_bf16x3: K == 0 needs the plain epilogue");
-    RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
+    if (!accumulate) RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
     return 0;
   }
-  X3Plan pl = x3_plan(M, N, K, epilogue == kEpiStore);
+  X3Plan pl = x3_plan(M, N, K);
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, &pw);
   if (wide) pl = pw;
+  // slab path: split-K partials (or the single product of an accumulating call) go to the workspace
+  // with the plain store, and x3_reduce_kernel applies the real epilogue
+  const bool slab = pl.S > 1 || accumulate;
   float* out = C;
-  if (pl.S > 1) {
+  if (slab) {
     const size_t need = (size_t)pl.S * (size_t)(M * N) * sizeof(float);
     RQ_CHECK_ARG(workspace != nullptr && ws_bytes >= need && ldc == N,
-                 "rq_gemm_bf16x3: split-K needs ldc == N and workspace %zu >= %zu bytes", ws_bytes, need);
+                 "rq_gemm_bf16x3: split-K / accumulate needs ldc == N and workspace %zu >= %zu bytes", ws_bytes, need);
     out = static_cast<float*>(workspace);
   }
+  const int epi_k = slab ? (int)kEpiStore : epilogue;   // the epilogue the GEMM kernel itself runs
   const dim3 grid((unsigned)(pl.per * 8)), block(256);
   const int64_t ldo = pl.S > 1 ? N : ldc;
   const int code = (a_kcontig ? 16 : 0) | (asp ? 8 : 0) | (b_kcontig ? 4 : 0) | (bsp ? 2 : 0);
@@ -1255,24 +1338,24 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                      K, pl.tiles_n, pl.tiles, pl.chunk, out, ldo, ep)
     const bool drop = ep.thr != 0;
     const int kc = (a_kcontig ? 2 : 0) | (b_kcontig ? 1 : 0);
-    if (epilogue == kEpiStore) {
+    if (epi_k == kEpiStore) {
       switch (kc) {
         case 3: RQ_X3W(true, true, kEpiStore, false); break;
         case 2: RQ_X3W(true, false, kEpiStore, false); break;
         case 1: RQ_X3W(false, true, kEpiStore, false); break;
         default: RQ_X3W(false, false, kEpiStore, false); break;
       }
-    } else if (epilogue == kEpiSiluFwd && kc == 3) {
+    } else if (epi_k == kEpiSiluFwd && kc == 3) {
       if (drop) RQ_X3W(true, true, kEpiSiluFwd, true); else RQ_X3W(true, true, kEpiSiluFwd, false);
-    } else if (epilogue == kEpiSiluBwd && kc == 2) {
+    } else if (epi_k == kEpiSiluBwd && kc == 2) {
       if (drop) RQ_X3W(true, false, kEpiSiluBwd, true); else RQ_X3W(true, false, kEpiSiluBwd, false);
-    } else if (epilogue == kEpiAdd && kc == 3) {
+    } else if (epi_k == kEpiAdd && kc == 3) {
       RQ_X3W(true, true, kEpiAdd, false);
     } else {
       launched = false;
     }
 #undef RQ_X3W
-  } else if (epilogue == kEpiStore) {
+  } else if (epi_k == kEpiStore) {
     switch (code) {
       // every layout with fp32 operands (the generic entry point)
       case 16 | 4: RQ_X3(true, false, true, false, kEpiStore); break;
@@ -1289,13 +1372,13 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
       case 2: RQ_X3(false, false, false, true, kEpiStore); break;
       default: launched = false;
     }
-  } else if (epilogue == kEpiSiluFwd) {
+  } else if (epi_k == kEpiSiluFwd) {
     switch (code) {
       case 16 | 4 | 2: RQ_X3(true, false, true, true, kEpiSiluFwd); break;
       case 16 | 8 | 4 | 2: RQ_X3(true, true, true, true, kEpiSiluFwd); break;
       default: launched = false;
     }
-  } else if (epilogue == kEpiSiluBwd) {
+  } else if (epi_k == kEpiSiluBwd) {
     switch (code) {
       case 16 | 2: RQ_X3(true, false, false, true, kEpiSiluBwd); break;
       case 16 | 8 | 2: RQ_X3(true, true, false, true, kEpiSiluBwd); break;
@@ -1312,12 +1395,29 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
   RQ_CHECK_ARG(launched, "rq_gemm_bf16x3: operand combination (a_kcontig %d, a_split %d, b_kcontig %d, b_split %d) "
                          "not built for epilogue %d", a_kcontig, (int)asp, b_kcontig, (int)bsp, epilogue);
   RQ_LAUNCH_CHECK("gemm_bf16x3_kernel");
-  if (pl.S > 1) {
+  if (slab) {
     const int64_t n = M * N;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(256), 0, s, out, pl.S, n, C);
-    RQ_LAUNCH_CHECK("wgrad_reduce_kernel(gemm_bf16x3)");
+    const dim3 rg((unsigned)((n / 4 + 63) / 64)), rb(256);
+    const bool drop = ep.thr != 0 && (epilogue == kEpiSiluFwd || epilogue == kEpiSiluBwd);
+#define RQ_X3R(EP, DR, AC) hipLaunchKernelGGL((x3_reduce_kernel<EP, DR, AC>), rg, rb, 0, s, out, pl.S, n, (int)N, C, ep)
+    switch (epilogue) {
+      case kEpiStore: if (accumulate) RQ_X3R(kEpiStore, false, true); else RQ_X3R(kEpiStore, false, false); break;
+      case kEpiSiluFwd: if (drop) RQ_X3R(kEpiSiluFwd, true, false); else RQ_X3R(kEpiSiluFwd, false, false); break;
+      case kEpiSiluBwd: if (drop) RQ_X3R(kEpiSiluBwd, true, false); else RQ_X3R(kEpiSiluBwd, false, false); break;
+      default: RQ_X3R(kEpiAdd, false, false); break;
+    }
+#undef RQ_X3R
+    RQ_LAUNCH_CHECK("x3_reduce_kernel");
   }
   return 0;
+}
+
+int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                      void* workspace, size_t ws_bytes, void* stream) {
+  return rq_gemm_bf16x3_ex2(A, A_lo, lda, a_kcontig, B, B_lo, ldb, b_kcontig, M, N, K, C, ldc, epilogue, Z, H_hi, H_lo,
+                            ldh, p, seed, 0, workspace, ws_bytes, stream);
 }
 
 int rq_gemm_x3w_enable(int enable) {
@@ -1331,7 +1431,7 @@ int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_sp
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, a_split, b_split, a_kcontig, b_kcontig, epilogue, &pw);
-  if (splits) *splits = wide ? pw.S : x3_plan(M, N, K, epilogue == kEpiStore).S;
+  if (splits) *splits = wide ? pw.S : x3_plan(M, N, K).S;
   return wide ? 1 : 0;
 }
 
@@ -1367,9 +1467,14 @@ int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, ui
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream) {
   RQ_CHECK_ARG(n >= 0 && (n == 0 || (x && hi && lo)), "rq_split_bf16x3: bad arguments");
   if (n == 0) return 0;
-  const int64_t blocks = (n + 1023) / 1024;
-  hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
-                     (hipStream_t)stream, x, n, hi, lo);
+  const bool vec = n % 4 == 0 && (uintptr_t)x % 16 == 0 && ((uintptr_t)hi | (uintptr_t)lo) % 8 == 0;
+  // vector path: 8 elements per thread per iteration; a grid of 8 x 256 workgroups keeps every CU busy
+  const int64_t blocks = vec ? (n / 4 + 511) / 512 : (n + 255) / 256;
+  const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
+  if (vec)
+    hipLaunchKernelGGL((split_bf16x3_kernel<true>), grid, dim3(256), 0, (hipStream_t)stream, x, n, hi, lo);
+  else
+    hipLaunchKernelGGL((split_bf16x3_kernel<false>), grid, dim3(256), 0, (hipStream_t)stream, x, n, hi, lo);
   RQ_LAUNCH_CHECK("split_bf16x3_kernel");
   return 0;
 }

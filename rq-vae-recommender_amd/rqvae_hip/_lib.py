@@ -48,6 +48,9 @@ _SIGS = {
     "rq_gemm_bf16x3": ([_P, _I64, _I, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I),
     "rq_gemm_bf16x3_ex": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
                            _U64, _P, _SZ, _P], _I),
+    "rq_gemm_bf16x3_workspace2": ([_I64, _I64, _I64, _I], _SZ),
+    "rq_gemm_bf16x3_ex2": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
+                            _U64, _I, _P, _SZ, _P], _I),
     "rq_gemm_bf16x3_choice": ([_I64, _I64, _I64, _I, _I, _I, _I, _I, _P], _I),
     "rq_gemm_x3w_enable": ([_I], _I),
     "rq_split_bf16x3": ([_P, _I64, _P, _P, _P], _I),

@@ -260,21 +260,24 @@ EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD, EPI_ADD = 0, 1, 2, 3
 _X3_WS = {}
 
 
-def _x3_workspace(M: int, N: int, K: int) -> int:
-    """Split-K slab bytes of rq_gemm_bf16x3 for a shape (host-only plan, memoised per shape)."""
-    key = (M, N, K)
+def _x3_workspace(M: int, N: int, K: int, accumulate: bool = False) -> int:
+    """Slab bytes of rq_gemm_bf16x3_ex2 for a shape (split-K partials, or the single slab of an
+    accumulating call; host-only plan, memoised per shape)."""
+    key = (M, N, K, accumulate)
     nb = _X3_WS.get(key)
     if nb is None:
-        nb = _X3_WS[key] = int(_lib.load().rq_gemm_bf16x3_workspace(M, N, K))
+        nb = _X3_WS[key] = int(_lib.load().rq_gemm_bf16x3_workspace2(M, N, K, int(accumulate)))
     return nb
 
 
 def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
-            Z: torch.Tensor = None, p: float = 0.0, seed: int = 0):
-    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex). a / b: fp32
+            Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
+            accumulate: bool = False):
+    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex2). a / b: fp32
     tensors or Split. Returns C (EPI_STORE; EPI_ADD: A B^T + Z), (C, H) (EPI_SILU_FWD: C = z,
     H = split(Dropout(SiLU(z)))) or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split
-    of shape (M, N)."""
+    of shape (M, N). `out`: the (M, N) contiguous fp32 destination of C; `accumulate` (EPI_STORE
+    only): out += A B^T."""
     def desc(t):
         if isinstance(t, Split):
             return t.hi, t.lo, t.hi.shape[-1], 1
@@ -283,16 +286,21 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     ah, al, lda, asp = desc(a)
     bh, bl, ldb, bsp = desc(b)
     dev = ah.device
-    C = None if epilogue == EPI_SILU_BWD else torch.empty((M, N), device=dev, dtype=torch.float32)
+    if accumulate and (epilogue != EPI_STORE or out is None):
+        raise RqHipError("gemm_x3: accumulate needs the plain epilogue and an output tensor")
+    if out is not None and not (out.is_contiguous() and out.dtype == torch.float32 and out.shape == (M, N)):
+        raise RqHipError(f"gemm_x3: out must be a contiguous fp32 ({M}, {N}) tensor")
+    C = None if epilogue == EPI_SILU_BWD else (out if out is not None else
+                                                torch.empty((M, N), device=dev, dtype=torch.float32))
     H = None
     if epilogue in (EPI_SILU_FWD, EPI_SILU_BWD):
         H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
-    nbytes = _x3_workspace(M, N, K) if epilogue == EPI_STORE else 0
+    nbytes = _x3_workspace(M, N, K, accumulate)
     ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8) if nbytes else None
-    args = ("rq_gemm_bf16x3_ex", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
+    args = ("rq_gemm_bf16x3_ex2", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
             M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
-            float(p), int(seed), ptr(ws), nbytes, stream_handle(dev))
+            float(p), int(seed), int(accumulate), ptr(ws), nbytes, stream_handle(dev))
     if TIMER.wants("gemm_bf16x3"):
         TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call, *args)
     else:

@@ -92,7 +92,8 @@ def test_x3w_fused_epilogues_equal_x3_kernel(device, wide_on, p):
     """SiLU forward (C = z, H = split(Dropout(SiLU(z)))), SiLU backward and the residual add: no
     split-K in either kernel, so wide and 128-tile results must be identical bit for bit."""
     ops = wide_on
-    M, K, N = 8192, 768, 512
+    M, K, N = 16384, 768, 512   # enough tiles that neither kernel splits K (split-K reduces in another order)
+    assert all(ops.gemm_x3_choice(16384, n, k, True, True, True, True)[1] == 1 for n, k in ((512, 768), (768, 512)))
     gen = torch.Generator(device=device).manual_seed(3)
     x32 = torch.randn(M, K, generator=gen, device=device)
     x = ops.split_bf16x3(x32)
