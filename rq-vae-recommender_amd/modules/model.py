@@ -25,6 +25,7 @@ from modules.transformer.model import TransformerEncoderDecoder
 from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
 from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged, row_counts
 from rqvae_hip import gemm_tuning
+from rqvae_hip import ops as hip_ops
 
 # As the reference (modules/model.py:27): fp32 matmuls at 'high' precision (split-bf16 GEMM on
 # gfx950, rqvae_hip.ops.gemm_bf16x3); 'highest' restores the exact-fp32 library path.
@@ -111,8 +112,16 @@ class EncoderDecoderRetrievalModel(nn.Module):
         return self.transformer(x=transformer_input, context=transformer_context, padding_mask=batch.seq_mask,
                                 jagged=True)
 
+    def _gemm_weights(self):
+        return [m.weight for m in self.modules() if isinstance(m, nn.Linear)]
+
     def forward(self, batch: TokenizedSeqBatch) -> ModelOutput:
         B = batch.seq_mask.shape[0]
+        # every Linear weight split once per forward in a few launches (no-op at 'highest')
+        with hip_ops.weight_split_scope(self._gemm_weights()):
+            return self._forward(batch, B)
+
+    def _forward(self, batch: TokenizedSeqBatch, B: int) -> ModelOutput:
         trnsf_out = self._predict(batch)
         if self.training or not self.enable_generation:
             predict_out = self.out_proj(jagged_to_flattened_tensor(trnsf_out))

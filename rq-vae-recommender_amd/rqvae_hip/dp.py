@@ -110,6 +110,33 @@ def all_gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
     return torch.cat([p[:b - a] for p, (a, b) in zip(parts, spans)], 0)
 
 
+# Parameters whose weight gradient a HIP op may add straight into the flat bucket (C += g^T x in the
+# GEMM's slab reduction) instead of returning it to autograd, which would run an AccumulateGrad add
+# kernel per parameter per step into the flat view. id(param) -> (flat view, hook).
+_DIRECT = {}
+
+
+def direct_grad(p) -> Optional[torch.Tensor]:
+    """The flat-bucket view p's gradient may be accumulated into in place (GradBuckets with flat
+    buffers, p.grad currently that view), else None. The caller adds its gradient into the view,
+    returns None to autograd for p and calls direct_grad_done(p)."""
+    e = _DIRECT.get(id(p))
+    if e is None or torch.is_grad_enabled():
+        return None
+    g = p.grad
+    if g is None or g.data_ptr() != e[0].data_ptr():
+        return None
+    return e[0]
+
+
+def direct_grad_done(p) -> None:
+    """What AccumulateGrad's post-accumulate hook would do for p (GradBuckets usage tracking and the
+    overlapped exchange)."""
+    e = _DIRECT.get(id(p))
+    if e is not None:
+        e[1](p)
+
+
 class GradBuckets:
     """Flat gradient buffers + bucketed async all-reduce for a module's parameters."""
 
@@ -153,8 +180,10 @@ class GradBuckets:
                 if cur:
                     self._make_bucket(cur, dt, dev)
         for bi, b in enumerate(self.buckets):   # usage tracking (+ overlapped launches when overlap)
-            for p in b["params"]:
-                p.register_post_accumulate_grad_hook(self._make_hook(bi))
+            for p, v in zip(b["params"], b["views"]):
+                hook = self._make_hook(bi)
+                p.register_post_accumulate_grad_hook(hook)
+                _DIRECT[id(p)] = (v, hook)
 
     def _make_bucket(self, ps, dt, dev):
         n = sum(p.numel() for p in ps)

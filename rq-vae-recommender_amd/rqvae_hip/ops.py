@@ -8,6 +8,7 @@
 
 All kernels run on torch's current HIP stream; tensors must be on the GPU (no CPU path).
 """
+import contextlib
 import math
 from typing import NamedTuple
 
@@ -256,6 +257,60 @@ def split_bf16x3_many(xs) -> list:
     return out
 
 
+_WSPLIT = {}   # id(weight) -> (Split, weight): the current forward's pre-split weights (weight_split_scope)
+
+
+@contextlib.contextmanager
+def weight_split_scope(params):
+    """Split every GEMM weight among `params` (2-D fp32 device tensors, both dims % 8) once, in a few
+    multi-tensor launches (rq_split_bf16x3_multi, 16 per launch), for the forward run inside the
+    scope: the Linear / MLP ops take their split operand from here instead of one split launch per
+    weight per call (the decoder: ~32 -> 3 launches per step). Only at matmul precision 'high'."""
+    ws = [p for p in params if p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 and p.shape[0] % 8 == 0
+          and p.shape[1] % 8 == 0] if matmul_high() else []
+    prev = dict(_WSPLIT)
+    with torch.no_grad():
+        for i in range(0, len(ws), 16):
+            for w, sp in zip(ws[i:i + 16], split_bf16x3_many([w.detach() for w in ws[i:i + 16]])):
+                _WSPLIT[id(w)] = (sp, w)
+    try:
+        yield
+    finally:
+        _WSPLIT.clear()
+        _WSPLIT.update(prev)
+
+
+def split_weight(w: torch.Tensor) -> Split:
+    """w's split planes: from the enclosing weight_split_scope, else one split launch."""
+    e = _WSPLIT.get(id(w))
+    return e[0] if e is not None and e[1] is w else split_bf16x3(w)
+
+
+def split_weights(weights) -> list:
+    """split_weight of each, with the uncached ones split in one multi-tensor launch."""
+    out = [(_WSPLIT.get(id(w)) or (None, None)) for w in weights]
+    miss = [i for i, (sp, w) in enumerate(out) if sp is None or w is not weights[i]]
+    res = [sp for sp, _ in out]
+    for j in range(0, len(miss), 16):
+        idx = miss[j:j + 16]
+        for i, sp in zip(idx, split_bf16x3_many([weights[i] for i in idx])):
+            res[i] = sp
+    return res
+
+
+def _wgrad_into(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: int):
+    """dW = g^T inp for `weight` (split-bf16 GEMM): added straight into weight's flat gradient bucket
+    when dp.GradBuckets owns one (returns None: autograd must not accumulate it again), else a new
+    (O, I) tensor for autograd."""
+    from . import dp
+    sink = dp.direct_grad(weight)
+    if sink is None:
+        return gemm_x3(g, g_kc, inp, inp_kc, O, I, rows)
+    gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True)
+    dp.direct_grad_done(weight)
+    return None
+
+
 EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD, EPI_ADD = 0, 1, 2, 3
 _X3_WS = {}
 
@@ -359,8 +414,9 @@ def _mlp_forward(a, wsp, rows: int, p: float, seeds):
     return out, zs, hs
 
 
-def _mlp_backward(gcur, x_in, wsp, zs, hs, rows: int, p: float, seeds, need_w, need_x: bool):
-    """The chain's backward from the output grad gcur (fp32 or Split): (dx fp32 or None, [dW])."""
+def _mlp_backward(gcur, x_in, wsp, zs, hs, rows: int, p: float, seeds, need_w, need_x: bool, weights):
+    """The chain's backward from the output grad gcur (fp32 or Split): (dx fp32 or None, [dW]); a
+    weight grad added straight into its flat gradient bucket comes back as None (_wgrad_into)."""
     n = len(wsp)
     dws = [None] * n
     dx = None
@@ -368,7 +424,7 @@ def _mlp_backward(gcur, x_in, wsp, zs, hs, rows: int, p: float, seeds, need_w, n
         O, I = wsp[i].hi.shape
         inp = x_in if i == 0 else hs[i - 1]
         if need_w[i]:
-            dws[i] = gemm_x3(gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
+            dws[i] = _wgrad_into(weights[i], gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
         if i > 0:
             gcur = gemm_x3(gcur, True, wsp[i], False, rows, I, O, EPI_SILU_BWD, Z=zs[i - 1], p=p, seed=seeds[i - 1])
         elif need_x:
@@ -396,7 +452,7 @@ def _mlp_prologue(x, p: float, weights):
     n = len(weights)
     x2 = x.reshape(-1, weights[0].shape[1]).contiguous()
     rows = x2.shape[0]
-    wsp = split_bf16x3_many(weights) if len(weights) <= 16 else [split_bf16x3(w) for w in weights]
+    wsp = split_weights(weights)
     seeds = [next_seed() if p > 0 else 0 for _ in range(n - 1)]
     x_in = split_bf16x3(x2) if _presplit_input(rows, weights, n) else x2
     return x_in, rows, wsp, seeds
@@ -416,7 +472,7 @@ class MLPFunction(torch.autograd.Function):
     def forward(ctx, x, p: float, *weights):
         x_in, rows, wsp, seeds = _mlp_prologue(x, p, weights)
         out, zs, hs = _mlp_forward(x_in, wsp, rows, p, seeds)
-        ctx.n, ctx.p, ctx.seeds, ctx.xshape = len(weights), float(p), seeds, x.shape
+        ctx.n, ctx.p, ctx.seeds, ctx.xshape, ctx.weights = len(weights), float(p), seeds, x.shape, weights
         ctx.save_for_backward(*_mlp_save(ctx, x_in, wsp, zs, hs))
         return out.view(*x.shape[:-1], weights[-1].shape[0])
 
@@ -426,7 +482,8 @@ class MLPFunction(torch.autograd.Function):
         rows = (x_in.hi if ctx.x_split else x_in).shape[0]
         gcur = g.reshape(rows, -1).contiguous()
         dx, dws = _mlp_backward(gcur, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[2:],
-                                ctx.needs_input_grad[0])
+                                ctx.needs_input_grad[0], ctx.weights)
+        ctx.weights = None
         return (None if dx is None else dx.view(ctx.xshape), None, *dws)
 
 
@@ -452,7 +509,7 @@ class MLPL2ReconFunction(torch.autograd.Function):
         recon = torch.empty((rows,), device=pre.device, dtype=torch.float32)
         norms = torch.empty((rows,), device=pre.device, dtype=torch.float32)
         call("rq_l2norm_recon_fwd", ptr(pre), ptr(x2), rows, C, ptr(recon), ptr(norms), stream_handle(pre.device))
-        ctx.n, ctx.p, ctx.seeds, ctx.eshape = len(weights), float(p), seeds, e.shape
+        ctx.n, ctx.p, ctx.seeds, ctx.eshape, ctx.weights = len(weights), float(p), seeds, e.shape, weights
         ctx.save_for_backward(*_mlp_save(ctx, x_in, wsp, zs, hs), pre, x2, norms)
         return recon.view(e.shape[:-1])
 
@@ -466,7 +523,8 @@ class MLPL2ReconFunction(torch.autograd.Function):
         call("rq_l2norm_recon_bwd_split", ptr(pre), ptr(x2), ptr(norms), ptr(g_recon.contiguous()), rows, C, ptr(g.hi),
              ptr(g.lo), stream_handle(pre.device))
         de, dws = _mlp_backward(g, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[3:],
-                                ctx.needs_input_grad[0])
+                                ctx.needs_input_grad[0], ctx.weights)
+        ctx.weights = None
         return (None if de is None else de.view(ctx.eshape), None, None, *dws)
 
 
@@ -486,6 +544,7 @@ class LinearFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
+        ctx.weight = weight
         ctx.has_bias = bias is not None
         ctx.high = matmul_high()
         O, I = weight.shape
@@ -493,7 +552,7 @@ class LinearFunction(torch.autograd.Function):
         if ctx.high and x.numel() > 0:
             x2 = x.reshape(-1, I)
             if I % 8 == 0:   # split the weight once: forward and data grad read it without converting
-                ctx.wsp = split_bf16x3(weight)
+                ctx.wsp = split_weight(weight)
                 y = gemm_x3(x2, True, ctx.wsp, True, x2.shape[0], O, I)
             else:
                 y = linear_fwd_high(x2, weight)
@@ -518,13 +577,15 @@ class LinearFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             x2 = x.reshape(-1, I)
             if high:
-                dW = linear_wgrad_high(g2, x2)
+                if ctx.needs_input_grad[1]:
+                    dW = _wgrad_into(ctx.weight, g2.contiguous(), False, x2.contiguous(), False, O, I, g2.shape[0])
                 db = g2.sum(0) if ctx.has_bias else None
             elif _wgrad_choice(g2, x2, ctx.has_bias) == "hip":
                 dW, db = linear_wgrad(g2, x2, ctx.has_bias)
             else:   # library GEMM: small row counts, or measured faster for this shape
                 dW = g2.t() @ x2
                 db = g2.sum(0) if ctx.has_bias else None
+        ctx.weight = None
         return gx, dW, db if ctx.has_bias else None
 
 
@@ -538,10 +599,10 @@ class LinearAddFunction(torch.autograd.Function):
     def forward(ctx, x, weight, r):
         O, I = weight.shape
         x2 = x.reshape(-1, I)
-        wsp = split_bf16x3(weight)
+        wsp = split_weight(weight)
         y = gemm_x3(x2, True, wsp, True, x2.shape[0], O, I, EPI_ADD, Z=r.reshape(-1, O).contiguous())
         ctx.save_for_backward(x, weight)
-        ctx.wsp = wsp
+        ctx.wsp, ctx.weight = wsp, weight
         return y.view(*x.shape[:-1], O)
 
     @staticmethod
@@ -554,7 +615,9 @@ class LinearAddFunction(torch.autograd.Function):
             gx = gemm_x3(g2, True, ctx.wsp, False, g2.shape[0], I, O).view(x.shape)
         ctx.wsp = None
         if ctx.needs_input_grad[1]:
-            dW = linear_wgrad_high(g2, x.reshape(-1, I))
+            dW = _wgrad_into(ctx.weight, g2.contiguous(), False, x.reshape(-1, I).contiguous(), False, O, I,
+                             g2.shape[0])
+        ctx.weight = None
         return gx, dW, g if ctx.needs_input_grad[2] else None
 
 
