@@ -103,6 +103,13 @@ int rq_rmsnorm_dropout_fwd(const float* x, const float* w, int64_t B, int64_t D,
 int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
                            float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
                            void* stream);
+/* rq_rmsnorm_dropout_bwd with two fusions: gres (NULL or B x D) is added to gx — the gradient that
+ * reaches x along the residual stream (modules/transformer/model.py:75-82: x feeds both the norm and
+ * the residual add; autograd would sum the two in a separate pass) — and accumulate_gw = 1 adds the
+ * weight gradient into gw instead of overwriting it (a flat data-parallel gradient bucket). */
+int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
+                            void* workspace, size_t ws_bytes, void* stream);
 
 /* Elementwise dropout fusions over n fp32 elements (n % 4 == 0, 16-byte aligned), same mask
  * generator as above (element index = position in the buffer):

@@ -557,6 +557,231 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
   store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
 }
 
+// ------------------------------------------------------------------------ short sequences
+// Short-sequence forms (the decoder's Amazon contexts, <= 81 tokens, and its 5 future tokens): one
+// workgroup per (sequence, head) stages the head's WHOLE key range (forward, dQ) or query range (dK/dV)
+// through LDS in a single round trip — every load of the stage in flight at once, one barrier — and
+// its NW waves then run their 16-row tiles (wave w: tiles w, w + NW, ...) against every staged tile.
+// The chunked kernels above stage 32 rows per round trip and re-stage K/V once per 32-query
+// workgroup; at n ~ 45 that is 2-3 serial round trips per workgroup and 2-3 workgroups per head.
+// CH = staged rows (>= the longest range, multiple of 16, <= 128).
+// Stage rows [0, CH) of a strided source (rows >= n zero) into LDS [CH][HD+4] with NT threads, in
+// pieces of at most 8 float4 per thread per source (a one-wave workgroup staging 96 rows at once would
+// hold 24 float4 per source in VGPRs and drop to one wave per SIMD).
+template <int HD, int NT, int CH>
+__device__ __forceinline__ void stage2(const float* __restrict__ a, int64_t sa, const float* __restrict__ b, int64_t sb,
+                                       int n, float* da, float* db, int tid) {
+  constexpr int PIECE = CH * (HD / 4) <= 8 * NT ? CH : (8 * NT) / (HD / 4);
+  static_assert(CH % PIECE == 0, "piece");
+#pragma unroll
+  for (int r0 = 0; r0 < CH; r0 += PIECE) {
+    RowStage<HD, NT, PIECE> sta, stb;
+    sta.load(a, sa, r0, n, tid);
+    stb.load(b, sb, r0, n, tid);
+    sta.store(da + r0 * (HD + 4), tid);
+    stb.store(db + r0 * (HD + 4), tid);
+  }
+}
+
+template <int NTL, typename F>
+__device__ __forceinline__ void dispatch_short(int nt, F& f) {
+  switch (nt) {
+    case 1: f.template run<1, true>(); break;
+    case 2: if constexpr (NTL >= 2) f.template run<2, true>(); break;
+    case 3: if constexpr (NTL >= 3) f.template run<3, true>(); break;
+    case 4: if constexpr (NTL >= 4) f.template run<4, true>(); break;
+    case 5: if constexpr (NTL >= 5) f.template run<5, true>(); break;
+    case 6: if constexpr (NTL >= 6) f.template run<6, true>(); break;
+    case 7: if constexpr (NTL >= 7) f.template run<7, true>(); break;
+    case 8: if constexpr (NTL >= 8) f.template run<8, true>(); break;
+    default: break;
+  }
+}
+
+template <int HD, int NW, int CH>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_short_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
+  constexpr int LD = HD + 4, DT = HD / 16, NTL = CH / 16;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
+  float* K_s = smem;
+  float* V_s = smem + CH * LD;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(out, so, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  stage2<HD, 64 * NW, CH>(k + k0 * sk + hh * HD, sk, v + k0 * sv + hh * HD, sv, lk, K_s, V_s, tid);
+  __syncthreads();
+  const float sl2 = scale * kLog2e;
+  for (int qt = wave; qt * 16 < lq; qt += NW) {
+    const int qb = qt * 16, qi = qb + (lane & 15);
+    const bool qv = qi < lq;
+    float qf[HD / 4];
+    load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+    f32x4 o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    const int kend = causal ? min(lk, qb + 16) : lk;
+    const int nt = __builtin_amdgcn_readfirstlane((kend + 15) >> 4);
+    FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, lk, qi, causal, sl2, &m, &l, o};
+    dispatch_short<NTL>(nt, fc);
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qv) {
+      store_rowT<HD>(out + (q0 + qi) * so + hh * HD, o, l > 0.f ? 1.f / l : 0.f, lane);
+      if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (m + log2f(l)) * kLn2 : 0.f;
+    }
+  }
+}
+
+template <int HD, int NW, int CH>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_dq_short_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
+    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ delta_out) {
+  constexpr int LD = HD + 4, DT = HD / 16, NTL = CH / 16;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
+  float* K_s = smem;
+  float* V_s = smem + CH * LD;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  stage2<HD, 64 * NW, CH>(k + k0 * sk + hh * HD, sk, v + k0 * sv + hh * HD, sv, lk, K_s, V_s, tid);
+  __syncthreads();
+  const float sl2 = scale * kLog2e;
+  for (int qt = wave; qt * 16 < lq; qt += NW) {
+    const int qb = qt * 16, qi = qb + (lane & 15);
+    const bool qv = qi < lq;
+    const int64_t qrow = q0 + (qv ? qi : 0);
+    float qf[HD / 4], dof[HD / 4];
+    load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv, qf);
+    load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv, dof);
+    float delta = 0.f;
+    {
+      float of[HD / 4];
+      load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+#pragma unroll
+      for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+      delta += __shfl_xor(delta, 16, 64);
+      delta += __shfl_xor(delta, 32, 64);
+      if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
+    }
+    f32x4 acc[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kend = causal ? min(lk, qb + 16) : lk;
+    const int nt = __builtin_amdgcn_readfirstlane((kend + 15) >> 4);
+    DqChunk<HD> fc{K_s, V_s, qf, dof, lane, 0, lk, qi, causal, sl2,
+                   qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f, delta, acc};
+    dispatch_short<NTL>(nt, fc);
+    if (qv) store_rowT<HD>(dq + (q0 + qi) * sdq + hh * HD, acc, scale, lane);
+  }
+}
+
+template <int HD, int NW, int CH>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_short_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
+    const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dk, int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk) {
+  constexpr int LD = HD + 4, DT = HD / 16, NTL = CH / 16;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD + 2 * CH];
+  float* Q_s = smem;
+  float* O_s = smem + CH * LD;   // dO
+  float* lse_s = O_s + CH * LD;
+  float* dl_s = lse_s + CH;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[b], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[b], Tk, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lk <= 0) return;
+  for (int r = tid; r < CH; r += 64 * NW) {
+    const bool ok = r < lq;
+    lse_s[r] = ok ? lse[(int64_t)hh * Tq + q0 + r] * kLog2e : 0.f;
+    dl_s[r] = ok ? delta[(int64_t)hh * Tq + q0 + r] : 0.f;
+  }
+  stage2<HD, 64 * NW, CH>(q + q0 * sq + hh * HD, sq, dout + q0 * sdo + hh * HD, sdo, lq, Q_s, O_s, tid);
+  __syncthreads();
+  const float sl2 = scale * kLog2e;
+  const int nqt = (lq + 15) >> 4;
+  for (int kt = wave; kt * 16 < lk; kt += NW) {
+    const int kb = kt * 16, kj = kb + (lane & 15);
+    const bool kv = kj < lk;
+    const int64_t krow = k0 + (kv ? kj : 0);
+    float kf[HD / 4], vf[HD / 4];
+    load_frag<HD>(k + krow * sk + hh * HD + g * (HD / 4), kv, kf);
+    load_frag<HD>(v + krow * sv + hh * HD + g * (HD / 4), kv, vf);
+    f32x4 dka[DT], dva[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    const int t0 = __builtin_amdgcn_readfirstlane(causal ? (kb >> 4) : 0);   // query tiles wholly before the keys
+    const int nt = __builtin_amdgcn_readfirstlane(nqt - t0);
+    DkdvChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, lane, 0, t0, lq, kj, causal, sl2, dka, dva};
+    dispatch_short<NTL>(nt, fc);
+    if (kv) {
+      store_rowT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, lane);
+      store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
+    }
+  }
+}
+
+#ifndef RQ_ATTN_SHORT
+#define RQ_ATTN_SHORT 1   // 0: the chunked kernels for every length (A/B switch)
+#endif
+#ifndef RQ_ATTN_SHORT_MAX_STAGED
+#define RQ_ATTN_SHORT_MAX_STAGED 32   // longest staged range served by the short forms (A/B: 32 / 128)
+#endif
+constexpr int kShortMax = 128;   // longest staged range of the short forms
+
+// (waves, staged rows) of a short-form launch whose tiles run over `rows` (queries for fwd / dQ, keys
+// for dK/dV) against a staged range of `staged` rows; false when the chunked kernels serve it
+static bool short_plan(int64_t rows, int64_t staged, int* nw, int* ch) {
+  if (!RQ_ATTN_SHORT || rows > kShortMax || staged > kShortMax) return false;
+  // Measured on MI355X (decoder Amazon step, rocprofv3): the short forms win where the staged range
+  // is one 32-row chunk (decoder self-attention 5 x 5: fwd 11.6 -> 6.4 us, dQ 15.6 -> 8.9 us; the
+  // cross-attention dK/dV over 5 staged queries 41 -> 24 us) and lose at 96 staged rows (encoder
+  // self-attention, n <= 81: fwd 35 -> 39 us, dQ 54 -> 59 us, dK/dV 41 -> 64 us: 52 KB of LDS per
+  // workgroup leaves 3 workgroups per CU, and a one-wave workgroup would hold it alone), so longer
+  // staged ranges keep the chunked kernels.
+  if (staged > RQ_ATTN_SHORT_MAX_STAGED) return false;
+  *nw = rows <= 16 ? 1 : 4;
+  *ch = staged <= 32 ? 32 : (staged <= 64 ? 64 : (staged <= 96 ? 96 : 128));
+  return true;
+}
+
+#define RQ_SHORT_SWITCH(NW_, CH_, LAUNCH)                          \
+  do {                                                           \
+    if ((NW_) == 1) {                                            \
+      LAUNCH(1, 32);                                             \
+    } else {                                                     \
+      switch (CH_) {                                             \
+        case 32: LAUNCH(4, 32); break;                           \
+        case 64: LAUNCH(4, 64); break;                           \
+        case 96: LAUNCH(4, 96); break;                           \
+        default: LAUNCH(4, 128); break;                          \
+      }                                                          \
+    }                                                            \
+  } while (0)
+
 // Waves per workgroup by the longest row count: 16 rows per wave; short sequences (the Amazon
 // decoder's contexts <= 81 tokens, its 5-6 future tokens) use narrow workgroups so few waves idle
 // on padding, long ones (ML-32M <= 801, C5 <= 1281) share each staged 64-row chunk between 4 waves.
@@ -572,9 +797,22 @@ static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const fl
 }
 
 template <int HD>
-static void launch_fwd(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
+static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q, int64_t sq,
+                       const float* k,
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
                        float scale, float* out, int64_t so, float* lse, int64_t Tq) {
+  if constexpr (HD == 64) {
+    int nw = 0, ch = 0;
+    if (short_plan(max_q, max_k, &nw, &ch)) {
+      const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
+#define RQ_FS(NW_, CH_)                                                                                            \
+  hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NW_, CH_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, cq, ck, \
+                     causal, scale, out, so, lse, Tq)
+      RQ_SHORT_SWITCH(nw, ch, RQ_FS);
+#undef RQ_FS
+      return;
+    }
+  }
   switch (waves_for(max_q)) {
     case 1: fwd_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
     case 2: fwd_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
@@ -603,17 +841,54 @@ static void dkdv_nw(int64_t B, int64_t H, int64_t max_k, hipStream_t st, const f
 }
 
 template <int HD>
+static void launch_dq_chunked(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq,
+                              const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
+                              const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq,
+                              const int64_t* ck, int causal, float scale, float* dq, int64_t sdq, float* delta) {
+  switch (waves_for(max_q)) {
+    case 1: dq_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
+    case 2: dq_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
+    default: dq_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
+  }
+}
+
+template <int HD>
 static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q, int64_t sq,
                        const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
                        const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck,
                        int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv,
                        int64_t Tk, float* delta) {
   // dQ pass first: it also writes delta_q = dO.O, which the dK/dV pass reads per query chunk
-  switch (waves_for(max_q)) {
-    case 1: dq_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
-    case 2: dq_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
-    default: dq_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta); break;
+  bool dq_done = false, kv_done = false;
+  if constexpr (HD == 64) {
+    int nw = 0, ch = 0;
+    const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
+    if (short_plan(max_q, max_k, &nw, &ch)) {
+#define RQ_DQS(NW_, CH_)                                                                                              \
+  hipLaunchKernelGGL((attn_bwd_dq_short_kernel<HD, NW_, CH_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, \
+                     dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta)
+      RQ_SHORT_SWITCH(nw, ch, RQ_DQS);
+#undef RQ_DQS
+      dq_done = true;
+    }
+    if (short_plan(max_k, max_q, &nw, &ch)) {
+      if (!dq_done) {   // the dK/dV pass reads delta: chunked dQ first
+        launch_dq_chunked<HD>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq,
+                              sdq, delta);
+        dq_done = true;
+      }
+#define RQ_KVS(NW_, CH_)                                                                                                \
+  hipLaunchKernelGGL((attn_bwd_dkdv_short_kernel<HD, NW_, CH_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, dout, \
+                     sdo, lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk)
+      RQ_SHORT_SWITCH(nw, ch, RQ_KVS);
+#undef RQ_KVS
+      kv_done = true;
+    }
   }
+  if (!dq_done)
+    launch_dq_chunked<HD>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq,
+                          delta);
+  if (kv_done) return;
   switch (waves_for(max_k)) {
     case 1: dkdv_nw<HD, 1>(B, H, max_k, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk); break;
     case 2: dkdv_nw<HD, 2>(B, H, max_k, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta, Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk); break;
@@ -642,10 +917,10 @@ int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
-    case 16: launch_fwd<16>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 32: launch_fwd<32>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 64: launch_fwd<64>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 128: launch_fwd<128>(B, H, max_q, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_fwd");
   return 0;

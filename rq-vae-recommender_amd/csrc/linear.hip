@@ -1099,13 +1099,19 @@ struct SplitMulti {
   int count;
 };
 
+// VEC: every tensor's element count % 4 == 0 and its pointers aligned (16 B x, 8 B planes): one float4
+// and two 8-B plane stores per thread per iteration (start[] then counts float4 units); else scalar.
+template <bool VEC>
 __global__ void __launch_bounds__(256) split_bf16x3_multi_kernel(SplitMulti sm) {
   const int64_t total = sm.start[sm.count];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     int t = 0;
     while (t + 1 < sm.count && i >= sm.start[t + 1]) ++t;
     const int64_t j = i - sm.start[t];
-    split_store1(sm.x[t][j], sm.hi[t] + j, sm.lo[t] + j);
+    if constexpr (VEC)
+      split_store4(reinterpret_cast<const float4*>(sm.x[t])[j], sm.hi[t] + 4 * j, sm.lo[t] + 4 * j);
+    else
+      split_store1(sm.x[t][j], sm.hi[t] + j, sm.lo[t] + j);
   }
 }
 
@@ -1448,17 +1454,24 @@ int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, ui
   SplitMulti sm;
   sm.count = count;
   sm.start[0] = 0;
+  bool vec = true;
   for (int t = 0; t < count; ++t) {
     RQ_CHECK_ARG(n[t] >= 0 && (n[t] == 0 || (x[t] && hi[t] && lo[t])), "rq_split_bf16x3_multi: bad tensor %d", t);
+    vec = vec && n[t] % 4 == 0 && (uintptr_t)x[t] % 16 == 0 && ((uintptr_t)hi[t] | (uintptr_t)lo[t]) % 8 == 0;
+  }
+  for (int t = 0; t < count; ++t) {
     sm.x[t] = x[t];
     sm.hi[t] = hi[t];
     sm.lo[t] = lo[t];
-    sm.start[t + 1] = sm.start[t] + n[t];
+    sm.start[t + 1] = sm.start[t] + (vec ? n[t] / 4 : n[t]);
   }
   if (count == 0 || sm.start[count] == 0) return 0;
   const int64_t blocks = (sm.start[count] + 255) / 256;
-  hipLaunchKernelGGL(split_bf16x3_multi_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0,
-                     (hipStream_t)stream, sm);
+  const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
+  if (vec)
+    hipLaunchKernelGGL((split_bf16x3_multi_kernel<true>), grid, dim3(256), 0, (hipStream_t)stream, sm);
+  else
+    hipLaunchKernelGGL((split_bf16x3_multi_kernel<false>), grid, dim3(256), 0, (hipStream_t)stream, sm);
   RQ_LAUNCH_CHECK("split_bf16x3_multi_kernel");
   return 0;
 }

@@ -142,7 +142,8 @@ template <int VPL>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ rstd, const float* __restrict__ gy,
                                                           int64_t B, int D, uint32_t thr, float dscale, uint64_t seed,
-                                                          float* __restrict__ gx, float* __restrict__ gw_part) {
+                                                          const float* __restrict__ gres, float* __restrict__ gx,
+                                                          float* __restrict__ gw_part) {
   seed = epoch_seed(seed);
   __shared__ float4 part[4][VPL * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -184,9 +185,13 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
     for (int v = 0; v < VPL; ++v) {
       const int c = (v * 64 + lane) * 4;
       if (c >= D) continue;
-      *reinterpret_cast<float4*>(gx + r * D + c) =
-          make_float4(rs * gt[v].x - xv[v].x * k, rs * gt[v].y - xv[v].y * k, rs * gt[v].z - xv[v].z * k,
-                      rs * gt[v].w - xv[v].w * k);
+      float4 o = make_float4(rs * gt[v].x - xv[v].x * k, rs * gt[v].y - xv[v].y * k, rs * gt[v].z - xv[v].z * k,
+                             rs * gt[v].w - xv[v].w * k);
+      if (gres) {   // + the gradient reaching x along other paths (the residual stream): one pass
+        const float4 e = *reinterpret_cast<const float4*>(gres + r * D + c);
+        o = make_float4(o.x + e.x, o.y + e.y, o.z + e.z, o.w + e.w);
+      }
+      *reinterpret_cast<float4*>(gx + r * D + c) = o;
     }
   }
 #pragma unroll
@@ -212,7 +217,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
 // its 16 row lanes q sum s = q, q+16, ... (4 loads in flight), then the 16 partials are added in q
 // order through LDS. Deterministic, no atomics; D/64 workgroups of long independent sums.
 __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict__ P, int S, int64_t n,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out, int accumulate) {
   __shared__ float4 red[16][16];
   const int c = threadIdx.x & 15, q = threadIdx.x >> 4;
   const int64_t j = ((int64_t)blockIdx.x * 16 + c) * 4;
@@ -240,6 +245,10 @@ __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict
     for (int w = 1; w < 16; ++w) {
       const float4 v = red[w][c];
       r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    if (accumulate) {   // out += sum: a parameter gradient accumulated in place (flat DP bucket)
+      const float4 o = *reinterpret_cast<const float4*>(out + j);
+      r = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
     }
     *reinterpret_cast<float4*>(out + j) = r;
   }
@@ -443,14 +452,14 @@ int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float e
   return rq_rmsnorm_dropout_fwd(x, w, B, D, eps, 0.f, 0, y, rstd, stream);
 }
 
-int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
-                           float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
-                           void* stream) {
+int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
+                            void* workspace, size_t ws_bytes, void* stream) {
   RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_bwd: need D %% 4 == 0, D <= 4096");
   RQ_CHECK_ARG(gw && (B == 0 || (x && w && rstd && gy && gx)), "rq_rmsnorm_bwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
   if (B == 0) {
-    RQ_HIP(hipMemsetAsync(gw, 0, (size_t)D * sizeof(float), s));
+    if (!accumulate_gw) RQ_HIP(hipMemsetAsync(gw, 0, (size_t)D * sizeof(float), s));
     return 0;
   }
   RQ_CHECK_ARG(workspace && ws_bytes >= rq_rmsnorm_bwd_workspace(B, D), "rq_rmsnorm_bwd: workspace too small");
@@ -459,13 +468,20 @@ int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, co
   dropout_params(p, &thr, &dscale);
   float* part = static_cast<float*>(workspace);
   const int nblk = (int)((B + kRmsRows - 1) / kRmsRows);
-#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, thr, dscale, seed, gx, part);
+#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, thr, dscale, seed, gres, gx, part);
   RMS_SWITCH((int)((D + 255) / 256), RMS_B)
 #undef RMS_B
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd");
-  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + 15) / 16)), dim3(256), 0, s, part, nblk, D, gw);
+  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + 15) / 16)), dim3(256), 0, s, part, nblk, D, gw,
+                     accumulate_gw);
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd(reduce)");
   return 0;
+}
+
+int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
+                           float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
+                           void* stream) {
+  return rq_rmsnorm_dropout_bwd2(x, w, rstd, gy, nullptr, B, D, p, seed, gx, gw, 0, workspace, ws_bytes, stream);
 }
 
 int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,

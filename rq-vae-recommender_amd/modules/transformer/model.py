@@ -66,9 +66,16 @@ class TransformerBlock(nn.Module):
         out = self._forward_jagged(jx, jkv, is_causal)
         return out if isinstance(x, Jagged) else _wrap_like(out.values(), x)
 
+    def _fork_ok(self, xv) -> bool:
+        norms = [self.attn_norm] + ([self.cross_attn_norm] if self.do_cross_attn else []) + [self.ff[0]]
+        return (all(hip_ops.rmsnorm_supported(xv, n.weight) for n in norms) and
+                len({n.eps for n in norms}) == 1)
+
     def _forward_jagged(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool) -> Jagged:
         use_cache = not self.training and self.enable_kv_cache
         xv = jx.values()
+        if self._fork_ok(xv):
+            return self._forward_fork(jx, jkv, is_causal, use_cache)
         # residual adds ride in the output-projection GEMMs' epilogue (h = x + MHA(..), h += CrossMHA(..))
         h = self.attention(jx.with_values(self.attn_norm.forward_dropout(xv, self.do)), is_causal=is_causal,
                            jagged=True, use_cache=use_cache, residual=xv).values()
@@ -80,6 +87,28 @@ class TransformerBlock(nn.Module):
         if drop.training and drop.p > 0 and hip_ops.dropout_fusable(h) and hip_ops.dropout_fusable(y):
             return jx.with_values(hip_ops.dropout_add(h, y, drop.p))   # h + Dropout(ff) in one pass
         return jx.with_values(h + drop(y))
+
+    def _forward_fork(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool, use_cache: bool) -> Jagged:
+        """Same block, with x's fan-out (norm branches + residual) and h's (ff norm + residual) as
+        hip_ops.rmsnorm_fork nodes: the residual gradients are added inside the norm backward kernels."""
+        xv = jx.values()
+        p = self.do.p if self.do.training else 0.0
+        norm, mlp, drop = self.ff
+        if self.do_cross_attn:
+            n1, n2, xr = hip_ops.rmsnorm_fork(xv, self.attn_norm.eps, self.attn_norm.weight, p,
+                                              self.cross_attn_norm.weight, p)
+        else:
+            n1, xr = hip_ops.rmsnorm_fork(xv, self.attn_norm.eps, self.attn_norm.weight, p)
+        h = self.attention(jx.with_values(n1), is_causal=is_causal, jagged=True, use_cache=use_cache,
+                           residual=xr).values()
+        if self.do_cross_attn:
+            h = self.cross_attention(x=jx.with_values(n2), x_kv=jkv, is_causal=False, jagged=True,
+                                     use_cache=use_cache, residual=h).values()
+        n3, hr = hip_ops.rmsnorm_fork(h, norm.eps, norm.weight)
+        y = mlp(n3)
+        if drop.training and drop.p > 0 and hip_ops.dropout_fusable(hr) and hip_ops.dropout_fusable(y):
+            return jx.with_values(hip_ops.dropout_add(hr, y, drop.p))
+        return jx.with_values(hr + drop(y))
 
     def reset_kv_cache(self):
         raise NotImplementedError("KV Cache currently not supported")

@@ -659,21 +659,87 @@ class RMSNormFunction(torch.autograd.Function):
         call("rq_rmsnorm_dropout_fwd", ptr(x2), ptr(weight), B, D, float(eps), float(p), int(seed), ptr(y), ptr(rstd),
              stream_handle(x.device))
         ctx.save_for_backward(x2, weight, rstd)
-        ctx.shape, ctx.p, ctx.seed = x.shape, float(p), int(seed)
+        ctx.shape, ctx.p, ctx.seed, ctx.weight = x.shape, float(p), int(seed), weight
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, gy):
         x2, weight, rstd = ctx.saved_tensors
-        B, D = x2.shape
-        gy2 = gy.contiguous().view(B, D)
-        gx = torch.empty_like(x2)
-        gw = torch.empty((D,), device=x2.device, dtype=torch.float32)
-        nbytes = _lib.load().rq_rmsnorm_bwd_workspace(B, D)
-        ws = torch.empty((nbytes,), device=x2.device, dtype=torch.uint8)
-        call("rq_rmsnorm_dropout_bwd", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2), B, D, ctx.p, ctx.seed, ptr(gx),
-             ptr(gw), ptr(ws), nbytes, stream_handle(x2.device))
+        gx, gw = _rmsnorm_bwd(x2, ctx.weight, rstd, gy, None, ctx.p, ctx.seed, ctx.needs_input_grad[1])
+        ctx.weight = None
         return gx.view(ctx.shape), gw, None, None, None
+
+
+def _rmsnorm_bwd(x2, weight, rstd, gy, gres, p: float, seed: int, need_w: bool):
+    """(gx [+ gres], gw) of one RMSNorm(+dropout) — gw added straight into the parameter's flat
+    gradient bucket when dp.GradBuckets owns one (then returned as None), rq_rmsnorm_dropout_bwd2."""
+    from . import dp
+    B, D = x2.shape
+    gy2 = gy.contiguous().view(B, D)
+    gx = torch.empty_like(x2)
+    sink = dp.direct_grad(weight) if need_w else None
+    gw = sink if sink is not None else torch.empty((D,), device=x2.device, dtype=torch.float32)
+    nbytes = _lib.load().rq_rmsnorm_bwd_workspace(B, D)
+    ws = torch.empty((nbytes,), device=x2.device, dtype=torch.uint8)
+    call("rq_rmsnorm_dropout_bwd2", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
+         ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
+         int(sink is not None), ptr(ws), nbytes, stream_handle(x2.device))
+    if sink is not None:
+        dp.direct_grad_done(weight)
+        return gx, None
+    return gx, (gw if need_w else None)
+
+
+class RMSNormForkFunction(torch.autograd.Function):
+    """x -> (RMSNorm_1(x) [dropout], [RMSNorm_2(x) [dropout]], x): the pre-norm block's fan-out of x to
+    its norm branches and to the residual stream (modules/transformer/model.py:75-82: h = x +
+    SelfAttn(Dropout(attn_norm(x))) [+ CrossAttn(Dropout(cross_attn_norm(x)))]; out = h +
+    Dropout(MLP(RMSNorm(h)))) as one node, so the backward adds the residual gradient inside the norm
+    backward kernels (rq_rmsnorm_dropout_bwd2 gres) instead of autograd summing the three branch
+    gradients with separate add kernels. Forward = the RMSNormFunction kernels."""
+
+    @staticmethod
+    def forward(ctx, x, eps: float, p1: float, seed1: int, p2: float, seed2: int, w1, w2):
+        require_gpu(x, w1, what="rmsnorm_fork")
+        D = x.shape[-1]
+        x2 = x.contiguous().view(-1, D)
+        B = x2.shape[0]
+        outs, saved = [], [x2]
+        for w, p, sd in ((w1, p1, seed1), (w2, p2, seed2)):
+            if w is None:
+                continue
+            y = torch.empty_like(x2)
+            rstd = torch.empty((B,), device=x.device, dtype=torch.float32)
+            call("rq_rmsnorm_dropout_fwd", ptr(x2), ptr(w), B, D, float(eps), float(p), int(sd), ptr(y), ptr(rstd),
+                 stream_handle(x.device))
+            outs.append(y.view(x.shape))
+            saved += [w, rstd]
+        ctx.save_for_backward(*saved)
+        ctx.shape, ctx.ps, ctx.seeds, ctx.ws = x.shape, (float(p1), float(p2)), (int(seed1), int(seed2)), (w1, w2)
+        return (*outs, x.view_as(x))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        saved = ctx.saved_tensors
+        x2 = saved[0]
+        n = (len(saved) - 1) // 2
+        g_pass = grads[n]
+        gres, gws = g_pass, [None, None]
+        for i in range(n):   # gx = norm_1' g_1 + norm_2' g_2 + g_pass, each norm backward adding the previous sum
+            w, rstd = saved[1 + 2 * i], saved[2 + 2 * i]
+            gres, gws[i] = _rmsnorm_bwd(x2, ctx.ws[i], rstd, grads[i], gres, ctx.ps[i], ctx.seeds[i],
+                                        ctx.needs_input_grad[6 + i])
+        ctx.ws = None
+        return gres.view(ctx.shape), None, None, None, None, None, gws[0], gws[1]
+
+
+def rmsnorm_fork(x: torch.Tensor, eps: float, w1: torch.Tensor, p1: float = 0.0, w2: torch.Tensor = None,
+                 p2: float = 0.0):
+    """(RMSNorm_w1(x) [dropout p1], [RMSNorm_w2(x) [dropout p2]], x) as one autograd node
+    (RMSNormForkFunction); the norms' dropout keys are drawn in argument order."""
+    s1 = next_seed() if p1 > 0 else 0
+    s2 = next_seed() if (w2 is not None and p2 > 0) else 0
+    return RMSNormForkFunction.apply(x, float(eps), float(p1), s1, float(p2), s2, w1, w2)
 
 
 def rmsnorm_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:

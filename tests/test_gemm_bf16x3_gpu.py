@@ -317,9 +317,11 @@ def test_linear_add_epilogue_matches_fp64(device):
     assert close(y, yd) and close(x.grad, xd.grad) and close(W.grad, Wd.grad) and close(r.grad, rd.grad)
 
 
-def test_split_many_matches_single(device):
+@pytest.mark.parametrize("shapes", [((512, 768), (3,), (256, 512), (1, 7)),             # scalar path
+                                    ((512, 768), (1024, 512), (8, 8), (64,), (1536, 512))])  # float4 path
+def test_split_many_matches_single(device, shapes):
     from rqvae_hip import ops
-    xs = [torch.randn(*s, device=device) for s in ((512, 768), (3,), (256, 512), (1, 7))]
+    xs = [torch.randn(*s, device=device) for s in shapes]
     many = ops.split_bf16x3_many(xs)
     for x, m in zip(xs, many):
         one = ops.split_bf16x3(x)

@@ -74,6 +74,9 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (2, 1281, 1281, 8, 64, False, True), # C5 longest context (256 items x 5 + 1)
     (3, 6, 1281, 8, 64, False, False),   # C5 cross-attention: L+2 future queries x 1281 keys
     (2, 6, 6, 8, 64, True, True),        # C5 decoder causal self-attention
+    (5, 128, 128, 8, 64, True, True),    # short forms: longest staged range (128 rows), causal
+    (4, 64, 100, 8, 64, False, False),   # short forms: 64 queries x 100 keys (dQ stages 112 keys)
+    (3, 17, 17, 8, 64, True, True),      # short forms: two query tiles per sequence, causal diagonal
     (4, 70, 70, 4, 32, True, True),
     (2, 40, 90, 2, 128, False, False),
     (5, 30, 30, 4, 16, True, True),      # small head dim (decoder fixtures: A=64, H=4)
