@@ -188,8 +188,9 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
  * factor. -1 for an empty shape. Host-only. */
 int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_split, int a_kcontig, int b_kcontig,
                           int epilogue, int* splits);
-/* Enable (1) / disable (0) the wide kernel for this process (default: on unless RQ_X3W=0 is set);
- * returns the previous setting. For A/B measurements and kernel-vs-kernel tests. */
+/* Enable (1) / disable (0) the wide kernel for this process (default: on unless RQ_X3W=0 is set; when on,
+ * a cost model of resident-workgroup rounds picks it per shape); 2 = force it wherever it can run.
+ * Returns the previous setting. For A/B measurements and kernel-vs-kernel tests. */
 int rq_gemm_x3w_enable(int enable);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);

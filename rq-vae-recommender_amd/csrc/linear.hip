@@ -1133,25 +1133,62 @@ static int64_t x3_split_cap(int64_t M, int64_t N) {
   return by_bytes > RQ_X3_MAX_SPLIT ? by_bytes : RQ_X3_MAX_SPLIT;
 }
 
-static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
-  X3Plan p;
-  p.tiles_n = (int)((N + kXT - 1) / kXT);
-  p.tiles = (int)((M + kXT - 1) / kXT) * p.tiles_n;
-  // split K only when the output tiles cannot fill the chip (weight gradients)
-  int64_t S = 1;
-  if (allow_split && p.tiles < x3_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
-    S = x3_slots() / p.tiles;
-    const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
-    if (S > max_s) S = max_s;
-    if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);   // slab traffic of the reduction grows with S
-    if (S < 1) S = 1;
+// Modelled time (us) of a plan, to choose the split-K factor and between the two kernels:
+//  * MMA: whole rounds of resident workgroups (a partly filled last round costs a full one) x the
+//    MACs a CU does per round, at the measured per-CU rates (128-tile kernel ~0.53 M fp32-MAC/us per
+//    CU with its two workgroups, ~0.4 for a lone workgroup; wide kernel 1.3x) — the wide kernel's
+//    256 x 256 tiles quantise into 4x coarser rounds (decoder context rows: a 1,536-wide projection is
+//    270 wide tiles, two rounds, the second nearly empty);
+//  * split-K: the slabs written and re-read, (S + 1) M N fp32 at ~5 TB/s, plus a ~4 us reduce launch.
+// Checked against tools/gemm_ab.py on MI355X (RQ-VAE and decoder shapes, both kernels forced).
+#ifndef RQ_X3W_SPEED
+#define RQ_X3W_SPEED 1.3
+#endif
+static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
+  const int64_t cus = resident_slots() / 2;
+  const int64_t wgs = (int64_t)p.tiles * p.S;
+  const double tile = wide ? (double)kWT2 * kWT2 : (double)kXT * kXT;
+  const double rate = 0.53 * (wide ? RQ_X3W_SPEED : 1.0);   // M MAC / us per CU
+  double t;
+  if (wgs <= cus) {   // at most one workgroup per CU
+    t = tile * (double)p.chunk / ((wide ? rate : 0.4) * 1e6);
+  } else {
+    const int64_t slots = wide ? cus : cus * kXWG;
+    const int64_t rounds = (wgs + slots - 1) / slots;
+    t = (double)rounds * (wide ? tile : kXWG * tile) * (double)p.chunk / (rate * 1e6);
   }
+  if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + 4.0;
+  return t;
+}
+
+static X3Plan x3_plan_s(int64_t M, int64_t N, int64_t K, int64_t S, bool wide) {
+  X3Plan p;
+  const int T = wide ? kWT2 : kXT, KS = wide ? 32 : kXK;
+  p.tiles_n = (int)((N + T - 1) / T);
+  p.tiles = (int)((M + T - 1) / T) * p.tiles_n;
   int64_t chunk = (K + S - 1) / S;
-  chunk = (chunk + kXK - 1) / kXK * kXK;
+  chunk = (chunk + KS - 1) / KS * KS;
   p.chunk = chunk;
   p.S = (int)((K + chunk - 1) / chunk);
   if (p.S < 1) p.S = 1;
-  p.per = (p.tiles * p.S + 7) / 8;
+  p.per = wide ? 0 : (p.tiles * p.S + 7) / 8;
+  return p;
+}
+
+static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
+  X3Plan p = x3_plan_s(M, N, K, 1, false);
+  // split K when the output tiles cannot fill the chip (weight gradients, the decoder's future rows)
+  // and the model says the slabs pay for themselves
+  if (allow_split && p.tiles < x3_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
+    int64_t S = x3_slots() / p.tiles;
+    const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
+    if (S > max_s) S = max_s;
+    if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);   // slab traffic of the reduction grows with S
+    if (S > 1) {
+      const X3Plan q = x3_plan_s(M, N, K, S, false);
+      if (x3_plan_time(q, M, N, false) < x3_plan_time(p, M, N, false)) p = q;
+    }
+  }
   return p;
 }
 
@@ -1167,7 +1204,7 @@ static bool x3w_enabled() {
     const char* e = getenv("RQ_X3W");
     g_x3w = (e && e[0] == '0') ? 0 : 1;
   }
-  return g_x3w == 1;
+  return g_x3w >= 1;
 }
 
 // Plan of the wide kernel, or false when the 128-tile kernel serves the shape better: k steps
@@ -1178,21 +1215,17 @@ static bool x3w_plan(int64_t M, int64_t N, int64_t K, bool allow_split, X3Plan* 
   auto fits = [](int64_t R) { return R % kWT2 == 0 || R >= 2048; };
   if (!fits(M) || !fits(N)) return false;
   const int cus = resident_slots() / 2;
-  p->tiles_n = (int)((N + kWT2 - 1) / kWT2);
-  p->tiles = (int)((M + kWT2 - 1) / kWT2) * p->tiles_n;
-  int64_t S = 1;
+  *p = x3_plan_s(M, N, K, 1, true);
   if (allow_split && p->tiles < cus / 2 && (M * N) % 4 == 0) {
-    S = cus / p->tiles;
+    int64_t S = cus / p->tiles;
     const int64_t max_s = K / (32 * RQ_X3W_MIN_STEPS);
     if (S > max_s) S = max_s;
     if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);
-    if (S < 1) S = 1;
+    if (S > 1) {
+      const X3Plan q = x3_plan_s(M, N, K, S, true);
+      if (x3_plan_time(q, M, N, true) < x3_plan_time(*p, M, N, true)) *p = q;
+    }
   }
-  int64_t chunk = (K + S - 1) / S;
-  chunk = (chunk + 31) / 32 * 32;
-  p->chunk = chunk;
-  p->S = (int)((K + chunk - 1) / chunk);
-  p->per = 0;
   return (int64_t)p->tiles * p->S >= cus / 4;
 }
 
@@ -1203,7 +1236,8 @@ static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool
                        X3Plan* p) {
   const bool combo = epilogue == kEpiStore || (epilogue == kEpiSiluFwd && a_kc && b_kc) ||
                      (epilogue == kEpiSiluBwd && a_kc && !b_kc) || (epilogue == kEpiAdd && a_kc && b_kc);
-  return asp && bsp && combo && x3w_plan(M, N, K, true, p);
+  if (!(asp && bsp && combo && x3w_plan(M, N, K, true, p))) return false;
+  return g_x3w == 2 || x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K), M, N, false);   // 2: forced
 }
 
 }  // namespace rqhip
@@ -1427,8 +1461,8 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
 }
 
 int rq_gemm_x3w_enable(int enable) {
-  const int prev = x3w_enabled() ? 1 : 0;
-  g_x3w = enable ? 1 : 0;
+  const int prev = x3w_enabled() ? g_x3w : 0;
+  g_x3w = enable == 2 ? 2 : (enable ? 1 : 0);
   return prev;
 }
 

@@ -376,9 +376,10 @@ def gemm_x3_choice(M: int, N: int, K: int, a_split: bool, b_split: bool, a_kcont
     return ("wide" if k == 1 else "x3"), int(s.value)
 
 
-def gemm_x3w_enable(enable: bool) -> bool:
-    """Turn the wide split-bf16 GEMM kernel on / off for this process; returns the previous state."""
-    return bool(_lib.load().rq_gemm_x3w_enable(int(enable)))
+def gemm_x3w_enable(enable) -> int:
+    """Wide split-bf16 GEMM kernel for this process: False off, True on (chosen per shape by the
+    round cost model), 2 forced wherever it can run (kernel tests); returns the previous state."""
+    return int(_lib.load().rq_gemm_x3w_enable(2 if enable == 2 else int(bool(enable))))
 
 
 def mlp_fusable(x: torch.Tensor, weights) -> bool:

@@ -38,7 +38,7 @@ def _mk(M, N, K, a_kc, b_kc, gen, device, integer):
 @pytest.fixture
 def wide_on():
     ops = _ops()
-    prev = ops.gemm_x3w_enable(True)
+    prev = ops.gemm_x3w_enable(2)   # forced: these tests are about the wide kernel itself
     yield ops
     ops.gemm_x3w_enable(prev)
 
@@ -77,13 +77,13 @@ def test_x3w_random_within_bound_and_repeatable(device, wide_on, a_kc, b_kc, M, 
 
 def _both(ops, fn):
     """fn() under the wide kernel and under the 128-tile kernel."""
-    ops.gemm_x3w_enable(True)
+    ops.gemm_x3w_enable(2)
     w = fn()
     ops.gemm_x3w_enable(False)
     try:
         o = fn()
     finally:
-        ops.gemm_x3w_enable(True)
+        ops.gemm_x3w_enable(2)
     return w, o
 
 
@@ -114,7 +114,7 @@ def test_x3w_fused_epilogues_equal_x3_kernel(device, wide_on, p):
     aw = ops.gemm_x3(x, True, W, True, M, N, K, ops.EPI_ADD, Z=r)
     ops.gemm_x3w_enable(False)
     ao = ops.gemm_x3(x32, True, W, True, M, N, K, ops.EPI_ADD, Z=r)
-    ops.gemm_x3w_enable(True)
+    ops.gemm_x3w_enable(2)
     assert torch.equal(aw, ao)
 
 

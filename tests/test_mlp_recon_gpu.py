@@ -45,7 +45,7 @@ def _ref64(e, x, ws):
 @pytest.mark.parametrize("p", [0.0, 0.3])
 def test_mlp_l2norm_recon_equals_composition(device, p):
     ops = _ops()
-    prev = ops.gemm_x3w_enable(True)
+    prev = ops.gemm_x3w_enable(2)   # forced: the split gradient's path onto the wide kernel
     try:
         B, dims = 16384, [64, 128, 256, 512, 768]   # no split-K on the last data grad for either kernel
         gen = torch.Generator(device=device).manual_seed(21)
@@ -87,7 +87,7 @@ def test_mlp_l2norm_recon_equals_composition(device, p):
 
 def test_mlp_presplit_input_equals_fp32_input(device):
     ops = _ops()
-    prev = ops.gemm_x3w_enable(True)
+    prev = ops.gemm_x3w_enable(2)
     try:
         B, dims = 8192, [768, 512, 256]
         gen = torch.Generator(device=device).manual_seed(5)
@@ -97,7 +97,7 @@ def test_mlp_presplit_input_equals_fp32_input(device):
         assert ops._presplit_input(B, ws, len(ws))
 
         def run(wide):
-            ops.gemm_x3w_enable(wide)
+            ops.gemm_x3w_enable(2 if wide else False)
             for w in ws:
                 w.grad = None
             x.grad = None

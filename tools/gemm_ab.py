@@ -26,6 +26,10 @@ CASES = [
     (512, 256, 65536, False, False, "dec2 wgrad"),
     (20480, 1536, 512, True, True, "decoder qkv fwd"), (20480, 1024, 512, True, True, "decoder ff fwd"),
     (1536, 512, 20480, False, False, "decoder qkv wgrad"),
+    (11332, 1536, 512, True, True, "dec-ctx qkv fwd"), (11332, 1024, 512, True, True, "dec-ctx ff1 fwd"),
+    (11332, 512, 1024, True, True, "dec-ctx ff2 fwd"), (11332, 512, 1536, True, False, "dec-ctx qkv dgrad"),
+    (11332, 512, 512, True, True, "dec-ctx out fwd"), (1536, 512, 11332, False, False, "dec-ctx qkv wgrad"),
+    (1024, 512, 11332, False, False, "dec-ctx ff1 wgrad"), (512, 512, 11332, False, False, "dec-ctx out wgrad"),
 ]
 
 
@@ -58,11 +62,13 @@ for M, N, K, akc, bkc, tag in CASES:
     sa, sb = ops.split_bf16x3(a), ops.split_bf16x3(b)
     out = {}
     for wide in [k == "wide" for k in kernels]:
-        ops.gemm_x3w_enable(wide)
+        ops.gemm_x3w_enable(2 if wide else False)   # forced either way
         kern, S = ops.gemm_x3_choice(M, N, K, True, True, akc, bkc)
         us = timed(lambda: ops.gemm_x3(sa, akc, sb, bkc, M, N, K))
         out[kern] = us
         print(json.dumps({"case": tag, "M": M, "N": N, "K": K, "kernel": kern, "splits": S, "us": round(us, 2),
                           "tflops": round(2.0 * M * N * K / us / 1e6, 1)}), flush=True)
     ops.gemm_x3w_enable(True)
+    print(json.dumps({"case": tag, "model_picks": ops.gemm_x3_choice(M, N, K, True, True, akc, bkc)[0],
+                      "measured_best": min(out, key=out.get)}), flush=True)
     del a, b, sa, sb
