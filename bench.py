@@ -78,9 +78,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     ap.add_argument("--no-graph", action="store_true", help="decoder steps eager instead of hipGraph replays")
+    ap.add_argument("--wgrad-stream", action="store_true",
+                    help="decoder weight grads on a side stream (A/B: measured 7.59 vs 7.24 ms main-stream, off)")
     ap.add_argument("--no-dm", action="store_true", help="skip the ML-32M decoder lines")
     ap.add_argument("--dm-batch", type=int, default=0, help="with --decoder-only: the ML-32M config at this batch")
     return ap.parse_args()
+
+
+WGRAD_STREAM = [False]
 
 
 def make_items(n, dim, gen, device):
@@ -222,6 +227,7 @@ def cpu_baseline(budget_s, B=2048):
 
 def main():
     args = parse()
+    WGRAD_STREAM[0] = args.wgrad_stream
     from rqvae_hip import dp, ops
     from data.schemas import SeqBatch
     rk, ws, lr = dp.init_from_env()
@@ -576,6 +582,9 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
                                      max_pos=cfg["max_items"] * cfg["sem_id_dim"]).to(device).train()
     buckets = dp.GradBuckets(m.parameters(), overlap=not graphs, flat_views=graphs)
     buckets.broadcast_params()
+    # optional: weight grads accumulate into the flat buckets on a side stream (overlapping the
+    # data-grad chain) — measured slower on MI355X (7.59 vs 7.24 ms per Amazon step), so off by default
+    ops.wgrad_stream_enable(graphs and WGRAD_STREAM[0])
     opt = make_adamw(m.parameters(), cfg["lr"], cfg["wd"])
     batches = [synthetic_tokenized_batch(B, cfg["max_items"], cfg["sem_id_dim"], cfg["K"], 50 + 97 * rk + i, device)
                for i in range(4)]

@@ -233,6 +233,8 @@ class GradBuckets:
         b = self.buckets[bi]
         if b["expect"] == 0:   # every parameter of the bucket is unused on every rank
             return
+        from . import ops
+        ops.join_wgrad_stream()   # weight grads accumulated on the side stream land before the exchange
         self._pending[bi] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, async_op=True)
 
     def zero_grad(self):
@@ -258,6 +260,8 @@ class GradBuckets:
         ws = world()
         if not self.active:
             return
+        from . import ops
+        ops.join_wgrad_stream()
         if ws > 1:
             for bi in range(len(self.buckets)):
                 self._launch(bi)

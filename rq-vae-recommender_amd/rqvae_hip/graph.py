@@ -83,6 +83,7 @@ class GraphedSteps:
         self.buckets.zero_grad()
         loss = self.loss_fn(self.static)
         loss.backward()
+        ops.join_wgrad_stream()   # side-stream weight grads rejoin inside the capture
         ops.seed_epoch_advance()
         return loss.detach()
 

@@ -298,15 +298,58 @@ def split_weights(weights) -> list:
     return res
 
 
+_SIDE = {"on": False, "streams": {}, "used": False}
+
+
+def wgrad_stream_enable(on: bool) -> bool:
+    """Run the weight-grad GEMMs that accumulate into flat gradient buckets (_wgrad_into's direct path)
+    on a side stream: they depend on nothing downstream in the backward, so they overlap the data-grad
+    chain, attention and norm backward kernels (a parallel branch of a captured graph). Consumers of
+    the gradients must call join_wgrad_stream() first (GradBuckets.synchronize / _launch and
+    graph.GraphedSteps do). Returns the previous setting."""
+    prev = _SIDE["on"]
+    _SIDE["on"] = bool(on)
+    return prev
+
+
+def _side_stream(device):
+    s = _SIDE["streams"].get(device.index)
+    if s is None:
+        s = _SIDE["streams"][device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
+def join_wgrad_stream() -> None:
+    """Make the current stream wait for every weight grad launched on the side stream."""
+    if _SIDE["used"]:
+        for s in _SIDE["streams"].values():
+            torch.cuda.current_stream(s.device).wait_stream(s)
+        _SIDE["used"] = False
+
+
+def _operand_tensors(t):
+    return [t.hi, t.lo] if isinstance(t, Split) else [t]
+
+
 def _wgrad_into(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: int):
     """dW = g^T inp for `weight` (split-bf16 GEMM): added straight into weight's flat gradient bucket
-    when dp.GradBuckets owns one (returns None: autograd must not accumulate it again), else a new
-    (O, I) tensor for autograd."""
+    when dp.GradBuckets owns one (returns None: autograd must not accumulate it again) — on the side
+    stream when wgrad_stream_enable(True) — else a new (O, I) tensor for autograd."""
     from . import dp
     sink = dp.direct_grad(weight)
     if sink is None:
         return gemm_x3(g, g_kc, inp, inp_kc, O, I, rows)
-    gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True)
+    if _SIDE["on"]:
+        main = torch.cuda.current_stream(sink.device)
+        side = _side_stream(sink.device)
+        side.wait_stream(main)          # operands and the zeroed bucket are ready
+        with torch.cuda.stream(side):   # the split-K slab workspace is allocated on the side stream too
+            gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True)
+        for t in _operand_tensors(g) + _operand_tensors(inp):
+            t.record_stream(side)       # freed operands are not reused until the side stream is past them
+        _SIDE["used"] = True
+    else:
+        gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True)
     dp.direct_grad_done(weight)
     return None
 
