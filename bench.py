@@ -155,12 +155,13 @@ def quantize_algorithmic_bytes(B, D, K, L):
     return 4 * B * D + 4 * L * K * (D + 1) + 4 * B * (2 * L * D + D + 1) + 8 * B * L
 
 
-def pmc_traffic(timeout_s=75, regex="rq_fwd", script=("pmc_quantize.py", "5")):
+def pmc_traffic(timeout_s=75, regex="rq_fwd", script=("pmc_quantize.py", "5"), launches=None):
     """HBM bytes per launch of the kernels matching `regex` from two rocprofv3 --pmc passes
     (FETCH_SIZE, WRITE_SIZE: they do not fit one TCC pass) over a short driver (tools/pmc_*.py) that
     runs the same kernel at the same shape, as child processes (this process never execs). Both
     counters are in KiB; FETCH_SIZE is doubled (gfx950 tallies 128-B streaming reads at 64 B,
-    MI355X_MICROARCH.md 'HBM')."""
+    MI355X_MICROARCH.md 'HBM'). With `launches`, one logical launch is several dispatches (a split-K GEMM
+    and its slab reduction): the counters of every matched dispatch are summed and divided by it."""
     import csv
     import shutil
     import subprocess
@@ -183,7 +184,7 @@ def pmc_traffic(timeout_s=75, regex="rq_fwd", script=("pmc_quantize.py", "5")):
             v = sorted(float(row["Counter_Value"]) for row in csv.DictReader(open(path)) if row["Counter_Name"] == ctr)
             if not v:
                 return None, f"{ctr}: no {regex} dispatches recorded"
-            vals[ctr] = v[len(v) // 2]
+            vals[ctr] = sum(v) / launches if launches else v[len(v) // 2]
     fetch = 2.0 * vals["FETCH_SIZE"] * 1024
     write = vals["WRITE_SIZE"] * 1024
     return dict(bytes=fetch + write, fetch_bytes_x2=fetch, write_bytes=write), None
@@ -340,8 +341,9 @@ def main():
         if gemm is not None:
             M, N, K, akc, bkc = gemm["shape"]
             asp, bsp = gemm["operands_split"]
-            gtraffic, gtraffic_note = pmc_traffic(regex="gemm_bf16x3", script=(
-                "pmc_gemm.py", str(M), str(N), str(K), str(akc), str(bkc), "5", str(asp), str(bsp)))
+            gtraffic, gtraffic_note = pmc_traffic(
+                regex="gemm_bf16x3_kernel|gemm_x3w_kernel|x3_reduce_kernel", launches=5, script=(
+                    "pmc_gemm.py", str(M), str(N), str(K), str(akc), str(bkc), "5", str(asp), str(bsp)))
     q_roof = {"kernel": "rq_quantize_fwd", "bound": "mfma", "achieved": round(achieved, 3),
               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
               "traffic": round(traffic["bytes"]) if traffic else None, "launch_ms": round(q_ms, 4),
