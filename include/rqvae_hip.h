@@ -184,14 +184,18 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
                        int accumulate, void* workspace, size_t ws_bytes, void* stream);
 
 /* Which kernel rq_gemm_bf16x3_ex runs for a call: 1 = the wide 256 x 256-tile kernel (both operands
- * split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile kernel; *splits (optional) = its split-K
- * factor. -1 for an empty shape. Host-only. */
+ * split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile kernel, 2 = its 64 x 64-tile form (launches
+ * whose 128-tiles cannot fill the chip); *splits (optional) = its split-K factor. -1 for an empty
+ * shape. Host-only. */
 int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_split, int a_kcontig, int b_kcontig,
                           int epilogue, int* splits);
 /* Enable (1) / disable (0) the wide kernel for this process (default: on unless RQ_X3W=0 is set; when on,
  * a cost model of resident-workgroup rounds picks it per shape); 2 = force it wherever it can run.
  * Returns the previous setting. For A/B measurements and kernel-vs-kernel tests. */
 int rq_gemm_x3w_enable(int enable);
+/* 64 x 64-tile form of the 128-tile kernel: 0 never, 1 (default unless RQ_X3S=0/2 is set) where the
+ * time model prefers it, 2 forced wherever the 128-tile kernel would run. Returns the previous mode. */
+int rq_gemm_x3s_enable(int mode);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
 /* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device

@@ -268,18 +268,30 @@ __device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2
 __device__ __forceinline__ int row_swz(int rr) { return kXCPR == 4 ? ((rr >> 2) & 3) : ((rr >> 3) & 1); }
 __device__ __forceinline__ int row_off(int rr, int c) { return rr * (2 * kXK) + ((c ^ row_swz(rr)) << 4); }
 
-// One operand's staging registers (a 128 x 32 tile per stage, 256 threads). Operand formats:
-//   fp32  (SP = false): 4 float4 per thread, split into (hi, lo) bf16 while written to LDS;
+// One operand's staging registers (a TR x 32 tile per stage, 256 threads; TR = 128 or 64 rows of m / n).
+// Operand formats:
+//   fp32  (SP = false): TR / 32 float4 per thread, split into (hi, lo) bf16 while written to LDS;
 //   split (SP = true):  two bf16 planes (hi, lo) of the operand's shape, produced once upstream
-//                       (rq_split_bf16x3, or a GEMM epilogue): 2 + 2 16-byte chunks per thread,
-//                       copied to LDS as they are.
-template <bool KC, bool SP>
+//                       (rq_split_bf16x3, or a GEMM epilogue): TR / 64 + TR / 64 16-byte chunks per
+//                       thread, copied to LDS as they are.
+// The LDS images do not depend on TR (a 64-row tile uses the first 64 rows of a row image and the
+// first 64 columns of a column image's 256-B rows, with the same swizzles).
+template <bool KC, bool SP, int TR = 128>
 struct XStage {
+  static_assert(TR == 128 || (TR == 64 && kXK == 32), "tile rows (64-row tiles need 32-deep k stages)");
+  // fp32, k-contig: float4 per thread (two per 16-B bf16 chunk of the row image)
+  static constexpr int NJ_FK = 2 * TR * kXCPR / 256;
+  // fp32, m/n-contig: CT threads across the TR columns (4 each), KR k-rows per pass
+  static constexpr int CT_F = TR / 4, KR_F = 256 / CT_F, NJ_FM = kXK / KR_F;
+  // split, k-contig: hi + lo 16-B chunks per thread
+  static constexpr int NJ_SK = TR * kXCPR / 256;
+  // split, m/n-contig: CT threads across the TR columns (8 each), KR k-rows per pass
+  static constexpr int CT_S = TR / 8, KR_S = 256 / CT_S, NJ_SM = kXK / KR_S;
   uint4 v[4];
   bool ok[4];
   bool full;   // every k of the stage < k_hi (all but a split's / the matrix's last stage): no masking
 
-  // rows [r0, r0 + 128) of the operand (clamped to R - 1: they feed only outputs >= R, never
+  // rows [r0, r0 + TR) of the operand (clamped to R - 1: they feed only outputs >= R, never
   // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time. The
   // per-lane part of each address does not depend on the stage, so a full stage's load is a
   // uniform base (X + kb) plus a loop-invariant lane offset.
@@ -290,7 +302,7 @@ struct XStage {
       const float* __restrict__ X = static_cast<const float*>(Xv);
       if constexpr (KC) {   // thread: chunk tid % CPR of rows tid / CPR (+ 256 / CPR), 2 float4 per chunk
 #pragma unroll
-        for (int j = 0; j < kXK / 8; ++j) {
+        for (int j = 0; j < NJ_FK; ++j) {
           const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * (j >> 1), R - 1);
           const int64_t lane = row * ld + (tid % kXCPR) * 8 + 4 * (j & 1);
           if (full) {
@@ -301,13 +313,13 @@ struct XStage {
             v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
           }
         }
-      } else {              // thread: 4 consecutive rows (tid % 32) * 4, k rows tid/32 + 8j
-        const int64_t col = min(r0 + 4 * (tid & 31), R - 4);
+      } else {              // thread: 4 consecutive rows 4 (tid % CT), k rows tid / CT + KR j
+        const int64_t col = min(r0 + 4 * (tid % CT_F), R - 4);
 #pragma unroll
-        for (int j = 0; j < kXK / 8; ++j) {
-          const int64_t k = kb + (tid >> 5) + 8 * j;
+        for (int j = 0; j < NJ_FM; ++j) {
+          const int64_t k = kb + (tid / CT_F) + KR_F * j;
           if (full) {
-            v[j] = *reinterpret_cast<const uint4*>(X + kb * ld + ((tid >> 5) + 8 * j) * ld + col);
+            v[j] = *reinterpret_cast<const uint4*>(X + kb * ld + ((tid / CT_F) + KR_F * j) * ld + col);
           } else {
             ok[j] = k < k_hi;
             v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
@@ -319,7 +331,7 @@ struct XStage {
       const uint16_t* __restrict__ Xl = static_cast<const uint16_t*>(Xlv);
       if constexpr (KC) {   // thread: chunk tid % CPR of rows tid / CPR (+ 256 / CPR)
 #pragma unroll
-        for (int j = 0; j < kXK / 16; ++j) {
+        for (int j = 0; j < NJ_SK; ++j) {
           const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * j, R - 1);
           const int64_t k = kb + (tid % kXCPR) * 8;
           int64_t o;
@@ -332,14 +344,14 @@ struct XStage {
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
         }
-      } else {              // thread: 8 consecutive rows (tid % 16) * 8, k rows tid/16 and tid/16 + 16
-        const int64_t col = min(r0 + 8 * (tid & 15), R - 8);
+      } else {              // thread: 8 consecutive rows 8 (tid % CT), k rows tid / CT + KR j
+        const int64_t col = min(r0 + 8 * (tid % CT_S), R - 8);
 #pragma unroll
-        for (int j = 0; j < kXK / 16; ++j) {
-          const int64_t k = kb + (tid >> 4) + 16 * j;
+        for (int j = 0; j < NJ_SM; ++j) {
+          const int64_t k = kb + (tid / CT_S) + KR_S * j;
           int64_t o;
           if (full) {
-            o = kb * ld + ((tid >> 4) + 16 * j) * ld + col;
+            o = kb * ld + ((tid / CT_S) + KR_S * j) * ld + col;
           } else {
             ok[j] = k < k_hi;
             o = (ok[j] ? k : k_lo) * ld + col;
@@ -355,9 +367,10 @@ struct XStage {
 
   __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, int tid) const {
     if constexpr (!SP) {
+      constexpr int NJ = KC ? NJ_FK : NJ_FM;
       float4 w[4];
 #pragma unroll
-      for (int j = 0; j < kXK / 8; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const float4 f = __builtin_bit_cast(float4, v[j]);
         if (full) {
           w[j] = f;
@@ -368,7 +381,7 @@ struct XStage {
       }
       if constexpr (KC) {
 #pragma unroll
-        for (int c2 = 0; c2 < kXK / 16; ++c2) {
+        for (int c2 = 0; c2 < NJ_FK / 2; ++c2) {
           const int rr = (tid / kXCPR) + (256 / kXCPR) * c2, c = tid % kXCPR;
           const int off = row_off(rr, c);
           uint4 h, l;
@@ -380,10 +393,10 @@ struct XStage {
           *reinterpret_cast<uint4*>(lo_plane + off) = l;
         }
       } else {
-        const int m = 4 * (tid & 31);
+        const int m = 4 * (tid % CT_F);
 #pragma unroll
-        for (int j = 0; j < kXK / 8; ++j) {
-          const int kr = (tid >> 5) + 8 * j;
+        for (int j = 0; j < NJ_FM; ++j) {
+          const int kr = (tid / CT_F) + KR_F * j;
           const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
           uint2 h, l;
           split_bf16x2(w[j].x, w[j].y, h.x, l.x);
@@ -393,8 +406,9 @@ struct XStage {
         }
       }
     } else {
+      constexpr int NJ = KC ? NJ_SK : NJ_SM;
 #pragma unroll
-      for (int j = 0; j < kXK / 16; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         uint4 h = v[j], l = v[2 + j];
         if (!full) {
           const bool k = ok[j];
@@ -406,8 +420,8 @@ struct XStage {
           const int rr = (tid / kXCPR) + (256 / kXCPR) * j, c = tid % kXCPR;
           off = row_off(rr, c);
         } else {
-          const int kr = (tid >> 4) + 16 * j;
-          off = 256 * kr + (((tid & 15) ^ col_swz(kr)) << 4);
+          const int kr = (tid / CT_S) + KR_S * j;
+          off = 256 * kr + (((tid % CT_S) ^ col_swz(kr)) << 4);
         }
         *reinterpret_cast<uint4*>(hi_plane + off) = h;
         *reinterpret_cast<uint4*>(lo_plane + off) = l;
@@ -468,6 +482,10 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 
 #ifndef RQ_X3_DEPTH
 #define RQ_X3_DEPTH 2    // register stage sets in flight (2 or 3; 3 spills on the transposed-B variants)
+#endif
+
+#ifndef RQ_X3S_DEPTH
+#define RQ_X3S_DEPTH 4   // stage sets in flight of the 64-tile form (its stages are 4x shorter)
 #endif
 
 #ifndef RQ_X3_SETPRIO
@@ -570,14 +588,14 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
 #if RQ_X3_MFMA16
 #define RQ_X3_MMA                                                                                             \
   {                                                                                                           \
-    bf16x8_t fa_h[4], fa_l[4], fb_h[4], fb_l[4];                                                              \
-    _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                                           \
-      fa_h[p] = xfrag16<AKC>(ah, wm * 64 + 16 * p, lane);                                                     \
-      fa_l[p] = xfrag16<AKC>(al, wm * 64 + 16 * p, lane);                                                     \
-      fb_h[p] = xfrag16<BKC>(bh, wn * 64 + 16 * p, lane);                                                     \
-      fb_l[p] = xfrag16<BKC>(bl, wn * 64 + 16 * p, lane);                                                     \
+    bf16x8_t fa_h[kP], fa_l[kP], fb_h[kP], fb_l[kP];                                                          \
+    _Pragma("unroll") for (int p = 0; p < kP; ++p) {                                                          \
+      fa_h[p] = xfrag16<AKC>(ah, wm * kWTile + 16 * p, lane);                                                 \
+      fa_l[p] = xfrag16<AKC>(al, wm * kWTile + 16 * p, lane);                                                 \
+      fb_h[p] = xfrag16<BKC>(bh, wn * kWTile + 16 * p, lane);                                                 \
+      fb_l[p] = xfrag16<BKC>(bl, wn * kWTile + 16 * p, lane);                                                 \
     }                                                                                                         \
-    _Pragma("unroll") for (int p = 0; p < 4; ++p) _Pragma("unroll") for (int q = 0; q < 4; ++q) {            \
+    _Pragma("unroll") for (int p = 0; p < kP; ++p) _Pragma("unroll") for (int q = 0; q < kP; ++q) {          \
       acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);              \
       acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);              \
       acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);              \
@@ -601,7 +619,9 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
   }
 #endif
 
-template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false>
+// TS = output tile (128, or 64 for launches whose 128-tiles cannot fill the chip: the decoder's 1,280
+// future-token rows): 4 waves of (TS / 2)^2 outputs, the same k order (so the same result) either way.
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false, int TS = 128>
 __global__ void __launch_bounds__(256, kXWG)
 gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
                    const void* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S,
@@ -612,18 +632,20 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
   if (lw >= tiles * S) return;
   const int s = lw / tiles, t = lw % tiles;
-  const int m0 = (t / tiles_n) * kXT, n0 = (t % tiles_n) * kXT;
+  const int m0 = (t / tiles_n) * TS, n0 = (t % tiles_n) * TS;
+  static_assert(TS == 128 || (TS == 64 && RQ_X3_MFMA16), "64-row tiles run on the 16x16x32 MFMA");
+  constexpr int kWTile = TS / 2, kP = TS / 32;   // per-wave tile, 16-row MFMA tiles per wave side
   const int64_t k_lo = (int64_t)s * chunk;
   const int64_t k_hi = k_lo + chunk < K ? k_lo + chunk : K;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
 
 #if RQ_X3_MFMA16
-  floatx4v acc[4][4];
+  floatx4v acc[kP][kP];
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
+  for (int p = 0; p < kP; ++p)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[p][q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < kP; ++q) acc[p][q] = floatx4v{0.f, 0.f, 0.f, 0.f};
 #else
   floatx16 acc[2][2];
 #pragma unroll
@@ -636,23 +658,26 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 
   auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
   const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
-  // RQ_X3_DEPTH register stage sets: stage st + DEPTH is loaded while stage st is multiplied and
-  // stage st + 1 (loaded earlier) is written to the other LDS buffer, so each load has DEPTH stages
-  // of MFMA work to land in (HBM latency under load is ~2-4k cycles, one stage ~1.5k).
-  XStage<AKC, ASP> sa0, sa1;
-  XStage<BKC, BSP> sb0, sb1;
-#if RQ_X3_DEPTH == 3
-  XStage<AKC, ASP> sa2;
-  XStage<BKC, BSP> sb2;
-#endif
+  // kDepth register stage sets: stage st + kDepth is loaded while stage st is multiplied and
+  // stage st + 1 (loaded earlier) is written to the other LDS buffer, so each load has kDepth stages
+  // of MFMA work to land in (HBM latency under load is ~2-4k cycles, one 128-tile stage ~1.5k; a
+  // 64-tile stage is 4x less MFMA work, so that form keeps 4 stages in flight).
+  constexpr int kDepth = TS == 64 ? RQ_X3S_DEPTH : RQ_X3_DEPTH;
+  static_assert(kDepth >= 2 && kDepth <= 4, "stage sets");
+  XStage<AKC, ASP, TS> sa0, sa1, sa2, sa3;
+  XStage<BKC, BSP, TS> sb0, sb1, sb2, sb3;
   sa0.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
   sb0.load(B, Bl, ldb, n0, N, k_lo, k_lo, k_hi, tid);
   sa1.load(A, Al, lda, m0, M, k_lo + (int64_t)min(1, nst - 1) * kXK, k_lo, k_hi, tid);
   sb1.load(B, Bl, ldb, n0, N, k_lo + (int64_t)min(1, nst - 1) * kXK, k_lo, k_hi, tid);
-#if RQ_X3_DEPTH == 3
-  sa2.load(A, Al, lda, m0, M, k_lo + (int64_t)min(2, nst - 1) * kXK, k_lo, k_hi, tid);
-  sb2.load(B, Bl, ldb, n0, N, k_lo + (int64_t)min(2, nst - 1) * kXK, k_lo, k_hi, tid);
-#endif
+  if constexpr (kDepth >= 3) {
+    sa2.load(A, Al, lda, m0, M, k_lo + (int64_t)min(2, nst - 1) * kXK, k_lo, k_hi, tid);
+    sb2.load(B, Bl, ldb, n0, N, k_lo + (int64_t)min(2, nst - 1) * kXK, k_lo, k_hi, tid);
+  }
+  if constexpr (kDepth >= 4) {
+    sa3.load(A, Al, lda, m0, M, k_lo + (int64_t)min(3, nst - 1) * kXK, k_lo, k_hi, tid);
+    sb3.load(B, Bl, ldb, n0, N, k_lo + (int64_t)min(3, nst - 1) * kXK, k_lo, k_hi, tid);
+  }
   sa0.store(plane(0, 0, 0), plane(0, 0, 1), tid);
   sb0.store(plane(0, 1, 0), plane(0, 1, 1), tid);
   __syncthreads();
@@ -661,7 +686,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   {                                                                                                           \
     const int st_ = (ST), buf = st_ & 1;                                                                      \
     {  /* unconditional (past the end: the last stage again, an L2 hit) so vmcnt counts stay static */       \
-      const int64_t kb = k_lo + (int64_t)min(st_ + RQ_X3_DEPTH, nst - 1) * kXK;                               \
+      const int64_t kb = k_lo + (int64_t)min(st_ + kDepth, nst - 1) * kXK;                                    \
       LA.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);                                                        \
       LB.load(B, Bl, ldb, n0, N, kb, k_lo, k_hi, tid);                                                        \
     }                                                                                                         \
@@ -695,18 +720,26 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
   SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
 #endif
-#if RQ_X3_DEPTH == 3
-  for (int st = 0; st < nst; st += 3) {
-    RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)   // set j % 3 holds stage j: reload set (st % 3) with st + 3
-    if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2)
-    if (st + 2 < nst) RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0)
+  // set j % kDepth holds stage j: after multiplying stage st its set is reloaded with st + kDepth
+  if constexpr (kDepth == 4) {
+    for (int st = 0; st < nst; st += 4) {
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)
+      if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2)
+      if (st + 2 < nst) RQ_X3_STAGE(st + 2, sa2, sb2, sa3, sb3)
+      if (st + 3 < nst) RQ_X3_STAGE(st + 3, sa3, sb3, sa0, sb0)
+    }
+  } else if constexpr (kDepth == 3) {
+    for (int st = 0; st < nst; st += 3) {
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)
+      if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2)
+      if (st + 2 < nst) RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0)
+    }
+  } else {
+    for (int st = 0; st < nst; st += 2) {
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)
+      if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0)
+    }
   }
-#else
-  for (int st = 0; st < nst; st += 2) {
-    RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)   // set 0 held stage st (already in LDS): reload it with st + 2
-    if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0)
-  }
-#endif
 #undef RQ_X3_STAGE
 #undef RQ_X3_BODY
 #undef RQ_X3_MMA
@@ -715,7 +748,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
 #if RQ_X3_MFMA16
   // 16x16 C/D map of D = B A^T: column (lane & 15) = m, row 4 (lane >> 4) + j = n (j = register).
-  constexpr int kPM = 4, kPN = 4, kG = 1;
+  constexpr int kPM = kP, kPN = kP, kG = 1;
 #else
   // 32x32 C/D map: column (lane & 31) = m, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5) = n: register
   // quad g holds n = 8 g + 4 (lane >> 5) + 0..3.
@@ -724,7 +757,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 #pragma unroll
   for (int p = 0; p < kPM; ++p) {
 #if RQ_X3_MFMA16
-    const int m = m0 + wm * 64 + 16 * p + (lane & 15);
+    const int m = m0 + wm * kWTile + 16 * p + (lane & 15);
 #else
     const int m = m0 + wm * 64 + 32 * p + (lane & 31);
 #endif
@@ -734,7 +767,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 #pragma unroll
         for (int g = 0; g < kG; ++g) {
 #if RQ_X3_MFMA16
-          const int n = n0 + wn * 64 + 16 * q + 4 * (lane >> 4);
+          const int n = n0 + wn * kWTile + 16 * q + 4 * (lane >> 4);
           const float4 v = make_float4(acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]);
 #else
           const int n = n0 + wn * 64 + 32 * q + 8 * g + 4 * (lane >> 5);
@@ -1118,6 +1151,7 @@ __global__ void __launch_bounds__(256) split_bf16x3_multi_kernel(SplitMulti sm) 
 struct X3Plan {
   int tiles_n, tiles, S, per;
   int64_t chunk;
+  int ts;   // output tile of the 128-tile kernel family: 128 or 64 (the wide kernel: 256)
 };
 
 static int x3_slots() { return resident_slots() / 2 * kXWG; }
@@ -1144,14 +1178,21 @@ static int64_t x3_split_cap(int64_t M, int64_t N) {
 #ifndef RQ_X3W_SPEED
 #define RQ_X3W_SPEED 1.3
 #endif
+#ifndef RQ_X3S_RATE1
+#define RQ_X3S_RATE1 0.3    // 64-tile kernel, one workgroup per CU: M fp32-MAC / us
+#endif
+#ifndef RQ_X3S_RATE2
+#define RQ_X3S_RATE2 0.35   // 64-tile kernel, two workgroups per CU
+#endif
 static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   const int64_t cus = resident_slots() / 2;
   const int64_t wgs = (int64_t)p.tiles * p.S;
-  const double tile = wide ? (double)kWT2 * kWT2 : (double)kXT * kXT;
-  const double rate = 0.53 * (wide ? RQ_X3W_SPEED : 1.0);   // M MAC / us per CU
+  const bool small = p.ts == 64;
+  const double tile = wide ? (double)kWT2 * kWT2 : (double)p.ts * p.ts;
+  const double rate = small ? RQ_X3S_RATE2 : 0.53 * (wide ? RQ_X3W_SPEED : 1.0);   // M MAC / us per CU
   double t;
   if (wgs <= cus) {   // at most one workgroup per CU
-    t = tile * (double)p.chunk / ((wide ? rate : 0.4) * 1e6);
+    t = tile * (double)p.chunk / ((wide ? rate : (small ? RQ_X3S_RATE1 : 0.4)) * 1e6);
   } else {
     const int64_t slots = wide ? cus : cus * kXWG;
     const int64_t rounds = (wgs + slots - 1) / slots;
@@ -1161,9 +1202,10 @@ static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   return t;
 }
 
-static X3Plan x3_plan_s(int64_t M, int64_t N, int64_t K, int64_t S, bool wide) {
+static X3Plan x3_plan_s(int64_t M, int64_t N, int64_t K, int64_t S, bool wide, int ts = kXT) {
   X3Plan p;
-  const int T = wide ? kWT2 : kXT, KS = wide ? 32 : kXK;
+  const int T = wide ? kWT2 : ts, KS = wide ? 32 : kXK;
+  p.ts = T;
   p.tiles_n = (int)((N + T - 1) / T);
   p.tiles = (int)((M + T - 1) / T) * p.tiles_n;
   int64_t chunk = (K + S - 1) / S;
@@ -1175,21 +1217,49 @@ static X3Plan x3_plan_s(int64_t M, int64_t N, int64_t K, int64_t S, bool wide) {
   return p;
 }
 
-static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
-  X3Plan p = x3_plan_s(M, N, K, 1, false);
-  // split K when the output tiles cannot fill the chip (weight gradients, the decoder's future rows)
-  // and the model says the slabs pay for themselves
+// RQ_X3S=0 in the environment (or rq_gemm_x3s_enable(0)) keeps the 128-tile kernel for every shape,
+// 2 forces the 64-tile kernel (A/B runs, kernel tests); 1 (default) lets the time model choose.
+static int g_x3s = -1;
+static int x3s_mode() {
+  if (g_x3s < 0) {
+    const char* e = getenv("RQ_X3S");
+    g_x3s = (e && e[0] == '0') ? 0 : ((e && e[0] == '2') ? 2 : 1);
+  }
+  return g_x3s;
+}
+
+// Best split-K plan of one tile size: split K when the output tiles cannot fill the chip (weight
+// gradients, the decoder's future rows) and the model says the slabs pay for themselves.
+static X3Plan x3_plan_t(int64_t M, int64_t N, int64_t K, bool allow_split, int ts) {
+  X3Plan p = x3_plan_s(M, N, K, 1, false, ts);
   if (allow_split && p.tiles < x3_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
     int64_t S = x3_slots() / p.tiles;
     const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
     if (S > max_s) S = max_s;
     if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);   // slab traffic of the reduction grows with S
+    if (ts == 64) {   // small tiles: the best of S = 2, 4, ... up to the one-round heuristic
+      for (int64_t s2 = 2; s2 < S; s2 *= 2) {
+        const X3Plan q = x3_plan_s(M, N, K, s2, false, ts);
+        if (x3_plan_time(q, M, N, false) < x3_plan_time(p, M, N, false)) p = q;
+      }
+    }
     if (S > 1) {
-      const X3Plan q = x3_plan_s(M, N, K, S, false);
+      const X3Plan q = x3_plan_s(M, N, K, S, false, ts);
       if (x3_plan_time(q, M, N, false) < x3_plan_time(p, M, N, false)) p = q;
     }
   }
   return p;
+}
+
+// 128-tile kernel, or its 64-tile form where the time model prefers it (the 128-tiles of a
+// 1,280-row operand are 40 workgroups: split-K slabs and their reduction cost more than the GEMM).
+static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
+  const X3Plan p = x3_plan_t(M, N, K, allow_split, kXT);
+  const int mode = x3s_mode();
+  if (mode == 0) return p;
+  const X3Plan q = x3_plan_t(M, N, K, allow_split, 64);
+  if (mode == 2) return q;
+  return x3_plan_time(q, M, N, false) < x3_plan_time(p, M, N, false) ? q : p;
 }
 
 #ifndef RQ_X3W_MIN_STEPS
@@ -1290,9 +1360,9 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
 static size_t x3_workspace_bytes(int64_t M, int64_t N, int64_t K, bool accumulate) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   // the larger of the two kernels' split-K slabs (which one runs depends on the operand formats)
-  const X3Plan p = x3_plan(M, N, K);
+  const X3Plan p = x3_plan_t(M, N, K, true, kXT), q = x3_plan_t(M, N, K, true, 64);
   X3Plan pw;
-  int S = p.S;
+  int S = p.S > q.S ? p.S : q.S;   // either tile size may run (rq_gemm_x3s_enable can switch between calls)
   if (x3w_plan(M, N, K, true, &pw) && pw.S > S) S = pw.S;
   if (accumulate && S < 1) S = 1;
   return (S > 1 || accumulate) ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
@@ -1359,8 +1429,14 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   const int64_t ldo = pl.S > 1 ? N : ldc;
   const int code = (a_kcontig ? 16 : 0) | (asp ? 8 : 0) | (b_kcontig ? 4 : 0) | (bsp ? 2 : 0);
 #define RQ_X3D(AK, AS, BK, BS, EP, DR)                                                                               \
-  hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR>), grid, block, 0, s, A, A_lo, lda, B, B_lo, ldb,     \
-                     (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep)
+  do {                                                                                                               \
+    if (pl.ts == 64)                                                                                                 \
+      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR, 64>), grid, block, 0, s, A, A_lo, lda, B, B_lo,  \
+                         ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep);         \
+    else                                                                                                             \
+      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR>), grid, block, 0, s, A, A_lo, lda, B, B_lo, ldb, \
+                         (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep);              \
+  } while (0)
 #define RQ_X3(AK, AS, BK, BS, EP)                                                                                    \
   do {                                                                                                               \
     if ((EP == kEpiSiluFwd || EP == kEpiSiluBwd) && ep.thr != 0)                                                      \
@@ -1460,6 +1536,12 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
                             ldh, p, seed, 0, workspace, ws_bytes, stream);
 }
 
+int rq_gemm_x3s_enable(int mode) {
+  const int prev = x3s_mode();
+  g_x3s = mode == 2 ? 2 : (mode ? 1 : 0);
+  return prev;
+}
+
 int rq_gemm_x3w_enable(int enable) {
   const int prev = x3w_enabled() ? g_x3w : 0;
   g_x3w = enable == 2 ? 2 : (enable ? 1 : 0);
@@ -1471,8 +1553,9 @@ int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_sp
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, a_split, b_split, a_kcontig, b_kcontig, epilogue, &pw);
-  if (splits) *splits = wide ? pw.S : x3_plan(M, N, K).S;
-  return wide ? 1 : 0;
+  const X3Plan pl = x3_plan(M, N, K);
+  if (splits) *splits = wide ? pw.S : pl.S;
+  return wide ? 1 : (pl.ts == 64 ? 2 : 0);
 }
 
 int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,

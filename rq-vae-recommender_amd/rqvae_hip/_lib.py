@@ -54,6 +54,7 @@ _SIGS = {
                             _U64, _I, _P, _SZ, _P], _I),
     "rq_gemm_bf16x3_choice": ([_I64, _I64, _I64, _I, _I, _I, _I, _I, _P], _I),
     "rq_gemm_x3w_enable": ([_I], _I),
+    "rq_gemm_x3s_enable": ([_I], _I),
     "rq_split_bf16x3": ([_P, _I64, _P, _P, _P], _I),
     "rq_split_bf16x3_multi": ([_I, _P, _P, _P, _P, _P], _I),
     "rq_unique_workspace": ([_I64], _SZ),

@@ -21,6 +21,16 @@ def _ops():
     return ops
 
 
+@pytest.fixture(autouse=True)
+def _x3_tiles_only():
+    """These tests are about the 128-tile kernel's split-K path: keep the 64-tile form (which serves
+    1,280-row launches unsplit) out of the way."""
+    ops = _ops()
+    prev = ops.gemm_x3s_enable(0)
+    yield
+    ops.gemm_x3s_enable(prev)
+
+
 def _close(a, b, tol):
     return float((a - b).abs().max()) <= tol * max(1e-30, float(b.abs().max()))
 

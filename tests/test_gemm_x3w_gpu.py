@@ -120,9 +120,9 @@ def test_x3w_fused_epilogues_equal_x3_kernel(device, wide_on, p):
 
 def test_x3w_not_chosen_for_fp32_or_small(device, wide_on):
     ops = wide_on
-    assert ops.gemm_x3_choice(65536, 512, 768, False, True, True, True)[0] == "x3"      # fp32 operand
-    assert ops.gemm_x3_choice(65536, 128, 256, True, True, True, True)[0] == "x3"       # N = 128: half tile
-    assert ops.gemm_x3_choice(64, 64, 64, True, True, True, True)[0] == "x3"
-    assert ops.gemm_x3_choice(65536, 512, 100, True, True, True, True)[0] == "x3"       # K % 32
+    assert ops.gemm_x3_choice(65536, 512, 768, False, True, True, True)[0] != "wide"      # fp32 operand
+    assert ops.gemm_x3_choice(65536, 128, 256, True, True, True, True)[0] != "wide"       # N = 128: half tile
+    assert ops.gemm_x3_choice(64, 64, 64, True, True, True, True)[0] != "wide"
+    assert ops.gemm_x3_choice(65536, 512, 100, True, True, True, True)[0] != "wide"       # K % 32
     ops.gemm_x3w_enable(False)
-    assert ops.gemm_x3_choice(65536, 512, 768, True, True, True, True)[0] == "x3"
+    assert ops.gemm_x3_choice(65536, 512, 768, True, True, True, True)[0] != "wide"
