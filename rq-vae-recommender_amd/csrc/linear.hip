@@ -485,7 +485,7 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #endif
 
 #ifndef RQ_X3S_DEPTH
-#define RQ_X3S_DEPTH 4   // stage sets in flight of the 64-tile form (its stages are 4x shorter)
+#define RQ_X3S_DEPTH 2   // stage sets in flight of the 64-tile form (A/B on MI355X: 2, 3, 4 within 3 %)
 #endif
 
 #ifndef RQ_X3_SETPRIO
