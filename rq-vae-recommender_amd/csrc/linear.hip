@@ -263,9 +263,18 @@ constexpr int kXBuf = 2 * kXOp;                // A + B
 constexpr int kXLds = 2 * kXBuf;               // double buffer: 64 KiB
 
 __device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
-// Row image: row rr of 2 kXK bytes, 16-B chunk c stored at c ^ row_swz(rr) (conflict-free for 16
-// consecutive rows at one chunk, and for the staging writes).
+// Row image: row rr of 2 kXK bytes, 16-B chunk c stored at c ^ row_swz(rr). With the 16x16x32 MFMA
+// (default) a fragment read (xfrag16) is a ds_read_b128 whose lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32) touch rows {0-3, 12-15} at chunk c and rows 4-11 at chunk c ^ 1: the
+// swizzle (rr >> 2) & 2 puts the four rows of equal rr % 4 on four distinct 16-B bank slots (the
+// wide kernel's image; (rr >> 2) & 3, designed for the 32x32x16 reads, was 2-way conflicted here:
+// SQ_LDS_BANK_CONFLICT 2.6 cycles per LDS instruction). Staging writes (ds_write_b128, 8-lane
+// groups over 2 rows) stay conflict-free.
+#if RQ_X3_BK16 || (defined(RQ_X3_MFMA16) && !RQ_X3_MFMA16)
 __device__ __forceinline__ int row_swz(int rr) { return kXCPR == 4 ? ((rr >> 2) & 3) : ((rr >> 3) & 1); }
+#else
+__device__ __forceinline__ int row_swz(int rr) { return (rr >> 2) & 2; }
+#endif
 __device__ __forceinline__ int row_off(int rr, int c) { return rr * (2 * kXK) + ((c ^ row_swz(rr)) << 4); }
 
 // One operand's staging registers (a TR x 32 tile per stage, 256 threads; TR = 128 or 64 rows of m / n).
