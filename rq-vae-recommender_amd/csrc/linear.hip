@@ -297,42 +297,32 @@ struct XStage {
   // split, m/n-contig: CT threads across the TR columns (8 each), KR k-rows per pass
   static constexpr int CT_S = TR / 8, KR_S = 256 / CT_S, NJ_SM = kXK / KR_S;
   uint4 v[4];
-  bool ok[4];
-  bool full;   // every k of the stage < k_hi (all but a split's / the matrix's last stage): no masking
+  bool ok[4];   // k of the loaded vector < k_hi (else it read k_lo and is zeroed at store time)
 
   // rows [r0, r0 + TR) of the operand (clamped to R - 1: they feed only outputs >= R, never
-  // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time. The
-  // per-lane part of each address does not depend on the stage, so a full stage's load is a
-  // uniform base (X + kb) plus a loop-invariant lane offset.
+  // written); k in [kb, kb + 32), positions >= k_hi read k_lo and are zeroed at store time. Every
+  // load is unconditional and its address branch-free (a select), so the compiler can count the
+  // loads in flight statically: with separate full-stage / masked-stage load paths it merged the
+  // paths' counts and waited vmcnt(0) at the top of every k iteration, draining the prefetch.
   __device__ __forceinline__ void load(const void* __restrict__ Xv, const void* __restrict__ Xlv, int64_t ld, int r0,
                                        int R, int64_t kb, int64_t k_lo, int64_t k_hi, int tid) {
-    full = kb + kXK <= k_hi;
     if constexpr (!SP) {
       const float* __restrict__ X = static_cast<const float*>(Xv);
       if constexpr (KC) {   // thread: chunk tid % CPR of rows tid / CPR (+ 256 / CPR), 2 float4 per chunk
 #pragma unroll
         for (int j = 0; j < NJ_FK; ++j) {
           const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * (j >> 1), R - 1);
-          const int64_t lane = row * ld + (tid % kXCPR) * 8 + 4 * (j & 1);
-          if (full) {
-            v[j] = *reinterpret_cast<const uint4*>(X + kb + lane);
-          } else {
-            const int64_t k = kb + (tid % kXCPR) * 8 + 4 * (j & 1);
-            ok[j] = k < k_hi;
-            v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
-          }
+          const int64_t k = kb + (tid % kXCPR) * 8 + 4 * (j & 1);
+          ok[j] = k < k_hi;
+          v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
         }
       } else {              // thread: 4 consecutive rows 4 (tid % CT), k rows tid / CT + KR j
         const int64_t col = min(r0 + 4 * (tid % CT_F), R - 4);
 #pragma unroll
         for (int j = 0; j < NJ_FM; ++j) {
           const int64_t k = kb + (tid / CT_F) + KR_F * j;
-          if (full) {
-            v[j] = *reinterpret_cast<const uint4*>(X + kb * ld + ((tid / CT_F) + KR_F * j) * ld + col);
-          } else {
-            ok[j] = k < k_hi;
-            v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
-          }
+          ok[j] = k < k_hi;
+          v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
         }
       }
     } else {
@@ -343,13 +333,8 @@ struct XStage {
         for (int j = 0; j < NJ_SK; ++j) {
           const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * j, R - 1);
           const int64_t k = kb + (tid % kXCPR) * 8;
-          int64_t o;
-          if (full) {
-            o = kb + row * ld + (tid % kXCPR) * 8;
-          } else {
-            ok[j] = k < k_hi;
-            o = row * ld + (ok[j] ? k : k_lo);
-          }
+          ok[j] = k < k_hi;
+          const int64_t o = row * ld + (ok[j] ? k : k_lo);
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
         }
@@ -358,21 +343,14 @@ struct XStage {
 #pragma unroll
         for (int j = 0; j < NJ_SM; ++j) {
           const int64_t k = kb + (tid / CT_S) + KR_S * j;
-          int64_t o;
-          if (full) {
-            o = kb * ld + ((tid / CT_S) + KR_S * j) * ld + col;
-          } else {
-            ok[j] = k < k_hi;
-            o = (ok[j] ? k : k_lo) * ld + col;
-          }
+          ok[j] = k < k_hi;
+          const int64_t o = (ok[j] ? k : k_lo) * ld + col;
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
         }
       }
     }
   }
-
-  __device__ __forceinline__ bool okj(int j) const { return full || ok[j]; }
 
   __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, int tid) const {
     if constexpr (!SP) {
@@ -381,12 +359,8 @@ struct XStage {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const float4 f = __builtin_bit_cast(float4, v[j]);
-        if (full) {
-          w[j] = f;
-        } else {
-          const bool k = ok[j];
-          w[j] = make_float4(k ? f.x : 0.f, k ? f.y : 0.f, k ? f.z : 0.f, k ? f.w : 0.f);
-        }
+        const bool k = ok[j];
+        w[j] = make_float4(k ? f.x : 0.f, k ? f.y : 0.f, k ? f.z : 0.f, k ? f.w : 0.f);
       }
       if constexpr (KC) {
 #pragma unroll
@@ -418,12 +392,10 @@ struct XStage {
       constexpr int NJ = KC ? NJ_SK : NJ_SM;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        uint4 h = v[j], l = v[2 + j];
-        if (!full) {
-          const bool k = ok[j];
-          h = make_uint4(k ? h.x : 0u, k ? h.y : 0u, k ? h.z : 0u, k ? h.w : 0u);
-          l = make_uint4(k ? l.x : 0u, k ? l.y : 0u, k ? l.z : 0u, k ? l.w : 0u);
-        }
+        const bool k = ok[j];
+        const uint4 h0 = v[j], l0 = v[2 + j];
+        const uint4 h = make_uint4(k ? h0.x : 0u, k ? h0.y : 0u, k ? h0.z : 0u, k ? h0.w : 0u);
+        const uint4 l = make_uint4(k ? l0.x : 0u, k ? l0.y : 0u, k ? l0.z : 0u, k ? l0.w : 0u);
         int off;
         if constexpr (KC) {
           const int rr = (tid / kXCPR) + (256 / kXCPR) * j, c = tid % kXCPR;
@@ -691,9 +663,10 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   sb0.store(plane(0, 1, 0), plane(0, 1, 1), tid);
   __syncthreads();
 
-#define RQ_X3_STAGE(ST, LA, LB, SA, SB)                                                                       \
+#define RQ_X3_STAGE(ST, LA, LB, SA, SB, ON)                                                                   \
   {                                                                                                           \
     const int st_ = (ST), buf = st_ & 1;                                                                      \
+    const bool on_ = (ON);                                                                                    \
     {  /* unconditional (past the end: the last stage again, an L2 hit) so vmcnt counts stay static */       \
       const int64_t kb = k_lo + (int64_t)min(st_ + kDepth, nst - 1) * kXK;                                    \
       LA.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);                                                        \
@@ -715,7 +688,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 #define RQ_X3_BODY(SA, SB)                                                                                    \
   SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
   SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                  \
-  RQ_X3_MMA                                                                                                   \
+  if (on_) RQ_X3_MMA                                                                                          \
   _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                          \
     __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                                                        \
     __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                                                        \
@@ -723,30 +696,34 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
   }
 #else
 #define RQ_X3_BODY(SA, SB)                                                                                    \
-  RQ_X3_PRIO(1)                                                                                               \
-  RQ_X3_MMA                                                                                                   \
-  RQ_X3_PRIO(0)                                                                                               \
+  if (on_) {                                                                                                  \
+    RQ_X3_PRIO(1)                                                                                             \
+    RQ_X3_MMA                                                                                                 \
+    RQ_X3_PRIO(0)                                                                                             \
+  }                                                                                                           \
   SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
   SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
 #endif
-  // set j % kDepth holds stage j: after multiplying stage st its set is reloaded with st + kDepth
+  // set j % kDepth holds stage j: after multiplying stage st its set is reloaded with st + kDepth.
+  // Every stage slot of an iteration issues its loads, stores and barrier; only the MFMAs of slots
+  // past the last stage are skipped (a skipped slot's loads would leave the counts path-dependent).
   if constexpr (kDepth == 4) {
     for (int st = 0; st < nst; st += 4) {
-      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)
-      if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2)
-      if (st + 2 < nst) RQ_X3_STAGE(st + 2, sa2, sb2, sa3, sb3)
-      if (st + 3 < nst) RQ_X3_STAGE(st + 3, sa3, sb3, sa0, sb0)
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+      RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2, st + 1 < nst)
+      RQ_X3_STAGE(st + 2, sa2, sb2, sa3, sb3, st + 2 < nst)
+      RQ_X3_STAGE(st + 3, sa3, sb3, sa0, sb0, st + 3 < nst)
     }
   } else if constexpr (kDepth == 3) {
     for (int st = 0; st < nst; st += 3) {
-      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)
-      if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2)
-      if (st + 2 < nst) RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0)
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+      RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2, st + 1 < nst)
+      RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0, st + 2 < nst)
     }
   } else {
     for (int st = 0; st < nst; st += 2) {
-      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1)
-      if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0)
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+      RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0, st + 1 < nst)
     }
   }
 #undef RQ_X3_STAGE
