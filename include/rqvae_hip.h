@@ -259,11 +259,32 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream);
+/* varlen_attn_fwd with a caller-provided int scratch `order` of B entries (may be NULL): for long ranges
+ * (max_k > 128, 2 <= B <= 4096) the launch first ranks the sequences longest-first into it and the
+ * kernel dispatches their workgroups in that order (no straggler tail); results are identical. */
+int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
+                     void* stream);
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
                     float* delta, void* stream);
+/* Same contract as varlen_attn_bwd; where hd == 64 and the key / query ranges are longer than the short
+ * forms serve (the decoder's encoder self-attention), ONE fused launch computes dQ, dK and dV per key
+ * block with S and dP formed once per tile pair (after a delta = rowsum(dO*O) pre-pass); dQ of
+ * sequences longer than one key block is summed from per-block partials in block order by a reduction
+ * launch (deterministic, no atomics). ws: caller-provided scratch of at least
+ * varlen_attn_bwd_ws_elems(...) floats (0 -> ws may be NULL; it also holds the longest-first sequence
+ * order of the fused launch, as varlen_attn_fwd2). Other shapes run varlen_attn_bwd. */
+int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
+                             int64_t* elems);
+int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
+                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
+                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
+                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
+                     float* delta, float* ws, int64_t ws_elems, void* stream);
 
 /* AdamW step (torch.optim.AdamW as stepped by train_rqvae.py:168-172 / train_decoder.py:203) over
  * every fp32 parameter of a group, one launch per 64 tensors. segs: HOST array of nseg records of 5

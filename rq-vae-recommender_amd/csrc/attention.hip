@@ -200,6 +200,27 @@ __device__ __forceinline__ void dispatch_tiles(int nt, bool interior, F& f) {
   f.template run<NTL, true>();
 }
 
+// ------------------------------------------------------------------------- sequence order
+// Longest-first dispatch order of the sequences (LPT): order[r] = the sequence of rank r by segment
+// length (descending, ties by index). The chunked forward and the fused backward map grid z through it,
+// so the longest sequences' workgroups (whose run time grows with the length) start first and the
+// launch does not end on one long straggler. One workgroup, lengths staged in LDS, B <= kOrderMax.
+constexpr int kOrderMax = 4096;
+__global__ void __launch_bounds__(1024) attn_order_kernel(const int64_t* __restrict__ cu, int B, int* __restrict__ order) {
+  __shared__ int len[kOrderMax];
+  for (int b = threadIdx.x; b < B; b += 1024) len[b] = (int)(cu[b + 1] - cu[b]);
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += 1024) {
+    const int lb = len[b];
+    int rank = 0;
+    for (int j = 0; j < B; ++j) rank += (len[j] > lb) || (len[j] == lb && j < b);
+    order[rank] = b;
+  }
+}
+
+// sequence of grid slice z (z < B): through the LPT order when one is given
+__device__ __forceinline__ int seq_of(const int* __restrict__ order, int z) { return order ? order[z] : z; }
+
 // ---------------------------------------------------------------------------------------- fwd
 template <int HD>
 struct FwdChunk {
@@ -258,17 +279,18 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restri
                                                         int64_t sk, const float* __restrict__ v, int64_t sv,
                                                         const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
                                                         int causal, float scale, float* __restrict__ out, int64_t so,
-                                                        float* __restrict__ lse, int64_t Tq) {
+                                                        float* __restrict__ lse, int64_t Tq, const int* __restrict__ order) {
   constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
   __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
   float* K_s = smem;
   float* V_s = smem + CH * LD;
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4;
-  if (b == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
-    zero_rows<HD, 64 * NW>(out, so, cu_q[b], Tq, hh, tid);
+  if (z == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
+    zero_rows<HD, 64 * NW>(out, so, cu_q[z], Tq, hh, tid);
     return;
   }
+  const int b = seq_of(order, z);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   const int qwg = blockIdx.x * 16 * NW;
@@ -557,6 +579,247 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
   store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
 }
 
+// ------------------------------------------------------------------ bwd: fused dQ, dK, dV
+// One launch per key block of KB = 16 NW keys computes S and dP ONCE per (query tile, key tile)
+// pair — 5 MFMA products per pair (S, dP, dV, dK, dQ) instead of the two-pass form's 7 (the dQ pass
+// recomputes S and dP). The block's dS (CH queries x KB keys) goes through LDS so each wave can
+// form dQ rows over ALL KB keys against the staged K block: dQ^T(16 q) += K^T dS^T. A sequence with
+// one key block (lk <= KB) gets dQ written directly; longer ones write one partial per key block
+// into `part` (nkb_max, Tq, H*HD) and attn_dq_reduce_kernel sums them in key-block order — no
+// atomics, bitwise deterministic. delta = rowsum(dO * O) comes from attn_delta_kernel beforehand.
+template <int HD>
+struct FusedChunk {
+  const float* Q_s;
+  const float* O_s;
+  const float* lse_s;
+  const float* dl_s;
+  const float* kf;
+  const float* vf;
+  float* dS_s;   // [CH][KB + 4]: this wave writes columns [16 wave, 16 wave + 16)
+  int lane, qc, t0, lq, kj, causal, col, ldS;
+  bool kv;
+  float sl2;
+  f32x4* dka;
+  f32x4* dva;
+  template <int NTT, bool MASK>
+  __device__ __forceinline__ void run() { groups<NTT, MASK>(t0); }
+  template <int N, bool MASK>
+  __device__ __forceinline__ void groups(int tb) {
+    constexpr int NG = N < RQ_ATTN_BWD_GROUP ? N : RQ_ATTN_BWD_GROUP;
+    group<NG, MASK>(tb);
+    if constexpr (N > NG) groups<N - NG, MASK>(tb + NG);
+  }
+  template <int NG, bool MASK>
+  __device__ __forceinline__ void group(int tb) {
+    constexpr int LD = HD + 4;
+    const int g = lane >> 4;
+    const float* Qt = Q_s + tb * 16 * LD;
+    const float* Ot = O_s + tb * 16 * LD;
+    f32x4 s[NG], dp[NG];
+#pragma unroll
+    for (int t = 0; t < NG; ++t) { s[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    tiles_x_frag2<HD, NG>(Qt, *reinterpret_cast<const float(*)[HD / 4]>(kf), Ot,
+                          *reinterpret_cast<const float(*)[HD / 4]>(vf), lane, s, dp);   // S, dP = dO V^T
+#pragma unroll
+    for (int t = 0; t < NG; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = (tb + t) * 16 + 4 * g + i;
+        float p = exp2_fast(__builtin_fmaf(s[t][i], sl2, -lse_s[qr]));
+        if constexpr (MASK) {
+          const int qq = qc + qr;
+          if (!(qq < lq && (!causal || kj <= qq))) p = 0.f;
+        }
+        s[t][i] = p;
+        dp[t][i] = p * (dp[t][i] - dl_s[qr]);   // dS
+        dS_s[qr * ldS + col] = kv ? dp[t][i] : 0.f;
+      }
+    f32x4(&dk_)[HD / 16] = *reinterpret_cast<f32x4(*)[HD / 16]>(dka);
+    f32x4(&dv_)[HD / 16] = *reinterpret_cast<f32x4(*)[HD / 16]>(dva);
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+      colsT_x_acc<HD>(Ot + t * 16 * LD, s[t], lane, dv_);    // dV^T += dO^T P
+      colsT_x_acc<HD>(Qt + t * 16 * LD, dp[t], lane, dk_);   // dK^T += Q^T dS
+    }
+  }
+};
+
+// delta[h][t] = sum_d dO[t][h HD + d] * O[t][h HD + d] over every allocated row (16 lanes per (row, head))
+template <int HD>
+__global__ void __launch_bounds__(256) attn_delta_kernel(const float* __restrict__ out, int64_t so,
+                                                         const float* __restrict__ dout, int64_t sdo, int64_t Tq,
+                                                         int64_t H, float* __restrict__ delta) {
+  constexpr int LPR = HD / 4 < 16 ? HD / 4 : 16;   // lanes per (row, head)
+  constexpr int PER = HD / (4 * LPR);              // float4 per lane
+  const int64_t item = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  float acc = 0.f;
+  const bool ok = item < Tq * H;
+  const int64_t t = ok ? item / H : 0, hh = ok ? item % H : 0;
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = (j * LPR + sub) * 4;
+      const float4 a = *reinterpret_cast<const float4*>(out + t * so + hh * HD + c);
+      const float4 b = *reinterpret_cast<const float4*>(dout + t * sdo + hh * HD + c);
+      acc += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (ok && sub == 0) delta[hh * Tq + t] = acc;
+}
+
+template <int HD, int NW, int CH>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
+    const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ part, float* __restrict__ dk,
+    int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk, const int* __restrict__ order) {
+  constexpr int LD = HD + 4, DT = HD / 16, KB = 16 * NW, NTL = CH / 16, LDS_ = KB + 4;
+  constexpr int DSPLIT = NW >= NTL ? NW / NTL : 1, DTW = DT / DSPLIT;
+  static_assert(DT % DSPLIT == 0, "dQ split");
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD + 2 * CH + KB * LD + CH * LDS_];
+  float* Q_s = smem;
+  float* O_s = Q_s + CH * LD;   // dO
+  float* lse_s = O_s + CH * LD;
+  float* dl_s = lse_s + CH;
+  float* K_s = dl_s + CH;       // the block's KB key rows (A operand of dQ^T = K^T dS^T)
+  float* dS_s = K_s + KB * LD;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  if (z == (int)gridDim.z - 1) {              // tail slice: gradient rows past the last sequence
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[z], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[z], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[z], Tq, hh, tid);
+    return;
+  }
+  const int b = seq_of(order, z);
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  const int kwg = blockIdx.x * KB;
+  if (kwg >= lk) {
+    if (lk == 0) zero_rows<HD, 64 * NW>(dq, sdq, q0, q0 + lq, hh, tid);   // no keys: dQ = 0 (grid-stride over x)
+    return;
+  }
+  const int nkb = (lk + KB - 1) / KB;
+  const int kb = kwg + wave * 16, kj = kb + (lane & 15);
+  const bool wave_on = kb < lk, kv = kj < lk;
+  const int64_t krow = k0 + (kv ? kj : 0);
+  float kf[HD / 4], vf[HD / 4];
+  load_frag<HD>(k + krow * sk + hh * HD + g * (HD / 4), kv, kf);
+  load_frag<HD>(v + krow * sv + hh * HD + g * (HD / 4), kv, vf);
+  {
+    RowStage<HD, 64 * NW, KB> stk;
+    stk.load(k + k0 * sk + hh * HD, sk, kwg, lk, tid);
+    stk.store(K_s, tid);                      // published by the first chunk's barrier
+  }
+  f32x4 dka[DT], dva[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  const int qstart = causal ? (kwg / CH) * CH : 0;
+  const float* qb_ = q + q0 * sq + hh * HD;
+  const float* ob_ = dout + q0 * sdo + hh * HD;
+  const float* lse_h = lse + (int64_t)hh * Tq + q0;
+  const float* dl_h = delta + (int64_t)hh * Tq + q0;
+  const int64_t HH = (int64_t)gridDim.y * HD;
+  float* dst;
+  int64_t dstride;
+  float mul;
+  if (nkb == 1) { dst = dq + q0 * sdq + hh * HD; dstride = sdq; mul = scale; }
+  else { dst = part + ((int64_t)blockIdx.x * Tq + q0) * HH + hh * HD; dstride = HH; mul = 1.f; }
+  RowStage<HD, 64 * NW, CH> stq, sto;
+  FusedChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, dS_s, lane, 0, 0, lq, kj, causal, wave * 16 + (lane & 15), LDS_, kv,
+                    scale * kLog2e, dka, dva};
+  for (int qc = qstart; qc < lq; qc += CH) {
+    stq.load(qb_, sq, qc, lq, tid);
+    sto.load(ob_, sdo, qc, lq, tid);
+    const bool ok = tid < CH && qc + tid < lq;
+    const float lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
+    const float dl_r = ok ? dl_h[qc + tid] : 0.f;
+    __syncthreads();                          // previous chunk's Q/dO/dS reads are done
+    stq.store(Q_s, tid);
+    sto.store(O_s, tid);
+    if (tid < CH) {
+      lse_s[tid] = lse_r;
+      dl_s[tid] = dl_r;
+    }
+    __syncthreads();
+    const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);
+    const int nt = __builtin_amdgcn_readfirstlane(wave_on ? max(0, min(NTL, (lq - qc + 15) >> 4) - t0) : 0);
+    // dS columns of tiles this wave does not compute are zero (K_s rows past lk are zero too, but
+    // stale LDS could hold NaN bit patterns)
+    for (int t = 0; t < NTL; ++t)
+      if (t < t0 || t >= t0 + nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dS_s[(t * 16 + 4 * g + i) * LDS_ + fc.col] = 0.f;
+    fc.qc = qc;
+    fc.t0 = t0;
+    dispatch_tiles<NTL>(nt, !causal && qc + CH <= lq, fc);
+    __syncthreads();                          // dS of every wave in LDS
+    // dQ^T (16 queries x DTW*16 dims) += K^T dS^T over the block's keys (key tiles past lk are zero)
+    const int nkt = __builtin_amdgcn_readfirstlane(min(NW, (lk - kwg + 15) >> 4));
+    for (int u = wave; u < NTL * DSPLIT; u += NW) {
+      const int qt = u % NTL, d0 = (u / NTL) * DTW;
+      if (qc + qt * 16 >= lq) continue;
+      f32x4 acc[DTW];
+#pragma unroll
+      for (int j = 0; j < DTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* dsrow = dS_s + (qt * 16 + (lane & 15)) * LDS_ + 4 * g;
+      for (int kt = 0; kt < nkt; ++kt) {
+        const float4 w4 = *reinterpret_cast<const float4*>(dsrow + kt * 16);
+        const float w[4] = {w4.x, w4.y, w4.z, w4.w};
+        const float* base = K_s + (kt * 16 + 4 * g) * LD + d0 * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < DTW; ++j) acc[j] = mfma4(base[i * LD + j * 16], w[i], acc[j]);
+      }
+      const int qi = qc + qt * 16 + (lane & 15);
+      if (qi < lq) {
+        float* rowp = dst + (int64_t)qi * dstride + d0 * 16 + 4 * g;
+#pragma unroll
+        for (int j = 0; j < DTW; ++j)
+          *reinterpret_cast<float4*>(rowp + j * 16) =
+              make_float4(acc[j][0] * mul, acc[j][1] * mul, acc[j][2] * mul, acc[j][3] * mul);
+      }
+    }
+  }
+  if (!kv) return;
+  store_rowT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, lane);
+  store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
+}
+
+// dQ rows of sequences with more than one key block: scale * sum over key blocks (in block order) of
+// the fused kernel's partials. Causal: query r sees key blocks kb <= r / KB only (the others never
+// wrote row r). One thread per float4 of a (row, head) slice; grid (row blocks of 16, H, B).
+template <int HD, int KB>
+__global__ void __launch_bounds__(256) attn_dq_reduce_kernel(const float* __restrict__ part, int64_t Tq,
+                                                             const int64_t* __restrict__ cu_q,
+                                                             const int64_t* __restrict__ cu_k, int causal, float scale,
+                                                             float* __restrict__ dq, int64_t sdq) {
+  constexpr int F4 = HD / 4, RPB = 256 / F4;   // rows per block
+  const int b = blockIdx.z, hh = blockIdx.y;
+  const int64_t q0 = cu_q[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - cu_k[b]);
+  const int nkb = (lk + KB - 1) / KB;
+  if (nkb <= 1) return;                        // written directly by the fused kernel
+  const int r = blockIdx.x * RPB + threadIdx.x / F4, c = (threadIdx.x % F4) * 4;
+  if (r >= lq) return;
+  const int n = causal ? min(nkb, r / KB + 1) : nkb;
+  const int64_t HH = (int64_t)gridDim.y * HD;
+  const float* p = part + (q0 + r) * HH + hh * HD + c;
+  const int64_t slab = Tq * HH;
+  float4 s = *reinterpret_cast<const float4*>(p);
+  for (int j = 1; j < n; ++j) {
+    const float4 a = *reinterpret_cast<const float4*>(p + j * slab);
+    s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+  }
+  *reinterpret_cast<float4*>(dq + (q0 + r) * sdq + hh * HD + c) =
+      make_float4(s.x * scale, s.y * scale, s.z * scale, s.w * scale);
+}
+
 // ------------------------------------------------------------------------ short sequences
 // Short-sequence forms (the decoder's Amazon contexts, <= 81 tokens, and its 5 future tokens): one
 // workgroup per (sequence, head) stages the head's WHOLE key range (forward, dQ) or query range (dK/dV)
@@ -787,20 +1050,26 @@ static bool short_plan(int64_t rows, int64_t staged, int* nw, int* ch) {
 // on padding, long ones (ML-32M <= 801, C5 <= 1281) share each staged 64-row chunk between 4 waves.
 static int waves_for(int64_t rows) { return rows <= 16 ? 1 : (rows <= 96 ? 2 : 4); }
 
+#ifndef RQ_ATTN_LPT
+#define RQ_ATTN_LPT 1   // longest-first sequence order for long ranges (A/B switch)
+#endif
+// LPT order where a workgroup's run time varies enough with the sequence to leave a straggler tail
+static bool lpt_plan(int64_t B, int64_t max_len) { return RQ_ATTN_LPT && B >= 2 && B <= kOrderMax && max_len > 128; }
+
 template <int HD, int NW>
 static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
                    int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal, float scale,
-                   float* out, int64_t so, float* lse, int64_t Tq) {
+                   float* out, int64_t so, float* lse, int64_t Tq, const int* order) {
   dim3 g((unsigned)std::max<int64_t>(1, (max_q + 16 * NW - 1) / (16 * NW)), (unsigned)H, (unsigned)B + 1);   // + tail slice
   hipLaunchKernelGGL((attn_fwd_kernel<HD, NW>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
-                     so, lse, Tq);
+                     so, lse, Tq, order);
 }
 
 template <int HD>
 static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q, int64_t sq,
                        const float* k,
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
-                       float scale, float* out, int64_t so, float* lse, int64_t Tq) {
+                       float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order) {
   if constexpr (HD == 64) {
     int nw = 0, ch = 0;
     if (short_plan(max_q, max_k, &nw, &ch)) {
@@ -813,10 +1082,15 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
       return;
     }
   }
+  const int* ord = nullptr;
+  if (order && lpt_plan(B, max_k)) {
+    hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, ck, (int)B, order);
+    ord = order;
+  }
   switch (waves_for(max_q)) {
-    case 1: fwd_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
-    case 2: fwd_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
-    default: fwd_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+    case 1: fwd_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord); break;
+    case 2: fwd_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord); break;
+    default: fwd_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord); break;
   }
 }
 
@@ -896,6 +1170,71 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
   }
 }
 
+// Fused backward (one launch for dQ, dK, dV: attn_bwd_fused_kernel) where the two-pass form would use the
+// chunked dK/dV kernel; the short forms keep the decoder's 5-token self- and cross-attention.
+#ifndef RQ_ATTN_FUSED
+#define RQ_ATTN_FUSED 1
+#endif
+#ifndef RQ_ATTN_FUSED_NW
+#define RQ_ATTN_FUSED_NW 4   // waves per workgroup = key block / 16
+#endif
+#ifndef RQ_ATTN_FUSED_CH
+#define RQ_ATTN_FUSED_CH 32  // staged query rows per LDS round trip (A/B on MI355X: 32 beats 64 by 4-5 %)
+#endif
+#ifndef RQ_ATTN_FUSED_MIN_K
+#define RQ_ATTN_FUSED_MIN_K 129   // shorter key ranges keep the two-pass form (Amazon n <= 81: 0.25 vs 0.30 ms)
+#endif
+constexpr int kFusedKB = 16 * RQ_ATTN_FUSED_NW;
+
+static bool fused_plan(int64_t hd, int64_t max_q, int64_t max_k) {
+  if (!RQ_ATTN_FUSED || hd != 64 || max_k < RQ_ATTN_FUSED_MIN_K) return false;
+  int nw = 0, ch = 0;
+  return !short_plan(max_k, max_q, &nw, &ch);
+}
+
+// floats of dQ partials the fused backward needs: one (Tq, H*hd) slab per key block when a sequence may
+// span more than one block
+static int64_t fused_part_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq) {
+  if (!fused_plan(hd, max_q, max_k)) return 0;
+  const int64_t nkb = (max_k + kFusedKB - 1) / kFusedKB;
+  return nkb > 1 ? nkb * Tq * H * hd : 0;
+}
+// + B ints of LPT order (float slots)
+static int64_t fused_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq) {
+  if (!fused_plan(hd, max_q, max_k)) return 0;
+  return fused_part_elems(H, hd, max_q, max_k, Tq) + (lpt_plan(B, max_q) ? B : 0);
+}
+
+template <int HD>
+static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q,
+                             int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
+                             int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq,
+                             const int64_t* ck, int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk,
+                             float* dv, int64_t sdv, int64_t Tk, float* delta, float* ws) {
+  if constexpr (HD == 64) {
+    constexpr int NW = RQ_ATTN_FUSED_NW, CH = RQ_ATTN_FUSED_CH, KB = 16 * NW;
+    const int* ord = nullptr;
+    if (lpt_plan(B, max_q)) {   // the order lives after the dQ partials in ws
+      int* o = reinterpret_cast<int*>(ws + fused_part_elems(H, HD, max_q, max_k, Tq));
+      hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, cq, (int)B, o);
+      ord = o;
+    }
+    constexpr int LPR = HD / 4 < 16 ? HD / 4 : 16;
+    const int64_t threads = Tq * H * LPR;
+    if (threads > 0)
+      hipLaunchKernelGGL((attn_delta_kernel<HD>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, out, so, dout,
+                         sdo, Tq, H, delta);
+    const dim3 g((unsigned)std::max<int64_t>(1, (max_k + KB - 1) / KB), (unsigned)H, (unsigned)B + 1);   // + tail slice
+    hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, NW, CH>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse,
+                       delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord);
+    if ((max_k + KB - 1) / KB > 1 && max_q > 0) {
+      constexpr int RPB = 256 / (HD / 4);
+      const dim3 gr((unsigned)((max_q + RPB - 1) / RPB), (unsigned)H, (unsigned)B);
+      hipLaunchKernelGGL((attn_dq_reduce_kernel<HD, KB>), gr, dim3(256), 0, st, ws, Tq, cq, ck, causal, scale, dq, sdq);
+    }
+  }
+}
+
 static bool attn_args_ok(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k) {
   // max_q / max_k bound the grid's x extent and every in-kernel int index (row * stride fits int64)
   return B >= 0 && B < 65535 && H >= 1 && H <= 65535 && (hd == 16 || hd == 32 || hd == 64 || hd == 128) && max_q >= 0 &&
@@ -908,22 +1247,30 @@ using namespace rqhip;
 
 extern "C" {
 
-int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                    const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
+int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
+                     void* stream) {
   RQ_CHECK_ARG(q && k && v && cu_q && cu_k && out && lse, "varlen_attn_fwd: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
-    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
-    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq); break;
+    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
+    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
+    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
+    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_fwd");
   return 0;
+}
+
+int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                    const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
+  return varlen_attn_fwd2(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq,
+                          nullptr, stream);
 }
 
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
@@ -946,6 +1293,37 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
     case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_bwd");
+  return 0;
+}
+
+int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
+                             int64_t* elems) {
+  RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_bwd_ws_elems: bad shape");
+  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq);
+  return 0;
+}
+
+int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
+                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
+                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
+                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
+                     float* delta, float* ws, int64_t ws_elems, void* stream) {
+  if (!fused_plan(hd, max_q, max_k))
+    return varlen_attn_bwd(q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, B, H, hd, max_q, max_k, causal,
+                           scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, stream);
+  RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv && delta,
+               "varlen_attn_bwd2: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd2: bad shape (hd must be 16/32/64/128, B<65535)");
+  RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0 && sdo % 4 == 0 && sdq % 4 == 0 &&
+                   sdk % 4 == 0 && sdv % 4 == 0,
+               "varlen_attn_bwd2: row strides must be x4");
+  const int64_t need = fused_ws_elems(B, H, hd, max_q, max_k, Tq);
+  RQ_CHECK_ARG(ws_elems >= need && (need == 0 || ws), "varlen_attn_bwd2: workspace smaller than varlen_attn_bwd_ws_elems");
+  if (B == 0) return 0;
+  launch_bwd_fused<64>(B, H, max_q, max_k, (hipStream_t)stream, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q,
+                       cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, ws);
+  RQ_LAUNCH_CHECK("varlen_attn_bwd2");
   return 0;
 }
 

@@ -72,6 +72,11 @@ _SIGS = {
                          _I64, _P], _I),
     "varlen_attn_bwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
                          _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I),
+    "varlen_attn_bwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _P], _I),
+    "varlen_attn_fwd2": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
+                          _I64, _P, _P], _I),
+    "varlen_attn_bwd2": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
+                          _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P, _I64, _P], _I),
     "rq_seed_epoch_advance": ([_P], _I),
     "rq_seed_epoch_set": ([_U64, _P], _I),
     "rq_adamw_step": ([_P, _I64, _F, _F, _F, _F, _F, _F, _F, _P], _I),

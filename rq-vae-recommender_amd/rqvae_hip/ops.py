@@ -1073,6 +1073,27 @@ class JaggedToPaddedValues(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------ attention
+ATTN_FUSED_BWD = True   # varlen_attn_bwd2 (fused dQ/dK/dV where it applies); False: the two-pass form (A/B)
+
+
+def _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv):
+    """Backward launch(es) of varlen attention into dq / dk / dv (row-strided views)."""
+    Tq, A = q.shape
+    delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
+    args = (ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0), ptr(dout),
+            dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, int(max_q), int(max_k), int(causal),
+            float(scale), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), k.shape[0], ptr(delta))
+    if not ATTN_FUSED_BWD:
+        TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd", *args, stream_handle(q.device))
+        return
+    import ctypes
+    n = ctypes.c_int64(0)
+    call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, ctypes.byref(n))
+    ws = torch.empty((int(n.value),), device=q.device, dtype=torch.float32) if n.value else None
+    TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd2", *args, ptr(ws) if ws is not None else None,
+                 int(n.value), stream_handle(q.device))
+
+
 class VarlenAttentionFunction(torch.autograd.Function):
     """softmax(q k^T * scale [causal]) v per segment; q/k/v are (T, H*hd) row views (any row stride)."""
 
@@ -1086,9 +1107,10 @@ class VarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        call("varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
+        order = torch.empty((B,), device=q.device, dtype=torch.int32)   # scratch: longest-first sequence order
+        call("varlen_attn_fwd2", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
              B, num_heads, hd, int(max_q), int(max_k), int(causal), float(scale), ptr(out), out.stride(0), ptr(lse), Tq,
-             stream_handle(q.device))
+             ptr(order), stream_handle(q.device))
         ctx.save_for_backward(q, k, v, out, lse, cu_q, cu_k)
         ctx.cfg = (num_heads, bool(causal), int(max_q), int(max_k), float(scale))
         return out
@@ -1103,11 +1125,7 @@ class VarlenAttentionFunction(torch.autograd.Function):
         dq = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         dk = torch.empty((k.shape[0], A), device=q.device, dtype=torch.float32)
         dv = torch.empty((v.shape[0], A), device=q.device, dtype=torch.float32)
-        delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
-        call("varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-             out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, max_q, max_k,
-             int(causal), scale, ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), k.shape[0],
-             ptr(delta), stream_handle(q.device))
+        _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv)
         return dq, dk, dv, None, None, None, None, None, None, None
 
 
@@ -1136,9 +1154,10 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+        order = torch.empty((B,), device=q.device, dtype=torch.int32)   # scratch: longest-first sequence order
+        TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd2", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
                      v.stride(0), ptr(cu_q), ptr(cu_k), B, num_heads, hd, int(max_q), int(max_k), int(causal),
-                     float(scale), ptr(out), out.stride(0), ptr(lse), Tq, stream_handle(q.device))
+                     float(scale), ptr(out), out.stride(0), ptr(lse), Tq, ptr(order), stream_handle(q.device))
         if self_attn:
             ctx.save_for_backward(qsrc, out, lse, cu_q, cu_k)
         else:
@@ -1161,13 +1180,8 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         gkv_src = gq_src if self_attn else torch.empty_like(kvsrc)
         q, k, v = qsrc[:, :A], src_kv[:, koff:koff + A], src_kv[:, koff + A:koff + 2 * A]
         dq, dk, dv = gq_src[:, :A], gkv_src[:, koff:koff + A], gkv_src[:, koff + A:koff + 2 * A]
-        Tq = q.shape[0]
         B = cu_q.shape[0] - 1
-        delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
-        TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
-                     v.stride(0), ptr(out), out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q),
-                     ptr(cu_k), B, H, A // H, max_q, max_k, int(causal), scale, ptr(dq), dq.stride(0), ptr(dk),
-                     dk.stride(0), ptr(dv), dv.stride(0), k.shape[0], ptr(delta), stream_handle(q.device))
+        _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv)
         return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None
 
 

@@ -37,6 +37,12 @@ def test_library_exports_declared_symbols():
     rc = typed.rq_quantize_fwd(None, 4, 48, None, None, 8, 1, 3, 0.25, None, None, None, None, None, None)
     assert rc == -22 and b"null pointer" in typed.rq_last_error()
     assert typed.rq_quantize_bwd_workspace(1024, 64, 256, 3) > 1024 * 64 * 3 * 4
+    # fused attention backward scratch: one dQ partial slab per 64-key block when sequences span several
+    n = ctypes.c_int64(-1)
+    assert typed.varlen_attn_bwd_ws_elems(64, 6, 64, 801, 801, 1000, ctypes.byref(n)) == 0 and n.value == 13 * 1000 * 384 + 64
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 64, 64, 500, ctypes.byref(n)) == 0 and n.value == 0   # one block
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 5, 500, ctypes.byref(n)) == 0 and n.value == 0     # short forms
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 48, 5, 5, 500, ctypes.byref(n)) == -22
 
 
 def test_ops_refuse_cpu_tensors():

@@ -81,9 +81,13 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (2, 40, 90, 2, 128, False, False),
     (5, 30, 30, 4, 16, True, True),      # small head dim (decoder fixtures: A=64, H=4)
     (4, 20, 33, 4, 16, False, False),
+    (3, 200, 200, 6, 64, True, True),    # causal over several 64-key blocks (fused dQ partials, causal reduce)
+    (4, 150, 260, 6, 64, False, False),  # long ragged q x k, lq != lk
 ])
-def test_varlen_attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
+@pytest.mark.parametrize("fused", [True, False])
+def test_varlen_attention_vs_oracle(device, monkeypatch, B, max_q, max_k, H, hd, causal, same, fused):
     from rqvae_hip import ops
+    monkeypatch.setattr(ops, "ATTN_FUSED_BWD", fused)
     g = gi.rng(B * 131 + max_q + hd)
     q, k, v, do, cq, ck = _varlen_case(g, B, max_q, max_k, H, hd, same)
     A_ = H * hd
@@ -107,18 +111,56 @@ def test_varlen_attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same
     chk(vt.grad, dv, 1e-4, 1e-3, "dv")
 
 
-def test_varlen_attention_deterministic(device):
+@pytest.mark.parametrize("n", [81, 400])
+def test_varlen_attention_deterministic(device, n):
     from rqvae_hip import ops
     g = gi.rng(11)
-    q, k, v, do, cq, ck = _varlen_case(g, 16, 81, 81, 8, 64, True)
+    q, k, v, do, cq, ck = _varlen_case(g, 16, n, n, 8, 64, True)
+    mx = int(np.diff(cq).max())
     outs = []
     for _ in range(2):
         qt, kt, vt = (torch.from_numpy(a.reshape(a.shape[0], -1)).to(device).requires_grad_(True) for a in (q, k, v))
-        o = ops.varlen_attention(qt, kt, vt, torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device), 8, False, 81, 81)
+        o = ops.varlen_attention(qt, kt, vt, torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device), 8, False, mx, mx)
         o.backward(torch.from_numpy(do.reshape(do.shape[0], -1)).to(device))
         outs.append((o.detach(), qt.grad, kt.grad, vt.grad))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("lq,lk", [([40, 50, 33], [200, 0, 140]), ([170, 0, 150], [170, 0, 150])])
+def test_varlen_attention_fused_empty_and_tail(device, lq, lk):
+    """Fused backward vs the two-pass form on ragged ranges with an empty segment and zero-padded tail
+    rows (row bucketing): empty-key / empty-query segments and tail rows get zero gradients."""
+    from rqvae_hip import ops
+    g = gi.rng(sum(lq) + sum(lk))
+    H, hd = 6, 64
+    A_ = H * hd
+    cq = torch.tensor(np.concatenate([[0], np.cumsum(lq)]), device=device)
+    ck = torch.tensor(np.concatenate([[0], np.cumsum(lk)]), device=device)
+    Tq, Tk = int(cq[-1]) + 7, int(ck[-1]) + 5   # allocated rows past the last segment
+    q0 = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
+    k0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
+    v0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
+    do = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
+    res = {}
+    for fused in (True, False):
+        ops.ATTN_FUSED_BWD = fused
+        try:
+            qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
+            o = ops.varlen_attention(qt, kt, vt, cq, ck, H, False, max(lq), max(lk))
+            o.backward(do)
+        finally:
+            ops.ATTN_FUSED_BWD = True
+        res[fused] = (o.detach(), qt.grad, kt.grad, vt.grad)
+    for a, b, what in zip(res[True], res[False], ("out", "dq", "dk", "dv")):
+        assert torch.isfinite(a).all(), what
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5, msg=what)
+    _, dq, dk, dv = res[True]
+    assert torch.count_nonzero(dq[int(cq[-1]):]) == 0 and torch.count_nonzero(dk[int(ck[-1]):]) == 0
+    assert torch.count_nonzero(dv[int(ck[-1]):]) == 0
+    for b in range(len(lq)):
+        if lk[b] == 0:
+            assert torch.count_nonzero(dq[int(cq[b]):int(cq[b + 1])]) == 0
 
 
 @pytest.mark.parametrize("bucket", [False, True])

@@ -28,7 +28,7 @@ def t(fn, iters=20):
     return a.elapsed_time(b) / iters
 
 
-def case(name, B, H, hd, max_items, dev, L1=4):
+def case(name, B, H, hd, max_items, dev, L1=4, cross=False):
     g = np.random.Generator(np.random.PCG64(7))
     lens = L1 * g.integers(2, max_items + 1, size=B) + 1
     cu = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).to(dev)
@@ -38,14 +38,26 @@ def case(name, B, H, hd, max_items, dev, L1=4):
     q, k, v = qkv[:, :A], qkv[:, A:2 * A], qkv[:, 2 * A:]
     mx = int(lens.max())
     fwd = lambda: ops.varlen_attention(q, k, v, cu, cu, H, False, mx, mx)  # noqa: E731
+    if cross:   # decoder cross-attention: L+2 future queries per sequence x its context keys
+        nq = L1 + 1
+        cq = torch.arange(0, B + 1, device=dev, dtype=torch.int64) * nq
+        qc = torch.randn(B * nq, A, device=dev, requires_grad=True)
+        fwd = lambda: ops.varlen_attention(qc, k, v, cq, cu, H, False, nq, mx)  # noqa: E731
+        lens = np.sqrt(nq * lens.astype(np.float64))   # FLOPs ~ nq * n
     out = fwd()
     go = torch.randn_like(out)
     fb = lambda: torch.autograd.grad(fwd(), qkv, go)  # noqa: E731
-    ms_f, ms_fb = t(fwd), t(fb)
+    if cross:
+        fb = lambda: torch.autograd.grad(fwd(), (qc, qkv), go)  # noqa: E731
     fl = 4.0 * hd * H * float((lens.astype(np.float64) ** 2).sum())
-    print(json.dumps(dict(case=name, tokens=T, max_len=mx, fwd_ms=round(ms_f, 4), fwd_bwd_ms=round(ms_fb, 4),
-                          fwd_tflops=round(fl / ms_f / 1e9, 1), fwd_bwd_tflops=round(3.5 * fl / ms_fb / 1e9, 1))),
-          flush=True)
+    for fused in (True, False):
+        ops.ATTN_FUSED_BWD = fused
+        ms_f, ms_fb = t(fwd), t(fb)
+        print(json.dumps(dict(case=name, fused_bwd=fused, tokens=T, max_len=mx, fwd_ms=round(ms_f, 4),
+                              fwd_bwd_ms=round(ms_fb, 4), bwd_ms=round(ms_fb - ms_f, 4),
+                              fwd_tflops=round(fl / ms_f / 1e9, 1), bwd_tflops=round(2 * fl / (ms_fb - ms_f) / 1e9, 1))),
+              flush=True)
+    ops.ATTN_FUSED_BWD = True
 
 
 def main():
@@ -57,6 +69,8 @@ def main():
     case("amazon", 256, 8, 64, 20, dev)
     case("ml32m", 64, 6, 64, 200, dev)
     case("c5", 64, 8, 64, 256, dev, L1=5)
+    case("ml32m_cross", 64, 6, 64, 200, dev, cross=True)
+    case("c5_cross", 64, 8, 64, 256, dev, L1=5, cross=True)
 
 
 if __name__ == "__main__":
