@@ -1,0 +1,8 @@
+#!/bin/bash
+# rocprofv3 kernel trace of the RQ-VAE headline step alone (bench.py without decoder / extras / PMC / CPU leg)
+set -u
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out"; mkdir -p "$O"; export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o rqonly -- python3 "$R/bench.py" --no-cpu-baseline \
+  --no-pmc --no-extras --no-decoder > "$O/prof_rqonly.json" 2> "$O/prof_rqonly.err" || { tail "$O/prof_rqonly.err"; exit 1; }
+cat "$O/prof_rqonly.json"
