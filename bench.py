@@ -452,7 +452,49 @@ def measure_extras(model, device, x):
     except Exception as e:  # report, never hide
         out["b64_hipgraph_error"] = repr(e)[:300]
     out["quantize_synthetic"] = measure_quantize_synthetic(device)
+    out["jagged_c5"] = measure_jagged_c5(device)
     return out
+
+
+def measure_jagged_c5(device, B=4096, max_items=256, L1=5, D=128, reps=10):
+    """BASELINE configs[4] jagged half at HBM scale: B user sequences of 5 U{2..256} + 1 context rows
+    (<= 1281) x D = 128 fp32 embeddings, padded -> jagged (with the reference's +1-1 rounding) and back
+    (the backward's zero-filled scatter), HIP events over `reps` launches. Algorithmic bytes: gather
+    2 * 4 D sum(n) (valid rows read + written), scatter 4 D (B N + sum(n))."""
+    from rqvae_hip import ops
+    from rqvae_hip._lib import call, ptr, stream_handle
+    g = np.random.Generator(np.random.PCG64(5))
+    lens = L1 * g.integers(2, max_items + 1, size=B) + 1
+    N = L1 * max_items + 1
+    x = torch.randn(B, N, D, device=device)
+    off = ops.jagged_offsets(torch.from_numpy(lens).to(device), N)
+    T = int(lens.sum())
+    vals = torch.empty((T, D), device=device)
+    back = torch.empty_like(x)
+    st = stream_handle(device)
+    gather = lambda: call("jagged_from_padded_rows", ptr(x), B, N, D, ptr(off), ptr(vals), T, 0, 1, st)  # noqa: E731
+    scatter = lambda: call("jagged_to_padded", ptr(vals), ptr(off), B, N, D, ptr(back), 0, st)  # noqa: E731
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+    tg, ts = timed(gather), timed(scatter)
+    gb_g, gb_s = 2.0 * 4 * D * T / 1e9, 4.0 * D * (B * N + T) / 1e9
+    res = {"shape": {"sequences": B, "max_rows": N, "D": D, "valid_rows": T}, "gather_ms": round(tg, 4),
+           "scatter_ms": round(ts, 4), "gather_GBps": round(gb_g / (tg * 1e-3), 1),
+           "scatter_GBps": round(gb_s / (ts * 1e-3), 1),
+           "gather_hbm_frac": round(gb_g / (tg * 1e-3) / HBM_PEAK_GBS, 4),
+           "scatter_hbm_frac": round(gb_s / (ts * 1e-3) / HBM_PEAK_GBS, 4)}
+    del x, vals, back
+    torch.cuda.empty_cache()
+    return res
 
 
 def measure_quantize_synthetic(device, B=16384, D=1024, K=2048, L=4):
