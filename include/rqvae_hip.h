@@ -266,6 +266,16 @@ int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, con
                      const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                      int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
                      void* stream);
+/* varlen_attn_fwd2 with one float scratch `ws` of varlen_attn_fwd_ws_elems(...) floats: the LPT order
+ * (B ints, padded to 16 B) and, for <= 16 queries per sequence over > 128 keys (non-causal: the decoder's
+ * cross-attention), split-key partials — one one-wave workgroup per 128-key block, merged per query in
+ * block order by a combine launch (deterministic). */
+int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
+                             int64_t* elems);
+int varlen_attn_fwd3(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
+                     int64_t ws_elems, void* stream);
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,

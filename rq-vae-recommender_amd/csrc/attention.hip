@@ -579,6 +579,105 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
   store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
 }
 
+// ------------------------------------------------------------- fwd: split keys (few queries)
+// Few queries over a long key range (the decoder's cross-attention: 5-6 future tokens x a context of
+// up to 801 / 1281 rows): the chunked forward gives each (sequence, head) ONE wave that walks every
+// 32-key chunk serially. Here key block j of kSplitKB keys is its own one-wave workgroup (FwdChunk over
+// the block, the same online softmax), which writes its unnormalised partial (o, m, l) to `part`;
+// attn_fwd_combine_kernel merges a query's blocks in block order (deterministic):
+// M = max m_j, L = sum l_j 2^(m_j - M), o = sum o_j 2^(m_j - M) / L, lse = (M + log2 L) ln 2.
+// part layout: o (nsplit, Tq, H, HD) then m, l (nsplit, H, Tq) each.
+constexpr int kSplitKB = 128;
+template <int HD>
+__global__ void __launch_bounds__(64) attn_fwd_split_kernel(const float* __restrict__ q, int64_t sq,
+                                                            const float* __restrict__ k, int64_t sk,
+                                                            const float* __restrict__ v, int64_t sv,
+                                                            const int64_t* __restrict__ cu_q,
+                                                            const int64_t* __restrict__ cu_k, float scale, int64_t Tq,
+                                                            float* __restrict__ part, int nsplit) {
+  constexpr int CH = 32, LD = HD + 4, DT = HD / 16;
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
+  float* K_s = smem;
+  float* V_s = smem + CH * LD;
+  const int b = blockIdx.z, hh = blockIdx.y, j = blockIdx.x, lane = threadIdx.x, g = lane >> 4;
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  const int kbeg = j * kSplitKB;
+  if (lq <= 0 || kbeg >= lk) return;         // no partial for this block (the combine skips it)
+  const int kend = min(lk, kbeg + kSplitKB);
+  const int qi = lane & 15;
+  const bool qv = qi < lq;
+  float qf[HD / 4];
+  load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  RowStage<HD, 64, CH> stk, stv;
+  FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, kend, qi, 0, scale * kLog2e, &m, &l, o};
+  for (int kc = kbeg; kc < kend; kc += CH) {
+    stk.load(kb_, sk, kc, kend, lane);
+    stv.load(vb_, sv, kc, kend, lane);
+    __syncthreads();
+    stk.store(K_s, lane);
+    stv.store(V_s, lane);
+    __syncthreads();
+    const int nt = __builtin_amdgcn_readfirstlane(min(CH / 16, (kend - kc + 15) >> 4));
+    fc.kc = kc;
+    dispatch_tiles<CH / 16>(nt, kc + CH <= kend, fc);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qv) return;
+  const int64_t H = gridDim.y, row = q0 + qi;
+  store_rowT<HD>(part + (((int64_t)j * Tq + row) * H + hh) * HD, o, 1.f, lane);
+  if (g == 0) {
+    float* ml = part + (int64_t)nsplit * Tq * H * HD;
+    ml[((int64_t)j * H + hh) * Tq + row] = m;
+    ml[((int64_t)(nsplit + j) * H + hh) * Tq + row] = l;
+  }
+}
+
+// one 16-lane group per (query row, head): the split partials' merge, out / lse rows; rows past the last
+// sequence (grid row z == B) get zeros
+template <int HD>
+__global__ void __launch_bounds__(256) attn_fwd_combine_kernel(const float* __restrict__ part, int nsplit,
+                                                               const int64_t* __restrict__ cu_q,
+                                                               const int64_t* __restrict__ cu_k, int64_t Tq,
+                                                               float* __restrict__ out, int64_t so,
+                                                               float* __restrict__ lse) {
+  constexpr int F4 = HD / 4, RPB = 256 / F4;
+  const int z = blockIdx.z, hh = blockIdx.y, c = (threadIdx.x % F4) * 4;
+  const int64_t H = gridDim.y;
+  if (z == (int)gridDim.z - 1) {              // tail slice
+    zero_rows<HD, 256>(out, so, cu_q[z], Tq, hh, threadIdx.x);
+    return;
+  }
+  const int64_t q0 = cu_q[z];
+  const int lq = (int)(cu_q[z + 1] - q0), lk = (int)(cu_k[z + 1] - cu_k[z]);
+  const int r = blockIdx.x * RPB + threadIdx.x / F4;
+  if (r >= lq) return;
+  const int64_t row = q0 + r;
+  const int n = (lk + kSplitKB - 1) / kSplitKB;
+  const float* ml = part + (int64_t)nsplit * Tq * H * HD;
+  float M = -INFINITY;
+  for (int j = 0; j < n; ++j) M = fmaxf(M, ml[((int64_t)j * H + hh) * Tq + row]);
+  float L = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < n; ++j) {
+    const float mj = ml[((int64_t)j * H + hh) * Tq + row];
+    const float w = M == -INFINITY ? 0.f : exp2_fast(mj - M);
+    L += ml[((int64_t)(nsplit + j) * H + hh) * Tq + row] * w;
+    const float4 a = *reinterpret_cast<const float4*>(part + (((int64_t)j * Tq + row) * H + hh) * HD + c);
+    acc.x += a.x * w; acc.y += a.y * w; acc.z += a.z * w; acc.w += a.w * w;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  *reinterpret_cast<float4*>(out + row * so + hh * HD + c) = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+  if (c == 0) lse[hh * Tq + row] = L > 0.f ? (M + log2f(L)) * kLn2 : 0.f;
+}
+
 // ------------------------------------------------------------------ bwd: fused dQ, dK, dV
 // One launch per key block of KB = 16 NW keys computes S and dP ONCE per (query tile, key tile)
 // pair — 5 MFMA products per pair (S, dP, dV, dK, dQ) instead of the two-pass form's 7 (the dQ pass
@@ -1056,6 +1155,18 @@ static int waves_for(int64_t rows) { return rows <= 16 ? 1 : (rows <= 96 ? 2 : 4
 // LPT order where a workgroup's run time varies enough with the sequence to leave a straggler tail
 static bool lpt_plan(int64_t B, int64_t max_len) { return RQ_ATTN_LPT && B >= 2 && B <= kOrderMax && max_len > 128; }
 
+#ifndef RQ_ATTN_SPLIT
+#define RQ_ATTN_SPLIT 1   // split-key forward for <= 16 queries over > 128 keys (A/B switch)
+#endif
+// split-key forward: one query tile per sequence, non-causal, long key ranges (cross-attention)
+static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal) {
+  return RQ_ATTN_SPLIT && hd == 64 && !causal && max_q <= 16 && max_k > 128;
+}
+static int64_t split_ws_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal) {
+  if (!split_plan(hd, max_q, max_k, causal)) return 0;
+  return (max_k + kSplitKB - 1) / kSplitKB * Tq * H * (hd + 2);
+}
+
 template <int HD, int NW>
 static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
                    int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal, float scale,
@@ -1069,8 +1180,17 @@ template <int HD>
 static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q, int64_t sq,
                        const float* k,
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
-                       float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order) {
+                       float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order, float* split_ws) {
   if constexpr (HD == 64) {
+    if (split_ws && split_plan(HD, max_q, max_k, causal)) {
+      const int nsplit = (int)((max_k + kSplitKB - 1) / kSplitKB);
+      hipLaunchKernelGGL((attn_fwd_split_kernel<HD>), dim3((unsigned)nsplit, (unsigned)H, (unsigned)B), dim3(64), 0, st, q,
+                         sq, k, sk, v, sv, cq, ck, scale, Tq, split_ws, nsplit);
+      constexpr int RPB = 256 / (HD / 4);
+      hipLaunchKernelGGL((attn_fwd_combine_kernel<HD>), dim3((unsigned)std::max<int64_t>(1, (max_q + RPB - 1) / RPB),
+                         (unsigned)H, (unsigned)B + 1), dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq, out, so, lse);
+      return;
+    }
     int nw = 0, ch = 0;
     if (short_plan(max_q, max_k, &nw, &ch)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
@@ -1247,30 +1367,56 @@ using namespace rqhip;
 
 extern "C" {
 
-int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
-                     void* stream) {
+static int attn_fwd_impl(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                         const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                         int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
+                         float* split_ws, void* stream) {
   RQ_CHECK_ARG(q && k && v && cu_q && cu_k && out && lse, "varlen_attn_fwd: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   switch (hd) {
-    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
-    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
-    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
-    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order); break;
+    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
+    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
+    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
+    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_fwd");
   return 0;
 }
 
+int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
+                     void* stream) {
+  return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq, order,
+                       nullptr, stream);
+}
+
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
-  return varlen_attn_fwd2(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq,
-                          nullptr, stream);
+  return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq, nullptr,
+                       nullptr, stream);
+}
+
+int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
+                             int64_t* elems) {
+  RQ_CHECK_ARG(elems, "varlen_attn_fwd_ws_elems: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_fwd_ws_elems: bad shape");
+  *elems = ((B + 3) & ~(int64_t)3) + split_ws_elems(H, hd, max_q, max_k, Tq, causal);   // order (B ints, 16-B padded) + split-key partials
+  return 0;
+}
+
+int varlen_attn_fwd3(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
+                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
+                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
+                     int64_t ws_elems, void* stream) {
+  const int64_t ob = (B + 3) & ~(int64_t)3, sp = split_ws_elems(H, hd, max_q, max_k, Tq, causal);
+  RQ_CHECK_ARG(ws && ws_elems >= ob + sp, "varlen_attn_fwd3: workspace smaller than varlen_attn_fwd_ws_elems");
+  return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq,
+                       reinterpret_cast<int*>(ws), sp ? ws + ob : nullptr, stream);
 }
 
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,

@@ -72,6 +72,9 @@ _SIGS = {
                          _I64, _P], _I),
     "varlen_attn_bwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
                          _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I),
+    "varlen_attn_fwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _I, _P], _I),
+    "varlen_attn_fwd3": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
+                          _I64, _P, _I64, _P], _I),
     "varlen_attn_bwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _P], _I),
     "varlen_attn_fwd2": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
                           _I64, _P, _P], _I),

@@ -1073,6 +1073,18 @@ class JaggedToPaddedValues(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------ attention
+def _attn_fwd(q, k, v, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, lse):
+    """Forward launch(es) (varlen_attn_fwd3: scratch for the LPT order and split-key partials)."""
+    import ctypes
+    Tq = q.shape[0]
+    n = ctypes.c_int64(0)
+    call("varlen_attn_fwd_ws_elems", B, H, hd, int(max_q), int(max_k), Tq, int(causal), ctypes.byref(n))
+    ws = torch.empty((max(1, int(n.value)),), device=q.device, dtype=torch.float32)
+    TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd3", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+                 v.stride(0), ptr(cu_q), ptr(cu_k), B, H, hd, int(max_q), int(max_k), int(causal), float(scale),
+                 ptr(out), out.stride(0), ptr(lse), Tq, ptr(ws), ws.numel(), stream_handle(q.device))
+
+
 ATTN_FUSED_BWD = True   # varlen_attn_bwd2 (fused dQ/dK/dV where it applies); False: the two-pass form (A/B)
 
 
@@ -1107,10 +1119,7 @@ class VarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        order = torch.empty((B,), device=q.device, dtype=torch.int32)   # scratch: longest-first sequence order
-        call("varlen_attn_fwd2", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(cu_q), ptr(cu_k),
-             B, num_heads, hd, int(max_q), int(max_k), int(causal), float(scale), ptr(out), out.stride(0), ptr(lse), Tq,
-             ptr(order), stream_handle(q.device))
+        _attn_fwd(q, k, v, cu_q, cu_k, B, num_heads, hd, max_q, max_k, causal, scale, out, lse)
         ctx.save_for_backward(q, k, v, out, lse, cu_q, cu_k)
         ctx.cfg = (num_heads, bool(causal), int(max_q), int(max_k), float(scale))
         return out
@@ -1154,10 +1163,7 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        order = torch.empty((B,), device=q.device, dtype=torch.int32)   # scratch: longest-first sequence order
-        TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd2", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
-                     v.stride(0), ptr(cu_q), ptr(cu_k), B, num_heads, hd, int(max_q), int(max_k), int(causal),
-                     float(scale), ptr(out), out.stride(0), ptr(lse), Tq, ptr(order), stream_handle(q.device))
+        _attn_fwd(q, k, v, cu_q, cu_k, B, num_heads, hd, max_q, max_k, causal, scale, out, lse)
         if self_attn:
             ctx.save_for_backward(qsrc, out, lse, cu_q, cu_k)
         else:

@@ -127,6 +127,47 @@ def test_varlen_attention_deterministic(device, n):
         assert torch.equal(a, b)
 
 
+def test_varlen_attention_split_keys_cross(device):
+    """Split-key forward (<= 16 queries over > 128 keys: the decoder's cross-attention) vs the fp64 oracle
+    on ragged contexts incl. one shorter than a key block and an empty one, with zero-padded tail rows."""
+    from rqvae_hip import ops
+    g = gi.rng(2024)
+    H, hd, nq = 6, 64, 6
+    lk = [801, 0, 100, 300, 129]
+    A_ = H * hd
+    B = len(lk)
+    cq = np.arange(B + 1, dtype=np.int64) * nq
+    ck = np.concatenate([[0], np.cumsum(lk)]).astype(np.int64)
+    Tq = int(cq[-1]) + 5
+    q = g.standard_normal((Tq, H, hd), dtype=np.float32)
+    k = g.standard_normal((ck[-1], H, hd), dtype=np.float32)
+    v = g.standard_normal((ck[-1], H, hd), dtype=np.float32)
+    do = g.standard_normal((Tq, H, hd), dtype=np.float32)
+    qt = torch.from_numpy(q.reshape(Tq, A_)).to(device).requires_grad_(True)
+    kt = torch.from_numpy(k.reshape(-1, A_)).to(device).requires_grad_(True)
+    vt = torch.from_numpy(v.reshape(-1, A_)).to(device).requires_grad_(True)
+    out = ops.varlen_attention(qt, kt, vt, torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device), H, False,
+                               nq, max(lk))
+    out.backward(torch.from_numpy(do.reshape(Tq, A_)).to(device))
+    o = out.detach().cpu().double().numpy().reshape(Tq, H, hd)
+    dq = qt.grad.cpu().double().numpy().reshape(Tq, H, hd)
+    assert np.count_nonzero(o[cq[-1]:]) == 0 and np.count_nonzero(dq[cq[-1]:]) == 0
+    for b in range(B):
+        s0, s1 = cq[b], cq[b + 1]
+        if lk[b] == 0:
+            assert np.count_nonzero(o[s0:s1]) == 0 and np.count_nonzero(dq[s0:s1]) == 0
+            continue
+        cqb = np.array([0, nq], np.int64)
+        ckb = np.array([0, lk[b]], np.int64)
+        kb_, vb_ = k[ck[b]:ck[b + 1]], v[ck[b]:ck[b + 1]]
+        ref, _ = A.attn_fwd(q[s0:s1], kb_, vb_, cqb, ckb, False)
+        rdq, rdk, rdv = A.attn_bwd(q[s0:s1], kb_, vb_, do[s0:s1], cqb, ckb, False)
+        assert np.all(np.abs(o[s0:s1] - ref) <= 2e-5 + 2e-4 * np.abs(ref)), b
+        assert np.all(np.abs(dq[s0:s1] - rdq) <= 1e-4 + 1e-3 * np.abs(rdq)), b
+        gk = kt.grad.cpu().double().numpy().reshape(-1, H, hd)[ck[b]:ck[b + 1]]
+        assert np.all(np.abs(gk - rdk) <= 1e-4 + 1e-3 * np.abs(rdk)), b
+
+
 @pytest.mark.parametrize("lq,lk", [([40, 50, 33], [200, 0, 140]), ([170, 0, 150], [170, 0, 150])])
 def test_varlen_attention_fused_empty_and_tail(device, lq, lk):
     """Fused backward vs the two-pass form on ragged ranges with an empty segment and zero-padded tail
