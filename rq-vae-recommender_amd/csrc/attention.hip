@@ -33,6 +33,7 @@
 #include "common.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -581,14 +582,13 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
 
 // ------------------------------------------------------------- fwd: split keys (few queries)
 // Few queries over a long key range (the decoder's cross-attention: 5-6 future tokens x a context of
-// up to 801 / 1281 rows): the chunked forward gives each (sequence, head) ONE wave that walks every
-// 32-key chunk serially. Here key block j of kSplitKB keys is its own one-wave workgroup (FwdChunk over
-// the block, the same online softmax), which writes its unnormalised partial (o, m, l) to `part`;
-// attn_fwd_combine_kernel merges a query's blocks in block order (deterministic):
+// up to 81 / 801 / 1281 rows): the chunked forward gives each (sequence, head) ONE wave that walks every
+// 32-key chunk serially. Here key block j of kSplitKB (32 for ranges <= 128, else 128) keys is its own
+// one-wave workgroup (FwdChunk over the block, the same online softmax), which writes its unnormalised
+// partial (o, m, l) to `part`; attn_fwd_combine_kernel merges a query's blocks in block order (deterministic):
 // M = max m_j, L = sum l_j 2^(m_j - M), o = sum o_j 2^(m_j - M) / L, lse = (M + log2 L) ln 2.
 // part layout: o (nsplit, Tq, H, HD) then m, l (nsplit, H, Tq) each.
-constexpr int kSplitKB = 128;
-template <int HD>
+template <int HD, int kSplitKB>
 __global__ void __launch_bounds__(64) attn_fwd_split_kernel(const float* __restrict__ q, int64_t sq,
                                                             const float* __restrict__ k, int64_t sk,
                                                             const float* __restrict__ v, int64_t sv,
@@ -642,7 +642,7 @@ __global__ void __launch_bounds__(64) attn_fwd_split_kernel(const float* __restr
 
 // one 16-lane group per (query row, head): the split partials' merge, out / lse rows; rows past the last
 // sequence (grid row z == B) get zeros
-template <int HD>
+template <int HD, int kSplitKB>
 __global__ void __launch_bounds__(256) attn_fwd_combine_kernel(const float* __restrict__ part, int nsplit,
                                                                const int64_t* __restrict__ cu_q,
                                                                const int64_t* __restrict__ cu_k, int64_t Tq,
@@ -1159,12 +1159,17 @@ static bool lpt_plan(int64_t B, int64_t max_len) { return RQ_ATTN_LPT && B >= 2 
 #define RQ_ATTN_SPLIT 1   // split-key forward for <= 16 queries over > 128 keys (A/B switch)
 #endif
 // split-key forward: one query tile per sequence, non-causal, long key ranges (cross-attention)
+#ifndef RQ_ATTN_SPLIT_MIN_K
+#define RQ_ATTN_SPLIT_MIN_K 129   // key ranges from here use the split-key forward (A/B: at the Amazon
+#endif                            // contexts, <= 81 keys in 32-key blocks, it ties the chunked form)
 static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal) {
-  return RQ_ATTN_SPLIT && hd == 64 && !causal && max_q <= 16 && max_k > 128;
+  return RQ_ATTN_SPLIT && hd == 64 && !causal && max_q <= 16 && max_k >= RQ_ATTN_SPLIT_MIN_K;
 }
+static int split_kb(int64_t max_k) { return max_k <= 128 ? 32 : 128; }   // 32: RQ_ATTN_SPLIT_MIN_K <= 128 builds
 static int64_t split_ws_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal) {
   if (!split_plan(hd, max_q, max_k, causal)) return 0;
-  return (max_k + kSplitKB - 1) / kSplitKB * Tq * H * (hd + 2);
+  const int kb = split_kb(max_k);
+  return (max_k + kb - 1) / kb * Tq * H * (hd + 2);
 }
 
 template <int HD, int NW>
@@ -1183,12 +1188,17 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                        float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order, float* split_ws) {
   if constexpr (HD == 64) {
     if (split_ws && split_plan(HD, max_q, max_k, causal)) {
-      const int nsplit = (int)((max_k + kSplitKB - 1) / kSplitKB);
-      hipLaunchKernelGGL((attn_fwd_split_kernel<HD>), dim3((unsigned)nsplit, (unsigned)H, (unsigned)B), dim3(64), 0, st, q,
-                         sq, k, sk, v, sv, cq, ck, scale, Tq, split_ws, nsplit);
+      const int kb = split_kb(max_k);
+      const int nsplit = (int)((max_k + kb - 1) / kb);
       constexpr int RPB = 256 / (HD / 4);
-      hipLaunchKernelGGL((attn_fwd_combine_kernel<HD>), dim3((unsigned)std::max<int64_t>(1, (max_q + RPB - 1) / RPB),
-                         (unsigned)H, (unsigned)B + 1), dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq, out, so, lse);
+      const dim3 gs((unsigned)nsplit, (unsigned)H, (unsigned)B);
+      const dim3 gc((unsigned)std::max<int64_t>(1, (max_q + RPB - 1) / RPB), (unsigned)H, (unsigned)B + 1);
+#define RQ_SPL(KB_)                                                                                                \
+  hipLaunchKernelGGL((attn_fwd_split_kernel<HD, KB_>), gs, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, scale, Tq, \
+                     split_ws, nsplit);                                                                            \
+  hipLaunchKernelGGL((attn_fwd_combine_kernel<HD, KB_>), gc, dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq, out, so, lse)
+      if (kb == 32) { RQ_SPL(32); } else { RQ_SPL(128); }
+#undef RQ_SPL
       return;
     }
     int nw = 0, ch = 0;
@@ -1304,10 +1314,21 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #ifndef RQ_ATTN_FUSED_MIN_K
 #define RQ_ATTN_FUSED_MIN_K 129   // shorter key ranges keep the two-pass form (Amazon n <= 81: 0.25 vs 0.30 ms)
 #endif
+#ifndef RQ_ATTN_FUSED_MIN_K_FEWQ
+#define RQ_ATTN_FUSED_MIN_K_FEWQ 129   // the same threshold for <= 16 queries per sequence (cross-attention;
+#endif                                 // A/B from 33 keys: Amazon decoder step 6.53 -> 6.60 ms, fewq_ab.txt)
 constexpr int kFusedKB = 16 * RQ_ATTN_FUSED_NW;
 
 static bool fused_plan(int64_t hd, int64_t max_q, int64_t max_k) {
-  if (!RQ_ATTN_FUSED || hd != 64 || max_k < RQ_ATTN_FUSED_MIN_K) return false;
+  if (!RQ_ATTN_FUSED || hd != 64) return false;
+  // few queries (cross-attention): their own threshold
+  // (RQ_ATTN_FEWQ_MIN_K in the environment overrides the threshold: in-process A/B of the decoder step)
+  static const int64_t fewq_min = [] {
+    const char* e = getenv("RQ_ATTN_FEWQ_MIN_K");
+    return e ? (int64_t)atoll(e) : (int64_t)RQ_ATTN_FUSED_MIN_K_FEWQ;
+  }();
+  if (max_q <= 16) return max_k >= fewq_min;
+  if (max_k < RQ_ATTN_FUSED_MIN_K) return false;
   int nw = 0, ch = 0;
   return !short_plan(max_k, max_q, &nw, &ch);
 }

@@ -69,6 +69,7 @@ def main():
     case("amazon", 256, 8, 64, 20, dev)
     case("ml32m", 64, 6, 64, 200, dev)
     case("c5", 64, 8, 64, 256, dev, L1=5)
+    case("amazon_cross", 256, 8, 64, 20, dev, cross=True)
     case("ml32m_cross", 64, 6, 64, 200, dev, cross=True)
     case("c5_cross", 64, 8, 64, 256, dev, L1=5, cross=True)
 
