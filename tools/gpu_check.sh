@@ -12,10 +12,10 @@ export TMPDIR=/tmp
 
 run() {   # name, seconds, command...
   local name="$1" secs="$2"; shift 2
-  echo "[$(date +%T)] $name: $*"
+  echo "[$(date +%T)] $name: $*" >&2
   timeout -k 10 "$secs" "$@"
   local rc=$?
-  echo "[$(date +%T)] $name exit $rc"
+  echo "[$(date +%T)] $name exit $rc" >&2
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 
