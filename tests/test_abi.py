@@ -42,7 +42,11 @@ def test_library_exports_declared_symbols():
     assert typed.varlen_attn_bwd_ws_elems(64, 6, 64, 801, 801, 1000, ctypes.byref(n)) == 0 and n.value == 13 * 1000 * 384 + 64
     assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 64, 64, 500, ctypes.byref(n)) == 0 and n.value == 0   # one block
     assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 5, 500, ctypes.byref(n)) == 0 and n.value == 0     # short forms
-    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 81, 500, ctypes.byref(n)) == 0 and n.value == 2 * 500 * 512   # cross
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 81, 500, ctypes.byref(n)) == 0 and n.value == 0   # short cross
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 801, 500, ctypes.byref(n)) == 0 and n.value == 13 * 500 * 512
+    # forward scratch: LPT order (16-B padded) + split-key partials for few queries over > 128 keys
+    assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 0, ctypes.byref(n)) == 0 and n.value == 8 + 7 * 500 * 8 * 66
+    assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 1, ctypes.byref(n)) == 0 and n.value == 8   # causal
     assert typed.varlen_attn_bwd_ws_elems(4, 8, 48, 5, 5, 500, ctypes.byref(n)) == -22
 
 
