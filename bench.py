@@ -191,15 +191,15 @@ def pmc_traffic(timeout_s=75, regex="rq_fwd", script=("pmc_quantize.py", "5"), l
 
 
 def cpu_baseline(budget_s, B=2048):
-    """Oracle (numpy) RqVae train step, same shapes, bounded sample of ~budget_s seconds."""
-    try:
-        from threadpoolctl import threadpool_info, threadpool_limits
-    except ImportError:  # pragma: no cover
-        threadpool_limits, threadpool_info = None, None
+    """The RqVae train step (fwd + bwd + AdamW) as eager PyTorch on the host CPU (oracle/rqvae_torch.py,
+    checked against the pinned numpy oracle in tests/test_oracle.py), same dims, on this process's
+    CPU share (torch.set_num_threads), bounded sample of ~budget_s seconds."""
     from oracle import rqvae as R
+    from oracle.rqvae_torch import RqVaeTorchCPU
     import gen_inputs as gi  # tests/golden (seeded synthetic inputs)
     threads = cpu_threads()
-    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     try:
         D, K, L, inp, hid = CFG["D"], CFG["K"], CFG["L"], CFG["input_dim"], CFG["hidden"]
         st = {f"encoder.mlp.{2 * j}.weight": w for j, w in enumerate(gi.mlp_weights([inp] + hid + [D], 5))}
@@ -208,22 +208,21 @@ def cpu_baseline(budget_s, B=2048):
         res0, _ = R.mlp_fwd(enc_items, [st[f"encoder.mlp.{2 * j}.weight"] for j in range(len(hid) + 1)], False)
         for l in range(L):
             st[f"layers.{l}.embedding.weight"] = res0[l * K:(l + 1) * K].copy()
-        orc = R.RqVaeOracle(st, L)
-        x = gi.items(B, inp, 8)
-        orc.train_step(x, CFG["lr"], CFG["wd"])          # warm-up
+        m = RqVaeTorchCPU(st, L, lr=CFG["lr"], weight_decay=CFG["wd"])
+        x = torch.from_numpy(gi.items(B, inp, 8))
+        m.train_step(x)          # warm-up
         n, t0 = 0, time.perf_counter()
         while True:
-            orc.train_step(x, CFG["lr"], CFG["wd"])
+            m.train_step(x)
             n += 1
-            if time.perf_counter() - t0 >= budget_s or n >= 200:
+            if time.perf_counter() - t0 >= budget_s or n >= 400:
                 break
         dt = time.perf_counter() - t0
     finally:
-        if ctx is not None:
-            ctx.__exit__(None, None, None)
+        torch.set_num_threads(prev)
     return dict(value=round(n * B / dt, 1), unit="items/s", cores=threads, kind="port", cpu_model=cpu_model(),
-                sample=f"{n} numpy-oracle RqVae train steps (fwd+bwd+AdamW) at B={B}, ML-32M dims, "
-                       f"{dt:.1f} s on {threads} host threads")
+                sample=f"{n} eager torch-CPU RqVae train steps (fwd+bwd+AdamW, oracle/rqvae_torch.py) at B={B}, "
+                       f"ML-32M dims, {dt:.1f} s on {threads} host threads")
 
 
 def main():

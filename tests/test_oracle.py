@@ -169,3 +169,20 @@ def test_decoder_oracle_vs_reference(golden, tag):
             assert g.double().norm().item() == pytest.approx(float(z["grad__" + n + "__norm"]), rel=2e-5), n
         checked += 1
     assert checked == len(names) and shapes
+
+
+def test_rqvae_torch_cpu_matches_numpy_oracle():
+    """bench.py's eager torch-CPU RQ-VAE baseline (oracle/rqvae_torch.py) computes the pinned numpy
+    oracle's step: same ids, loss and parameter gradients (rotation-trick mode, small dims)."""
+    from oracle.rqvae_torch import RqVaeTorchCPU
+    inp, hid, D, K, L, B = 96, [64, 32], 16, 32, 3, 256
+    st = {f"encoder.mlp.{2 * j}.weight": w for j, w in enumerate(gi.mlp_weights([inp] + hid + [D], 1))}
+    st.update({f"decoder.mlp.{2 * j}.weight": w for j, w in enumerate(gi.mlp_weights([D] + hid[::-1] + [inp], 2))})
+    st.update({f"layers.{l}.embedding.weight": gi.residual_rows(K, D, 10 + l, 0.5) for l in range(L)})
+    x = gi.items(B, inp, 3)
+    out, grads = R.RqVaeOracle(st, L).forward_backward(x)
+    loss, ids, tgrads = RqVaeTorchCPU(st, L).forward_backward(x)
+    assert np.array_equal(ids, out["sem_ids"])
+    assert loss == pytest.approx(float(out["loss"]), rel=1e-5)
+    for k, g in grads.items():
+        np.testing.assert_allclose(tgrads[k], g, rtol=2e-4, atol=1e-6, err_msg=k)
