@@ -260,9 +260,25 @@ constexpr int kXWG = RQ_X3_BK16 ? 3 : 2;       // resident workgroups per CU
 constexpr int kXPlane = kXT * kXK * 2;         // bytes of one bf16 plane (8 KiB)
 constexpr int kXOp = 2 * kXPlane;              // hi + lo planes of one operand
 constexpr int kXBuf = 2 * kXOp;                // A + B
-constexpr int kXLds = 2 * kXBuf;               // double buffer: 64 KiB
+constexpr int kXLds = 2 * kXBuf;               // double buffer: 64 KiB (the 64-tile form: half)
+static_assert(kXLds == 65536, "LDS of the 128-tile form");
 
 __device__ __forceinline__ int col_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+#ifndef RQ_X3S_COMPACT
+#define RQ_X3S_COMPACT 1   // 64-tile form: 128-B column-image rows and 32 KiB of LDS (4 workgroups / CU)
+#endif
+constexpr int kXWG64 = RQ_X3S_COMPACT ? 4 : kXWG;   // resident workgroups per CU of the 64-tile form
+// Byte offset of 16-B chunk `c` of k-row kr in a column image of TR columns: 256-B rows with col_swz
+// for TR = 128 (and the wide kernel); for TR = 64 (compact) 128-B rows with a swizzle over the 8 chunks,
+// s = 2 ((kr >> 1) & 1) + 4 ((kr >> 3) & 1): a ds_read_b64_tr_b16 half-wave touches k-rows {4u..4u+3,
+// 4u+8..4u+11} (+16), chunk pairs (c0, c0 + 1) with c0 even — the even rows land on banks 0-31 and the
+// odd rows on 32-63, each row's pair at a distinct s: conflict-free; the staging stores write whole
+// 128-B rows per 8- / 16-lane group.
+template <int TR>
+__device__ __forceinline__ int col_off(int kr, int c) {
+  if constexpr (TR == 64 && RQ_X3S_COMPACT) return 128 * kr + ((c ^ ((((kr >> 1) & 1) << 1) | (((kr >> 3) & 1) << 2))) << 4);
+  else return 256 * kr + ((c ^ col_swz(kr)) << 4);
+}
 // Row image: row rr of 2 kXK bytes, 16-B chunk c stored at c ^ row_swz(rr). With the 16x16x32 MFMA
 // (default) a fragment read (xfrag16) is a ds_read_b128 whose lane groups {0-3,12-15,20-27},
 // {4-11,16-19,28-31} (+32) touch rows {0-3, 12-15} at chunk c and rows 4-11 at chunk c ^ 1: the
@@ -380,7 +396,7 @@ struct XStage {
 #pragma unroll
         for (int j = 0; j < NJ_FM; ++j) {
           const int kr = (tid / CT_F) + KR_F * j;
-          const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
+          const int off = col_off<TR>(kr, m >> 3) + (((m >> 2) & 1) << 3);
           uint2 h, l;
           split_bf16x2(w[j].x, w[j].y, h.x, l.x);
           split_bf16x2(w[j].z, w[j].w, h.y, l.y);
@@ -402,7 +418,7 @@ struct XStage {
           off = row_off(rr, c);
         } else {
           const int kr = (tid / CT_S) + KR_S * j;
-          off = 256 * kr + (((tid % CT_S) ^ col_swz(kr)) << 4);
+          off = col_off<TR>(kr, tid % CT_S);
         }
         *reinterpret_cast<uint4*>(hi_plane + off) = h;
         *reinterpret_cast<uint4*>(lo_plane + off) = l;
@@ -437,7 +453,7 @@ __device__ __forceinline__ bf16x8_t xfrag(const char* plane, int rb, int s, int 
 }
 
 // 16x16x32 operand fragment (8 bf16: row rb + lane % 16, k = 8 (lane / 16) + 0..7 of the stage).
-template <bool KC>
+template <bool KC, int TR = 128>
 __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane) {
   if constexpr (KC) {
     const int rr = rb + (lane & 15), c = lane >> 4;
@@ -451,7 +467,7 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int kr = 8 * G + 4 * u + q;
-      const int off = 256 * kr + (((m >> 3) ^ col_swz(kr)) << 4) + (((m >> 2) & 1) << 3);
+      const int off = col_off<TR>(kr, m >> 3) + (((m >> 2) & 1) << 3);
       t[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) s16x4_t*)(plane + off));
     }
@@ -571,10 +587,10 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
   {                                                                                                           \
     bf16x8_t fa_h[kP], fa_l[kP], fb_h[kP], fb_l[kP];                                                          \
     _Pragma("unroll") for (int p = 0; p < kP; ++p) {                                                          \
-      fa_h[p] = xfrag16<AKC>(ah, wm * kWTile + 16 * p, lane);                                                 \
-      fa_l[p] = xfrag16<AKC>(al, wm * kWTile + 16 * p, lane);                                                 \
-      fb_h[p] = xfrag16<BKC>(bh, wn * kWTile + 16 * p, lane);                                                 \
-      fb_l[p] = xfrag16<BKC>(bl, wn * kWTile + 16 * p, lane);                                                 \
+      fa_h[p] = xfrag16<AKC, TS>(ah, wm * kWTile + 16 * p, lane);                                             \
+      fa_l[p] = xfrag16<AKC, TS>(al, wm * kWTile + 16 * p, lane);                                             \
+      fb_h[p] = xfrag16<BKC, TS>(bh, wn * kWTile + 16 * p, lane);                                             \
+      fb_l[p] = xfrag16<BKC, TS>(bl, wn * kWTile + 16 * p, lane);                                             \
     }                                                                                                         \
     _Pragma("unroll") for (int p = 0; p < kP; ++p) _Pragma("unroll") for (int q = 0; q < kP; ++q) {          \
       acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);              \
@@ -603,12 +619,14 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
 // TS = output tile (128, or 64 for launches whose 128-tiles cannot fill the chip: the decoder's 1,280
 // future-token rows): 4 waves of (TS / 2)^2 outputs, the same k order (so the same result) either way.
 template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false, int TS = 128>
-__global__ void __launch_bounds__(256, kXWG)
+__global__ void __launch_bounds__(256, TS == 64 ? kXWG64 : kXWG)
 gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
                    const void* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S,
                    int64_t chunk, int per, float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
   ep.seed = epoch_seed(ep.seed);
-  __shared__ __attribute__((aligned(16))) char lds[kXLds];
+  // the 64-tile form's compact images: half of every plane (row image: 64 rows; column image: 128-B rows)
+  constexpr int kPl = (TS == 64 && RQ_X3S_COMPACT) ? kXPlane / 2 : kXPlane;
+  __shared__ __attribute__((aligned(16))) char lds[8 * kPl];
   const int bid = blockIdx.x;
   const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
   if (lw >= tiles * S) return;
@@ -637,7 +655,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
       for (int r = 0; r < 16; ++r) acc[p][q][r] = 0.f;
 #endif
 
-  auto plane = [&](int buf, int op, int hl) { return lds + buf * kXBuf + op * kXOp + hl * kXPlane; };
+  auto plane = [&](int buf, int op, int hl) { return lds + buf * 4 * kPl + op * 2 * kPl + hl * kPl; };
   const int nst = (int)((k_hi - k_lo + kXK - 1) / kXK);
   // kDepth register stage sets: stage st + kDepth is loaded while stage st is multiplied and
   // stage st + 1 (loaded earlier) is written to the other LDS buffer, so each load has kDepth stages
@@ -1153,6 +1171,18 @@ static int64_t x3_split_cap(int64_t M, int64_t N) {
   return by_bytes > RQ_X3_MAX_SPLIT ? by_bytes : RQ_X3_MAX_SPLIT;
 }
 
+// The 64-tile form's compact LDS (32 KiB) lets 4 workgroups share a CU. A launch that fits in 2 per CU
+// gets 32 KiB of padding LDS instead (dynamic, unused), so the dispatcher spreads it over every CU rather
+// than packing them 4 per CU onto fewer CUs (measured: 1280 x 1536 x 512, 480 workgroups: 14.5 us spread,
+// 24.8 us packed; 26,880 x 384 x 1152, 2,520 workgroups: 122.6 -> 109.1 us at 4 per CU).
+static int x3s_resident(int64_t wgs) {
+  return RQ_X3S_COMPACT && wgs > (int64_t)resident_slots() ? kXWG64 : kXWG;
+}
+template <typename P>
+static unsigned x3s_pad_lds(const P& pl) {
+  return RQ_X3S_COMPACT && x3s_resident((int64_t)pl.tiles * pl.S) == kXWG ? 32768u : 0u;
+}
+
 // Modelled time (us) of a plan, to choose the split-K factor and between the two kernels:
 //  * MMA: whole rounds of resident workgroups (a partly filled last round costs a full one) x the
 //    MACs a CU does per round, at the measured per-CU rates (128-tile kernel ~0.53 M fp32-MAC/us per
@@ -1168,7 +1198,7 @@ static int64_t x3_split_cap(int64_t M, int64_t N) {
 #define RQ_X3S_RATE1 0.3    // 64-tile kernel, one workgroup per CU: M fp32-MAC / us
 #endif
 #ifndef RQ_X3S_RATE2
-#define RQ_X3S_RATE2 0.35   // 64-tile kernel, two workgroups per CU
+#define RQ_X3S_RATE2 0.35   // 64-tile kernel, kXWG64 workgroups per CU
 #endif
 static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   const int64_t cus = resident_slots() / 2;
@@ -1180,9 +1210,10 @@ static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   if (wgs <= cus) {   // at most one workgroup per CU
     t = tile * (double)p.chunk / ((wide ? rate : (small ? RQ_X3S_RATE1 : 0.4)) * 1e6);
   } else {
-    const int64_t slots = wide ? cus : cus * kXWG;
+    const int per_cu = wide ? 1 : (small ? x3s_resident(wgs) : kXWG);
+    const int64_t slots = cus * per_cu;
     const int64_t rounds = (wgs + slots - 1) / slots;
-    t = (double)rounds * (wide ? tile : kXWG * tile) * (double)p.chunk / (rate * 1e6);
+    t = (double)rounds * per_cu * tile * (double)p.chunk / (rate * 1e6);
   }
   if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + 4.0;
   return t;
@@ -1218,8 +1249,9 @@ static int x3s_mode() {
 // gradients, the decoder's future rows) and the model says the slabs pay for themselves.
 static X3Plan x3_plan_t(int64_t M, int64_t N, int64_t K, bool allow_split, int ts) {
   X3Plan p = x3_plan_s(M, N, K, 1, false, ts);
-  if (allow_split && p.tiles < x3_slots() / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
-    int64_t S = x3_slots() / p.tiles;
+  const int64_t slots_t = (int64_t)(resident_slots() / 2) * kXWG;   // split-K fills the 2-per-CU slots
+  if (allow_split && p.tiles < slots_t / 2 && (M * N) % 4 == 0) {   // slab reduction reads float4
+    int64_t S = slots_t / p.tiles;
     const int64_t max_s = (K + RQ_X3_MIN_STAGES * kXK - 1) / (RQ_X3_MIN_STAGES * kXK);   // min stages per workgroup
     if (S > max_s) S = max_s;
     if (S > x3_split_cap(M, N)) S = x3_split_cap(M, N);   // slab traffic of the reduction grows with S
@@ -1417,7 +1449,8 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
 #define RQ_X3D(AK, AS, BK, BS, EP, DR)                                                                               \
   do {                                                                                                               \
     if (pl.ts == 64)                                                                                                 \
-      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR, 64>), grid, block, 0, s, A, A_lo, lda, B, B_lo,  \
+      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR, 64>), grid, block, x3s_pad_lds(pl), s, A, A_lo,  \
+                         lda, B, B_lo,                                                                               \
                          ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep);         \
     else                                                                                                             \
       hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR>), grid, block, 0, s, A, A_lo, lda, B, B_lo, ldb, \

@@ -11,7 +11,13 @@ shapes = [(1280,512,512,1,1,0,1),(1280,1536,512,1,1,0,1),(1280,1024,512,1,1,0,1)
           (1280,512,1536,1,0,0,1),(512,512,1280,0,0,0,0),(1536,512,1280,0,0,0,0),(1024,512,1280,0,0,1,0),
           (512,1024,1280,0,0,0,1),(256,512,1280,0,0,0,0),(1280,256,512,1,1,0,1),(1280,128,512,1,0,0,1),
           (11332,512,512,1,1,0,1),(512,512,11332,0,0,0,0),(11332,1024,512,1,1,0,1),(11332,128,512,1,0,0,1),
-          (512,128,11332,0,0,0,0),(65536,128,256,1,1,1,1),(128,64,65536,0,0,1,1)]
+          (512,128,11332,0,0,0,0),(65536,128,256,1,1,1,1),(128,64,65536,0,0,1,1),
+          # decoder ML-32M context rows (B = 64 / GPU)
+          (26880,384,1152,1,0,0,1),(26880,384,1024,1,0,0,1),(26880,1152,384,1,1,0,1),(26880,384,384,1,1,0,1),
+          (1152,384,26880,0,0,0,0)]
+if len(sys.argv) > 1:   # A/B: another build of the library
+    from rqvae_hip import _lib
+    _lib._lib = _lib.load(sys.argv[1])
 def t(fn, n=30):
     """Device time per call: n calls captured in one hipGraph (host launch cost out of the picture)."""
     for _ in range(3): fn()
