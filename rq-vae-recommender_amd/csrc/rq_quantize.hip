@@ -412,22 +412,32 @@ __global__ void __launch_bounds__(256) sort_hist_kernel(const int64_t* __restric
 }
 
 // Per key: exclusive scan over blocks (in place) and the key's total -> key_off[l][k].
+// Per (level, key): exclusive scan over the histogram blocks in place (hist[l][blk][k] becomes the
+// key's first slot within the key for block blk) and the key's total into key_off[l][k]. 16 keys per
+// workgroup x 16 block segments (one thread each: a sum pass, then the write pass), segment sums
+// combined in LDS: the one-thread-per-key serial walk over 256 blocks was latency-bound (~13 us at
+// B = 65,536).
+constexpr int kScanSeg = 16;
 __global__ void __launch_bounds__(256) sort_keyscan_kernel(int* __restrict__ hist, int K, int nblk,
                                                             int* __restrict__ key_off) {
-  const int l = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
+  __shared__ int part[kScanSeg][16];
+  const int l = blockIdx.y, seg = threadIdx.x / 16, kk = threadIdx.x % 16, k = blockIdx.x * 16 + kk;
+  const int per = (nblk + kScanSeg - 1) / kScanSeg, b0 = seg * per, b1 = min(nblk, b0 + per);
   int* h = hist + (int64_t)l * nblk * K + k;
+  int sum = 0;
+  if (k < K)
+    for (int u = b0; u < b1; ++u) sum += h[(int64_t)u * K];
+  part[seg][kk] = sum;
+  __syncthreads();
+  if (k >= K) return;
   int run = 0;
-  int blk = 0;
-  for (; blk + 8 <= nblk; blk += 8) {
-    int v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = h[(int64_t)(blk + u) * K];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) { h[(int64_t)(blk + u) * K] = run; run += v[u]; }
+  for (int j = 0; j < seg; ++j) run += part[j][kk];
+  for (int u = b0; u < b1; ++u) {
+    const int x = h[(int64_t)u * K];
+    h[(int64_t)u * K] = run;
+    run += x;
   }
-  for (; blk < nblk; ++blk) { const int v = h[(int64_t)blk * K]; h[(int64_t)blk * K] = run; run += v; }
-  key_off[(int64_t)l * (K + 1) + k] = run;
+  if (seg == kScanSeg - 1) key_off[(int64_t)l * (K + 1) + k] = run;
 }
 
 // Exclusive scan of the per-key totals in place: key_off[l][k] = first slot of key k; [K] = B.
@@ -1590,7 +1600,7 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   }
   RQ_LAUNCH_CHECK("rq_bwd_rows");
   hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, l), dim3(256), k * sizeof(int), s, ids, b, l, k, nblk, hist);
-  hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 255) / 256, l), dim3(256), 0, s, hist, k, nblk, key_off);
+  hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 15) / 16, l), dim3(256), 0, s, hist, k, nblk, key_off);
   hipLaunchKernelGGL(sort_offsets_kernel, dim3(l), dim3(1024), 0, s, key_off, k, b);
   hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, l), dim3(256), (2 * k + kSortRows) * sizeof(int), s, ids, b, l, k,
                      nblk, hist, key_off, perm);
@@ -1629,7 +1639,7 @@ int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D,
   int* perm = key_off + (K + 1);
   float* segs = (float*)(((uintptr_t)(perm + B) + 15) & ~(uintptr_t)15);
   hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, 1), dim3(256), k * sizeof(int), s, keys, b, 1, k, nblk, hist);
-  hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 255) / 256, 1), dim3(256), 0, s, hist, k, nblk, key_off);
+  hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 15) / 16, 1), dim3(256), 0, s, hist, k, nblk, key_off);
   hipLaunchKernelGGL(sort_offsets_kernel, dim3(1), dim3(1024), 0, s, key_off, k, b);
   hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk, 1), dim3(256), (2 * k + kSortRows) * sizeof(int), s, keys, b, 1, k,
                      nblk, hist, key_off, perm);

@@ -68,7 +68,7 @@ def test_dedup_rank_large(device):
     assert np.array_equal(got, U.dedup_rank(ids))
 
 
-@pytest.mark.parametrize("B,D,K", [(20000, 8, 16), (65536, 64, 256), (3, 1024, 7), (1000, 16, 4096)])
+@pytest.mark.parametrize("B,D,K", [(20000, 8, 16), (65536, 64, 256), (3, 1024, 7), (1000, 16, 4096), (300000, 8, 300)])
 def test_segment_sum(device, B, D, K):
     from rqvae_hip import ops
     g = gi.rng(B + D + K)
