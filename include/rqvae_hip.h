@@ -207,6 +207,10 @@ int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, ui
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
  * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */
 size_t rq_unique_workspace(int64_t B);
+/* Workspace for these (B, L, K): where K^L <= 2^24 a byte map of K^L bytes (counted in one pass, no
+ * scattered atomics), else the hash table of rq_unique_workspace(B). rq_unique_count uses the map when
+ * K^L <= 2^24 and ws_bytes covers it. */
+size_t rq_unique_workspace2(int64_t B, int64_t L, int64_t K);
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
                     size_t ws_bytes, void* stream);
 

@@ -162,6 +162,6 @@ class RqVae(nn.Module):
         loss, recon_mean, rq_mean = hip_ops.loss_means(reconstruction, qloss)
         with torch.no_grad():
             embs_norm = hip_ops.row_norms(emb).T     # emb.norm(dim=-1) over (L, B, D)
-            p_unique_ids = hip_ops.unique_count(ids, self.codebook_size).to(torch.float32) / ids.shape[0]
+            p_unique_ids = torch.true_divide(hip_ops.unique_count(ids, self.codebook_size), ids.shape[0])
         return RqVaeComputedLosses(loss=loss, reconstruction_loss=recon_mean, rqvae_loss=rq_mean,
                                    embs_norm=embs_norm, p_unique_ids=p_unique_ids)

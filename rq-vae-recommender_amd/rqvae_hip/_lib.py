@@ -58,6 +58,7 @@ _SIGS = {
     "rq_split_bf16x3": ([_P, _I64, _P, _P, _P], _I),
     "rq_split_bf16x3_multi": ([_I, _P, _P, _P, _P, _P], _I),
     "rq_unique_workspace": ([_I64], _SZ),
+    "rq_unique_workspace2": ([_I64, _I64, _I64], _SZ),
     "rq_unique_count": ([_P, _I64, _I64, _I64, _P, _P, _SZ, _P], _I),
     "rq_l2norm_recon_fwd": ([_P, _P, _I64, _I64, _P, _P, _P], _I),
     "rq_row_norms": ([_P, _I64, _I64, _P, _P], _I),

@@ -924,7 +924,7 @@ def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     ids = ids.contiguous().to(torch.int64)
     B, L = ids.shape
     out = torch.empty((), device=ids.device, dtype=torch.int64)
-    nbytes = _lib.load().rq_unique_workspace(B)
+    nbytes = _lib.load().rq_unique_workspace2(B, L, int(K))
     ws = torch.empty((nbytes,), device=ids.device, dtype=torch.uint8)
     call("rq_unique_count", ptr(ids), B, L, int(K), ptr(out), ptr(ws), nbytes, stream_handle(ids.device))
     return out
