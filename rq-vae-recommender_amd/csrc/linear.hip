@@ -517,7 +517,8 @@ enum X3Epi : int {
   kEpiStore = 0,     // C = A B^T (fp32; split-K slabs when S > 1)
   kEpiSiluFwd = 1,   // C = z = A B^T (fp32, kept for the backward); H = split(Dropout(SiLU(z)))
   kEpiSiluBwd = 2,   // H = split(SiLU'(Z) * Dropout(A B^T)): the pre-activation grad of a hidden layer
-  kEpiAdd = 3,       // C = A B^T + Z (fp32; the residual add after an attention projection)
+  kEpiAdd = 3,       // C = A B^T + Z (fp32; the residual add after an attention projection); with dropout
+                     // C = Z + Dropout(A B^T) (the block output h + Dropout(MLP(.)))
 };
 
 struct X3Epilogue {
@@ -547,7 +548,16 @@ __device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, flo
     *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
   } else if constexpr (EPI == kEpiAdd) {
     const float4 r = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
-    *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+    if constexpr (DROP) {   // C = Z + Dropout(A B^T): dropout_add_fwd's mask (element m N + n) and arithmetic
+      const uint64_t e = (uint64_t)m * N + n;
+      float d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = keep1(ep.seed, e + j, ep.thr) ? ep.scale : 0.f;
+      *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) =
+          make_float4(r.x + v.x * d[0], r.y + v.y * d[1], r.z + v.z * d[2], r.w + v.w * d[3]);
+    } else {
+      *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+    }
   } else {
     const uint64_t e = (uint64_t)m * N + n;
     float d[4] = {1.f, 1.f, 1.f, 1.f};   // dropout multipliers (0 or 1 / (1 - p))
@@ -1458,8 +1468,8 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   } while (0)
 #define RQ_X3(AK, AS, BK, BS, EP)                                                                                    \
   do {                                                                                                               \
-    if ((EP == kEpiSiluFwd || EP == kEpiSiluBwd) && ep.thr != 0)                                                      \
-      RQ_X3D(AK, AS, BK, BS, EP, (EP == kEpiSiluFwd || EP == kEpiSiluBwd));                                         \
+    if (ep.thr != 0)                                                                                                 \
+      RQ_X3D(AK, AS, BK, BS, EP, (EP != kEpiStore));                                                                 \
     else                                                                                                             \
       RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
   } while (0)
@@ -1485,7 +1495,7 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
     } else if (epi_k == kEpiSiluBwd && kc == 2) {
       if (drop) RQ_X3W(true, false, kEpiSiluBwd, true); else RQ_X3W(true, false, kEpiSiluBwd, false);
     } else if (epi_k == kEpiAdd && kc == 3) {
-      RQ_X3W(true, true, kEpiAdd, false);
+      if (drop) RQ_X3W(true, true, kEpiAdd, true); else RQ_X3W(true, true, kEpiAdd, false);
     } else {
       launched = false;
     }
@@ -1522,6 +1532,7 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   } else {
     switch (code) {
       case 16 | 4 | 2: RQ_X3(true, false, true, true, kEpiAdd); break;   // Linear (split weight) + residual
+      case 16 | 8 | 4 | 2: RQ_X3(true, true, true, true, kEpiAdd); break;  // MLP chain's last layer + residual
       default: launched = false;
     }
   }
@@ -1533,13 +1544,13 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   if (slab) {
     const int64_t n = M * N;
     const dim3 rg((unsigned)((n / 4 + 63) / 64)), rb(256);
-    const bool drop = ep.thr != 0 && (epilogue == kEpiSiluFwd || epilogue == kEpiSiluBwd);
+    const bool drop = ep.thr != 0 && epilogue != kEpiStore;
 #define RQ_X3R(EP, DR, AC) hipLaunchKernelGGL((x3_reduce_kernel<EP, DR, AC>), rg, rb, 0, s, out, pl.S, n, (int)N, C, ep)
     switch (epilogue) {
       case kEpiStore: if (accumulate) RQ_X3R(kEpiStore, false, true); else RQ_X3R(kEpiStore, false, false); break;
       case kEpiSiluFwd: if (drop) RQ_X3R(kEpiSiluFwd, true, false); else RQ_X3R(kEpiSiluFwd, false, false); break;
       case kEpiSiluBwd: if (drop) RQ_X3R(kEpiSiluBwd, true, false); else RQ_X3R(kEpiSiluBwd, false, false); break;
-      default: RQ_X3R(kEpiAdd, false, false); break;
+      default: if (drop) RQ_X3R(kEpiAdd, true, false); else RQ_X3R(kEpiAdd, false, false); break;
     }
 #undef RQ_X3R
     RQ_LAUNCH_CHECK("x3_reduce_kernel");

@@ -13,8 +13,10 @@ Jagged inputs may be torch NJTs (drop-in) or dense ``ops.jagged.Jagged`` views; 
 unwrapped once at the module boundary and every row-wise op (RMSNorm, dropout, Linear, residual
 adds) runs on the dense (T, C) values, avoiding NJT's per-op Python dispatch.
 """
+import os
 from typing import List, Optional
 
+import torch
 from torch import nn
 from torch import Tensor
 
@@ -23,6 +25,9 @@ from modules.normalize import RMSNorm
 from modules.transformer.attention import AttentionInput, MultiHeadAttention, _wrap_like
 from ops.jagged import Jagged, as_jagged
 from rqvae_hip import ops as hip_ops
+
+# RQ_FF_RESIDUAL=0: keep the feed-forward output as MLP + dropout_add (in-process A/B)
+_FF_RESIDUAL = os.environ.get("RQ_FF_RESIDUAL", "1") != "0"
 
 
 class KVCacheOpsMixin:
@@ -83,10 +88,26 @@ class TransformerBlock(nn.Module):
             h = self.cross_attention(x=jx.with_values(self.cross_attn_norm.forward_dropout(xv, self.do)), x_kv=jkv,
                                      is_causal=False, jagged=True, use_cache=use_cache, residual=h).values()
         norm, mlp, drop = self.ff
-        y = mlp(norm(h))
+        n3 = norm(h)
+        fused = self._ff_residual(mlp, drop, n3, h)
+        if fused is not None:
+            return jx.with_values(fused)
+        y = mlp(n3)
         if drop.training and drop.p > 0 and hip_ops.dropout_fusable(h) and hip_ops.dropout_fusable(y):
             return jx.with_values(hip_ops.dropout_add(h, y, drop.p))   # h + Dropout(ff) in one pass
         return jx.with_values(h + drop(y))
+
+    @staticmethod
+    def _ff_residual(mlp, drop, x, h):
+        """h + Dropout(MLP(x)) with the residual and the output dropout in the MLP chain's last GEMM
+        epilogue (training with dropout at 'high' precision), else None."""
+        if not (_FF_RESIDUAL and drop.training and drop.p > 0 and hasattr(mlp, "_fused_chain")
+                and hip_ops.dropout_fusable(h)):
+            return None
+        chain = mlp._fused_chain(x)
+        if chain is None or h.shape[-1] != chain[0][-1].shape[0] or h.dtype != torch.float32:
+            return None
+        return hip_ops.mlp_chain_residual(x, chain[0], chain[1], h, drop.p)
 
     def _forward_fork(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool, use_cache: bool) -> Jagged:
         """Same block, with x's fan-out (norm branches + residual) and h's (ff norm + residual) as
@@ -105,6 +126,9 @@ class TransformerBlock(nn.Module):
             h = self.cross_attention(x=jx.with_values(n2), x_kv=jkv, is_causal=False, jagged=True,
                                      use_cache=use_cache, residual=h).values()
         n3, hr = hip_ops.rmsnorm_fork(h, norm.eps, norm.weight)
+        fused = self._ff_residual(mlp, drop, n3, hr)
+        if fused is not None:
+            return jx.with_values(fused)
         y = mlp(n3)
         if drop.training and drop.p > 0 and hip_ops.dropout_fusable(hr) and hip_ops.dropout_fusable(y):
             return jx.with_values(hip_ops.dropout_add(hr, y, drop.p))

@@ -447,8 +447,9 @@ def _presplit_input(rows: int, weights, n_layers: int) -> bool:
     return gemm_x3_choice(rows, O, I, True, True, True, True, epi)[0] == "wide"
 
 
-def _mlp_forward(a, wsp, rows: int, p: float, seeds):
-    """The chain's forward GEMMs from input a (fp32 or Split): (out fp32, zs, hs)."""
+def _mlp_forward(a, wsp, rows: int, p: float, seeds, residual=None, p_out: float = 0.0, seed_out: int = 0):
+    """The chain's forward GEMMs from input a (fp32 or Split): (out fp32, zs, hs). With `residual`
+    (rows, O) the last GEMM's epilogue returns residual + Dropout_{p_out}(out) instead."""
     n = len(wsp)
     zs, hs = [], []
     out = None
@@ -459,6 +460,8 @@ def _mlp_forward(a, wsp, rows: int, p: float, seeds):
             zs.append(z)
             hs.append(h)
             a = h
+        elif residual is not None:
+            out = gemm_x3(a, True, w, True, rows, O, I, EPI_ADD, Z=residual, p=p_out, seed=seed_out)
         else:
             out = gemm_x3(a, True, w, True, rows, O, I)
     return out, zs, hs
@@ -540,6 +543,42 @@ class MLPFunction(torch.autograd.Function):
 def mlp_chain(x: torch.Tensor, weights, p: float = 0.0) -> torch.Tensor:
     """Fused Linear-SiLU-[Dropout]-...-Linear at 'high' precision (MLPFunction)."""
     return MLPFunction.apply(x, float(p), *weights)
+
+
+class MLPResidualFunction(torch.autograd.Function):
+    """h + Dropout_{p_out}(MLP(x)): the transformer block's feed-forward output (modules/transformer/
+    model.py:76-82, `x + Dropout(MLP(RMSNorm(x)))`) as MLPFunction whose last GEMM epilogue adds the
+    residual and applies the output dropout (the mask of the standalone dropout_add kernel, so the
+    backward regenerates it with rq_dropout_bwd): one launch fewer per block than MLP + dropout_add."""
+
+    @staticmethod
+    def forward(ctx, x, h, p: float, p_out: float, *weights):
+        x_in, rows, wsp, seeds = _mlp_prologue(x, p, weights)
+        seed_out = next_seed()
+        out, zs, hs = _mlp_forward(x_in, wsp, rows, p, seeds, residual=h.reshape(rows, -1).contiguous(),
+                                   p_out=p_out, seed_out=seed_out)
+        ctx.n, ctx.p, ctx.seeds, ctx.xshape, ctx.weights = len(weights), float(p), seeds, x.shape, weights
+        ctx.p_out, ctx.seed_out = float(p_out), seed_out
+        ctx.save_for_backward(*_mlp_save(ctx, x_in, wsp, zs, hs))
+        return out.view(*x.shape[:-1], weights[-1].shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x_in, wsp, zs, hs, _ = _mlp_load(ctx, ctx.n, ctx.saved_tensors)
+        rows = (x_in.hi if ctx.x_split else x_in).shape[0]
+        g2 = g.reshape(rows, -1).contiguous()
+        gy = torch.empty_like(g2)
+        call("rq_dropout_bwd", ptr(g2), g2.numel(), ctx.p_out, ctx.seed_out, ptr(gy), stream_handle(g2.device))
+        dx, dws = _mlp_backward(gy, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[4:],
+                                ctx.needs_input_grad[0], ctx.weights)
+        ctx.weights = None
+        gh = g if ctx.needs_input_grad[1] else None
+        return (None if dx is None else dx.view(ctx.xshape), gh, None, None, *dws)
+
+
+def mlp_chain_residual(x: torch.Tensor, weights, p: float, h: torch.Tensor, p_out: float) -> torch.Tensor:
+    """h + Dropout_{p_out}(MLP(x)) at 'high' precision in the chain's launches (MLPResidualFunction)."""
+    return MLPResidualFunction.apply(x, h, float(p), float(p_out), *weights)
 
 
 class MLPL2ReconFunction(torch.autograd.Function):

@@ -178,3 +178,31 @@ def test_packed_attention_matches_unpacked(device, cross):
     assert torch.equal(qs.grad, q2.grad)
     if cross:
         assert torch.equal(kvs.grad, kv2.grad)
+
+
+@pytest.mark.parametrize("rows", [1280, 11332])
+def test_mlp_residual_dropout_equals_composition(device, rows):
+    """h + Dropout(MLP(x)) with the residual and the output dropout in the chain's last GEMM epilogue
+    (ops.mlp_chain_residual) equals mlp_chain followed by dropout_add under the same dropout keys:
+    bitwise output and gradients (x, h, weights)."""
+    from rqvae_hip import ops
+    torch.set_float32_matmul_precision("high")
+    g = torch.Generator(device=device).manual_seed(rows)
+    A, F = 512, 1024
+    x0 = torch.randn(rows, A, generator=g, device=device)
+    h0 = torch.randn(rows, A, generator=g, device=device)
+    w0 = [torch.randn(F, A, generator=g, device=device) * 0.04, torch.randn(A, F, generator=g, device=device) * 0.03]
+    go = torch.randn(rows, A, generator=g, device=device)
+    res = []
+    for fused in (True, False):
+        x, h = x0.clone().requires_grad_(True), h0.clone().requires_grad_(True)
+        ws = [w.clone().requires_grad_(True) for w in w0]
+        ops._SEED["n"] = 0
+        if fused:
+            out = ops.mlp_chain_residual(x, ws, 0.3, h, 0.3)
+        else:
+            out = ops.dropout_add(h, ops.mlp_chain(x, ws, 0.3), 0.3)
+        out.backward(go)
+        res.append((out.detach(), x.grad, h.grad, *[w.grad for w in ws]))
+    for a, b, what in zip(res[0], res[1], ("out", "dx", "dh", "dw0", "dw1")):
+        assert torch.equal(a, b), f"{what}: max abs diff {(a - b).abs().max().item():.3e}"
