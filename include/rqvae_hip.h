@@ -162,7 +162,9 @@ int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, i
  * (X = hi, X_lo = lo) of the operand's shape; split operands need their contiguous axis and ld
  * % 8 == 0. The epilogue turns the tile into:
  *   0  C = A B^T
- *   3  C = A B^T + Z                                             (a residual add after a projection)
+ *   3  C = A B^T + Z                                             (a residual add after a projection);
+ *      with p > 0: C = Z + Dropout_p(A B^T), the mask of rq_dropout_add_fwd (element m N + n), so
+ *      rq_dropout_bwd regenerates it — the transformer block's h + Dropout(MLP(..)) in the MLP's last GEMM
  *   1  C = z = A B^T, and H = split(Dropout_p(SiLU(z)))          (a hidden layer's forward)
  *   2  H = split(SiLU'(Z) * Dropout_p(A B^T)), C unused          (its pre-activation grad)
  * H_hi / H_lo: bf16 planes (M, N) of row stride ldh; Z: (M, N) of stride ldc. The dropout mask is
