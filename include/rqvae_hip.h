@@ -62,6 +62,13 @@ int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* code
                          int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
                          float* qloss, float* emb_sum, int impl, void* stream);
 
+/* rq_quantize_fwd plus emb_norms (L,B) = |emb_out[l][b]|_2, the embs_norm diagnostic of
+ * RqVae.forward (modules/rqvae.py:151). The 16x16 kernel (impl 4 under auto) writes the norms from
+ * its level epilogue; every other kernel is followed by one rq_row_norms pass over emb_out. */
+int rq_quantize_fwd2(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
+                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
+                     float* emb_sum, float* emb_norms, void* stream);
+
 /* Backward of rq_quantize_fwd (the autograd graph of modules/quantize.py:99-156 chained by
  * modules/rqvae.py:129): grads of emb_out (g_emb, (L,B,D) or NULL), of sum_l emb_out
  * (g_emb_sum, (B,D) or NULL), of residuals (g_res, (L,B,D) or NULL) and of qloss (g_qloss,

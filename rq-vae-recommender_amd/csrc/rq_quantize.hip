@@ -903,7 +903,8 @@ constexpr int kR16Items = 128;   // items per 8-wave workgroup
 __global__ void __launch_bounds__(512, 2)
 rq_fwd_r16_kernel(const float* __restrict__ x, int B, const float* __restrict__ cbs, const float* __restrict__ csq,
                   int K, int L, int mode, float beta, int64_t* __restrict__ ids, float* __restrict__ emb_out,
-                  float* __restrict__ res, float* __restrict__ qloss, float* __restrict__ emb_sum) {
+                  float* __restrict__ res, float* __restrict__ qloss, float* __restrict__ emb_sum,
+                  float* __restrict__ enorm) {
   constexpr int D = 64, QD = 16;
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   const int KP = (K + 31) & ~31;                     // rows padded to whole tile pairs
@@ -1069,6 +1070,13 @@ rq_fwd_r16_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
     }
     ql = ql + (dl + beta * dl);
     if (valid && g == 0) ids[(int64_t)b * L + l] = id;
+    if (enorm != nullptr) {   // |emb_out[l][b]| (RqVae.forward's embs_norm, modules/rqvae.py:151)
+      float n2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < QD; ++k) n2 = __builtin_fmaf(out[k], out[k], n2);
+      n2 = rsum(n2);
+      if (valid && g == 0) enorm[(int64_t)l * B + b] = sqrtf(n2);
+    }
 #pragma unroll
     for (int k = 0; k < QD; ++k) {
       pend[k] = out[k];
@@ -1084,11 +1092,12 @@ rq_fwd_r16_kernel(const float* __restrict__ x, int B, const float* __restrict__ 
 }
 
 static int launch_fwd_r16(int B, hipStream_t s, const float* x, const float* cbs, const float* csq, int K, int L,
-                          int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es) {
+                          int mode, float beta, int64_t* ids, float* eo, float* res, float* ql, float* es,
+                          float* enorm) {
   const int KP = (K + 31) & ~31;
   const size_t lds = (size_t)KP * (64 + 1) * sizeof(float);
   hipLaunchKernelGGL(rq_fwd_r16_kernel, dim3((B + kR16Items - 1) / kR16Items), dim3(512), lds, s, x, B, cbs, csq, K, L,
-                     mode, beta, ids, eo, res, ql, es);
+                     mode, beta, ids, eo, res, ql, es, enorm);
   return 0;
 }
 
@@ -1481,11 +1490,31 @@ int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks
                               0, stream);
 }
 
+int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream);   // rowwise.hip
+static int quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
+                        int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
+                        float* qloss, float* emb_sum, int impl, float* emb_norms, void* stream);
+
 int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
                          int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
                          float* qloss, float* emb_sum, int impl, void* stream) {
+  return quantize_fwd(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss, emb_sum, impl,
+                      nullptr, stream);
+}
+
+int rq_quantize_fwd2(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
+                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
+                     float* emb_sum, float* emb_norms, void* stream) {
+  return quantize_fwd(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss, emb_sum, 0,
+                      emb_norms, stream);
+}
+
+static int quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
+                        int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
+                        float* qloss, float* emb_sum, int impl, float* emb_norms, void* stream) {
   int lpi, epl;
-  RQ_CHECK_ARG(x && codebooks && cb_sqnorm && ids && emb_out && residuals && qloss, "rq_quantize_fwd: null pointer");
+  RQ_CHECK_ARG(codebooks && cb_sqnorm && (B == 0 || (x && ids && emb_out && residuals && qloss)),
+               "rq_quantize_fwd: null pointer");   // an empty batch may come as NULL buffers
   RQ_CHECK_ARG(row_split((int)D, lpi, epl), "rq_quantize_fwd: D=%lld must be a power of two in [8, 1024]", (long long)D);
   RQ_CHECK_ARG(K >= 1 && K <= (1 << 20) && L >= 1 && L <= 64, "rq_quantize_fwd: bad K=%lld / L=%lld", (long long)K,
                (long long)L);
@@ -1501,8 +1530,13 @@ int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* code
   const bool r16_ok = D == 64 && K <= 288;   // two 65 * K * 4-byte images per CU
   if (impl == 0) impl = (r16_ok && B >= 32768) ? 4 : D <= 64 ? 2 : (split_ok ? 3 : 1);
   RQ_CHECK_ARG(impl != 4 || r16_ok, "rq_quantize_fwd_impl: 16x16 register kernel needs D == 64 and K <= 288");
+  if (emb_norms != nullptr && impl != 4) {   // only the 16x16 kernel fuses the norms: one extra row pass otherwise
+    const int rc = quantize_fwd(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss,
+                                emb_sum, impl, nullptr, stream);
+    return rc != 0 ? rc : rq_row_norms(emb_out, L * B, D, emb_norms, stream);
+  }
   if (impl == 4) {
-    launch_fwd_r16(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum);
+    launch_fwd_r16(b, s, x, codebooks, cb_sqnorm, k, l, mode, beta, ids, emb_out, residuals, qloss, emb_sum, emb_norms);
     RQ_LAUNCH_CHECK("rq_quantize_fwd(register 16x16)");
     return 0;
   }

@@ -115,12 +115,13 @@ class RqVae(nn.Module):
             return None
         return modes.pop()
 
-    def quantize_levels(self, res0: Tensor, gumbel_t: float):
-        """All levels -> (emb (L,B,D), res (L,B,D), ids (B,L), qloss (B,), emb_sum (B,D))."""
+    def quantize_levels(self, res0: Tensor, gumbel_t: float, with_norms: bool = False):
+        """All levels -> (emb (L,B,D), res (L,B,D), ids (B,L), qloss (B,), emb_sum (B,D)
+        [, |emb| (L,B) without grad when with_norms])."""
         mode = self._fused_kernel_mode()
         if mode is not None:
             codebooks = torch.stack([layer.codebook() for layer in self.layers])
-            return hip_ops.rq_quantize(res0, codebooks, mode, self.commitment_weight)
+            return hip_ops.rq_quantize(res0, codebooks, mode, self.commitment_weight, with_norms)
         # generic per-level path (k-means init pending, gumbel / cosine layers)
         res, qloss = res0, 0
         embs, ress, ids = [], [], []
@@ -132,7 +133,11 @@ class RqVae(nn.Module):
             embs.append(q.embeddings)
             ids.append(q.ids)
         emb = torch.stack(embs)
-        return emb, torch.stack(ress), torch.stack(ids, 1), qloss, emb.sum(0)
+        out = (emb, torch.stack(ress), torch.stack(ids, 1), qloss, emb.sum(0))
+        if with_norms:
+            with torch.no_grad():
+                out += (hip_ops.row_norms(emb),)     # emb.norm(dim=-1) over (L, B, D)
+        return out
 
     def get_semantic_ids(self, x: Tensor, gumbel_t: float = 0.001) -> RqVaeOutput:
         emb, res, ids, qloss, _ = self.quantize_levels(self.encode(x), gumbel_t)
@@ -141,7 +146,9 @@ class RqVae(nn.Module):
 
     def forward(self, batch: SeqBatch, gumbel_t: float) -> RqVaeComputedLosses:
         x = batch.x
-        emb, _, ids, qloss, emb_sum = self.quantize_levels(self.encode(x), gumbel_t)
+        # the level loop also returns embs_norm = |emb_l| (modules/rqvae.py:151 of the reference),
+        # written from the fused kernel's level epilogue
+        emb, _, ids, qloss, emb_sum, emb_norms = self.quantize_levels(self.encode(x), gumbel_t, with_norms=True)
         n = self.n_cat_feats
         head = self.decoder.mlp
         if n == 0 and isinstance(head[-1], L2NormalizationLayer) and x.dtype == torch.float32:
@@ -161,7 +168,7 @@ class RqVae(nn.Module):
         # loss = mean(recon + qloss) and the two logged means in one deterministic pass
         loss, recon_mean, rq_mean = hip_ops.loss_means(reconstruction, qloss)
         with torch.no_grad():
-            embs_norm = hip_ops.row_norms(emb).T     # emb.norm(dim=-1) over (L, B, D)
+            embs_norm = emb_norms.T
             p_unique_ids = torch.true_divide(hip_ops.unique_count(ids, self.codebook_size), ids.shape[0])
         return RqVaeComputedLosses(loss=loss, reconstruction_loss=recon_mean, rqvae_loss=rq_mean,
                                    embs_norm=embs_norm, p_unique_ids=p_unique_ids)

@@ -28,6 +28,7 @@ _SIGS = {
     "rq_codebook_sqnorm": ([_P, _I64, _I64, _P, _P], _I),
     "rq_quantize_fwd": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P], _I),
     "rq_quantize_fwd_impl": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _I, _P], _I),
+    "rq_quantize_fwd2": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P, _P], _I),
     "rq_quantize_bwd_workspace": ([_I64, _I64, _I64, _I64], _SZ),
     "rq_quantize_bwd": ([_P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I),
     "rq_segment_sum_workspace": ([_I64, _I64], _SZ),

@@ -72,11 +72,11 @@ class RqQuantizeFunction(torch.autograd.Function):
     """Fused RqVae level loop (modules/rqvae.py:114-138 over modules/quantize.py:99-156).
 
     forward(x (B,D), codebooks (L,K,D)) -> emb_out (L,B,D), residuals (L,B,D), ids (B,L),
-    qloss (B,), emb_sum (B,D).
+    qloss (B,), emb_sum (B,D) [, emb_norms (L,B) = |emb_out[l][b]| (no grad) when with_norms].
     """
 
     @staticmethod
-    def forward(ctx, x, codebooks, mode: int, beta: float):
+    def forward(ctx, x, codebooks, mode: int, beta: float, with_norms: bool = False):
         require_gpu(x, codebooks, what="rq_quantize")
         assert x.dim() == 2 and codebooks.dim() == 3 and x.shape[1] == codebooks.shape[2]
         assert x.dtype == torch.float32 and codebooks.dtype == torch.float32, "fp32 path (reference default)"
@@ -93,16 +93,24 @@ class RqQuantizeFunction(torch.autograd.Function):
         es = torch.empty((B, D), device=dev, dtype=torch.float32)
         s = stream_handle(dev)
         call("rq_codebook_sqnorm", ptr(cbs), L * K, D, ptr(csq), s)
-        TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L, int(mode),
-                     float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), s)
+        if with_norms:
+            norms = torch.empty((L, B), device=dev, dtype=torch.float32)
+            TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd2", ptr(x), B, D, ptr(cbs), ptr(csq), K, L,
+                         int(mode), float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), ptr(norms), s)
+        else:
+            TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L,
+                         int(mode), float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), s)
         ctx.save_for_backward(res, ids, cbs)
         ctx.mode, ctx.beta = int(mode), float(beta)
         ctx.mark_non_differentiable(ids)
         ctx.set_materialize_grads(False)   # unused outputs arrive as None = NULL (no (L,B,D) zero fills)
+        if with_norms:
+            ctx.mark_non_differentiable(ids, norms)
+            return emb, res, ids, ql, es, norms
         return emb, res, ids, ql, es
 
     @staticmethod
-    def backward(ctx, g_emb, g_res, g_ids, g_ql, g_es):
+    def backward(ctx, g_emb, g_res, g_ids, g_ql, g_es, *g_norms):
         res, ids, cbs = ctx.saved_tensors
         L, B, D = res.shape
         K = cbs.shape[1]
@@ -114,11 +122,12 @@ class RqQuantizeFunction(torch.autograd.Function):
         TIMER.around("rq_quantize_bwd", call, "rq_quantize_bwd", ptr(res), ptr(ids), ptr(cbs), B, D, K, L, ctx.mode,
                      ctx.beta, ptr(_c(g_emb)), ptr(_c(g_es)), ptr(_c(g_res)), ptr(_c(g_ql)), ptr(gx), ptr(gcb), ptr(ws),
                      nbytes, stream_handle(dev))
-        return gx, gcb, None, None
+        return gx, gcb, None, None, None
 
 
-def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25):
-    return RqQuantizeFunction.apply(x, codebooks, mode, beta)
+def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25, with_norms=False):
+    """(emb_out, residuals, ids, qloss, emb_sum[, emb_norms]) — see RqQuantizeFunction."""
+    return RqQuantizeFunction.apply(x, codebooks, mode, beta, with_norms)
 
 
 def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int, with_counts: bool = True):

@@ -174,6 +174,22 @@ def test_unique_count(device):
         assert got == np.unique(ids, axis=0).shape[0]
 
 
+@pytest.mark.parametrize("B,D,K,L", [(40000, 64, 256, 3), (5000, 64, 256, 3), (1000, 128, 300, 2), (0, 64, 256, 3)])
+def test_quantize_emb_norms(device, B, D, K, L):
+    """rq_quantize(with_norms=True): |emb_out[l][b]| from the 16x16 kernel's level epilogue (B >= 32768,
+    D = 64) or from the row-norm pass after the other kernels; every other output bitwise unchanged."""
+    from rqvae_hip import ops
+    g = torch.Generator().manual_seed(B + D)
+    x = torch.randn(B, D, generator=g).to(device)
+    cbs = torch.randn(L, K, D, generator=g).to(device)
+    a = ops.rq_quantize(x, cbs, ops.MODE_ROTATION, 0.25)
+    b = ops.rq_quantize(x, cbs, ops.MODE_ROTATION, 0.25, with_norms=True)
+    assert len(b) == 6 and b[5].shape == (L, B) and not b[5].requires_grad
+    for u, v in zip(a, b[:5]):
+        assert torch.equal(u, v)
+    torch.testing.assert_close(b[5], b[0].norm(dim=-1), rtol=1e-6, atol=1e-6)
+
+
 def test_train_step_matches_oracle_trace(golden, device):
     """Three full RqVae train steps (fwd + bwd + AdamW) on GPU track the oracle's trace."""
     from data.schemas import SeqBatch
