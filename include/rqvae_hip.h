@@ -223,6 +223,11 @@ size_t rq_unique_workspace2(int64_t B, int64_t L, int64_t K);
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
                     size_t ws_bytes, void* stream);
 
+/* Rows per wave of the l2norm + reconstruction kernels (1, 2 or 4; other values leave it unchanged);
+ * returns the previous setting. Results are bitwise independent of it (per-row arithmetic is the same);
+ * the initial value comes from the environment variable RQ_L2R_RPW (default 1). */
+int rq_l2norm_recon_rows_per_wave(int rpw);
+
 /* Fused decoder head of RqVae.forward (modules/rqvae.py:145-150): x_hat = l2norm(pre) (decoder MLP's
  * final L2NormalizationLayer, F.normalize eps 1e-12) and recon[b] = sum_c (x_hat - x)^2
  * (modules/loss.py:5-10). pre, x: (B, C) fp32, C % 4 == 0, C <= 4096. fwd writes recon (B,) and

@@ -11,90 +11,124 @@
 //        written fp32, or (rq_l2norm_recon_bwd_split) as the split-bf16 planes the next data-grad /
 //        weight-grad GEMMs of the 'high' path consume directly (same bytes as fp32).
 #include "common.h"
+#include <stdlib.h>
 
 namespace rqhip {
 
-template <int VPL>   // float4 vectors per lane (C = 256 * VPL)
+template <int VPL, int RPW>   // float4 vectors per lane (C = 256 * VPL); rows per wave, all loads issued first
 __global__ void __launch_bounds__(256) l2norm_recon_fwd_kernel(const float* __restrict__ pre, const float* __restrict__ x,
                                                                 int64_t B, int C, float* __restrict__ recon,
                                                                 float* __restrict__ nrm) {
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= B) return;
-  const float* p = pre + r * C;
-  const float* q = x + r * C;
-  float4 pv[VPL], xv[VPL];
-  float s = 0.f;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (r0 >= B) return;
+  float4 pv[RPW][VPL], xv[RPW][VPL];
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int c = (v * 64 + lane) * 4;
-    const bool ok = c < C;
-    pv[v] = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    xv[v] = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    s += pv[v].x * pv[v].x + pv[v].y * pv[v].y + pv[v].z * pv[v].z + pv[v].w * pv[v].w;
-  }
-  s = group_sum<64>(s);
-  const float n = fmaxf(sqrtf(s), 1e-12f);
-  float acc = 0.f;
+  for (int i = 0; i < RPW; ++i) {
+    const bool row = r0 + i < B;
+    const float* p = pre + (r0 + i) * C;
+    const float* q = x + (r0 + i) * C;
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    if ((v * 64 + lane) * 4 >= C) continue;
-    const float d0 = pv[v].x / n - xv[v].x, d1 = pv[v].y / n - xv[v].y;
-    const float d2 = pv[v].z / n - xv[v].z, d3 = pv[v].w / n - xv[v].w;
-    acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      const bool ok = row && c < C;
+      pv[i][v] = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      xv[i][v] = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
-  acc = group_sum<64>(acc);
-  if (lane == 0) {
-    recon[r] = acc;
-    nrm[r] = sqrtf(s);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v)
+      s += pv[i][v].x * pv[i][v].x + pv[i][v].y * pv[i][v].y + pv[i][v].z * pv[i][v].z + pv[i][v].w * pv[i][v].w;
+    s = group_sum<64>(s);
+    const float n = fmaxf(sqrtf(s), 1e-12f);
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      if ((v * 64 + lane) * 4 >= C) continue;
+      const float d0 = pv[i][v].x / n - xv[i][v].x, d1 = pv[i][v].y / n - xv[i][v].y;
+      const float d2 = pv[i][v].z / n - xv[i][v].z, d3 = pv[i][v].w / n - xv[i][v].w;
+      acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    acc = group_sum<64>(acc);
+    if (lane == 0 && r0 + i < B) {
+      recon[r0 + i] = acc;
+      nrm[r0 + i] = sqrtf(s);
+    }
   }
 }
 
-template <int VPL, bool SPLIT>
+template <int VPL, bool SPLIT, int RPW>
 __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __restrict__ pre, const float* __restrict__ x,
                                                                 const float* __restrict__ nrm,
                                                                 const float* __restrict__ g_recon, int64_t B, int C,
                                                                 float* __restrict__ g_pre, uint16_t* __restrict__ g_hi,
                                                                 uint16_t* __restrict__ g_lo) {
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= B) return;
-  const float* p = pre + r * C;
-  const float* q = x + r * C;
-  const float raw = nrm[r];
-  const float n = fmaxf(raw, 1e-12f);
-  const float g2 = 2.f * g_recon[r];
-  float4 yv[VPL], gy[VPL];
-  float dot = 0.f;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (r0 >= B) return;
+  float4 av[RPW][VPL], bv[RPW][VPL];
+  float raw[RPW], g2[RPW];
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int c = (v * 64 + lane) * 4;
-    const bool ok = c < C;
-    const float4 a = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 b = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    yv[v] = make_float4(a.x / n, a.y / n, a.z / n, a.w / n);
-    gy[v] = make_float4(g2 * (yv[v].x - b.x), g2 * (yv[v].y - b.y), g2 * (yv[v].z - b.z), g2 * (yv[v].w - b.w));
-    dot += gy[v].x * yv[v].x + gy[v].y * yv[v].y + gy[v].z * yv[v].z + gy[v].w * yv[v].w;
-  }
-  dot = group_sum<64>(dot);
-  const bool clamped = !(raw > 1e-12f);
+  for (int i = 0; i < RPW; ++i) {
+    const bool row = r0 + i < B;
+    const float* p = pre + (r0 + i) * C;
+    const float* q = x + (r0 + i) * C;
+    raw[i] = row ? nrm[r0 + i] : 1.f;
+    g2[i] = row ? 2.f * g_recon[r0 + i] : 0.f;
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int c = (v * 64 + lane) * 4;
-    if (c >= C) continue;
-    float4 o;
-    if (clamped) {
-      o = make_float4(gy[v].x / n, gy[v].y / n, gy[v].z / n, gy[v].w / n);
-    } else {
-      o = make_float4((gy[v].x - yv[v].x * dot) / n, (gy[v].y - yv[v].y * dot) / n, (gy[v].z - yv[v].z * dot) / n,
-                      (gy[v].w - yv[v].w * dot) / n);
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      const bool ok = row && c < C;
+      av[i][v] = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      bv[i][v] = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if constexpr (SPLIT)
-      split_store4(o, g_hi + r * C + c, g_lo + r * C + c);
-    else
-      *reinterpret_cast<float4*>(g_pre + r * C + c) = o;
+  }
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int64_t r = r0 + i;
+    const float n = fmaxf(raw[i], 1e-12f);
+    float4 yv[VPL], gy[VPL];
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const float4 a = av[i][v], b = bv[i][v];
+      yv[v] = make_float4(a.x / n, a.y / n, a.z / n, a.w / n);
+      gy[v] = make_float4(g2[i] * (yv[v].x - b.x), g2[i] * (yv[v].y - b.y), g2[i] * (yv[v].z - b.z),
+                          g2[i] * (yv[v].w - b.w));
+      dot += gy[v].x * yv[v].x + gy[v].y * yv[v].y + gy[v].z * yv[v].z + gy[v].w * yv[v].w;
+    }
+    dot = group_sum<64>(dot);
+    if (r >= B) continue;
+    const bool clamped = !(raw[i] > 1e-12f);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      if (c >= C) continue;
+      float4 o;
+      if (clamped) {
+        o = make_float4(gy[v].x / n, gy[v].y / n, gy[v].z / n, gy[v].w / n);
+      } else {
+        o = make_float4((gy[v].x - yv[v].x * dot) / n, (gy[v].y - yv[v].y * dot) / n, (gy[v].z - yv[v].z * dot) / n,
+                        (gy[v].w - yv[v].w * dot) / n);
+      }
+      if constexpr (SPLIT)
+        split_store4(o, g_hi + r * C + c, g_lo + r * C + c);
+      else
+        *reinterpret_cast<float4*>(g_pre + r * C + c) = o;
+    }
   }
 }
+
+// Rows per wave of the two kernels above (1 = one row per wave; 2 / 4 keep more bytes in flight per
+// wave with fewer workgroups). rq_l2norm_recon_rows_per_wave() sets it (A/B); RQ_L2R_RPW at load.
+static int g_l2r_rpw = [] {
+  const char* e = getenv("RQ_L2R_RPW");
+  const int v = e ? atoi(e) : 1;
+  return (v == 2 || v == 4) ? v : 1;
+}();
 
 // ---------------------------------------------------------------------------------------
 // RMSNorm (modules/normalize.py:22-32): t = x * rsqrt(mean(x^2) + eps), y = t * w.
@@ -334,20 +368,31 @@ using namespace rqhip;
 
 extern "C" {
 
+int rq_l2norm_recon_rows_per_wave(int rpw) {
+  const int prev = g_l2r_rpw;
+  if (rpw == 1 || rpw == 2 || rpw == 4) g_l2r_rpw = rpw;
+  return prev;
+}
+
 int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
                         void* stream) {
   RQ_CHECK_ARG(pre && x && recon && norms, "rq_l2norm_recon_fwd: null pointer");
   RQ_CHECK_ARG(B >= 0 && C > 0 && C % 4 == 0 && C <= 4096, "rq_l2norm_recon_fwd: need C %% 4 == 0, C <= 4096");
   if (B == 0) return 0;
-  dim3 g((unsigned)((B + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
   const int vpl = (int)((C + 255) / 256);
+  const int rpw = vpl <= 4 ? g_l2r_rpw : 1;   // register budget: RPW * VPL * 8 floats of loads per lane
+  const dim3 g((unsigned)((B + 4 * rpw - 1) / (4 * rpw)));
+#define L2R_LAUNCH(V, R) hipLaunchKernelGGL((l2norm_recon_fwd_kernel<V, R>), g, dim3(256), 0, s, pre, x, B, (int)C, recon, norms)
+#define L2R_CASE(V) case V: if (rpw == 4) L2R_LAUNCH(V, 4); else if (rpw == 2) L2R_LAUNCH(V, 2); else L2R_LAUNCH(V, 1); break;
+#define L2R_CASE1(V) case V: L2R_LAUNCH(V, 1); break;
   switch (vpl) {
-#define L2R_CASE(V) case V: hipLaunchKernelGGL((l2norm_recon_fwd_kernel<V>), g, dim3(256), 0, s, pre, x, B, (int)C, recon, norms); break;
-    L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE(5) L2R_CASE(6) L2R_CASE(7) L2R_CASE(8)
-    L2R_CASE(9) L2R_CASE(10) L2R_CASE(11) L2R_CASE(12) L2R_CASE(13) L2R_CASE(14) L2R_CASE(15) L2R_CASE(16)
-#undef L2R_CASE
+    L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
+    L2R_CASE1(9) L2R_CASE1(10) L2R_CASE1(11) L2R_CASE1(12) L2R_CASE1(13) L2R_CASE1(14) L2R_CASE1(15) L2R_CASE1(16)
   }
+#undef L2R_CASE
+#undef L2R_CASE1
+#undef L2R_LAUNCH
   RQ_LAUNCH_CHECK("rq_l2norm_recon_fwd");
   return 0;
 }
@@ -356,24 +401,25 @@ static int l2norm_recon_bwd_launch(const float* pre, const float* x, const float
                                    int64_t B, int64_t C, float* g_pre, uint16_t* g_hi, uint16_t* g_lo, void* stream) {
   RQ_CHECK_ARG(B >= 0 && C > 0 && C % 4 == 0 && C <= 4096, "rq_l2norm_recon_bwd: need C %% 4 == 0, C <= 4096");
   if (B == 0) return 0;
-  dim3 g((unsigned)((B + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
   const int vpl = (int)((C + 255) / 256);
+  const int rpw = vpl <= 4 ? g_l2r_rpw : 1;
+  const dim3 g((unsigned)((B + 4 * rpw - 1) / (4 * rpw)));
   const bool sp = g_hi != nullptr;
+#define L2R_LAUNCH(V, SP, R)                                                                                     \
+  hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, SP, R>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, \
+                     g_pre, g_hi, g_lo)
+#define L2R_R(V, SP) if (rpw == 4) L2R_LAUNCH(V, SP, 4); else if (rpw == 2) L2R_LAUNCH(V, SP, 2); else L2R_LAUNCH(V, SP, 1);
+#define L2R_CASE(V) case V: if (sp) { L2R_R(V, true) } else { L2R_R(V, false) } break;
+#define L2R_CASE1(V) case V: if (sp) L2R_LAUNCH(V, true, 1); else L2R_LAUNCH(V, false, 1); break;
   switch (vpl) {
-#define L2R_CASE(V)                                                                                                 \
-  case V:                                                                                                           \
-    if (sp)                                                                                                         \
-      hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, true>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, \
-                         g_pre, g_hi, g_lo);                                                                        \
-    else                                                                                                            \
-      hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, false>), g, dim3(256), 0, s, pre, x, norms, g_recon, B,        \
-                         (int)C, g_pre, g_hi, g_lo);                                                                \
-    break;
-    L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE(5) L2R_CASE(6) L2R_CASE(7) L2R_CASE(8)
-    L2R_CASE(9) L2R_CASE(10) L2R_CASE(11) L2R_CASE(12) L2R_CASE(13) L2R_CASE(14) L2R_CASE(15) L2R_CASE(16)
-#undef L2R_CASE
+    L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
+    L2R_CASE1(9) L2R_CASE1(10) L2R_CASE1(11) L2R_CASE1(12) L2R_CASE1(13) L2R_CASE1(14) L2R_CASE1(15) L2R_CASE1(16)
   }
+#undef L2R_CASE
+#undef L2R_CASE1
+#undef L2R_R
+#undef L2R_LAUNCH
   RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd");
   return 0;
 }

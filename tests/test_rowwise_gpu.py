@@ -28,6 +28,31 @@ def test_l2norm_recon_vs_torch(device, B, C):
     assert torch.isfinite(a.grad).all()
 
 
+@pytest.mark.parametrize("B,C", [(65537, 768), (5, 96), (3, 4), (1001, 1024), (9, 1000)])
+def test_l2norm_recon_rows_per_wave_bitwise(device, B, C):
+    """The 2- and 4-rows-per-wave forms (ragged last wave included) give the 1-row results bitwise."""
+    from rqvae_hip import _lib, ops
+    g = torch.Generator(device=device).manual_seed(B * 3 + C)
+    pre = torch.randn(B, C, generator=g, device=device)
+    pre[-1] = 0.0
+    x = F.normalize(torch.randn(B, C, generator=g, device=device), dim=-1)
+    gr = torch.rand(B, generator=g, device=device)
+    lib = _lib.load()
+    outs = []
+    prev = lib.rq_l2norm_recon_rows_per_wave(1)
+    try:
+        for rpw in (1, 2, 4):
+            lib.rq_l2norm_recon_rows_per_wave(rpw)
+            a = pre.clone().requires_grad_(True)
+            r = ops.l2norm_recon_loss(a, x)
+            (r * gr).sum().backward()
+            outs.append((r.detach(), a.grad))
+    finally:
+        lib.rq_l2norm_recon_rows_per_wave(prev)
+    for r, ga in outs[1:]:
+        assert torch.equal(r, outs[0][0]) and torch.equal(ga, outs[0][1])
+
+
 @pytest.mark.parametrize("shape", [(11000, 512), (7, 128), (3, 5, 4096), (1, 4), (0, 64)])
 def test_rmsnorm_fused_matches_fp64(device, shape):
     """Fused RMSNorm vs the reference formula (modules/normalize.py:22-32) in fp64.
