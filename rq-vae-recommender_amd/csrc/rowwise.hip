@@ -247,39 +247,46 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
   }
 }
 
-// out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): a workgroup owns 16 float4 columns;
-// its 16 row lanes q sum s = q, q+16, ... (4 loads in flight), then the 16 partials are added in q
-// order through LDS. Deterministic, no atomics; D/64 workgroups of long independent sums.
+// out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): a workgroup owns kRedCols float4
+// columns; its 256 / kRedCols row lanes q sum s = q, q + 64, ... (8 loads in flight), then the 64
+// partials are combined by a fixed-shape tree through LDS. Deterministic, no atomics. Few columns per
+// workgroup: at D = 512 and ~700 partials the sum is latency-bound, so more workgroups with shorter
+// chains (32 x 11 loads per lane, not 8 x 44).
+constexpr int kRedCols = 4;
 __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict__ P, int S, int64_t n,
                                                          float* __restrict__ out, int accumulate) {
-  __shared__ float4 red[16][16];
-  const int c = threadIdx.x & 15, q = threadIdx.x >> 4;
-  const int64_t j = ((int64_t)blockIdx.x * 16 + c) * 4;
+  constexpr int kQ = 256 / kRedCols;
+  __shared__ float4 red[kQ][kRedCols];
+  const int c = threadIdx.x % kRedCols, q = threadIdx.x / kRedCols;
+  const int64_t j = ((int64_t)blockIdx.x * kRedCols + c) * 4;
   const bool ok = j < n;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
     int s = q;
-    for (; s + 48 < S; s += 64) {
-      float4 v[4];
+    for (; s + 7 * kQ < S; s += 8 * kQ) {
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 16 * u) * n + j);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + kQ * u) * n + j);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+      for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
     }
-    for (; s < S; s += 16) {
+    for (; s < S; s += kQ) {
       const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
   }
   red[q][c] = a;
   __syncthreads();
+#pragma unroll
+  for (int h = kQ / 2; h >= 1; h >>= 1) {
+    if (q < h) {
+      const float4 u = red[q][c], v = red[q + h][c];
+      red[q][c] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+    }
+    __syncthreads();
+  }
   if (q == 0 && ok) {
     float4 r = red[0][c];
-#pragma unroll
-    for (int w = 1; w < 16; ++w) {
-      const float4 v = red[w][c];
-      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
-    }
     if (accumulate) {   // out += sum: a parameter gradient accumulated in place (flat DP bucket)
       const float4 o = *reinterpret_cast<const float4*>(out + j);
       r = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
@@ -518,7 +525,7 @@ int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, c
   RMS_SWITCH((int)((D + 255) / 256), RMS_B)
 #undef RMS_B
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd");
-  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + 15) / 16)), dim3(256), 0, s, part, nblk, D, gw,
+  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + kRedCols - 1) / kRedCols)), dim3(256), 0, s, part, nblk, D, gw,
                      accumulate_gw);
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd(reduce)");
   return 0;
