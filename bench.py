@@ -709,6 +709,12 @@ def decoder_kernel_stats(m, buckets, batch, ctx_lens, cfg, reps=3):
     n = np.asarray(ctx_lens, np.float64)
     A, nf, Le, Ld, Bn = cfg["A"], cfg["sem_id_dim"] + 1, cfg["layers"] // 2, cfg["layers"] // 2, len(ctx_lens)
     attn_fwd = Le * 4 * A * (n * n).sum() + Ld * 4 * A * nf * n.sum() + Ld * 4 * A * nf * nf * Bn
+    # algorithmic HBM bytes (fp32, each operand touched once): fwd reads q, k, v and writes o; bwd reads
+    # q, k, v, o, dO and writes dq, dk, dv. Encoder self-attention over the T context rows, decoder
+    # self-attention over the Tf future rows, cross-attention Tf queries over T keys.
+    T, Tf = n.sum(), nf * Bn
+    attn_fwd_bytes = 4 * A * (Le * 4 * T + Ld * 4 * Tf + Ld * (2 * Tf + 2 * T))
+    attn_bwd_bytes = 4 * A * (Le * 8 * T + Ld * 8 * Tf + Ld * (4 * Tf + 4 * T))
     for _ in range(2):
         buckets.zero_grad()
         m(batch).loss.backward()
@@ -730,8 +736,14 @@ def decoder_kernel_stats(m, buckets, batch, ctx_lens, cfg, reps=3):
                          "fwd_TFLOPs": round(attn_fwd / (f_step * 1e-3) / 1e12, 2),
                          "bwd_TFLOPs": round(2 * attn_fwd / (b_step * 1e-3) / 1e12, 2),
                          "frac_fp32_peak": round(3 * attn_fwd / ((f_step + b_step) * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "fwd_GBps": round(attn_fwd_bytes / (f_step * 1e-3) / 1e9, 1),
+                         "bwd_GBps": round(attn_bwd_bytes / (b_step * 1e-3) / 1e9, 1),
+                         "frac_hbm_peak": round((attn_fwd_bytes + attn_bwd_bytes) / ((f_step + b_step) * 1e-3) / 1e9
+                                                / HBM_PEAK_GBS, 4),
                          "note": "algorithmic attention FLOPs per step (fwd 4 A sum_b n_q n_k over the 12 "
-                                 "calls; bwd = 2 x fwd) / device time of the varlen_attn launches"},
+                                 "calls; bwd = 2 x fwd) / device time of the varlen_attn launches; GBps / "
+                                 "frac_hbm_peak: algorithmic bytes (fwd q, k, v read + o written; bwd q, k, v, o, "
+                                 "dO read + dq, dk, dv written, fp32, once each) over the same device time"},
            "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
            "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
            "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}
