@@ -4,6 +4,7 @@ SemIdEmbedder: one table of sem_ids_dim*K + 1 rows; token (type t, id s) -> row 
 padded positions (seq_mask False) -> the padding row (index sem_ids_dim*K, padding_idx).
 UserIdEmbedder: user_id mod num_buckets -> row of a num_buckets table.
 """
+import os
 from typing import NamedTuple
 
 import torch
@@ -11,6 +12,9 @@ from torch import nn
 from torch import Tensor
 
 from rqvae_hip import ops as hip_ops
+
+# RQ_EMB_PAIR=0: gather cat([seq, fut]) and slice (in-process A/B of the paired embedding)
+_EMB_PAIR = os.environ.get("RQ_EMB_PAIR", "1") != "0"
 
 
 class Embedding(nn.Embedding):
@@ -46,9 +50,14 @@ class SemIdEmbedder(nn.Module):
                            torch.full_like(batch.sem_ids, self.padding_idx))
         if batch.sem_ids_fut is None:
             return SemIdEmbeddingBatch(seq=self.emb(rows), fut=None)
-        # one gather (and one backward reduction) for the context and future tokens of the table
+        fut_rows = self._rows(batch.token_type_ids_fut, batch.sem_ids_fut)
+        w = self.emb.weight
+        if _EMB_PAIR and hip_ops.embedding_supported(w) and rows.is_cuda and self.emb.max_norm is None:
+            # one backward reduction for the context and future tokens of the table (no slice backward)
+            seq, fut = hip_ops.embedding_pair(rows, fut_rows, w, self.padding_idx)
+            return SemIdEmbeddingBatch(seq=seq, fut=fut)
         N = rows.shape[1]
-        both = self.emb(torch.cat([rows, self._rows(batch.token_type_ids_fut, batch.sem_ids_fut)], dim=1))
+        both = self.emb(torch.cat([rows, fut_rows], dim=1))
         return SemIdEmbeddingBatch(seq=both[:, :N], fut=both[:, N:])
 
 

@@ -957,6 +957,41 @@ class EmbeddingFunction(torch.autograd.Function):
         return sums, None, None
 
 
+class EmbeddingPairFunction(torch.autograd.Function):
+    """Two row gathers from one table, (F.embedding(ia), F.embedding(ib)) for ia (B, Na), ib (B, Nb),
+    whose backward is ONE segmented sum over the (B, Na + Nb) gradient rows in the order of
+    F.embedding(cat([ia, ib], 1)) — the same reduction (and bits) as gathering the concatenated
+    indices and slicing the result, without the two slice-backward zero fills, copies and add."""
+
+    @staticmethod
+    def forward(ctx, weight, ia, ib, padding_idx):
+        require_gpu(weight, ia, ib, what="embedding_pair")
+        ctx.save_for_backward(ia, ib)
+        ctx.K, ctx.padding_idx = weight.shape[0], padding_idx
+        F_ = torch.nn.functional
+        return F_.embedding(ia, weight, padding_idx), F_.embedding(ib, weight, padding_idx)
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        ia, ib = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        E = (ga if ga is not None else gb).shape[-1]
+        ga = torch.zeros(ia.shape + (E,), device=ia.device) if ga is None else ga
+        gb = torch.zeros(ib.shape + (E,), device=ib.device) if gb is None else gb
+        keys = torch.cat([ia, ib], dim=1).reshape(-1)
+        if ctx.padding_idx is not None:   # padding rows are skipped (key -1): their row's grad is 0
+            keys = torch.where(keys == ctx.padding_idx, -1, keys)
+        g = torch.cat([ga, gb], dim=1).reshape(-1, E)
+        sums, _ = segment_sum(g, keys, ctx.K, with_counts=False)
+        return sums, None, None, None
+
+
+def embedding_pair(ia: torch.Tensor, ib: torch.Tensor, weight: torch.Tensor, padding_idx=None):
+    """(embedding(ia), embedding(ib)) with one backward reduction (EmbeddingPairFunction)."""
+    return EmbeddingPairFunction.apply(weight, ia, ib, padding_idx)
+
+
 def embedding_supported(weight: torch.Tensor) -> bool:
     K, E = weight.shape
     return weight.is_cuda and weight.dtype == torch.float32 and K <= 4096 and E <= 1024

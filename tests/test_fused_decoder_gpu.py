@@ -128,6 +128,29 @@ def test_embedding_segment_sum_backward(device):
     assert torch.equal(wr.grad, wr2.grad)
 
 
+def test_embedding_pair_equals_concatenated_gather(device):
+    """embedding_pair(ia, ib): outputs and table gradient bitwise equal to gathering cat([ia, ib], 1)
+    and slicing (the SemIdEmbedder's context + future tokens), a missing output gradient included."""
+    from rqvae_hip import ops
+    K, E = 1025, 128
+    g = torch.Generator(device=device).manual_seed(9)
+    w = torch.randn(K, E, device=device, generator=g)
+    ia = torch.randint(0, K, (256, 80), device=device, generator=g)
+    ia[:, 50:] = K - 1
+    ib = torch.randint(0, 1024, (256, 5), device=device, generator=g)
+    ga = torch.randn(256, 80, E, device=device, generator=g)
+    gb = torch.randn(256, 5, E, device=device, generator=g)
+    for use_b in (True, False):
+        w1 = w.clone().requires_grad_(True)
+        a, b = ops.embedding_pair(ia, ib, w1, K - 1)
+        ((a * ga).sum() + ((b * gb).sum() if use_b else 0)).backward()
+        w2 = w.clone().requires_grad_(True)
+        both = ops.embedding(torch.cat([ia, ib], 1), w2, K - 1)
+        ((both[:, :80] * ga).sum() + ((both[:, 80:] * gb).sum() if use_b else 0)).backward()
+        assert torch.equal(a, both[:, :80]) and torch.equal(b, both[:, 80:])
+        assert torch.equal(w1.grad, w2.grad)
+
+
 @pytest.mark.parametrize("N,D,K", [(20000, 128, 1025), (5000, 64, 7), (3, 8, 4096), (65536, 1024, 300)])
 def test_segment_sum_vs_index_add(device, N, D, K):
     """Deterministic segmented sum (light segments in one workgroup, heavy ones split and finalized)
