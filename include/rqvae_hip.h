@@ -223,6 +223,12 @@ size_t rq_unique_workspace2(int64_t B, int64_t L, int64_t K);
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
                     size_t ws_bytes, void* stream);
 
+/* out[j] (+)= sum_{s < S} P[s * n + j] for j < n, in a fixed order (deterministic, no atomics):
+ * the batch-sum gradient of a parameter broadcast over the batch — `pos + seq_emb` and
+ * `bos_emb.repeat(B, 1, 1)` of EncoderDecoderRetrievalModel._predict (modules/model.py:91-95).
+ * n % 4 == 0; P and out 16-byte aligned. accumulate != 0: out += sum. */
+int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate, void* stream);
+
 /* Rows per wave of the l2norm + reconstruction kernels (1, 2 or 4; other values leave it unchanged);
  * returns the previous setting. Results are bitwise independent of it (per-row arithmetic is the same);
  * the initial value comes from the environment variable RQ_L2R_RPW (default 1). */

@@ -375,6 +375,21 @@ using namespace rqhip;
 
 extern "C" {
 
+int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate, void* stream) {
+  RQ_CHECK_ARG((P || S == 0) && out, "rq_col_sum: null pointer");
+  RQ_CHECK_ARG(S >= 0 && S < (1ll << 31) && n > 0 && n % 4 == 0 && ((uintptr_t)P | (uintptr_t)out) % 16 == 0,
+               "rq_col_sum: need n %% 4 == 0 and 16-byte aligned P / out");
+  hipStream_t s = (hipStream_t)stream;
+  if (S == 0) {
+    if (!accumulate) RQ_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(float), s));
+    return 0;
+  }
+  hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((n / 4 + kRedCols - 1) / kRedCols)), dim3(256), 0, s, P,
+                     (int)S, n, out, accumulate);
+  RQ_LAUNCH_CHECK("rq_col_sum");
+  return 0;
+}
+
 int rq_l2norm_recon_rows_per_wave(int rpw) {
   const int prev = g_l2r_rpw;
   if (rpw == 1 || rpw == 2 || rpw == 4) g_l2r_rpw = rpw;

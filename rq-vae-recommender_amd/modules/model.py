@@ -10,6 +10,7 @@ Forward (training) path, jagged mode (the only working mode in the reference, SU
   over the L+1 positions and averaged over B; loss_d = per-position mean.
 The module-level Dropout(p=0.5) is hard-coded as in the reference (:67).
 """
+import os
 from typing import NamedTuple
 
 import torch
@@ -26,6 +27,9 @@ from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cach
 from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged, row_counts
 from rqvae_hip import gemm_tuning
 from rqvae_hip import ops as hip_ops
+
+# RQ_BATCH_SUM=0: torch's broadcast add / repeat (and their reduction backward) in the prologue (A/B)
+_BATCH_SUM = os.environ.get("RQ_BATCH_SUM", "1") != "0"
 
 # As the reference (modules/model.py:27): fp32 matmuls at 'high' precision (split-bf16 GEMM on
 # gfx950, rqvae_hip.ops.gemm_bf16x3); 'highest' restores the exact-fp32 library path.
@@ -89,8 +93,12 @@ class EncoderDecoderRetrievalModel(nn.Module):
         seq_emb, fut_emb = sem.seq, sem.fut                               # (B, N, E), (B, L+1, E)
         B, N, _ = seq_emb.shape
         pos = self.wpe(torch.arange(N, device=seq_emb.device)).unsqueeze(0)
-        ctx = torch.cat([user_emb, pos + seq_emb], dim=1)                 # (B, 1+N, E)
-        fut = self.bos_emb.repeat(B, 1, 1)
+        if _BATCH_SUM:   # the broadcast parameters' batch-sum gradients on one fixed-order HIP launch each
+            ctx = torch.cat([user_emb, hip_ops.batch_add(seq_emb, pos)], dim=1)          # (B, 1+N, E)
+            fut = hip_ops.batch_repeat(self.bos_emb.view(1, -1), B)
+        else:
+            ctx = torch.cat([user_emb, pos + seq_emb], dim=1)
+            fut = self.bos_emb.repeat(B, 1, 1)
         if fut_emb is not None:
             fut = torch.cat([fut, fut_emb + self.tte(batch.token_type_ids_fut)], dim=1)
         ctx_lengths = batch.seq_mask.sum(axis=1) + 1

@@ -63,6 +63,7 @@ _SIGS = {
     "rq_unique_count": ([_P, _I64, _I64, _I64, _P, _P, _SZ, _P], _I),
     "rq_l2norm_recon_fwd": ([_P, _P, _I64, _I64, _P, _P, _P], _I),
     "rq_l2norm_recon_rows_per_wave": ([_I], _I),
+    "rq_col_sum": ([_P, _I64, _I64, _P, _I, _P], _I),
     "rq_row_norms": ([_P, _I64, _I64, _P, _P], _I),
     "rq_loss_means": ([_P, _P, _I64, _P, _P], _I),
     "rq_l2norm_recon_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P], _I),

@@ -992,6 +992,61 @@ def embedding_pair(ia: torch.Tensor, ib: torch.Tensor, weight: torch.Tensor, pad
     return EmbeddingPairFunction.apply(weight, ia, ib, padding_idx)
 
 
+def col_sum(x: torch.Tensor) -> torch.Tensor:
+    """x (S, ...) -> sum over the leading axis, shape x.shape[1:], fixed order (rq_col_sum)."""
+    require_gpu(x, what="col_sum")
+    x = x.contiguous()
+    S, n = x.shape[0], math.prod(x.shape[1:])
+    out = torch.empty(x.shape[1:], device=x.device, dtype=torch.float32)
+    call("rq_col_sum", ptr(x), S, n, ptr(out), 0, stream_handle(x.device))
+    return out
+
+
+def _col_sum_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() >= 2 and math.prod(x.shape[1:]) % 4 == 0
+
+
+class BatchAddFunction(torch.autograd.Function):
+    """x + p with p (1, *rest) broadcast over x's leading batch axis (x (B, *rest)); p's gradient is
+    the batch sum of g on rq_col_sum (one fixed-order launch instead of torch's reduction)."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        return x + p
+
+    @staticmethod
+    def backward(ctx, g):
+        gp = col_sum(g).unsqueeze(0) if ctx.needs_input_grad[1] else None
+        return (g if ctx.needs_input_grad[0] else None), gp
+
+
+class BatchRepeatFunction(torch.autograd.Function):
+    """p (*rest) repeated B times along a new leading axis: (B, *rest); backward = batch sum of g."""
+
+    @staticmethod
+    def forward(ctx, p, B: int):
+        return p.unsqueeze(0).expand((B,) + tuple(p.shape)).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return col_sum(g), None
+
+
+def batch_add(x: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """x + p for p of shape (1, *x.shape[1:]) (modules/model.py:92 `pos + seq_emb`)."""
+    if _col_sum_ok(x) and p.shape[0] == 1 and p.shape[1:] == x.shape[1:] and p.dtype == x.dtype:
+        return BatchAddFunction.apply(x, p)
+    return x + p
+
+
+def batch_repeat(p: torch.Tensor, B: int) -> torch.Tensor:
+    """p repeated B times on a new leading axis (modules/model.py:93 `bos_emb.repeat(B, 1, 1)` for
+    p of shape (1, E): pass p.view(1, E) and get (B, 1, E))."""
+    if p.is_cuda and p.dtype == torch.float32 and p.numel() % 4 == 0 and B > 0:
+        return BatchRepeatFunction.apply(p, B)
+    return p.unsqueeze(0).repeat((B,) + (1,) * p.dim())
+
+
 def embedding_supported(weight: torch.Tensor) -> bool:
     K, E = weight.shape
     return weight.is_cuda and weight.dtype == torch.float32 and K <= 4096 and E <= 1024

@@ -151,6 +151,39 @@ def test_embedding_pair_equals_concatenated_gather(device):
         assert torch.equal(w1.grad, w2.grad)
 
 
+@pytest.mark.parametrize("B,rest", [(256, (80, 128)), (3, (1, 4)), (1000, (7, 12))])
+def test_batch_add_and_repeat(device, B, rest):
+    """batch_add / batch_repeat (modules/model.py:92-93): forward bitwise equal to torch's broadcast
+    add / repeat; the parameter gradient (fixed-order batch sum) within fp32 summation-order tolerance
+    of torch's and bitwise reproducible; col_sum of an empty batch is zero."""
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(B)
+    x = torch.randn((B,) + rest, device=device, generator=g)
+    p = torch.randn((1,) + rest, device=device, generator=g)
+    go = torch.randn((B,) + rest, device=device, generator=g)
+    grads = []
+    for _ in range(2):
+        xa, pa = x.clone().requires_grad_(True), p.clone().requires_grad_(True)
+        y = ops.batch_add(xa, pa)
+        y.backward(go)
+        grads.append(pa.grad)
+    xb, pb = x.clone().requires_grad_(True), p.clone().requires_grad_(True)
+    yb = pb + xb
+    yb.backward(go)
+    assert torch.equal(y, yb) and torch.equal(xa.grad, xb.grad)
+    torch.testing.assert_close(grads[0], pb.grad, rtol=1e-5, atol=1e-5)
+    assert torch.equal(grads[0], grads[1])
+    q = p[0].clone().requires_grad_(True)
+    r = ops.batch_repeat(q, B)
+    r.backward(go)
+    qt = p[0].clone().requires_grad_(True)
+    rt = qt.unsqueeze(0).repeat((B,) + (1,) * qt.dim())
+    rt.backward(go)
+    assert torch.equal(r, rt)
+    torch.testing.assert_close(q.grad, qt.grad, rtol=1e-5, atol=1e-5)
+    assert torch.all(ops.col_sum(torch.empty((0,) + rest, device=device)) == 0)
+
+
 @pytest.mark.parametrize("N,D,K", [(20000, 128, 1025), (5000, 64, 7), (3, 8, 4096), (65536, 1024, 300)])
 def test_segment_sum_vs_index_add(device, N, D, K):
     """Deterministic segmented sum (light segments in one workgroup, heavy ones split and finalized)
