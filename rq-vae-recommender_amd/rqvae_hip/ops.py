@@ -130,14 +130,17 @@ def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25, with_norms=False):
     return RqQuantizeFunction.apply(x, codebooks, mode, beta, with_norms)
 
 
-def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int, with_counts: bool = True):
+def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int, with_counts: bool = True, out: torch.Tensor = None):
     """(sums (K, D), counts (K,) or None) of `rows` grouped by `keys` — deterministic (no float
-    atomics). Rows whose key is outside [0, K) are skipped."""
+    atomics). Rows whose key is outside [0, K) are skipped. `out`: a contiguous fp32 (K, D) destination."""
     require_gpu(rows, keys, what="segment_sum")
     rows = rows.contiguous().float()
     keys = keys.contiguous().to(torch.int64)
     B, D = rows.shape
-    out = torch.empty((K, D), device=rows.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty((K, D), device=rows.device, dtype=torch.float32)
+    elif not (out.is_contiguous() and out.dtype == torch.float32 and tuple(out.shape) == (K, D)):
+        raise RqHipError(f"segment_sum: out must be a contiguous fp32 ({K}, {D}) tensor")
     counts = torch.empty((K,), device=rows.device, dtype=torch.int64) if with_counts else None
     nbytes = _lib.load().rq_segment_sum_workspace(B, K)
     ws = torch.empty((nbytes,), device=rows.device, dtype=torch.uint8)
@@ -933,6 +936,22 @@ def dropout_add(h: torch.Tensor, y: torch.Tensor, p: float) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------ embedding
+def _table_grad(g: torch.Tensor, keys: torch.Tensor, K: int, padding_idx) -> torch.Tensor:
+    """(K, E) embedding-table gradient: segmented sum of the rows g (n, E) by keys (n,), the padding
+    row's gradient zero (nn.Embedding(padding_idx)). Padding at the last row (the SemIdEmbedder
+    table): sum over the first K - 1 keys (the padding key falls outside and is skipped) into a
+    buffer whose last row is zeroed — no key rewrite pass."""
+    E = g.shape[-1]
+    if padding_idx is not None and padding_idx in (K - 1, -1) and K > 1:
+        out = torch.empty((K, E), device=g.device, dtype=torch.float32)
+        out[K - 1].zero_()
+        segment_sum(g, keys, K - 1, with_counts=False, out=out[:K - 1])
+        return out
+    if padding_idx is not None:   # padding rows are skipped (key -1): their row's grad is 0
+        keys = torch.where(keys == padding_idx, -1, keys)
+    return segment_sum(g, keys, K, with_counts=False)[0]
+
+
 class EmbeddingFunction(torch.autograd.Function):
     """F.embedding forward (a row gather); backward = deterministic segmented sum of the output
     gradient rows by index (rq_segment_sum: stable counting sort + fixed-order per-row sums), with the
@@ -949,12 +968,7 @@ class EmbeddingFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        E = g.shape[-1]
-        keys = idx.reshape(-1)
-        if ctx.padding_idx is not None:   # padding rows are skipped (key -1): their row's grad is 0
-            keys = torch.where(keys == ctx.padding_idx, -1, keys)
-        sums, _ = segment_sum(g.reshape(-1, E), keys, ctx.K, with_counts=False)
-        return sums, None, None
+        return _table_grad(g.reshape(-1, g.shape[-1]), idx.reshape(-1), ctx.K, ctx.padding_idx), None, None
 
 
 class EmbeddingPairFunction(torch.autograd.Function):
@@ -980,11 +994,8 @@ class EmbeddingPairFunction(torch.autograd.Function):
         ga = torch.zeros(ia.shape + (E,), device=ia.device) if ga is None else ga
         gb = torch.zeros(ib.shape + (E,), device=ib.device) if gb is None else gb
         keys = torch.cat([ia, ib], dim=1).reshape(-1)
-        if ctx.padding_idx is not None:   # padding rows are skipped (key -1): their row's grad is 0
-            keys = torch.where(keys == ctx.padding_idx, -1, keys)
         g = torch.cat([ga, gb], dim=1).reshape(-1, E)
-        sums, _ = segment_sum(g, keys, ctx.K, with_counts=False)
-        return sums, None, None, None
+        return _table_grad(g, keys, ctx.K, ctx.padding_idx), None, None, None
 
 
 def embedding_pair(ia: torch.Tensor, ib: torch.Tensor, weight: torch.Tensor, padding_idx=None):
