@@ -25,8 +25,9 @@ FLOPs 2MNK / mean device time, peak = bf16 dense MFMA / 3 products); roofline_qu
 (rq_quantize_fwd), algorithmic FLOPs 2*K*D*L per item, peak = fp32 MFMA 157.3
 TFLOP/s. traffic: HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 +
 WRITE_SIZE, child processes running the same kernel at the same shape, N=1 only) next to the
-algorithmic bytes. cpu_baseline: the pinned numpy oracle
-of the same train step (oracle/rqvae.py) on a bounded sample, timed on this host.
+algorithmic bytes. cpu_baseline: the same train step as eager torch-CPU (oracle/rqvae_torch.py, itself
+checked against the pinned numpy oracle oracle/rqvae.py in tests/test_oracle.py) on a bounded sample,
+timed on this host.
 
 decoder_amazon (configs[2]) / decoder_ml32m (configs[3], 8 and 64 sequences per GPU): decoder train
 steps replayed from one hipGraph per context row bucket (eager ms beside it), context tokens/s over
@@ -624,7 +625,9 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
                                      num_heads=cfg["H"], n_layers=cfg["layers"], num_embeddings=cfg["K"],
                                      sem_id_dim=cfg["sem_id_dim"], inference_verifier_fn=None,
                                      max_pos=cfg["max_items"] * cfg["sem_id_dim"]).to(device).train()
-    buckets = dp.GradBuckets(m.parameters(), overlap=not graphs, flat_views=graphs)
+    # overlap: bucket all-reduces launched from the grad hooks as backward produces them — captured
+    # inside each replayed graph with RCCL (GraphedSteps in-graph exchange), eager otherwise
+    buckets = dp.GradBuckets(m.parameters(), overlap=True, flat_views=graphs)
     buckets.broadcast_params()
     # optional: weight grads accumulate into the flat buckets on a side stream (overlapping the
     # data-grad chain) — measured slower on MI355X (7.59 vs 7.24 ms per Amazon step), so off by default
@@ -686,6 +689,9 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
            "ms_per_step": round(ms, 3), "per_gpu_batch": B, "n_gpus": ws, "parallelism": f"dp{ws}",
            "scaling": "weak", "step_mode": "hipgraph per row bucket" if graphs else "eager",
            "graphs_captured": len(gs.graphs) if gs is not None else 0,
+           "grad_exchange": ("none (1 rank)" if ws == 1 else
+                             ("in-graph, overlapped with backward" if gs is not None and gs.in_graph else
+                              "after the replay" if gs is not None else "eager, overlapped with backward")),
            "roofline": {"bound": "mfma", "achieved": round((dense + attn) / dt / 1e12, 2),
                         "peak": round(gemm_peak, 1), "unit": "TFLOP/s",
                         "frac": round((dense + attn) / dt / 1e12 / gemm_peak, 4),
@@ -694,6 +700,8 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
                         "attention_flops_share": round(attn / (dense + attn), 4),
                         "note": "algorithmic FLOPs (SURVEY 8d, step = 3 x forward); peak = split-bf16 GEMM ceiling "
                                 "(2.5 PF / 3); frac_of_step_roofline = (dense / 833 TF + attention / 157.3 TF) / step time"}}
+    if gs is not None and gs.capture_error:
+        out["graph_capture_error"] = gs.capture_error
     if stats and rk == 0:
         out["kernels"] = decoder_kernel_stats(m, buckets, batches[0], ctx_lens[0], cfg)
     if cpu_seconds > 0 and rk == 0 and ws == 1:

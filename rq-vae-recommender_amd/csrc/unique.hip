@@ -40,25 +40,43 @@ __global__ void __launch_bounds__(256) unique_insert_kernel(const int64_t* __res
   if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
 }
 
-// Small key spaces (K^L <= 2^24, e.g. ML-32M: 256^3): a byte map instead of the hash table — each row
-// stores 1 at its key (plain byte stores: racing writers all store 1), then one pass counts the set
-// bytes. No atomics on the scattered side (the table's device-scope CAS traffic took ~22 us at
-// B = 65,536; the map is ~3x cheaper including its 16 MiB memset).
+// Small key spaces (K^L <= 2^24, e.g. ML-32M: 256^3) at large batches: a byte map instead of the hash
+// table — each row stores 1 at its key (plain byte stores: racing writers all store 1), then one pass
+// counts the set bytes. No atomics on the scattered side (the table's device-scope CAS traffic took
+// ~22 us at B = 65,536; the map is ~3x cheaper including its 16 MiB memset). The map's memset and
+// counting pass cost O(K^L) whatever B is, so small batches (eval, B = 64..4,096) keep the hash table:
+// the map is used only when B >= K^L / kMapRowsDiv.
 constexpr int64_t kMapKeys = 1 << 24;
+constexpr int64_t kMapRowsDiv = 512;
 
+static bool use_byte_map(int64_t B, double keys) { return keys <= (double)kMapKeys && (double)B * kMapRowsDiv >= keys; }
+
+// A row with an id outside [0, K) has no slot in the map: it is not marked and counts as one distinct
+// tuple of its own (the quantizer never produces such ids; rq_unique_count is a public entry point, so
+// a bad row must not turn into an out-of-bounds store).
 __global__ void __launch_bounds__(256) unique_mark_kernel(const int64_t* __restrict__ ids, int64_t B, int L, int64_t K,
                                                            unsigned char* __restrict__ map,
+                                                           unsigned long long* __restrict__ bad,
                                                            unsigned long long* __restrict__ count) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r == 0) *count = 0ull;   // the count kernel runs after this launch
-  if (r >= B) return;
-  int64_t key = 0;
-  for (int l = L - 1; l >= 0; --l) key = key * K + ids[r * L + l];
-  map[key] = 1;
+  bool out_of_range = false;
+  if (r < B) {
+    int64_t key = 0;
+    for (int l = L - 1; l >= 0; --l) {
+      const int64_t v = ids[r * L + l];
+      out_of_range |= v < 0 || v >= K;
+      key = key * K + v;
+    }
+    if (!out_of_range) map[key] = 1;
+  }
+  const unsigned long long n = __popcll(__ballot(out_of_range));
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
 }
 
-// 16 bytes per thread per step; one atomic per workgroup
+// 16 bytes per thread per step; one atomic per workgroup (workgroup 0 adds the out-of-range rows)
 __global__ void __launch_bounds__(256) unique_map_count_kernel(const uint4* __restrict__ map, int64_t n16,
+                                                                const unsigned long long* __restrict__ bad,
                                                                 unsigned long long* __restrict__ count) {
   __shared__ unsigned int part[4];
   unsigned int c = 0;
@@ -70,7 +88,8 @@ __global__ void __launch_bounds__(256) unique_map_count_kernel(const uint4* __re
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(count, (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+  if (threadIdx.x == 0)
+    atomicAdd(count, (unsigned long long)(part[0] + part[1] + part[2] + part[3]) + (blockIdx.x == 0 ? *bad : 0ull));
 }
 
 }  // namespace rqhip
@@ -91,7 +110,8 @@ size_t rq_unique_workspace(int64_t B) { return (size_t)table_slots(B) * sizeof(u
 size_t rq_unique_workspace2(int64_t B, int64_t L, int64_t K) {
   double keys = 1;
   for (int64_t l = 0; l < L; ++l) keys *= (double)K;
-  return keys <= (double)kMapKeys ? (size_t)(((int64_t)keys + 15) / 16 * 16) : rq_unique_workspace(B);
+  // the map (rounded to 16 B) + the out-of-range row counter
+  return use_byte_map(B, keys) ? (size_t)(((int64_t)keys + 15) / 16 * 16 + 16) : rq_unique_workspace(B);
 }
 
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
@@ -104,15 +124,16 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
   hipStream_t s = (hipStream_t)stream;
   double keys = 1;
   for (int64_t l = 0; l < L; ++l) keys *= (double)K;
-  if (keys <= (double)kMapKeys && ws_bytes >= rq_unique_workspace2(B, L, K)) {
+  if (use_byte_map(B, keys) && ws_bytes >= rq_unique_workspace2(B, L, K)) {
     const int64_t nb = ((int64_t)keys + 15) / 16 * 16;
-    RQ_HIP(hipMemsetAsync(workspace, 0, (size_t)nb, s));
+    unsigned long long* bad = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + nb);
+    RQ_HIP(hipMemsetAsync(workspace, 0, (size_t)nb + 16, s));
     hipLaunchKernelGGL(unique_mark_kernel, dim3((unsigned)std::max<int64_t>(1, (B + 255) / 256)), dim3(256), 0, s, ids, B,
-                       (int)L, K, (unsigned char*)workspace, (unsigned long long*)out_count);
+                       (int)L, K, (unsigned char*)workspace, bad, (unsigned long long*)out_count);
     const int64_t n16 = nb / 16;
     // few workgroups: their one device-scope atomic each on a single address serialises (~10 ns apiece)
     hipLaunchKernelGGL(unique_map_count_kernel, dim3((unsigned)std::min<int64_t>(128, (n16 + 255) / 256)), dim3(256), 0, s,
-                       (const uint4*)workspace, n16, (unsigned long long*)out_count);
+                       (const uint4*)workspace, n16, bad, (unsigned long long*)out_count);
     RQ_LAUNCH_CHECK("rq_unique_count");
     return 0;
   }

@@ -13,7 +13,15 @@ train_decoder.py:171-173,196) and fixes its defects (SURVEY §5, Appendix A-5..A
     process (AdamW skips them; 1-rank and N-rank checkpoints stay identical);
   * buckets are all-reduced asynchronously as soon as backward has produced all their grads
     (post-accumulate-grad hooks), overlapping the RCCL ring with the rest of backward; the
-    optimizer step waits on the handles. Average = sum / world;
+    optimizer step waits on the handles. Average = sum / world. Buckets are LAUNCHED IN INDEX
+    ORDER on every rank (a ready bucket waits for its predecessors), so the collective sequence is
+    the same on every rank whatever order backward finishes them in — including a rank whose shard
+    is empty and that launches everything from `synchronize()`;
+  * a parameter may receive its gradient once per backward (as with DDP): a second contribution —
+    a HIP op accumulating into the flat bucket after the bucket's exchange may have started — raises;
+  * inside a captured hipGraph (rqvae_hip.graph.GraphedSteps, RCCL backend) the hooks' all-reduces
+    and the final wait / average are captured too (`finish()`), so the exchange of the replayed
+    step overlaps its backward; the caller's `synchronize()` after such a replay is a no-op;
   * gradient accumulation: backward passes run inside `no_sync()` except the last micro-batch
     (like DDP), so the exchange starts once, on the accumulated gradients.
 Loss normalisation for unequal shards (`shard_range` with a remainder, token-balanced decoder
@@ -114,6 +122,7 @@ def all_gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
 # GEMM's slab reduction) instead of returning it to autograd, which would run an AccumulateGrad add
 # kernel per parameter per step into the flat view. id(param) -> (flat view, hook).
 _DIRECT = {}
+_OWNER = {}   # id(param) -> (GradBuckets, bucket index)
 
 
 def direct_grad(p) -> Optional[torch.Tensor]:
@@ -126,6 +135,9 @@ def direct_grad(p) -> Optional[torch.Tensor]:
     g = p.grad
     if g is None or g.data_ptr() != e[0].data_ptr():
         return None
+    owner = _OWNER.get(id(p))
+    if owner is not None:
+        owner[0]._check_first(owner[1], p)   # a second contribution would race the bucket's exchange
     return e[0]
 
 
@@ -141,15 +153,17 @@ class GradBuckets:
     """Flat gradient buffers + bucketed async all-reduce for a module's parameters."""
 
     def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, overlap: bool = True,
-                 flat_views: bool = False):
+                 flat_views: bool = False, force_exchange: bool = False):
         """`params`: an iterable of parameters (buckets follow reverse registration order, ~ the order
         grads become ready), or a list of parameter groups given in the order their grads become
         ready (each group gets its own buckets, so an early group's all-reduce overlaps the rest of
         the backward — e.g. [decoder + codebooks, encoder] for the RQ-VAE).
         `overlap=False`: the exchange starts in `synchronize()` only (hooks just record which
-        parameters took part) — required when the backward is replayed from a captured hipGraph.
+        parameters took part).
         `flat_views=True`: gradients live in the flat buffers even with one process, so they sit
-        at fixed addresses that several captured graphs can share."""
+        at fixed addresses that several captured graphs can share.
+        `overlap=True` is also right for captured steps: GraphedSteps suspends the hooks where the
+        backend cannot be captured (gloo) and exchanges after the replay instead."""
         params = list(params)
         grouped = bool(params) and isinstance(params[0], (list, tuple))
         groups = [list(g) for g in params] if grouped else [list(reversed(params))]
@@ -157,14 +171,18 @@ class GradBuckets:
         groups = [[p for p in g if p.requires_grad and not (id(p) in seen or seen.add(id(p)))] for g in groups]
         self.params: List[torch.nn.Parameter] = [p for g in groups for p in g]
         self.average = average
+        # `force_exchange` (tests): run the collectives even with one process (a world-1 RCCL group
+        # exercises the captured exchange on a one-GPU box)
+        self.exchange = world() > 1 or force_exchange
         # single process without flat_views: no flat views (AccumulateGrad steals, no add_)
-        self.active = world() > 1 or flat_views
-        self.overlap = overlap and world() > 1
+        self.active = self.exchange or flat_views
+        self.overlap = overlap and self.exchange
         self.buckets = []
-        self._handles = []
         self._pending = {}
+        self._next = 0             # buckets [0, _next) are launched this pass (launch order = index order)
         self._sync = True          # False inside no_sync(): hooks record usage but launch nothing
         self._unused = None        # ids of params unused on every rank (decided at the first sync)
+        self._graph_done = False   # a captured replay already ran this step's exchange
         for g in (groups if self.active else []):
             by_dtype = {}
             for p in g:
@@ -184,6 +202,7 @@ class GradBuckets:
                 hook = self._make_hook(bi)
                 p.register_post_accumulate_grad_hook(hook)
                 _DIRECT[id(p)] = (v, hook)
+                _OWNER[id(p)] = (self, bi)
 
     def _make_bucket(self, ps, dt, dev):
         n = sum(p.numel() for p in ps)
@@ -195,8 +214,8 @@ class GradBuckets:
             p.grad = v          # grads accumulate in place into the flat buffer
             views.append(v)
             off += p.numel()
-        self.buckets.append(dict(params=ps, flat=flat, views=views, ready=0, used=set(), fired=set(),
-                                 expect=len(ps)))
+        self.buckets.append(dict(params=ps, flat=flat, views=views, used=set(), fired=set(), expect=len(ps),
+                                 ready=False))
 
     def _make_hook(self, bi):
         def hook(p):
@@ -210,10 +229,31 @@ class GradBuckets:
                 return
             # count this pass's grads only: after no_sync micro-batches `used` is already full, and a
             # launch on the first hook of the last micro-batch would reduce partial gradients
+            self._check_first(bi, p)
             b["fired"].add(id(p))
             if self.overlap and len(b["fired"]) == b["expect"]:
-                self._launch(bi)
+                b["ready"] = True
+                self._launch_ready()
         return hook
+
+    def _check_first(self, bi, p):
+        """With the exchange started from the hooks (overlap), a bucket may be all-reducing as soon as
+        its last parameter has fired: a second contribution to a fired parameter would race it."""
+        if self.overlap and self._sync and id(p) in self.buckets[bi]["fired"]:
+            raise RuntimeError("GradBuckets: a parameter received a second gradient contribution in one backward "
+                               "(used by two ops that accumulate into its flat bucket); its bucket's exchange may "
+                               "already be running. Use each parameter once per backward, or run the extra "
+                               "backward passes inside no_sync().")
+
+    def _launch_ready(self):
+        """Launch, in index order, every bucket whose predecessors are all launched and that is ready
+        (all its used parameters' grads produced, or nothing in it is used on any rank)."""
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            if not (b["ready"] or b["expect"] == 0):
+                return
+            self._launch(self._next)
+            self._next += 1
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -226,6 +266,7 @@ class GradBuckets:
             self._sync = prev
             for b in self.buckets:
                 b["fired"].clear()
+                b["ready"] = False
 
     def _launch(self, bi):
         if bi in self._pending:
@@ -247,33 +288,64 @@ class GradBuckets:
             b["flat"].zero_()
             b["used"].clear()
             b["fired"].clear()
+            b["ready"] = False
             for p, v in zip(b["params"], b["views"]):
                 if id(p) in unused:
                     continue
                 if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                     p.grad = v
         self._pending = {}
+        self._next = 0
 
     def synchronize(self):
         """Finish the exchange (launch buckets whose hooks did not all fire — params unused this
         step contribute zeros — then wait) and average."""
-        ws = world()
         if not self.active:
             return
-        from . import ops
-        ops.join_wgrad_stream()
-        if ws > 1:
-            for bi in range(len(self.buckets)):
-                self._launch(bi)
-            for bi, h in sorted(self._pending.items()):
-                h.wait()
-                if self.average:
-                    self.buckets[bi]["flat"].div_(ws)
-        self._pending = {}
+        if self._graph_done:   # the captured replay ran the exchange (GraphedSteps, in-graph mode)
+            self._graph_done = False
+        else:
+            self.finish()
         if self._unused is None:
             self._find_unused()
         for p in self._unused_params:
             p.grad = None
+
+    def finish(self):
+        """Launch what is left (in index order) and wait for every bucket, then average. Pure stream
+        work (no host sync): GraphedSteps captures it at the end of the replayed backward."""
+        from . import ops
+        ops.join_wgrad_stream()
+        if self.exchange:
+            while self._next < len(self.buckets):
+                self._launch(self._next)
+                self._next += 1
+            ws = world()
+            for bi, h in sorted(self._pending.items()):
+                h.wait()
+                if self.average and ws > 1:
+                    self.buckets[bi]["flat"].div_(ws)
+        self._pending = {}
+        self._next = 0
+
+    def mark_graph_exchanged(self):
+        """The step's exchange ran inside a replayed graph: the next synchronize() only finalises."""
+        self._graph_done = True
+
+    @contextlib.contextmanager
+    def suspended(self):
+        """Hooks record usage but launch nothing (graph warm-up passes: every rank must run exactly
+        one exchange per step, so warm-ups of a newly captured key must not communicate)."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+            for b in self.buckets:
+                b["fired"].clear()
+                b["ready"] = False
+            self._pending = {}
+            self._next = 0
 
     def _find_unused(self):
         """Once, at the first exchange: parameters whose grad hook fired on no rank. They are

@@ -1059,8 +1059,10 @@ def batch_repeat(p: torch.Tensor, B: int) -> torch.Tensor:
 
 
 def embedding_supported(weight: torch.Tensor) -> bool:
+    """Shapes the HIP gather + segmented-sum backward (rq_segment_sum: float4 rows) serve; other tables
+    take torch's embedding op."""
     K, E = weight.shape
-    return weight.is_cuda and weight.dtype == torch.float32 and K <= 4096 and E <= 1024
+    return (weight.is_cuda and weight.dtype == torch.float32 and K <= 4096 and 4 <= E <= 1024 and E % 4 == 0)
 
 
 def embedding(idx: torch.Tensor, weight: torch.Tensor, padding_idx=None) -> torch.Tensor:

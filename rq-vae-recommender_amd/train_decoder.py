@@ -8,6 +8,13 @@ shards (dp.balanced_partition over context lengths, so ranks finish together), e
 shard-mean loss by n_local * world / n_global (dp.shard_weight) so the averaged gradient is the
 gradient of the reference's global-batch mean (model.py:261), bucketed RCCL all-reduce overlapped
 with backward, no_sync() for all but the last micro-batch of an accumulation step.
+`cuda_graphs=True` (default; the reference compiles the model's forward with
+torch.compile(mode="reduce-overhead"), modules/model.py:247): forward + backward replayed from one
+hipGraph per (input shapes, context row bucket) (rqvae_hip.graph.GraphedSteps, the gradient exchange
+captured inside the graph with RCCL); the loss weight rides in as a device scalar. Gradient
+accumulation (> 1 micro-batch) runs eagerly. A rank whose token-balanced shard is empty (a short last
+batch with fewer sequences than ranks) runs no backward and joins the exchange from synchronize();
+buckets launch in index order on every rank, so the collective sequence still matches.
 The reference rejects non-AMAZON datasets and its ML-32M gin binds a non-existent parameter
 (SURVEY A-8); this entry accepts every RecDataset (the ML-32M config still fails on
 `train.attn_dropout`, exactly like gin). Checkpoints: plain state dicts with "scheduler".
@@ -29,6 +36,8 @@ from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
 from rqvae_hip import optim as hip_optim
+from rqvae_hip.graph import GraphedSteps
+from ops.jagged import copy_row_counts, register_row_counts
 
 
 def token_balanced_shard(seq_mask: torch.Tensor, rank: int, world: int) -> torch.Tensor:
@@ -41,6 +50,13 @@ def token_balanced_shard(seq_mask: torch.Tensor, rank: int, world: int) -> torch
     return torch.tensor(dp.balanced_partition(costs, world)[rank], dtype=torch.int64)
 
 
+
+# Last train() call: steady-state time per iteration (CUDA-synchronised once at the start and once at
+# the end of the measured span, nothing inside it), the step mode and the captured graphs — for the
+# bench's trainer line and the tests.
+LAST_RUN = {}
+
+
 @gin.configurable
 def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.01, dataset_folder="dataset/ml-1m",
           save_dir_root="out/", dataset=RecDataset.ML_1M, pretrained_rqvae_path=None, pretrained_decoder_path=None,
@@ -51,11 +67,12 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
           vae_n_cat_feats=18, vae_n_layers=3, decoder_embed_dim=64, dropout_p=0.1, attn_heads=8,
           attn_embed_dim=64, attn_layers=4, dataset_split="beauty", push_vae_to_hf=False,
           train_data_subsample=True, model_jagged_mode=True, vae_hf_model_name="edobotta/rqvae-amazon-beauty",
-          data_path=None, log_every=100, seed=0):
+          data_path=None, log_every=100, seed=0, cuda_graphs=True):
     if amp:
         raise NotImplementedError("amp: this build's decoder path is fp32 (reference default amp=False)")
     if push_vae_to_hf:
         raise NotImplementedError("HF hub upload is out of scope (network)")
+    LAST_RUN.clear()
     rank, world, local_rank = dp.init_from_env()
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
@@ -93,31 +110,70 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
         if "scheduler" in ck:
             sched.load_state_dict(ck["scheduler"])
         start_iter = ck["iter"] + 1
-    buckets = dp.GradBuckets(model.parameters())
+    use_graphs = cuda_graphs and gradient_accumulate_every == 1
+    buckets = dp.GradBuckets(model.parameters(), flat_views=use_graphs)
     buckets.broadcast_params()
+    bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
+
+    def graph_body(inp):
+        tok, w = inp
+        out = model(tok)
+        (out.loss * w).backward()
+        return out.loss.detach()
+
+    graphed = GraphedSteps(graph_body, lambda inp: model.context_rows(inp[0], bucket), buckets, run_backward=False,
+                           prepare=lambda static, inp: copy_row_counts(static[0].seq_mask, inp[0].seq_mask)
+                           ) if use_graphs else None
     t0, hist = time.time(), []
+    t_from = start_iter + min(5, (iterations - start_iter) // 2)   # measured span: [t_from, iterations)
+    t_mark, toks = None, 0
     for it in range(start_iter, iterations):
+        if it == t_from:
+            torch.cuda.synchronize()
+            t_mark = time.perf_counter()
         model.train()
-        buckets.zero_grad()
-        total = 0.0
+        if graphed is None:
+            buckets.zero_grad()
+        total = torch.zeros((), device=device)
         for micro in range(gradient_accumulate_every):
             data = next(loader)
             n_glob = data.seq_mask.shape[0]   # the loader's last batch of an epoch may be short
             mine = token_balanced_shard(data.seq_mask, rank, world)
-            if len(mine) == 0:   # fewer sequences than ranks: this rank contributes zero gradient
+            if len(mine) == 0:   # fewer sequences than ranks: zero gradient, exchange in synchronize()
+                if graphed is not None:
+                    buckets.zero_grad()
                 continue
-            data = batch_to(type(data)(*[v[mine] for v in data]), device)
-            out = model(tokenizer(data))
+            data = type(data)(*[v[mine] for v in data])
+            # host-side context row counts (the loader's batch is on the CPU): no device sync for the
+            # jagged total, and a captured step can be keyed by its row bucket
+            counts = (data.seq_mask.sum(1) * tokenizer.sem_ids_dim).tolist()
+            if t_mark is not None:
+                toks += sum(counts) + len(counts)   # context tokens (+ the user token per sequence)
+            tok = tokenizer(batch_to(data, device))
+            register_row_counts(tok.seq_mask, counts)
             # this rank's shard mean -> share of the GLOBAL-batch mean (unequal, token-balanced shards)
-            loss = out.loss * (dp.shard_weight(len(mine), n_glob) / gradient_accumulate_every)
+            w = dp.shard_weight(len(mine), n_glob) / gradient_accumulate_every
+            if graphed is not None:
+                total = total + graphed((tok, torch.tensor(w, device=device)))
+                continue
+            out = model(tok)
             last = micro == gradient_accumulate_every - 1
             with (contextlib.nullcontext() if last else buckets.no_sync()):
-                loss.backward()
+                (out.loss * w).backward()
             total = total + out.loss.detach() / gradient_accumulate_every
         buckets.synchronize()
         opt.step()
         sched.step()
         hist.append(total)
+        if it == iterations - 1 and t_mark is not None:
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t_mark
+            LAST_RUN.update(iter_ms=dt * 1e3 / max(1, iterations - t_from), timed_iters=iterations - t_from,
+                            ctx_tokens_per_s_rank=toks / dt, world=world,
+                            step_mode="hipgraph" if graphed is not None else "eager",
+                            graphs=len(graphed.graphs) if graphed is not None else 0,
+                            eager_steps=graphed.eager_steps if graphed is not None else iterations - start_iter,
+                            exchange="in-graph" if graphed is not None and graphed.in_graph else "hooks + synchronize")
         if rank == 0 and (it % log_every == 0 or it + 1 == iterations):
             print(json.dumps({"iter": it, "loss": float(torch.stack(hist).mean()), "lr": opt.param_groups[0]["lr"],
                               "elapsed_s": round(time.time() - t0, 2)}), flush=True)

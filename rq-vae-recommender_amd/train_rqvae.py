@@ -6,6 +6,12 @@ Differences from the reference loop (train_rqvae.py:24-250), all on the MI355X p
     draws a DISJOINT shard of every global batch (`split_batches` semantics), k-means init runs
     on rank 0 and is broadcast, gradients are all-reduced over RCCL;
   * no per-step `.item()` host syncs — losses are read back every `log_every` iterations;
+  * `cuda_graphs=True` (default; the reference compiles RqVae.forward with
+    torch.compile(mode="reduce-overhead"), modules/rqvae.py:140): after one eager probe step the
+    forward + backward (all micro-batches) is captured once and replayed every iteration
+    (rqvae_hip.graph.GraphedSteps) — the batch indices are drawn eagerly and copied into the graph's
+    static index buffer, the gradient exchange is captured inside the graph with RCCL, and the HIP
+    AdamW step (host-side bias corrections) runs after the replay;
   * checkpoints are plain state dicts {"iter", "model", "model_config", "optimizer"} (loadable with
     weights_only=True); swanlab logging is replaced by printed JSON lines (out of scope);
   * the loop runs `iterations + 1` times like the reference (SURVEY A-4).
@@ -29,6 +35,7 @@ from modules.tokenizer.semids import SemanticIdTokenizer
 from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
 from rqvae_hip import optim as hip_optim
+from rqvae_hip.graph import GraphedSteps
 
 
 def sample_batch_indices(gen: torch.Generator, n_items: int, global_batch: int, device) -> torch.Tensor:
@@ -39,6 +46,13 @@ def sample_batch_indices(gen: torch.Generator, n_items: int, global_batch: int, 
     return torch.randint(0, n_items, (global_batch,), generator=gen, device=device)
 
 
+
+# Last train() call: steady-state time per iteration (CUDA-synchronised once at the start and once at
+# the end of the measured span, nothing inside it), the step mode and the captured graphs — for the
+# bench's trainer line and the tests.
+LAST_RUN = {}
+
+
 @gin.configurable
 def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.01, dataset_folder="dataset/ml-1m",
           dataset=RecDataset.ML_1M, pretrained_rqvae_path=None, save_dir_root="out/", use_kmeans_init=True,
@@ -46,9 +60,11 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
           mixed_precision_type="fp16", gradient_accumulate_every=1, save_model_every=1000000, eval_every=50000,
           commitment_weight=0.25, vae_n_cat_feats=18, vae_input_dim=18, vae_embed_dim=16, vae_hidden_dims=[18, 18],
           vae_codebook_size=32, vae_codebook_normalize=False, vae_codebook_mode=QuantizeForwardMode.GUMBEL_SOFTMAX,
-          vae_sim_vq=False, vae_n_layers=3, dataset_split="beauty", data_path=None, log_every=100, seed=0):
+          vae_sim_vq=False, vae_n_layers=3, dataset_split="beauty", data_path=None, log_every=100, seed=0,
+          cuda_graphs=True):
     if amp:
         raise NotImplementedError("amp: the RQ-VAE hot path is fp32 (reference default amp=False)")
+    LAST_RUN.clear()
     rank, world, local_rank = dp.init_from_env()
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
@@ -94,29 +110,53 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
     # grads become ready decoder -> codebooks -> encoder: the first bucket's all-reduce overlaps the
     # encoder backward
     buckets = dp.GradBuckets([list(model.decoder.parameters()) + list(model.layers.parameters()),
-                              list(model.encoder.parameters())])
+                              list(model.encoder.parameters())], flat_views=cuda_graphs)
     buckets.broadcast_params()
+    acc = gradient_accumulate_every
 
+    def step_body(idx):
+        """Forward + backward of one iteration's micro-batches (idx: (acc, local batch) item indices);
+        the per-step statistics as one device tensor."""
+        total = 0.0
+        for micro in range(acc):
+            out = model(SeqBatch(None, None, None, items[idx[micro]], None, None), gumbel_t=0.2)
+            # shard mean -> global-batch mean under unequal shards (dp.shard_weight), / micro-batches
+            loss = out.loss * (w_shard / acc)
+            with (contextlib.nullcontext() if micro == acc - 1 else buckets.no_sync()):
+                loss.backward()
+            total = total + out.loss.detach() / acc
+        return torch.stack([total, out.reconstruction_loss.detach(), out.rqvae_loss.detach(),
+                            out.p_unique_ids.detach()])
+
+    graphed = GraphedSteps(step_body, lambda idx: 0, buckets, run_backward=False) if cuda_graphs else None
     gen = torch.Generator(device=device).manual_seed(seed + 17)   # same stream on every rank
     hist = []
     t0 = time.time()
+    last_it = start_iter + iterations
+    t_from = start_iter + min(5, iterations // 2)   # measured span: [t_from, last_it) (warm-up / captures before)
+    t_mark = None
     for it in range(start_iter, start_iter + 1 + iterations):
+        if it == t_from:
+            torch.cuda.synchronize()
+            t_mark = time.perf_counter()
         model.train()
-        buckets.zero_grad()
-        total = 0.0
-        for micro in range(gradient_accumulate_every):
-            idx = sample_batch_indices(gen, n_items, global_batch, device)[lo:hi]
-            out = model(SeqBatch(None, None, None, items[idx], None, None), gumbel_t=0.2)
-            # shard mean -> global-batch mean under unequal shards (dp.shard_weight), / micro-batches
-            loss = out.loss * (w_shard / gradient_accumulate_every)
-            last = micro == gradient_accumulate_every - 1
-            with (contextlib.nullcontext() if last else buckets.no_sync()):
-                loss.backward()
-            total = total + out.loss.detach() / gradient_accumulate_every
+        idx = torch.stack([sample_batch_indices(gen, n_items, global_batch, device)[lo:hi] for _ in range(acc)])
+        if graphed is not None:
+            stats = graphed(idx).clone()   # the graph's output buffer is rewritten by the next replay
+        else:
+            buckets.zero_grad()
+            stats = step_body(idx)
         buckets.synchronize()
         opt.step()
-        hist.append(torch.stack([total, out.reconstruction_loss.detach(), out.rqvae_loss.detach(),
-                                 out.p_unique_ids.detach()]))
+        hist.append(stats)
+        if it == last_it - 1 and t_mark is not None:
+            torch.cuda.synchronize()
+            LAST_RUN.update(iter_ms=(time.perf_counter() - t_mark) * 1e3 / max(1, last_it - t_from),
+                            timed_iters=last_it - t_from, batch_per_rank=hi - lo, world=world,
+                            step_mode="hipgraph" if graphed is not None else "eager",
+                            graphs=len(graphed.graphs) if graphed is not None else 0,
+                            eager_steps=graphed.eager_steps if graphed is not None else iterations + 1,
+                            exchange="in-graph" if graphed is not None and graphed.in_graph else "hooks + synchronize")
         if rank == 0 and (it % log_every == 0 or it == start_iter + iterations):
             vals = torch.stack(hist).mean(0).tolist()
             hist = []

@@ -6,7 +6,11 @@ gradient of the GLOBAL-batch mean loss — with equal shards, unequal shards (re
 dp.shard_weight), token-balanced variable-length shards (dp.balanced_partition) and gradient
 accumulation (no_sync on all but the last micro-batch); parameters unused on every rank keep
 grad None exactly as with one process, so AdamW steps give identical parameters at 1 and N ranks;
-corpus all-gather (dp.all_gather_rows).
+corpus all-gather (dp.all_gather_rows); the graphed step's in-graph exchange logic
+(rqvae_hip.graph.GraphedSteps with capture=False: the bodies that a GPU run captures, run eagerly, with
+the buckets' all-reduces launched from the hooks inside the body and finished at its end); a rank
+whose shard is empty (global batch < world) with buckets whose grad-ready order is not their index
+order (collectives must still be issued in the same order on every rank).
 """
 import os
 import socket
@@ -77,6 +81,10 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
         if mode == "grouped":   # parameter groups in grad-ready order (the bench's RQ-VAE layout)
             ps = list(model.parameters())
             buckets = dp.GradBuckets([ps[len(ps) // 2:][::-1], ps[:len(ps) // 2][::-1]], bucket_bytes=bucket_bytes)
+        elif mode == "empty":   # buckets in forward order: the last bucket's grads are ready first
+            buckets = dp.GradBuckets([list(model.parameters())], bucket_bytes=bucket_bytes)
+        elif mode == "graphed":
+            buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes, flat_views=True)
         else:
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
         buckets.broadcast_params()
@@ -84,9 +92,26 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
         x, lengths, toks = _data(gb)
         a, b = dp.shard_range(gb, r, w)
         mine = dp.balanced_partition(lengths, w)[r]
+        gs = None
+        if mode == "graphed":
+            from rqvae_hip.graph import GraphedSteps
+            gs = GraphedSteps(lambda xb: _loss(model, xb) * dp.shard_weight(b - a, gb), lambda xb: 0, buckets,
+                              capture=False, in_graph_exchange=True)
         for _ in range(2):                     # two steps: zero_grad must reset the flat buffers
+            if gs is not None:                 # step 1: eager probe; step 2: warm-ups + the in-body exchange
+                gs(x[a:b].clone())
+                assert gs.graphs or _ == 0
+                buckets.synchronize()
+                grads = {n: (None if p.grad is None else p.grad.detach().numpy().copy())
+                         for n, p in model.named_parameters()}
+                opt.step()
+                continue
             buckets.zero_grad()
-            if mode == "accum":                # two micro-batches: the global batch, then its reverse
+            if mode == "empty":
+                rows, lens = _seq_slice(toks, lengths, mine) if mine else (None, [])
+                if mine:
+                    (_seq_loss(model, rows, lens) * dp.shard_weight(len(mine), gb)).backward()
+            elif mode == "accum":                # two micro-batches: the global batch, then its reverse
                 for micro, xb in enumerate((x[a:b], x.flip(0)[a:b])):
                     loss = _loss(model, xb) * dp.shard_weight(b - a, gb) / 2
                     if micro == 0:
@@ -137,7 +162,7 @@ def _single_process(state0, gb, mode, world):
         opt.zero_grad(set_to_none=True)
         if mode == "accum":
             ((_loss(model, x) + _loss(model, x.flip(0))) / 2).backward()
-        elif mode == "tokens":
+        elif mode in ("tokens", "empty"):
             _seq_loss(model, toks, lengths).backward()
         else:
             _loss(model, x).backward()
@@ -152,10 +177,14 @@ def _single_process(state0, gb, mode, world):
     (2, 63, 1 << 20, "grouped"),    # unequal shards, grouped buckets
     (2, 64, 1 << 20, "accum"),      # gradient accumulation with no_sync
     (3, 61, 4096, "tokens"),        # token-balanced variable-length shards (unequal sequence counts)
+    (3, 2, 2048, "empty"),          # global batch < world: rank 2 has no sequences, several buckets
+    (2, 64, 2048, "graphed"),       # GraphedSteps bodies with the in-graph exchange (run eagerly)
 ])
 def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode):
     res = _run(world, gb, bucket_bytes, mode)
-    if mode != "tokens":   # contiguous shards: disjoint, cover the global batch
+    if mode == "empty":
+        assert [len(r[5]) for r in res] == [1, 1, 0]
+    if mode not in ("tokens", "empty"):   # contiguous shards: disjoint, cover the global batch
         spans = [r[1] for r in res]
         assert spans[0][0] == 0 and spans[-1][1] == gb and all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
     else:                  # token-balanced shards: a partition of the sequences
@@ -163,6 +192,9 @@ def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode
         assert allidx == list(range(gb))
     if bucket_bytes == 2048:
         assert res[0][4] > 1, "expected several buckets"
+    if mode == "empty":
+        allidx = sorted(i for r in res for i in r[5])
+        assert allidx == list(range(gb))
     # rank-0 broadcast + identical updates: parameters identical on all ranks after 2 AdamW steps
     for r in res[1:]:
         for n in r[2]:
@@ -177,7 +209,8 @@ def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode
         if ref is None:   # unused everywhere: grad None at N ranks as at 1 (AdamW skips it)
             assert got is None, n
             continue
-        assert torch.allclose(torch.from_numpy(got), ref, rtol=2e-5, atol=1e-7), n
+        # 'empty': two 1-sequence shards summed with a zero shard and rescaled (fp32 rounding ~1e-7)
+        assert torch.allclose(torch.from_numpy(got), ref, rtol=2e-5, atol=1e-6 if mode == "empty" else 1e-7), n
         for r in res[1:]:
             assert np.array_equal(r[3][n], got)
         assert np.allclose(res[0][2][n], p.detach().numpy(), rtol=1e-5, atol=1e-6), f"params {n}"

@@ -168,10 +168,18 @@ def test_backward_vs_oracle_and_determinism(device):
 def test_unique_count(device):
     from rqvae_hip import ops
     g = gi.rng(3)
-    for B, L, K in [(1, 3, 256), (5000, 3, 4), (65536, 3, 256), (20000, 4, 2048)]:
+    # byte-map path (K^L <= 2^24 and B large), hash path (small B or large K^L), both edges
+    for B, L, K in [(1, 3, 256), (5000, 3, 4), (65536, 3, 256), (32768, 3, 256), (4096, 3, 256), (20000, 4, 2048)]:
         ids = g.integers(0, K, size=(B, L))
         got = int(ops.unique_count(torch.from_numpy(ids).to(device), K))
         assert got == np.unique(ids, axis=0).shape[0]
+    # ids outside [0, K) on the byte-map path: no out-of-bounds store; each such row counts once
+    ids = g.integers(0, 256, size=(65536, 3))
+    ids[::1000, 1] = 256 + np.arange(ids[::1000].shape[0])
+    ids[5::1000, 2] = -1
+    bad = (ids < 0).any(1) | (ids >= 256).any(1)
+    got = int(ops.unique_count(torch.from_numpy(ids).to(device), 256))
+    assert got == np.unique(ids[~bad], axis=0).shape[0] + int(bad.sum())
 
 
 @pytest.mark.parametrize("B,D,K,L", [(40000, 64, 256, 3), (5000, 64, 256, 3), (1000, 128, 300, 2), (0, 64, 256, 3)])

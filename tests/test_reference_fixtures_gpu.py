@@ -155,7 +155,8 @@ def test_reference_checkpoint_resumes(golden, device):
 # ------------------------------------------------------------------------------------------ C1
 def test_train_rqvae_loss_trace_vs_reference(golden, device, monkeypatch, capsys, tmp_path):
     """25 steps of this build's train_rqvae.train() (Amazon dims, ROTATION_TRICK, AdamW, fused HIP
-    quantize, HIP AdamW) on the reference's batch order, initial MLP weights and post-k-means
+    quantize, HIP AdamW; its default hipGraph step: one eager probe step, then replays) on the reference's
+    batch order, initial MLP weights and post-k-means
     codebooks: the per-step loss / reconstruction / quantize losses and p_unique_ids track the
     reference's own train() (train_rqvae.py:135-157). This build's k-means (same np.random draws)
     is checked against the reference's codebooks separately (it runs the GPU distance kernel, so
@@ -207,6 +208,9 @@ def test_train_rqvae_loss_trace_vs_reference(golden, device, monkeypatch, capsys
              do_eval=True, save_dir_root=str(tmp_path) + "/", eval_every=10 ** 9, save_model_every=10 ** 9,
              log_every=1, seed=int(z["seed"]))
     assert calls["n"] == n_steps
+    # the drop-in trainer's default path: one eager probe step, then every step replayed from one graph
+    assert tr.LAST_RUN["step_mode"] == "hipgraph" and tr.LAST_RUN["graphs"] == 1, tr.LAST_RUN
+    assert tr.LAST_RUN["eager_steps"] == 1, tr.LAST_RUN
     lines = [json.loads(l) for l in capsys.readouterr().out.splitlines() if l.startswith('{"iter"')]
     steps = [l for l in lines if "loss" in l]
     assert len(steps) == n_steps

@@ -1,8 +1,10 @@
 """Next-rows on the GPU: corpus tokenizer + dedup, k-means codebook init, generation.
 
-Tokenizer and k-means are pinned by reference fixtures (tokenizer.npz, kmeans.npz); generation
-samples with torch.multinomial, whose GPU stream differs from the reference's, so it is checked
-by properties only (parity unpinned for the sampled tuples)."""
+Tokenizer and k-means are pinned by reference fixtures (tokenizer.npz, kmeans.npz). Generation is
+pinned against the reference in tests/test_reference_fixtures_gpu.py::test_generation_vs_reference
+(generation.npz, a deterministic sampler patched into both sides); here it is additionally checked
+for its structural properties with the real torch.multinomial sampler (beam shapes, sorted beams,
+train mode and the encoder cache restored)."""
 import numpy as np
 import pytest
 import torch
@@ -122,10 +124,11 @@ def test_generation_properties(golden, device):
                                          num_embeddings=max(K, 2000), sem_id_dim=L1,
                                          inference_verifier_fn=lambda x: tok.exists_prefix(x), max_pos=20 * L1).to(device)
     model.enable_generation = True
+    assert model.training
     batch = synthetic_tokenized_batch(3, 5, L1, K, 7, device)
     out = model.generate_next_sem_id(batch, top_k=True, temperature=1)
     assert out.sem_ids.shape == (3, 32, L1) and out.log_probas.shape == (3, 32)
     lp = out.log_probas.cpu()
     assert torch.all(lp[:, :-1] >= lp[:, 1:]), "beams sorted by cumulative log-probability"
-    assert model.training is False or True   # eval_mode restores the previous mode
+    assert model.training, "eval_mode restores the previous (train) mode"
     assert model.transformer.cached_enc_output is None

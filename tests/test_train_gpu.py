@@ -1,5 +1,6 @@
 """Drop-in training entry points (train_rqvae.train / train_decoder.train) run end to end on the GPU
-with the reference configs' shapes (few iterations), incl. k-means init, eval, checkpoint + resume."""
+with the reference configs' shapes (few iterations), incl. k-means init, eval, checkpoint + resume; their
+default hipGraph step (rqvae_hip.graph.GraphedSteps) against the eager step (cuda_graphs=False)."""
 import glob
 
 import pytest
@@ -49,3 +50,67 @@ def test_train_decoder_small(tmp_path, device):
                             attn_embed_dim=128, attn_layers=4, save_dir_root=str(tmp_path) + "/", log_every=2, **vae)
     assert m.sem_id_embedder.emb.weight.grad is not None
     assert glob.glob(str(tmp_path / "checkpoint_*.pt"))
+
+
+def _trace(capsys):
+    import json
+    return [json.loads(l) for l in capsys.readouterr().out.splitlines() if l.startswith('{"iter"') and '"loss"' in l]
+
+
+def test_train_rqvae_graphed_matches_eager(tmp_path, device, capsys):
+    """The graphed trainer replays the same kernels as the eager one: identical per-step losses."""
+    import numpy as np
+    import train_rqvae
+    from data.processed import RecDataset
+    from modules.quantize import QuantizeForwardMode
+    kw = dict(iterations=12, batch_size=64, learning_rate=0.0005, dataset=RecDataset.AMAZON, vae_input_dim=768,
+              vae_n_cat_feats=0, vae_hidden_dims=[512, 256, 128], vae_embed_dim=32, vae_codebook_size=256,
+              vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK, vae_n_layers=3, do_eval=False,
+              save_dir_root=str(tmp_path) + "/", save_model_every=10 ** 9, log_every=1, seed=3)
+    traces = {}
+    for graphs in (False, True):
+        np.random.seed(0)
+        capsys.readouterr()
+        train_rqvae.train(cuda_graphs=graphs, **kw)
+        traces[graphs] = _trace(capsys)
+        run = dict(train_rqvae.LAST_RUN)
+        assert run["step_mode"] == ("hipgraph" if graphs else "eager")
+        if graphs:
+            assert run["graphs"] == 1 and run["eager_steps"] == 1, run
+    assert len(traces[True]) == len(traces[False]) == 13
+    for a, b in zip(traces[False], traces[True]):
+        for k in ("loss", "rl", "vl", "p_unique_ids"):
+            assert a[k] == pytest.approx(b[k], rel=1e-6, abs=1e-9), (k, a, b)
+
+
+def test_train_decoder_graphed(tmp_path, device, capsys):
+    """The graphed decoder trainer: one graph per context row bucket, finite losses, gradients in the
+    flat buckets; its first (eager probe) step equals the eager trainer's first step."""
+    import numpy as np
+    import train_decoder
+    import train_rqvae
+    from data.processed import RecDataset
+    from modules.quantize import QuantizeForwardMode
+    vae = dict(vae_input_dim=768, vae_embed_dim=32, vae_hidden_dims=[512, 256, 128], vae_codebook_size=256,
+               vae_n_cat_feats=0, vae_n_layers=3)
+    np.random.seed(1)
+    train_rqvae.train(iterations=10, batch_size=256, dataset=RecDataset.AMAZON, do_eval=False, save_model_every=10,
+                      vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK, save_dir_root=str(tmp_path / "vae") + "/",
+                      **vae)
+    ckpt = sorted(glob.glob(str(tmp_path / "vae" / "checkpoint_*.pt")))[-1]
+    kw = dict(iterations=8, batch_size=32, learning_rate=0.0003, dataset=RecDataset.AMAZON, pretrained_rqvae_path=ckpt,
+              decoder_embed_dim=64, dropout_p=0.3, attn_heads=4, attn_embed_dim=128, attn_layers=4,
+              save_dir_root=str(tmp_path) + "/", save_model_every=10 ** 9, log_every=1, **vae)
+    traces = {}
+    for graphs in (False, True):
+        capsys.readouterr()
+        train_decoder.train(cuda_graphs=graphs, **kw)
+        traces[graphs] = _trace(capsys)
+        run = dict(train_decoder.LAST_RUN)
+        assert run["step_mode"] == ("hipgraph" if graphs else "eager")
+        if graphs:
+            assert run["graphs"] >= 1 and run["eager_steps"] == 1, run
+    assert len(traces[True]) == len(traces[False]) == 8
+    assert all(np.isfinite(t["loss"]) for t in traces[True])
+    # step 0 is eager in both modes (same seed, same batch, same dropout keys)
+    assert traces[True][0]["loss"] == pytest.approx(traces[False][0]["loss"], rel=1e-6)

@@ -51,6 +51,12 @@ for s in $steps; do
         python3 "$R/bench.py" --decoder-only > "$O/prof_decoder.json" 2> "$O/prof_decoder.err"
       cd "$R"
       cat "$O/prof_decoder.json" ;;
+    profdm8)   # C4 per-rank config: ML-32M decoder, 8 sequences per GPU
+      cd /tmp
+      run prof_dm8 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o dm8 -- \
+        python3 "$R/bench.py" --decoder-only --dm-batch 8 > "$O/prof_dm8.json" 2> "$O/prof_dm8.err"
+      cd "$R"
+      cat "$O/prof_dm8.json" ;;
     sqpmc)
       cd /tmp
       run pmc_sq 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \
