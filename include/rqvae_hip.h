@@ -205,6 +205,9 @@ int rq_gemm_x3w_enable(int enable);
 /* 64 x 64-tile form of the 128-tile kernel: 0 never, 1 (default unless RQ_X3S=0/2 is set) where the
  * time model prefers it, 2 forced wherever the 128-tile kernel would run. Returns the previous mode. */
 int rq_gemm_x3s_enable(int mode);
+/* LDS-DMA staged short attention forms (key ranges <= 128 rows, head dim 64): 1 (default unless
+ * RQ_ATTN_DMA=0 is set) on, 0 off (the register-staged kernels). Returns the previous setting. A/B switch. */
+int rq_attn_dma_enable(int enable);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
 /* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device
@@ -283,17 +286,14 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream);
-/* varlen_attn_fwd with a caller-provided int scratch `order` of B entries (may be NULL): for long ranges
- * (max_k > 128, 2 <= B <= 4096) the launch first ranks the sequences longest-first into it and the
- * kernel dispatches their workgroups in that order (no straggler tail); results are identical. */
-int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
-                     void* stream);
-/* varlen_attn_fwd2 with one float scratch `ws` of varlen_attn_fwd_ws_elems(...) floats: the LPT order
- * (B ints, padded to 16 B) and, for <= 16 queries per sequence over > 128 keys (non-causal: the decoder's
- * cross-attention), split-key partials — one one-wave workgroup per 128-key block, merged per query in
- * block order by a combine launch (deterministic). */
+/* varlen_attn_fwd with one float scratch `ws` of varlen_attn_fwd_ws_elems(...) floats (the product's entry,
+ * rqvae_hip/ops.py): for long ranges (max_k > 128, 2 <= B <= 4096) the launch first ranks the sequences
+ * longest-first into ws (B ints, padded to 16 B) and dispatches their workgroups in that order (no straggler
+ * tail), and for <= 16 queries per sequence over > 128 keys (non-causal: the decoder's cross-attention) it
+ * runs split-key partials in ws — one one-wave workgroup per 128-key block, merged per query in block order
+ * by a combine launch (deterministic). Same results as varlen_attn_fwd within fp32 summation order;
+ * varlen_attn_fwd itself (no scratch) is tested against the oracle at the same shapes
+ * (tests/test_jagged_attention_gpu.py::test_c_abi_entry_points_vs_oracle). */
 int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
                              int64_t* elems);
 int varlen_attn_fwd3(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
@@ -311,7 +311,7 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
  * sequences longer than one key block is summed from per-block partials in block order by a reduction
  * launch (deterministic, no atomics). ws: caller-provided scratch of at least
  * varlen_attn_bwd_ws_elems(...) floats (0 -> ws may be NULL; it also holds the longest-first sequence
- * order of the fused launch, as varlen_attn_fwd2). Other shapes run varlen_attn_bwd. */
+ * order of the fused launch, as varlen_attn_fwd3). Other shapes run varlen_attn_bwd. */
 int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
                              int64_t* elems);
 int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,

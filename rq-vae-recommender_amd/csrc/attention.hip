@@ -1106,6 +1106,672 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_short_kernel(
   }
 }
 
+// ----------------------------------------------------------- LDS-DMA staged short forms (HD = 64)
+// One workgroup of NW waves per (sequence, head) whose key range (forward) fits R <= 128 rows: the
+// head's K and V rows go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
+// staging VALU, every row of the head in flight at once), one wait + barrier, then each wave runs its
+// 16-query tiles (w, w + NW, ...) against ALL key tiles in one pass: the whole S^T row block of a query
+// tile stays in registers, so its max and sum are exact (no running rescale of O).
+// LDS image: a row of 64 fp32 (256 B = 16 chunks of 16 B) per key, no padding; chunk c of row r sits at
+// position c ^ swz(r) (the XOR goes on each DMA lane's SOURCE address, the LDS side of a DMA is
+// lane-linear: lane L of an instruction writes position L & 15 of row 4j + (L >> 4)). swz keeps both
+// fragment reads conflict-free (checked per ds_read_b128 lane group):
+//   K pattern  S^T = K Q^T:  lane (row = lane & 15, chunk = 4 (lane >> 4) + s), s = 0..3
+//   V pattern  O^T += V^T P^T: lane (row = 4 (lane >> 4) + i, chunk = lane & 15),  i = 0..3
+// The V product runs over a PERMUTED d: accumulator tile dt, row m holds d = 4 m + dt, so one
+// ds_read_b128 of V[key][4m .. 4m+3] feeds the 4 output tiles; each lane then owns the 16 contiguous
+// d = 16 (lane >> 4) + 4 i + dt of its query — whole float4 stores.
+// Rows past the sequence read its last row (finite data: masked keys get P = 0; never read past it).
+__device__ __forceinline__ int swz16(int r) {
+  r &= 15;
+  return r ^ ((((r >> 2) ^ (r >> 3)) & 1) << 2);
+}
+
+__device__ __forceinline__ void glds16f(const float* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// DMA rows [0, 16 nt) of two strided row sources (rows >= n read row n - 1) into two swizzled LDS images,
+// instruction j (4 rows) by wave j % NW.
+template <int NW>
+__device__ __forceinline__ void dma_rows2(const float* __restrict__ a, int64_t sa, const float* __restrict__ b,
+                                          int64_t sb, int n, int nt, char* da, char* db, int wave, int lane) {
+  const int ninstr = 4 * nt;
+  for (int j = wave; j < ninstr; j += NW) {
+    const int r = 4 * j + (lane >> 4);
+    const int64_t rr = min(r, n - 1);
+    const int c = (lane & 15) ^ swz16(r);
+    glds16f(a + rr * sa + 4 * c, da + j * 1024);
+    glds16f(b + rr * sb + 4 * c, db + j * 1024);
+  }
+}
+
+// float4 at chunk c of image row r
+__device__ __forceinline__ float4 lds_chunk(const char* img, int r, int c) {
+  return *reinterpret_cast<const float4*>(img + r * 256 + ((c ^ swz16(r)) << 4));
+}
+
+// One query tile of the DMA forward against its N key tiles (compile-time N: every array in registers).
+template <int N>
+__device__ __forceinline__ void fwd_dma_tile(const char* K_s, const char* V_s, const float (&qf)[16], int lane, int lk,
+                                             int qi, int causal, float sl2, f32x4 (&o)[4], float& mn_out, float& l_out) {
+  const int g = lane >> 4;
+  f32x4 st[N];
+#pragma unroll
+  for (int t = 0; t < N; ++t) st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // S^T (keys on rows): N independent MFMA chains
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    float4 a[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) a[t] = lds_chunk(K_s, t * 16 + (lane & 15), 4 * g + s4);
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+      st[t] = mfma4(a[t].x, qf[4 * s4], st[t]);
+      st[t] = mfma4(a[t].y, qf[4 * s4 + 1], st[t]);
+      st[t] = mfma4(a[t].z, qf[4 * s4 + 2], st[t]);
+      st[t] = mfma4(a[t].w, qf[4 * s4 + 3], st[t]);
+    }
+  }
+  // exact row max / sum over every key of the query (keys >= lk, causal keys > query: masked)
+  float mt = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = t * 16 + 4 * g + i;
+      if (!(key < lk && (!causal || key <= qi))) st[t][i] = -INFINITY;
+      mt = fmaxf(mt, st[t][i]);
+    }
+  mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+  mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+  const float mn = mt * sl2;
+  const bool none = mn == -INFINITY;          // no key (padding query rows, empty key range)
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      st[t][i] = none ? 0.f : exp2_fast(__builtin_fmaf(st[t][i], sl2, -mn));
+      l += st[t][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {             // O^T += V^T P^T, d permuted
+      const float4 vv = lds_chunk(V_s, t * 16 + 4 * g + i, lane & 15);
+      o[0] = mfma4(vv.x, st[t][i], o[0]);
+      o[1] = mfma4(vv.y, st[t][i], o[1]);
+      o[2] = mfma4(vv.z, st[t][i], o[2]);
+      o[3] = mfma4(vv.w, st[t][i], o[3]);
+    }
+  }
+  mn_out = mn;
+  l_out = l;
+}
+
+template <int NW, int R>
+__global__ void __launch_bounds__(64 * NW, R <= 64 ? 4 : 3) attn_fwd_dma_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
+  constexpr int HD = 64, NKT = R / 16;
+  static_assert(R % 16 == 0 && R <= 128, "staged rows");
+  __shared__ __attribute__((aligned(16))) char lds[2 * R * 256];
+  char* K_s = lds;
+  char* V_s = lds + R * 256;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
+    zero_rows<HD, 64 * NW>(out, so, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  const int nkt_all = min((lk + 15) >> 4, NKT);   // lk <= max_k <= R by the plan; never stage past the image
+  if (lk > 0) dma_rows2<NW>(k + k0 * sk + hh * HD, sk, v + k0 * sv + hh * HD, sv, lk, nkt_all, K_s, V_s, wave, lane);
+  const float sl2 = scale * kLog2e;
+  const int nqt = (lq + 15) >> 4;
+  float qf[HD / 4];
+  if (wave < nqt) {   // the first tile's Q rows fly with the DMAs
+    const int qi = wave * 16 + (lane & 15);
+    load_frag<HD>(q + (q0 + (qi < lq ? qi : 0)) * sq + hh * HD + g * (HD / 4), qi < lq, qf);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs (and Q) landed
+  __syncthreads();                                     // ... and every other wave's
+  for (int qt = wave; qt < nqt; qt += NW) {
+    const int qb = qt * 16, qi = qb + (lane & 15);
+    const bool qv = qi < lq;
+    if (qt != wave) load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+    const int kend = causal ? min(lk, qb + 16) : lk;
+    const int nkt = __builtin_amdgcn_readfirstlane(min((kend + 15) >> 4, NKT));
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float mn = -INFINITY, l = 0.f;
+    switch (nkt) {
+      case 1: fwd_dma_tile<1>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 2: if constexpr (NKT >= 2) fwd_dma_tile<2>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 3: if constexpr (NKT >= 3) fwd_dma_tile<3>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 4: if constexpr (NKT >= 4) fwd_dma_tile<4>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 5: if constexpr (NKT >= 5) fwd_dma_tile<5>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 6: if constexpr (NKT >= 6) fwd_dma_tile<6>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 7: if constexpr (NKT >= 7) fwd_dma_tile<7>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      case 8: if constexpr (NKT >= 8) fwd_dma_tile<8>(K_s, V_s, qf, lane, lk, qi, causal, sl2, o, mn, l); break;
+      default: break;                         // no key: zero output, lse 0
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qv) {
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      float* orow = out + (q0 + qi) * so + hh * HD + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(orow + 4 * i) = make_float4(o[0][i] * inv, o[1][i] * inv, o[2][i] * inv, o[3][i] * inv);
+      if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (mn + log2f(l)) * kLn2 : 0.f;
+    }
+  }
+}
+
+// dQ of one query tile against its N key tiles (DMA images of K and V): S^T and dP^T = V dO^T per key
+// tile (K pattern), P from the saved lse, dS^T = P (dP^T - delta), dQ^T += K^T dS^T (V pattern, d permuted).
+template <int N>
+__device__ __forceinline__ void dq_dma_tile(const char* K_s, const char* V_s, const float (&qf)[16],
+                                            const float (&dof)[16], int lane, int lk, int qi, int causal, float sl2,
+                                            float lse2, float delta, f32x4 (&acc)[4]) {
+  const int g = lane >> 4;
+  f32x4 st[N], dp[N];
+#pragma unroll
+  for (int t = 0; t < N; ++t) { st[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    float4 a[N], c[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+      a[t] = lds_chunk(K_s, t * 16 + (lane & 15), 4 * g + s4);
+      c[t] = lds_chunk(V_s, t * 16 + (lane & 15), 4 * g + s4);
+    }
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+      st[t] = mfma4(a[t].x, qf[4 * s4], st[t]);
+      dp[t] = mfma4(c[t].x, dof[4 * s4], dp[t]);
+      st[t] = mfma4(a[t].y, qf[4 * s4 + 1], st[t]);
+      dp[t] = mfma4(c[t].y, dof[4 * s4 + 1], dp[t]);
+      st[t] = mfma4(a[t].z, qf[4 * s4 + 2], st[t]);
+      dp[t] = mfma4(c[t].z, dof[4 * s4 + 2], dp[t]);
+      st[t] = mfma4(a[t].w, qf[4 * s4 + 3], st[t]);
+      dp[t] = mfma4(c[t].w, dof[4 * s4 + 3], dp[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = t * 16 + 4 * g + i;
+      float p = exp2_fast(__builtin_fmaf(st[t][i], sl2, -lse2));
+      if (!(key < lk && (!causal || key <= qi))) p = 0.f;
+      st[t][i] = p * (dp[t][i] - delta);      // dS^T
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {             // dQ^T += K^T dS^T
+      const float4 kk = lds_chunk(K_s, t * 16 + 4 * g + i, lane & 15);
+      acc[0] = mfma4(kk.x, st[t][i], acc[0]);
+      acc[1] = mfma4(kk.y, st[t][i], acc[1]);
+      acc[2] = mfma4(kk.z, st[t][i], acc[2]);
+      acc[3] = mfma4(kk.w, st[t][i], acc[3]);
+    }
+  }
+}
+
+// dQ (+ delta = rowsum(dO * O), saved for the dK/dV pass): one workgroup per (sequence, head), K / V by
+// LDS-DMA, waves over 16-query tiles against every key tile.
+template <int NW, int R>
+__global__ void __launch_bounds__(64 * NW, R <= 64 ? 4 : 3) attn_bwd_dq_dma_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
+    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ delta_out) {
+  constexpr int HD = 64, NKT = R / 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * R * 256];
+  char* K_s = lds;
+  char* V_s = lds + R * 256;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  const int nkt_all = min((lk + 15) >> 4, NKT);
+  if (lk > 0) dma_rows2<NW>(k + k0 * sk + hh * HD, sk, v + k0 * sv + hh * HD, sv, lk, nkt_all, K_s, V_s, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float sl2 = scale * kLog2e;
+  const int nqt = (lq + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += NW) {
+    const int qb = qt * 16, qi = qb + (lane & 15);
+    const bool qv = qi < lq;
+    const int64_t qrow = q0 + (qv ? qi : 0);
+    float qf[HD / 4], dof[HD / 4];
+    load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv, qf);
+    load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv, dof);
+    float delta = 0.f;
+    {
+      float of[HD / 4];
+      load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+#pragma unroll
+      for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+      delta += __shfl_xor(delta, 16, 64);
+      delta += __shfl_xor(delta, 32, 64);
+      if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
+    }
+    const float lse2 = qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f;
+    const int kend = causal ? min(lk, qb + 16) : lk;
+    const int nkt = __builtin_amdgcn_readfirstlane(min((kend + 15) >> 4, NKT));
+    f32x4 acc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    switch (nkt) {
+      case 1: dq_dma_tile<1>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 2: if constexpr (NKT >= 2) dq_dma_tile<2>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 3: if constexpr (NKT >= 3) dq_dma_tile<3>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 4: if constexpr (NKT >= 4) dq_dma_tile<4>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 5: if constexpr (NKT >= 5) dq_dma_tile<5>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 6: if constexpr (NKT >= 6) dq_dma_tile<6>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 7: if constexpr (NKT >= 7) dq_dma_tile<7>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      case 8: if constexpr (NKT >= 8) dq_dma_tile<8>(K_s, V_s, qf, dof, lane, lk, qi, causal, sl2, lse2, delta, acc); break;
+      default: break;
+    }
+    if (qv) {
+      float* row = dq + (q0 + qi) * sdq + hh * HD + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(row + 4 * i) =
+            make_float4(acc[0][i] * scale, acc[1][i] * scale, acc[2][i] * scale, acc[3][i] * scale);
+    }
+  }
+}
+
+// dK, dV of one key tile against its N query tiles (DMA images of Q and dO; lse / delta per query in LDS):
+// S = Q K^T, dP = dO V^T (queries on rows, K pattern), P, dS = P (dP - delta), dV^T += dO^T P and
+// dK^T += Q^T dS (V pattern, d permuted). Query tiles [t0, t0 + N).
+template <int N>
+__device__ __forceinline__ void dkdv_dma_tile(const char* Q_s, const char* O_s, const float* lse_s, const float* dl_s,
+                                              const float (&kf)[16], const float (&vf)[16], int lane, int t0, int lq,
+                                              int kj, int causal, float sl2, f32x4 (&dka)[4], f32x4 (&dva)[4]) {
+  const int g = lane >> 4;
+  f32x4 st[N], dp[N];
+#pragma unroll
+  for (int t = 0; t < N; ++t) { st[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    float4 a[N], c[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+      a[t] = lds_chunk(Q_s, (t0 + t) * 16 + (lane & 15), 4 * g + s4);
+      c[t] = lds_chunk(O_s, (t0 + t) * 16 + (lane & 15), 4 * g + s4);
+    }
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+      st[t] = mfma4(a[t].x, kf[4 * s4], st[t]);
+      dp[t] = mfma4(c[t].x, vf[4 * s4], dp[t]);
+      st[t] = mfma4(a[t].y, kf[4 * s4 + 1], st[t]);
+      dp[t] = mfma4(c[t].y, vf[4 * s4 + 1], dp[t]);
+      st[t] = mfma4(a[t].z, kf[4 * s4 + 2], st[t]);
+      dp[t] = mfma4(c[t].z, vf[4 * s4 + 2], dp[t]);
+      st[t] = mfma4(a[t].w, kf[4 * s4 + 3], st[t]);
+      dp[t] = mfma4(c[t].w, vf[4 * s4 + 3], dp[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int qr = (t0 + t) * 16 + 4 * g + i;
+      float p = exp2_fast(__builtin_fmaf(st[t][i], sl2, -lse_s[qr]));
+      if (!(qr < lq && (!causal || kj <= qr))) p = 0.f;
+      st[t][i] = p;
+      dp[t][i] = p * (dp[t][i] - dl_s[qr]);   // dS
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (t0 + t) * 16 + 4 * g + i;
+      const float4 oo = lds_chunk(O_s, r, lane & 15);   // dV^T += dO^T P
+      dva[0] = mfma4(oo.x, st[t][i], dva[0]);
+      dva[1] = mfma4(oo.y, st[t][i], dva[1]);
+      dva[2] = mfma4(oo.z, st[t][i], dva[2]);
+      dva[3] = mfma4(oo.w, st[t][i], dva[3]);
+      const float4 qq = lds_chunk(Q_s, r, lane & 15);   // dK^T += Q^T dS
+      dka[0] = mfma4(qq.x, dp[t][i], dka[0]);
+      dka[1] = mfma4(qq.y, dp[t][i], dka[1]);
+      dka[2] = mfma4(qq.z, dp[t][i], dka[2]);
+      dka[3] = mfma4(qq.w, dp[t][i], dka[3]);
+    }
+  }
+}
+
+template <int NW, int R>
+__global__ void __launch_bounds__(64 * NW, R <= 64 ? 4 : 3) attn_bwd_dkdv_dma_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
+    const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dk, int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk) {
+  constexpr int HD = 64, NQT = R / 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * R * 256];
+  __shared__ float lse_s[R], dl_s[R];
+  char* Q_s = lds;
+  char* O_s = lds + R * 256;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[b], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[b], Tk, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lk <= 0) return;
+  const int nqt_all = min((lq + 15) >> 4, NQT);
+  if (lq > 0) dma_rows2<NW>(q + q0 * sq + hh * HD, sq, dout + q0 * sdo + hh * HD, sdo, lq, nqt_all, Q_s, O_s, wave, lane);
+  for (int r = tid; r < R; r += 64 * NW) {
+    const bool ok = r < lq;
+    lse_s[r] = ok ? lse[(int64_t)hh * Tq + q0 + r] * kLog2e : 0.f;
+    dl_s[r] = ok ? delta[(int64_t)hh * Tq + q0 + r] : 0.f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float sl2 = scale * kLog2e;
+  for (int kt = wave; kt * 16 < lk; kt += NW) {
+    const int kb = kt * 16, kj = kb + (lane & 15);
+    const bool kvv = kj < lk;
+    const int64_t krow = k0 + (kvv ? kj : 0);
+    float kf[HD / 4], vf[HD / 4];
+    load_frag<HD>(k + krow * sk + hh * HD + g * (HD / 4), kvv, kf);
+    load_frag<HD>(v + krow * sv + hh * HD + g * (HD / 4), kvv, vf);
+    f32x4 dka[4], dva[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    const int t0 = __builtin_amdgcn_readfirstlane(causal ? min(kb >> 4, nqt_all) : 0);   // query tiles wholly before the keys
+    const int nt = __builtin_amdgcn_readfirstlane(nqt_all - t0);
+    switch (nt) {
+      case 1: dkdv_dma_tile<1>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 2: if constexpr (NQT >= 2) dkdv_dma_tile<2>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 3: if constexpr (NQT >= 3) dkdv_dma_tile<3>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 4: if constexpr (NQT >= 4) dkdv_dma_tile<4>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 5: if constexpr (NQT >= 5) dkdv_dma_tile<5>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 6: if constexpr (NQT >= 6) dkdv_dma_tile<6>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 7: if constexpr (NQT >= 7) dkdv_dma_tile<7>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      case 8: if constexpr (NQT >= 8) dkdv_dma_tile<8>(Q_s, O_s, lse_s, dl_s, kf, vf, lane, t0, lq, kj, causal, sl2, dka, dva); break;
+      default: break;
+    }
+    if (kvv) {
+      float* rk = dk + (k0 + kj) * sdk + hh * HD + 16 * g;
+      float* rv = dv + (k0 + kj) * sdv + hh * HD + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        *reinterpret_cast<float4*>(rk + 4 * i) =
+            make_float4(dka[0][i] * scale, dka[1][i] * scale, dka[2][i] * scale, dka[3][i] * scale);
+        *reinterpret_cast<float4*>(rv + 4 * i) = make_float4(dva[0][i], dva[1][i], dva[2][i], dva[3][i]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------- few queries over a short key range (HD = 64)
+// One query tile per (sequence, head) (the decoder's cross-attention: 5-6 future tokens over <= 128
+// context keys; its causal self-attention over 5-6 tokens): the key tiles are split over the NW waves of
+// the workgroup (wave w: tiles w, w + NW, ...) so each wave issues all the loads of its one or two tiles
+// at once, straight into registers in the two fragment layouts (K pattern for S^T, permuted-d V pattern
+// for the O^T product: no LDS staging, no reuse to stage for), and the waves' partial (m, l, O) — or dQ —
+// merge through LDS in wave order (deterministic).
+// Register fragments of key tile t of a strided row source (rows >= lk read row lk - 1):
+//   K pattern: row t*16 + (lane & 15), d = 16 (lane >> 4) + 0..15
+//   V pattern: rows t*16 + 4 (lane >> 4) + i, d = 4 (lane & 15) + 0..3   (permuted-d products)
+__device__ __forceinline__ void frag_kpat(const float* __restrict__ base, int64_t stride, int t, int lk, int lane,
+                                          float4 (&f)[4]) {
+  const int rk = min(t * 16 + (lane & 15), lk - 1);
+  const float* p = base + (int64_t)rk * stride + 16 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = *reinterpret_cast<const float4*>(p + 4 * j);
+}
+__device__ __forceinline__ void frag_vpat(const float* __restrict__ base, int64_t stride, int t, int lk, int lane,
+                                          float4 (&f)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rv = min(t * 16 + 4 * (lane >> 4) + i, lk - 1);
+    f[i] = *reinterpret_cast<const float4*>(base + (int64_t)rv * stride + 4 * (lane & 15));
+  }
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_fewq_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
+  constexpr int HD = 64, TPW = 2;   // key tiles per wave (<= 128 keys over 4 waves)
+  __shared__ __attribute__((aligned(16))) float part_o[NW][16][HD];
+  __shared__ float part_m[NW][16], part_l[NW][16];
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(out, so, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  const int qi = lane & 15;
+  const bool qv = qi < lq;
+  const int kend = causal ? min(lk, 16) : lk;
+  const int nkt = (kend + 15) >> 4;
+  float qf[HD / 4];
+  load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  float4 kp[TPW][4], vp[TPW][4];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    if (t < nkt) {
+      frag_kpat(kb_, sk, t, lk, lane, kp[j]);
+      frag_vpat(vb_, sv, t, lk, lane, vp[j]);
+    }
+  }
+  const float sl2 = scale * kLog2e;
+  f32x4 st[TPW];
+  float mt = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    st[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (t < nkt) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        st[j] = mfma4(kp[j][s4].x, qf[4 * s4], st[j]);
+        st[j] = mfma4(kp[j][s4].y, qf[4 * s4 + 1], st[j]);
+        st[j] = mfma4(kp[j][s4].z, qf[4 * s4 + 2], st[j]);
+        st[j] = mfma4(kp[j][s4].w, qf[4 * s4 + 3], st[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = t * 16 + 4 * g + i;
+        if (!(key < lk && (!causal || key <= qi))) st[j][i] = -INFINITY;
+        mt = fmaxf(mt, st[j][i]);
+      }
+    }
+  }
+  mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+  mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+  const float mn = mt * sl2;
+  const bool none = mn == -INFINITY;
+  float l = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    if (t < nkt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        st[j][i] = none ? 0.f : exp2_fast(__builtin_fmaf(st[j][i], sl2, -mn));
+        l += st[j][i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[0] = mfma4(vp[j][i].x, st[j][i], o[0]);
+        o[1] = mfma4(vp[j][i].y, st[j][i], o[1]);
+        o[2] = mfma4(vp[j][i].z, st[j][i], o[2]);
+        o[3] = mfma4(vp[j][i].w, st[j][i], o[3]);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *reinterpret_cast<float4*>(&part_o[wave][qi][16 * g + 4 * i]) = make_float4(o[0][i], o[1][i], o[2][i], o[3][i]);
+  if (g == 0) {
+    part_m[wave][qi] = mn;
+    part_l[wave][qi] = l;
+  }
+  __syncthreads();
+  // merge: thread -> (query r, 4 d); waves in order
+  constexpr int TPR = HD / 4;   // threads per query row
+  for (int e = tid; e < 16 * TPR; e += 64 * NW) {
+    const int r = e / TPR, c = (e % TPR) * 4;
+    if (r >= lq) continue;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, part_m[w][r]);
+    float L = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const float a = part_m[w][r] == -INFINITY ? 0.f : exp2_fast(part_m[w][r] - M);
+        L += part_l[w][r] * a;
+        const float4 pv = *reinterpret_cast<const float4*>(&part_o[w][r][c]);
+        acc.x += pv.x * a; acc.y += pv.y * a; acc.z += pv.z * a; acc.w += pv.w * a;
+      }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    *reinterpret_cast<float4*>(out + (q0 + r) * so + hh * HD + c) = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if (c == 0) lse[(int64_t)hh * Tq + q0 + r] = L > 0.f ? (M + log2f(L)) * kLn2 : 0.f;
+  }
+}
+
+// dQ (+ delta) of the one query tile: key tiles split over the waves as in the forward, partial dQ^T
+// summed through LDS in wave order.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_dq_fewq_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
+    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ delta_out) {
+  constexpr int HD = 64, TPW = 2;
+  __shared__ __attribute__((aligned(16))) float part[NW][16][HD];
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  const int qi = lane & 15;
+  const bool qv = qi < lq;
+  const int64_t qrow = q0 + (qv ? qi : 0);
+  const int kend = causal ? min(lk, 16) : lk;
+  const int nkt = (kend + 15) >> 4;
+  float qf[HD / 4], dof[HD / 4];
+  load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv, qf);
+  load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv, dof);
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  float4 kp[TPW][4], kv[TPW][4], vk[TPW][4];   // K (K pattern), K (V pattern), V (K pattern)
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    if (t < nkt) {
+      frag_kpat(kb_, sk, t, lk, lane, kp[j]);
+      frag_vpat(kb_, sk, t, lk, lane, kv[j]);
+      frag_kpat(vb_, sv, t, lk, lane, vk[j]);
+    }
+  }
+  float delta = 0.f;
+  {
+    float of[HD / 4];
+    load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    if (wave == 0 && qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
+  }
+  const float sl2 = scale * kLog2e;
+  const float lse2 = qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f;
+  f32x4 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    if (t < nkt) {
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        st = mfma4(kp[j][s4].x, qf[4 * s4], st);
+        dp = mfma4(vk[j][s4].x, dof[4 * s4], dp);
+        st = mfma4(kp[j][s4].y, qf[4 * s4 + 1], st);
+        dp = mfma4(vk[j][s4].y, dof[4 * s4 + 1], dp);
+        st = mfma4(kp[j][s4].z, qf[4 * s4 + 2], st);
+        dp = mfma4(vk[j][s4].z, dof[4 * s4 + 2], dp);
+        st = mfma4(kp[j][s4].w, qf[4 * s4 + 3], st);
+        dp = mfma4(vk[j][s4].w, dof[4 * s4 + 3], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = t * 16 + 4 * g + i;
+        float p = exp2_fast(__builtin_fmaf(st[i], sl2, -lse2));
+        if (!(key < lk && (!causal || key <= qi))) p = 0.f;
+        st[i] = p * (dp[i] - delta);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[0] = mfma4(kv[j][i].x, st[i], acc[0]);
+        acc[1] = mfma4(kv[j][i].y, st[i], acc[1]);
+        acc[2] = mfma4(kv[j][i].z, st[i], acc[2]);
+        acc[3] = mfma4(kv[j][i].w, st[i], acc[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *reinterpret_cast<float4*>(&part[wave][qi][16 * g + 4 * i]) = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+  __syncthreads();
+  constexpr int TPR = HD / 4;
+  for (int e = tid; e < 16 * TPR; e += 64 * NW) {
+    const int r = e / TPR, c = (e % TPR) * 4;
+    if (r >= lq) continue;
+    float4 s4 = *reinterpret_cast<const float4*>(&part[0][r][c]);
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      const float4 a = *reinterpret_cast<const float4*>(&part[w][r][c]);
+      s4.x += a.x; s4.y += a.y; s4.z += a.z; s4.w += a.w;
+    }
+    *reinterpret_cast<float4*>(dq + (q0 + r) * sdq + hh * HD + c) = make_float4(s4.x * scale, s4.y * scale, s4.z * scale, s4.w * scale);
+  }
+}
+
 #ifndef RQ_ATTN_SHORT
 #define RQ_ATTN_SHORT 1   // 0: the chunked kernels for every length (A/B switch)
 #endif
@@ -1172,6 +1838,31 @@ static int64_t split_ws_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_
   return (max_k + kb - 1) / kb * Tq * H * (hd + 2);
 }
 
+// LDS-DMA short forms (attn_fwd_dma_kernel): self-attention style launches (more than one query tile)
+// whose key range fits 128 staged rows. RQ_ATTN_DMA=0 in the environment or rq_attn_dma_enable(0)
+// keeps the register-staged kernels (A/B).
+static int g_attn_dma = -1;
+static bool attn_dma_on() {
+  if (g_attn_dma < 0) {
+    const char* e = getenv("RQ_ATTN_DMA");
+    g_attn_dma = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_dma != 0;
+}
+static int dma_rows_for(int64_t max_k) { return max_k <= 32 ? 32 : (max_k <= 64 ? 64 : (max_k <= 96 ? 96 : 128)); }
+static bool dma_fwd_plan(int64_t hd, int64_t max_q, int64_t max_k) {   // also the dQ pass
+  return attn_dma_on() && hd == 64 && max_q > 16 && max_k <= 128;
+}
+static bool dma_kv_plan(int64_t hd, int64_t max_q, int64_t max_k) {    // dK / dV pass: queries staged
+  return attn_dma_on() && hd == 64 && max_k > 16 && max_q <= 128;
+}
+// one query tile over <= 128 keys (cross-attention, the decoder's short causal self-attention): forward and
+// dQ with the key tiles split over the waves (attn_fwd_fewq_kernel / attn_bwd_dq_fewq_kernel)
+static bool fewq_plan(int64_t hd, int64_t max_q, int64_t max_k) {
+  return attn_dma_on() && hd == 64 && max_q <= 16 && max_k <= 128;
+}
+static int fewq_waves(int64_t max_k) { return max_k <= 16 ? 1 : (max_k <= 32 ? 2 : 4); }
+
 template <int HD, int NW>
 static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
                    int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal, float scale,
@@ -1199,6 +1890,29 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
   hipLaunchKernelGGL((attn_fwd_combine_kernel<HD, KB_>), gc, dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq, out, so, lse)
       if (kb == 32) { RQ_SPL(32); } else { RQ_SPL(128); }
 #undef RQ_SPL
+      return;
+    }
+    if (fewq_plan(HD, max_q, max_k)) {
+      const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
+      switch (fewq_waves(max_k)) {
+        case 1: hipLaunchKernelGGL((attn_fwd_fewq_kernel<1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+        case 2: hipLaunchKernelGGL((attn_fwd_fewq_kernel<2>), g, dim3(128), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+        default: hipLaunchKernelGGL((attn_fwd_fewq_kernel<4>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+      }
+      return;
+    }
+    if (dma_fwd_plan(HD, max_q, max_k)) {
+      const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
+#define RQ_FD(R_)                                                                                              \
+  hipLaunchKernelGGL((attn_fwd_dma_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, \
+                     out, so, lse, Tq)
+      switch (dma_rows_for(max_k)) {
+        case 32: RQ_FD(32); break;
+        case 64: RQ_FD(64); break;
+        case 96: RQ_FD(96); break;
+        default: RQ_FD(128); break;
+      }
+#undef RQ_FD
       return;
     }
     int nw = 0, ch = 0;
@@ -1267,7 +1981,30 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
   if constexpr (HD == 64) {
     int nw = 0, ch = 0;
     const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
-    if (short_plan(max_q, max_k, &nw, &ch)) {
+    if (fewq_plan(HD, max_q, max_k)) {
+#define RQ_DQF(NW_)                                                                                                   \
+  hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<NW_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, \
+                     lse, Tq, cq, ck, causal, scale, dq, sdq, delta)
+      switch (fewq_waves(max_k)) {
+        case 1: RQ_DQF(1); break;
+        case 2: RQ_DQF(2); break;
+        default: RQ_DQF(4); break;
+      }
+#undef RQ_DQF
+      dq_done = true;
+    } else if (dma_fwd_plan(HD, max_q, max_k)) {
+#define RQ_DQD(R_)                                                                                                  \
+  hipLaunchKernelGGL((attn_bwd_dq_dma_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, \
+                     Tq, cq, ck, causal, scale, dq, sdq, delta)
+      switch (dma_rows_for(max_k)) {
+        case 32: RQ_DQD(32); break;
+        case 64: RQ_DQD(64); break;
+        case 96: RQ_DQD(96); break;
+        default: RQ_DQD(128); break;
+      }
+#undef RQ_DQD
+      dq_done = true;
+    } else if (short_plan(max_q, max_k, &nw, &ch)) {
 #define RQ_DQS(NW_, CH_)                                                                                              \
   hipLaunchKernelGGL((attn_bwd_dq_short_kernel<HD, NW_, CH_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, \
                      dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, delta)
@@ -1275,7 +2012,24 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #undef RQ_DQS
       dq_done = true;
     }
-    if (short_plan(max_k, max_q, &nw, &ch)) {
+    if (dma_kv_plan(HD, max_q, max_k)) {
+      if (!dq_done) {   // the dK/dV pass reads delta: chunked dQ first
+        launch_dq_chunked<HD>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq,
+                              sdq, delta);
+        dq_done = true;
+      }
+#define RQ_KVD(R_)                                                                                                     \
+  hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse, delta, \
+                     Tq, cq, ck, causal, scale, dk, sdk, dv, sdv, Tk)
+      switch (dma_rows_for(max_q)) {
+        case 32: RQ_KVD(32); break;
+        case 64: RQ_KVD(64); break;
+        case 96: RQ_KVD(96); break;
+        default: RQ_KVD(128); break;
+      }
+#undef RQ_KVD
+      kv_done = true;
+    } else if (short_plan(max_k, max_q, &nw, &ch)) {
       if (!dq_done) {   // the dK/dV pass reads delta: chunked dQ first
         launch_dq_chunked<HD>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq,
                               sdq, delta);
@@ -1407,14 +2161,6 @@ static int attn_fwd_impl(const float* q, int64_t sq, const float* k, int64_t sk,
   return 0;
 }
 
-int varlen_attn_fwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
-                     void* stream) {
-  return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq, order,
-                       nullptr, stream);
-}
-
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
@@ -1461,6 +2207,12 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   }
   RQ_LAUNCH_CHECK("varlen_attn_bwd");
   return 0;
+}
+
+int rq_attn_dma_enable(int enable) {
+  const int prev = attn_dma_on() ? 1 : 0;
+  g_attn_dma = enable ? 1 : 0;
+  return prev;
 }
 
 int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,

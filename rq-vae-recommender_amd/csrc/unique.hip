@@ -19,6 +19,14 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long k) {
   return k;
 }
 
+// Hash path set-up in one launch (no memset nodes): every slot empty, the count zero.
+__global__ void __launch_bounds__(256) unique_table_init_kernel(unsigned long long* __restrict__ table, int64_t slots,
+                                                                 unsigned long long* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < slots) table[i] = kEmpty;
+  if (i == 0) *count = 0ull;
+}
+
 __global__ void __launch_bounds__(256) unique_insert_kernel(const int64_t* __restrict__ ids, int64_t B, int L, int64_t K,
                                                              unsigned long long* __restrict__ table, int64_t mask,
                                                              unsigned long long* __restrict__ count) {
@@ -139,8 +147,8 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
   }
   RQ_CHECK_ARG(ws_bytes >= rq_unique_workspace(B), "rq_unique_count: workspace too small");
   const int64_t slots = table_slots(B);
-  RQ_HIP(hipMemsetAsync(workspace, 0xFF, (size_t)slots * sizeof(unsigned long long), s));
-  RQ_HIP(hipMemsetAsync(out_count, 0, sizeof(int64_t), s));
+  hipLaunchKernelGGL(unique_table_init_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s,
+                     (unsigned long long*)workspace, slots, (unsigned long long*)out_count);
   if (B > 0)
     hipLaunchKernelGGL(unique_insert_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, ids, B, (int)L, K,
                        (unsigned long long*)workspace, slots - 1, (unsigned long long*)out_count);

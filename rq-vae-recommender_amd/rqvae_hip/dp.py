@@ -142,11 +142,12 @@ def direct_grad(p) -> Optional[torch.Tensor]:
 
 
 def direct_grad_done(p) -> None:
-    """What AccumulateGrad's post-accumulate hook would do for p (GradBuckets usage tracking and the
-    overlapped exchange)."""
-    e = _DIRECT.get(id(p))
-    if e is not None:
-        e[1](p)
+    """The caller has added its contribution into p's flat-bucket view. Nothing to do: the op returns
+    None for p to autograd, and the engine still runs p's AccumulateGrad node (with an undefined
+    gradient) once ALL of p's contributions of this backward are in — its post-accumulate hook is the
+    single point where GradBuckets marks p ready (firing here as well would count p twice, and could
+    start the bucket's exchange before a second op has added its share)."""
+    return None
 
 
 class GradBuckets:

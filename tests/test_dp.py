@@ -43,6 +43,38 @@ class _Net(torch.nn.Module):
         return self.mlp(x)
 
 
+class _DirectLinear(torch.autograd.Function):
+    """y = x W^T whose weight gradient is added straight into W's flat bucket view when GradBuckets owns
+    one (dp.direct_grad — what the HIP GEMMs do on the GPU) and handed to autograd as None."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        sink = dp.direct_grad(w)
+        if sink is None:
+            return g @ w, g.t() @ x
+        sink.add_(g.t() @ x)
+        dp.direct_grad_done(w)
+        return g @ w, None
+
+
+class _TiedNet(torch.nn.Module):
+    """One weight used by two direct-gradient ops per forward (and a plain Linear after them)."""
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.randn(24, 24) * 0.2)
+        self.head = torch.nn.Linear(24, 8, bias=False)
+
+    def forward(self, x):
+        return self.head(torch.tanh(_DirectLinear.apply(torch.tanh(_DirectLinear.apply(x, self.w)), self.w)))
+
+
 def _loss(model, x):
     """Per-row loss, mean over the rows (the reference's mean over the batch)."""
     return ((model(x) - 0.1) ** 2).sum(-1).mean()
@@ -77,13 +109,13 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
     try:
         r, w, _ = dp.init_from_env(backend="gloo")
         torch.manual_seed(100 + rank)          # different init per rank: broadcast must fix it
-        model = _Net()
+        model = _TiedNet() if mode == "tied" else _Net()
         if mode == "grouped":   # parameter groups in grad-ready order (the bench's RQ-VAE layout)
             ps = list(model.parameters())
             buckets = dp.GradBuckets([ps[len(ps) // 2:][::-1], ps[:len(ps) // 2][::-1]], bucket_bytes=bucket_bytes)
         elif mode == "empty":   # buckets in forward order: the last bucket's grads are ready first
             buckets = dp.GradBuckets([list(model.parameters())], bucket_bytes=bucket_bytes)
-        elif mode == "graphed":
+        elif mode in ("graphed", "tied"):
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes, flat_views=True)
         else:
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
@@ -153,7 +185,7 @@ def _run(world, gb, bucket_bytes, mode):
 
 def _single_process(state0, gb, mode, world):
     """Same two steps in one process: params after the first step + grads of the second step."""
-    model = _Net()
+    model = _TiedNet() if mode == "tied" else _Net()
     model.load_state_dict(state0)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
     x, lengths, toks = _data(gb)
@@ -179,6 +211,7 @@ def _single_process(state0, gb, mode, world):
     (3, 61, 4096, "tokens"),        # token-balanced variable-length shards (unequal sequence counts)
     (3, 2, 2048, "empty"),          # global batch < world: rank 2 has no sequences, several buckets
     (2, 64, 2048, "graphed"),       # GraphedSteps bodies with the in-graph exchange (run eagerly)
+    (2, 64, 1024, "tied"),          # one weight, two direct-gradient contributions per backward
 ])
 def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode):
     res = _run(world, gb, bucket_bytes, mode)
@@ -201,7 +234,7 @@ def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode
             assert np.array_equal(r[2][n], res[0][2][n]), n
     # single process from the same initial parameters (rank 0's init after broadcast = seed 100)
     torch.manual_seed(100)
-    state0 = _Net().state_dict()
+    state0 = (_TiedNet() if mode == "tied" else _Net()).state_dict()
     model, grads = _single_process(state0, gb, mode, world)
     for n, p in model.named_parameters():
         got = res[0][3][n]
@@ -214,7 +247,8 @@ def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode
         for r in res[1:]:
             assert np.array_equal(r[3][n], got)
         assert np.allclose(res[0][2][n], p.detach().numpy(), rtol=1e-5, atol=1e-6), f"params {n}"
-    assert np.array_equal(res[0][2]["unused.weight"], model.unused.weight.detach().numpy())
+    if mode != "tied":
+        assert np.array_equal(res[0][2]["unused.weight"], model.unused.weight.detach().numpy())
 
 
 def test_shard_range_partitions():

@@ -85,9 +85,21 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (4, 150, 260, 6, 64, False, False),  # long ragged q x k, lq != lk
 ])
 @pytest.mark.parametrize("fused", [True, False])
-def test_varlen_attention_vs_oracle(device, monkeypatch, B, max_q, max_k, H, hd, causal, same, fused):
-    from rqvae_hip import ops
+@pytest.mark.parametrize("dma", [True, False])
+def test_varlen_attention_vs_oracle(device, monkeypatch, B, max_q, max_k, H, hd, causal, same, fused, dma):
+    """Both backward forms, and the LDS-DMA short forms (key ranges <= 128, hd 64) on and off."""
+    from rqvae_hip import _lib, ops
     monkeypatch.setattr(ops, "ATTN_FUSED_BWD", fused)
+    lib = _lib.load()
+    prev = lib.rq_attn_dma_enable(int(dma))
+    try:
+        _attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same)
+    finally:
+        lib.rq_attn_dma_enable(prev)
+
+
+def _attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
+    from rqvae_hip import ops
     g = gi.rng(B * 131 + max_q + hd)
     q, k, v, do, cq, ck = _varlen_case(g, B, max_q, max_k, H, hd, same)
     A_ = H * hd
@@ -243,3 +255,48 @@ def test_decoder_model_vs_reference(golden, device, monkeypatch, bucket):
         elif key + "__norm" in z:
             assert p.grad.double().norm().item() == pytest.approx(float(z[key + "__norm"]), rel=1e-4)
             assert np.all(np.abs(p.grad[0].cpu().numpy() - z[key + "__row0"]) <= 1e-5 + 2e-3 * np.abs(z[key + "__row0"]))
+
+
+@pytest.mark.parametrize("B,max_q,max_k,H,causal,same", [
+    (7, 81, 81, 8, False, True),      # encoder self-attention (DA)
+    (9, 5, 5, 8, True, True),         # decoder causal self-attention
+    (6, 5, 81, 8, False, False),      # cross-attention (DA)
+    (2, 300, 300, 6, False, True),    # long context (DM-like)
+    (3, 6, 400, 8, False, False),     # few queries over a long key range
+])
+def test_c_abi_entry_points_vs_oracle(device, B, max_q, max_k, H, causal, same):
+    """The SURVEY §8(b)-named entries varlen_attn_fwd / varlen_attn_bwd (no scratch: no longest-first
+    order, no split-key partials, the two-pass backward) called directly through the C ABI — the
+    binding a reference-side maintainer would use — against the fp64 oracle."""
+    from rqvae_hip._lib import call, ptr, stream_handle
+    hd = 64
+    g = gi.rng(B * 7 + max_q + max_k)
+    q, k, v, do, cq, ck = _varlen_case(g, B, max_q, max_k, H, hd, same)
+    A_ = H * hd
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a.reshape(a.shape[0], -1))).to(device)  # noqa: E731
+    qt, kt, vt, dot = t(q), t(k), t(v), t(do)
+    cqt, ckt = torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device)
+    Tq, Tk = qt.shape[0], kt.shape[0]
+    mq, mk = int(np.diff(cq).max()), int(np.diff(ck).max())
+    scale = 1.0 / np.sqrt(hd)
+    out = torch.empty((Tq, A_), device=device)
+    lse = torch.empty((H, Tq), device=device)
+    st = stream_handle(device)
+    call("varlen_attn_fwd", ptr(qt), A_, ptr(kt), A_, ptr(vt), A_, ptr(cqt), ptr(ckt), B, H, hd, mq, mk, int(causal),
+         float(scale), ptr(out), A_, ptr(lse), Tq, st)
+    dq, dk, dv = (torch.empty((n, A_), device=device) for n in (Tq, Tk, Tk))
+    delta = torch.empty((H, Tq), device=device)
+    call("varlen_attn_bwd", ptr(qt), A_, ptr(kt), A_, ptr(vt), A_, ptr(out), A_, ptr(dot), A_, ptr(lse), Tq, ptr(cqt),
+         ptr(ckt), B, H, hd, mq, mk, int(causal), float(scale), ptr(dq), A_, ptr(dk), A_, ptr(dv), A_, Tk, ptr(delta), st)
+    torch.cuda.synchronize()
+    ref, _ = A.attn_fwd(q, k, v, cq, ck, causal)
+    rdq, rdk, rdv = A.attn_bwd(q, k, v, do, cq, ck, causal)
+
+    def chk(a, b, atol, rtol, what):
+        a = a.cpu().double().numpy().reshape(b.shape)
+        err = np.abs(a - b) - (atol + rtol * np.abs(b))
+        assert err.max() <= 0, f"{what}: max abs err {np.abs(a - b).max():.3e}"
+    chk(out, ref, 2e-5, 2e-4, "out")
+    chk(dq, rdq, 1e-4, 1e-3, "dq")
+    chk(dk, rdk, 1e-4, 1e-3, "dk")
+    chk(dv, rdv, 1e-4, 1e-3, "dv")

@@ -278,3 +278,24 @@ def test_split_path_vs_oracle(device, B, D, K, L, mode):
     same = (o["ids"] == outs[1]["ids"]).all(1)
     assert same.mean() > 0.998
     _close(o["emb"][:, same], outs[1]["emb"][:, same], 1e-5, 1e-6, "split vs tiled emb")
+
+
+@pytest.mark.parametrize("B", [64, 4096, 65536])
+def test_unique_count_graph_replay(device, B):
+    """unique_count captured in a hipGraph (the graphed trainers' p_unique_ids): every replay counts the
+    ids copied into the static input (hash path at small B, byte map at large B)."""
+    from rqvae_hip import ops
+    g = gi.rng(B)
+    static = torch.zeros((B, 3), dtype=torch.int64, device=device)
+    for _ in range(2):
+        ops.unique_count(static, 256)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = ops.unique_count(static, 256)
+    for rep in range(4):
+        ids = g.integers(0, 256 if rep % 2 else 8, size=(B, 3))
+        static.copy_(torch.from_numpy(ids))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert int(out) == np.unique(ids, axis=0).shape[0], (rep, int(out))

@@ -57,6 +57,14 @@ for s in $steps; do
         python3 "$R/bench.py" --decoder-only --dm-batch 8 > "$O/prof_dm8.json" 2> "$O/prof_dm8.err"
       cd "$R"
       cat "$O/prof_dm8.json" ;;
+    attnab)   # short-form attention: LDS-DMA kernels on (default) vs off, Amazon / cross shapes
+      run attn_dma1 200 python -u "$R/tools/attn_probe.py" > "$O/attn_dma1.jsonl" 2> "$O/attn_dma1.err"
+      RQ_ATTN_DMA=0 run attn_dma0 200 python -u "$R/tools/attn_probe.py" > "$O/attn_dma0.jsonl" 2> "$O/attn_dma0.err"
+      grep -h amazon "$O/attn_dma1.jsonl" "$O/attn_dma0.jsonl" ;;
+    keys)    # per-shape device times of the RQ-VAE step and of one decoder step (HIP events)
+      run keys_rq 200 python -u "$R/tools/gemm_keys.py" 5 > "$O/keys_rq.jsonl" 2> "$O/keys_rq.err"
+      run keys_dec 200 python -u "$R/tools/dec_gemm_keys.py" 5 > "$O/keys_dec.jsonl" 2> "$O/keys_dec.err"
+      tail -1 "$O/keys_rq.jsonl"; tail -1 "$O/keys_dec.jsonl" ;;
     sqpmc)
       cd /tmp
       run pmc_sq 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \

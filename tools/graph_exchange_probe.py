@@ -32,6 +32,7 @@ def main():
     torch.manual_seed(0)
     m = EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.0, num_heads=4, n_layers=4,
                                      num_embeddings=64, sem_id_dim=4, inference_verifier_fn=None, max_pos=80).to(dev)
+    m.eval()   # no dropout anywhere (the model's hard-coded Dropout(0.5) would draw different keys per step)
     ref = copy.deepcopy(m)
     buckets = dp.GradBuckets(m.parameters(), bucket_bytes=256 << 10, flat_views=True, force_exchange=True)
     gs = GraphedSteps(lambda b: m(b).loss, lambda b: 0, buckets,
