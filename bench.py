@@ -362,6 +362,29 @@ def main():
                              "ceiling is the bf16 dense MFMA peak (2.5 PFLOP/s) / 3",
                 **{k: v for k, v in gemm.items() if k != "achieved_tflops"},
                 "traffic_detail": gtraffic if gtraffic else gtraffic_note}
+    # the whole step against its roofline (6 P_mlp + 2 K D L FLOP per item; MLP matmuls on the
+    # split-bf16 ceiling, the quantize distances on fp32 MFMA) and its achieved HBM % (PMC bytes of every
+    # dispatch of whole steps, tools/pmc_rqstep.py)
+    ms_step = elapsed / args.steps * 1e3
+    dims = [CFG["input_dim"]] + CFG["hidden"] + [CFG["D"]]
+    p_mlp = 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))   # encoder + decoder weights
+    mlp_flops, q_flops = 6.0 * p_mlp * B, float(flops_per_item * B)
+    step_roof = {"flops_per_item": 6 * p_mlp + flops_per_item,
+                 "achieved_tflops": round((mlp_flops + q_flops) / (ms_step * 1e-3) / 1e12, 2),
+                 "frac_of_gemm_peak": round((mlp_flops + q_flops) / (ms_step * 1e-3) / 1e12 / (BF16_MFMA_PEAK_TFLOPS / 3), 4),
+                 "frac_of_step_roofline": round((mlp_flops / (BF16_MFMA_PEAK_TFLOPS / 3 * 1e12) +
+                                                 q_flops / (FP32_MFMA_PEAK_TFLOPS * 1e12)) / (ms_step * 1e-3), 4),
+                 "note": "frac_of_step_roofline = (MLP matmul FLOPs / 833 TF + quantize FLOPs / 157.3 TF) / step time"}
+    if not args.no_pmc and ws == 1 and B == 65536:
+        st_traffic, st_note = pmc_traffic(timeout_s=120, regex=".*", script=("pmc_rqstep.py", "6"), launches=6)
+        if st_traffic:
+            step_roof.update(hbm_bytes_per_step=round(st_traffic["bytes"]),
+                             achieved_hbm_GBps=round(st_traffic["bytes"] / (ms_step * 1e-3) / 1e9, 1),
+                             achieved_hbm_frac=round(st_traffic["bytes"] / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             hbm_note="PMC FETCH_SIZE x2 + WRITE_SIZE summed over every dispatch of 6 whole steps / 6 "
+                                      "(Infinity-Cache hits are counted as fetched), over the timed step time")
+        else:
+            step_roof["hbm_bytes_per_step"] = st_note
     line = {
         "metric": "decoder-train tokens/sec + RQ-VAE items/sec at 1/2/4/8 MI355X; achieved HBM %",
         "value": round(ws * B * args.steps / elapsed, 1),
@@ -386,6 +409,7 @@ def main():
                                "ROTATION_TRICK, AdamW", "global_batch": ws * B, "per_gpu_batch": B,
                    "parallelism": f"dp{ws}"},
         "roofline": roof,
+        "step_roofline": step_roof,
         "loss_last": round(loss, 5),
         "gemm_selection": "default heuristic" if args.no_tunable else "TunableOp (rqvae_hip.gemm_tuning)",
     }

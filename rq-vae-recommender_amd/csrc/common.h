@@ -43,6 +43,32 @@ constexpr int kBadArg = -22;
     }                                                                     \
   } while (0)
 
+// Zero `bytes` of device memory on `stream` with a kernel (16-B stores, byte tail). Used instead of
+// hipMemsetAsync on every path a train step may record into a hipGraph: on this stack (ROCm 7.0 runtime
+// under torch) a captured memset node was seen to miss replays (stale workspaces in p_unique_ids under
+// the graphed trainer), while kernels replay in stream order.
+template <int U>
+__global__ void __launch_bounds__(256) rq_zero_kernel(uint4* __restrict__ p, int64_t n16, unsigned char* __restrict__ tail,
+                                                      int ntail) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) p[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) tail[threadIdx.x] = 0;
+}
+
+static inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const uintptr_t a = (uintptr_t)p;
+  if (a % 16 != 0) return hipMemsetAsync(p, 0, bytes, s);   // unaligned: never the case for torch allocations
+  const int64_t n16 = (int64_t)(bytes / 16);
+  const int ntail = (int)(bytes % 16);
+  int64_t blocks = (n16 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(rq_zero_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, reinterpret_cast<uint4*>(p), n16,
+                     reinterpret_cast<unsigned char*>(p) + n16 * 16, ntail);
+  return hipGetLastError();
+}
+
 // Butterfly sum over an aligned group of G lanes (G power of two <= 64). Every lane of
 // the group ends with the identical value (pairwise adds are commutative).
 template <int G>

@@ -832,7 +832,7 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
 #define RQ_X3W_EPI_LDS 1   // epilogue through LDS in whole rows (0: straight from the accumulators)
 #endif
 #ifndef RQ_X3W_DIAG
-#define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs (wrong results)
+#define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs, 3 = no epilogue (wrong results)
 #endif
 #ifndef RQ_X3W_PRIO
 #define RQ_X3W_PRIO 1      // s_setprio(1) around each MFMA cluster (keeps hipcc from moving it)
@@ -1015,6 +1015,19 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
   if (!g1) RQ_W_BAR();   // balance group 1's extra barrier
 
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
+  if (RQ_X3W_DIAG == 3) {   // diagnostic build: no epilogue (the accumulators must look used)
+    float keep = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) keep += acc[h][g][i][j][0] + acc[h][g][i][j][3];
+    if (keep == 12345.678f && tid == 0) C[0] = keep;
+    return;
+  }
 #if RQ_X3W_EPI_LDS
   // Epilogue through LDS, one 128-row half of the tile at a time (128 KiB): the waves scatter their
   // accumulator quads into a [128][256] fp32 image (16-B chunk c of row r at c ^ (r & 15): the
@@ -1360,8 +1373,8 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
                "rq_linear_wgrad: pointers must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   if (Bn == 0) {
-    RQ_HIP(hipMemsetAsync(dW, 0, (size_t)(O * I) * sizeof(float), s));
-    if (db) RQ_HIP(hipMemsetAsync(db, 0, (size_t)O * sizeof(float), s));
+    RQ_HIP(zero_async(dW, (size_t)(O * I) * sizeof(float), s));
+    if (db) RQ_HIP(zero_async(db, (size_t)O * sizeof(float), s));
     return 0;
   }
   const WgradPlan p = wgrad_plan(Bn, O, I);

@@ -381,7 +381,7 @@ int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate,
                "rq_col_sum: need n %% 4 == 0 and 16-byte aligned P / out");
   hipStream_t s = (hipStream_t)stream;
   if (S == 0) {
-    if (!accumulate) RQ_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(float), s));
+    if (!accumulate) RQ_HIP(zero_async(out, (size_t)n * sizeof(float), s));
     return 0;
   }
   hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((n / 4 + kRedCols - 1) / kRedCols)), dim3(256), 0, s, P,
@@ -527,7 +527,7 @@ int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, c
   RQ_CHECK_ARG(gw && (B == 0 || (x && w && rstd && gy && gx)), "rq_rmsnorm_bwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
   if (B == 0) {
-    if (!accumulate_gw) RQ_HIP(hipMemsetAsync(gw, 0, (size_t)D * sizeof(float), s));
+    if (!accumulate_gw) RQ_HIP(zero_async(gw, (size_t)D * sizeof(float), s));
     return 0;
   }
   RQ_CHECK_ARG(workspace && ws_bytes >= rq_rmsnorm_bwd_workspace(B, D), "rq_rmsnorm_bwd: workspace too small");

@@ -1615,7 +1615,7 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
   int* perm = (int*)w;        w += (size_t)(L * B) * sizeof(int);
   float* segs = (float*)(((uintptr_t)w + 15) & ~(uintptr_t)15);
   if (B == 0) {
-    RQ_HIP(hipMemsetAsync(grad_codebooks, 0, (size_t)(L * K * D) * sizeof(float), s));
+    RQ_HIP(zero_async(grad_codebooks, (size_t)(L * K * D) * sizeof(float), s));
     return 0;
   }
   switch (D) {
@@ -1662,8 +1662,8 @@ int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D,
   RQ_CHECK_ARG(ws_bytes >= rq_segment_sum_workspace(B, K), "rq_segment_sum: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   if (B == 0) {
-    RQ_HIP(hipMemsetAsync(out, 0, (size_t)(K * D) * sizeof(float), s));
-    if (counts) RQ_HIP(hipMemsetAsync(counts, 0, (size_t)K * sizeof(int64_t), s));
+    RQ_HIP(zero_async(out, (size_t)(K * D) * sizeof(float), s));
+    if (counts) RQ_HIP(zero_async(counts, (size_t)K * sizeof(int64_t), s));
     return 0;
   }
   const int b = (int)B, d = (int)D, k = (int)K;

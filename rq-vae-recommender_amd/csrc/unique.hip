@@ -135,7 +135,7 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
   if (use_byte_map(B, keys) && ws_bytes >= rq_unique_workspace2(B, L, K)) {
     const int64_t nb = ((int64_t)keys + 15) / 16 * 16;
     unsigned long long* bad = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + nb);
-    RQ_HIP(hipMemsetAsync(workspace, 0, (size_t)nb + 16, s));
+    RQ_HIP(zero_async(workspace, (size_t)nb + 16, s));
     hipLaunchKernelGGL(unique_mark_kernel, dim3((unsigned)std::max<int64_t>(1, (B + 255) / 256)), dim3(256), 0, s, ids, B,
                        (int)L, K, (unsigned char*)workspace, bad, (unsigned long long*)out_count);
     const int64_t n16 = nb / 16;

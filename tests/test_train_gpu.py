@@ -101,9 +101,11 @@ def test_train_decoder_graphed(tmp_path, device, capsys):
     kw = dict(iterations=8, batch_size=32, learning_rate=0.0003, dataset=RecDataset.AMAZON, pretrained_rqvae_path=ckpt,
               decoder_embed_dim=64, dropout_p=0.3, attn_heads=4, attn_embed_dim=128, attn_layers=4,
               save_dir_root=str(tmp_path) + "/", save_model_every=10 ** 9, log_every=1, **vae)
+    from rqvae_hip import ops
     traces = {}
     for graphs in (False, True):
         capsys.readouterr()
+        ops._SEED["n"] = 0   # same dropout keys for the first (eager in both modes) step
         train_decoder.train(cuda_graphs=graphs, **kw)
         traces[graphs] = _trace(capsys)
         run = dict(train_decoder.LAST_RUN)

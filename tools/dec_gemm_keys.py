@@ -21,7 +21,10 @@ from rqvae_hip import dp, ops  # noqa: E402
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    cfg = bench.DEC_DM if "dm" in sys.argv[2:] else bench.DEC
+    cfg = dict(bench.DEC_DM if any(a.startswith("dm") for a in sys.argv[2:]) else bench.DEC)
+    for a in sys.argv[2:]:   # dm8: the ML-32M config at 8 sequences
+        if a.startswith("dm") and a[2:].isdigit():
+            cfg["B"] = int(a[2:])
     dev = torch.device("cuda", 0)
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel
@@ -57,6 +60,8 @@ def main():
         if k.startswith("gemm_bf16x3:"):
             M, N, K = (int(v) for v in k.split(":")[1].split("x"))
             r["tflops"] = round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 1)
+            f = [int(c) for c in k.split(":")[2]] + [0, 0, 0]
+            r["plan"] = ops.gemm_x3_choice(M, N, K, bool(f[2]), bool(f[3]), bool(f[0]), bool(f[1]), f[4])
         rows.append(r)
     for r in sorted(rows, key=lambda r: -r["us_per_step"]):
         print(json.dumps(r))

@@ -61,10 +61,23 @@ for s in $steps; do
       run attn_dma1 200 python -u "$R/tools/attn_probe.py" > "$O/attn_dma1.jsonl" 2> "$O/attn_dma1.err"
       RQ_ATTN_DMA=0 run attn_dma0 200 python -u "$R/tools/attn_probe.py" > "$O/attn_dma0.jsonl" 2> "$O/attn_dma0.err"
       grep -h amazon "$O/attn_dma1.jsonl" "$O/attn_dma0.jsonl" ;;
+    keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
+      run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
+      tail -1 "$O/keys_dm8.jsonl" ;;
     keys)    # per-shape device times of the RQ-VAE step and of one decoder step (HIP events)
       run keys_rq 200 python -u "$R/tools/gemm_keys.py" 5 > "$O/keys_rq.jsonl" 2> "$O/keys_rq.err"
       run keys_dec 200 python -u "$R/tools/dec_gemm_keys.py" 5 > "$O/keys_dec.jsonl" 2> "$O/keys_dec.err"
       tail -1 "$O/keys_rq.jsonl"; tail -1 "$O/keys_dec.jsonl" ;;
+    attnab2)   # same-process, alternating A/B of the attention forms at the Amazon decoder shapes
+      run attnab2 200 python -u "$R/tools/attn_ab2.py" 20 3 > "$O/attnab2.jsonl" 2> "$O/attnab2.err"
+      cat "$O/attnab2.jsonl" ;;
+    epiab)   # wide GEMM kernel with / without its epilogue (diagnostic build build_ab/x3w_noepi.so)
+      GEMM_AB_KERNELS=wide GEMM_AB_CASES="enc0,dec3 fwd,dec-ctx" run epiab_a 200 python -u "$R/tools/gemm_ab.py" 20 > "$O/epiab_a.jsonl" 2>&1
+      RQVAE_HIP_LIB="$R/build_ab/x3w_noepi.so" GEMM_AB_KERNELS=wide GEMM_AB_CASES="enc0,dec3 fwd,dec-ctx" run epiab_b 200 python -u "$R/tools/gemm_ab.py" 20 > "$O/epiab_b.jsonl" 2>&1
+      grep -h '"us"' "$O/epiab_a.jsonl" "$O/epiab_b.jsonl" ;;
+    decgemm)   # decoder context-row GEMM operand forms / kernels (tools/dec_gemm_probe.py)
+      run decgemm 200 python -u "$R/tools/dec_gemm_probe.py" 20 > "$O/decgemm.jsonl" 2> "$O/decgemm.err"
+      cat "$O/decgemm.jsonl" ;;
     sqpmc)
       cd /tmp
       run pmc_sq 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \
