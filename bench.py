@@ -327,6 +327,7 @@ def main():
     extras = {}
     if not args.no_extras and rk == 0 and ws == 1:
         extras = measure_extras(model, device, pool[0])
+        extras["trainers"] = measure_trainers()
 
     if rk != 0:
         if ws > 1:
@@ -427,6 +428,44 @@ def main():
     print(json.dumps(line), flush=True)
     if ws > 1:
         dist.barrier()
+
+
+def measure_trainers(iters=30):
+    """The drop-in trainers themselves (train_rqvae.train / train_decoder.train: data pipeline, hipGraph
+    step with the in-graph gradient exchange, AdamW, host loop) timed by their own LAST_RUN span — the
+    per-step time a user of the reference's scripts sees, beside the bench loop's. RQ-VAE at the bench
+    config (ML-32M dims, 65,536 items per step, synthetic 87,585-item corpus, k-means init); the decoder
+    at the Amazon config (256 sequences, tokenizer = the RQ-VAE checkpoint just written)."""
+    import contextlib
+    import glob
+    import io
+    import tempfile
+    import train_decoder
+    import train_rqvae
+    from data.processed import RecDataset
+    from modules.quantize import QuantizeForwardMode
+    out = {}
+    vae = dict(vae_input_dim=CFG["input_dim"], vae_embed_dim=CFG["D"], vae_hidden_dims=CFG["hidden"],
+               vae_codebook_size=CFG["K"], vae_n_cat_feats=0, vae_n_layers=CFG["L"])
+    with tempfile.TemporaryDirectory() as tmp, contextlib.redirect_stdout(io.StringIO()):
+        t0 = time.perf_counter()
+        train_rqvae.train(iterations=iters, batch_size=65536, learning_rate=CFG["lr"], weight_decay=CFG["wd"],
+                          dataset=RecDataset.ML_32M, do_eval=False, save_dir_root=tmp + "/vae/", log_every=10 ** 9,
+                          vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK, commitment_weight=CFG["beta"], **vae)
+        r = dict(train_rqvae.LAST_RUN)
+        out["rqvae_ml32m"] = {**r, "items_per_s": round(65536 / (r["iter_ms"] * 1e-3), 1),
+                              "wall_s": round(time.perf_counter() - t0, 1)}
+        ckpt = sorted(glob.glob(tmp + "/vae/checkpoint_*.pt"))[-1]
+        t0 = time.perf_counter()
+        train_decoder.train(iterations=iters, batch_size=DEC["B"], learning_rate=DEC["lr"], weight_decay=DEC["wd"],
+                            dataset=RecDataset.AMAZON, pretrained_rqvae_path=ckpt, decoder_embed_dim=DEC["E"],
+                            dropout_p=DEC["dropout"], attn_heads=DEC["H"], attn_embed_dim=DEC["A"],
+                            attn_layers=DEC["layers"], save_dir_root=tmp + "/dec/", log_every=10 ** 9, **vae)
+        r = dict(train_decoder.LAST_RUN)
+        out["decoder_amazon"] = {**{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()},
+                                 "wall_s": round(time.perf_counter() - t0, 1)}
+    out["rqvae_ml32m"]["iter_ms"] = round(out["rqvae_ml32m"]["iter_ms"], 3)
+    return out
 
 
 def measure_extras(model, device, x):

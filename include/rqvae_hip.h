@@ -184,8 +184,10 @@ int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kconti
  * fill the GPU (e.g. the decoder's 1,280 future-token rows), K is split for any epilogue: the partials
  * go to the workspace and a fixed-order reduction applies the epilogue (deterministic). accumulate = 1
  * (plain epilogue only): C += A B^T — a weight gradient added straight into an existing .grad buffer
- * (replaces autograd's AccumulateGrad add into data-parallel flat gradient buckets). Slab calls need
- * ldc == N and workspace >= rq_gemm_bf16x3_workspace2(M, N, K, accumulate) bytes. */
+ * (replaces autograd's AccumulateGrad add into data-parallel flat gradient buckets; an unsplit call
+ * adds in the GEMM's own epilogue, a split one in the reduction, both as C + (A B^T) in fp32). Split-K
+ * calls need ldc == N and workspace >= rq_gemm_bf16x3_workspace2(M, N, K, accumulate) bytes (0 when
+ * the shape never splits). */
 size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate);
 int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
                        int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
@@ -311,9 +313,17 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
  * sequences longer than one key block is summed from per-block partials in block order by a reduction
  * launch (deterministic, no atomics). ws: caller-provided scratch of at least
  * varlen_attn_bwd_ws_elems(...) floats (0 -> ws may be NULL; it also holds the longest-first sequence
- * order of the fused launch, as varlen_attn_fwd3). Other shapes run varlen_attn_bwd. */
+ * order of the fused launch, as varlen_attn_fwd3). Other shapes run varlen_attn_bwd. With a workspace
+ * of varlen_attn_bwd_ws_elems2(..., Tk, ...) floats the fused launch may also split each key block's
+ * query range over up to 4 workgroups when the grid cannot fill the GPU (few long sequences per GPU);
+ * their dK / dV partials are summed in split order by one more launch (deterministic). */
 int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
                              int64_t* elems);
+/* Query splits of the fused backward: n > 0 forces n (1 = off), 0 = automatic (the default;
+ * RQ_ATTN_QSPLIT in the environment sets the initial value). Returns the previous setting. */
+int rq_attn_qsplit_set(int n);
+int varlen_attn_bwd_ws_elems2(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int64_t Tk,
+                              int64_t* elems);
 int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                      int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                      const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,

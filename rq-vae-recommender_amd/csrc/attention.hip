@@ -580,6 +580,29 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
   store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
 }
 
+template <int HD>
+__global__ void __launch_bounds__(256) attn_kv_reduce_kernel(const float* __restrict__ kvpart, int qsplit, int64_t Tk,
+                                                             int64_t H, const int64_t* __restrict__ cu_k, int B,
+                                                             float scale, float* __restrict__ dk, int64_t sdk,
+                                                             float* __restrict__ dv, int64_t sdv) {
+  constexpr int F4 = HD / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t HH = H * HD;
+  const int64_t row = i / (H * F4), c = (i % (H * F4)) * 4;
+  if (row >= cu_k[B]) return;
+  const int64_t slab = Tk * HH;
+  const float* p = kvpart + row * HH + c;
+  float4 a = *reinterpret_cast<const float4*>(p), e = *reinterpret_cast<const float4*>(p + qsplit * slab);
+  for (int s = 1; s < qsplit; ++s) {
+    const float4 x = *reinterpret_cast<const float4*>(p + s * slab);
+    const float4 y = *reinterpret_cast<const float4*>(p + (qsplit + s) * slab);
+    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    e.x += y.x; e.y += y.y; e.z += y.z; e.w += y.w;
+  }
+  *reinterpret_cast<float4*>(dk + row * sdk + c) = make_float4(a.x * scale, a.y * scale, a.z * scale, a.w * scale);
+  *reinterpret_cast<float4*>(dv + row * sdv + c) = e;
+}
+
 // ------------------------------------------------------------- fwd: split keys (few queries)
 // Few queries over a long key range (the decoder's cross-attention: 5-6 future tokens x a context of
 // up to 81 / 801 / 1281 rows): the chunked forward gives each (sequence, head) ONE wave that walks every
@@ -775,7 +798,8 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
     int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
     const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ part, float* __restrict__ dk,
-    int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk, const int* __restrict__ order) {
+    int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk, const int* __restrict__ order, int qsplit,
+    float* __restrict__ kvpart) {
   constexpr int LD = HD + 4, DT = HD / 16, KB = 16 * NW, NTL = CH / 16, LDS_ = KB + 4;
   constexpr int DSPLIT = NW >= NTL ? NW / NTL : 1, DTW = DT / DSPLIT;
   static_assert(DT % DSPLIT == 0, "dQ split");
@@ -797,7 +821,8 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
   const int b = seq_of(order, z);
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-  const int kwg = blockIdx.x * KB;
+  const int kbi = (int)blockIdx.x / qsplit, qs = (int)blockIdx.x - kbi * qsplit;   // key block, query split
+  const int kwg = kbi * KB;
   if (kwg >= lk) {
     if (lk == 0) zero_rows<HD, 64 * NW>(dq, sdq, q0, q0 + lq, hh, tid);   // no keys: dQ = 0 (grid-stride over x)
     return;
@@ -827,11 +852,16 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
   int64_t dstride;
   float mul;
   if (nkb == 1) { dst = dq + q0 * sdq + hh * HD; dstride = sdq; mul = scale; }
-  else { dst = part + ((int64_t)blockIdx.x * Tq + q0) * HH + hh * HD; dstride = HH; mul = 1.f; }
+  else { dst = part + ((int64_t)kbi * Tq + q0) * HH + hh * HD; dstride = HH; mul = 1.f; }
+  // query split qs of qsplit: whole CH chunks [c_lo, c_hi) of the block's range (disjoint dQ rows;
+  // dK / dV partials per split, summed in split order by attn_kv_reduce_kernel)
+  const int nch = lq > qstart ? (lq - qstart + CH - 1) / CH : 0;
+  const int c_lo = qstart + (qs * nch / qsplit) * CH;
+  const int c_hi = min(lq, qstart + ((qs + 1) * nch / qsplit) * CH);
   RowStage<HD, 64 * NW, CH> stq, sto;
   FusedChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, dS_s, lane, 0, 0, lq, kj, causal, wave * 16 + (lane & 15), LDS_, kv,
                     scale * kLog2e, dka, dva};
-  for (int qc = qstart; qc < lq; qc += CH) {
+  for (int qc = c_lo; qc < c_hi; qc += CH) {
     stq.load(qb_, sq, qc, lq, tid);
     sto.load(ob_, sdo, qc, lq, tid);
     const bool ok = tid < CH && qc + tid < lq;
@@ -886,9 +916,18 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
     }
   }
   if (!kv) return;
-  store_rowT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, lane);
-  store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
+  if (qsplit == 1) {
+    store_rowT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, lane);
+    store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
+  } else {   // partials [2][qsplit][Tk][H HD], unscaled
+    store_rowT<HD>(kvpart + (((int64_t)qs * Tk + k0 + kj) * HH + hh * HD), dka, 1.f, lane);
+    store_rowT<HD>(kvpart + (((int64_t)(qsplit + qs) * Tk + k0 + kj) * HH + hh * HD), dva, 1.f, lane);
+  }
 }
+
+// dK = scale * sum_s dK_s, dV = sum_s dV_s over the fused backward's query splits, in split order
+// (deterministic), rows < cu_k[B] (the bucket tail was zeroed by the fused kernel's tail slice).
+
 
 // dQ rows of sequences with more than one key block: scale * sum over key blocks (in block order) of
 // the fused kernel's partials. Causal: query r sees key blocks kb <= r / KB only (the others never
@@ -2087,6 +2126,32 @@ static bool fused_plan(int64_t hd, int64_t max_q, int64_t max_k) {
   return !short_plan(max_k, max_q, &nw, &ch);
 }
 
+// Query splits of the fused backward: when (sequences x heads x key blocks) workgroups cannot fill the
+// chip twice over (ML-32M at 8 sequences per GPU: ~300 workgroups, each walking up to 801 queries), each
+// key block's query range is split over up to 4 workgroups (whole 32-query chunks, >= 2 per split);
+// their dK / dV partials are summed by attn_kv_reduce_kernel. RQ_ATTN_QSPLIT=n forces n (1 = off).
+static int g_attn_qsplit = -1;   // -1: RQ_ATTN_QSPLIT from the environment (0 = auto); rq_attn_qsplit_set
+static int fused_qsplit(int64_t B, int64_t H, int64_t max_q, int64_t max_k) {
+  if (g_attn_qsplit < 0) {
+    const char* e = getenv("RQ_ATTN_QSPLIT");
+    g_attn_qsplit = e ? std::max(0, atoi(e)) : 0;
+  }
+  const int forced = g_attn_qsplit;
+  if (max_q <= 16) return 1;
+  const int64_t max_by_len = std::max<int64_t>(1, max_q / (2 * RQ_ATTN_FUSED_CH));
+  if (forced > 0) return (int)std::min<int64_t>(std::min(forced, 8), max_by_len);
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int64_t wgs = B * H * ((max_k + kFusedKB - 1) / kFusedKB);
+  const int64_t want = (6 * (int64_t)cus + wgs - 1) / std::max<int64_t>(1, wgs);   // ~2 rounds of 3 per CU
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(want, 4), max_by_len));
+}
+
 // floats of dQ partials the fused backward needs: one (Tq, H*hd) slab per key block when a sequence may
 // span more than one block
 static int64_t fused_part_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq) {
@@ -2094,10 +2159,13 @@ static int64_t fused_part_elems(int64_t H, int64_t hd, int64_t max_q, int64_t ma
   const int64_t nkb = (max_k + kFusedKB - 1) / kFusedKB;
   return nkb > 1 ? nkb * Tq * H * hd : 0;
 }
-// + B ints of LPT order (float slots)
-static int64_t fused_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq) {
+// + B ints of LPT order (float slots, padded to 16 B) [+ the query splits' dK / dV partials, Tk >= 0]
+static int64_t fused_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
+                              int64_t Tk = -1) {
   if (!fused_plan(hd, max_q, max_k)) return 0;
-  return fused_part_elems(H, hd, max_q, max_k, Tq) + (lpt_plan(B, max_q) ? B : 0);
+  const int64_t base = fused_part_elems(H, hd, max_q, max_k, Tq) + (lpt_plan(B, max_q) ? ((B + 3) & ~(int64_t)3) : 0);
+  const int qs = Tk >= 0 ? fused_qsplit(B, H, max_q, max_k) : 1;
+  return base + (qs > 1 ? 2 * qs * Tk * H * hd : 0);
 }
 
 template <int HD>
@@ -2105,7 +2173,7 @@ static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k,
                              int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                              int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq,
                              const int64_t* ck, int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk,
-                             float* dv, int64_t sdv, int64_t Tk, float* delta, float* ws) {
+                             float* dv, int64_t sdv, int64_t Tk, float* delta, float* ws, int64_t ws_elems) {
   if constexpr (HD == 64) {
     constexpr int NW = RQ_ATTN_FUSED_NW, CH = RQ_ATTN_FUSED_CH, KB = 16 * NW;
     const int* ord = nullptr;
@@ -2119,9 +2187,18 @@ static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k,
     if (threads > 0)
       hipLaunchKernelGGL((attn_delta_kernel<HD>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, out, so, dout,
                          sdo, Tq, H, delta);
-    const dim3 g((unsigned)std::max<int64_t>(1, (max_k + KB - 1) / KB), (unsigned)H, (unsigned)B + 1);   // + tail slice
+    // query splits only when the caller sized the workspace for them (varlen_attn_bwd_ws_elems2)
+    int qs = fused_qsplit(B, H, max_q, max_k);
+    if (qs > 1 && ws_elems < fused_ws_elems(B, H, HD, max_q, max_k, Tq, Tk)) qs = 1;
+    float* kvpart = qs > 1 ? ws + fused_ws_elems(B, H, HD, max_q, max_k, Tq) : nullptr;
+    const dim3 g((unsigned)(std::max<int64_t>(1, (max_k + KB - 1) / KB) * qs), (unsigned)H, (unsigned)B + 1);   // + tail
     hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, NW, CH>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse,
-                       delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord);
+                       delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord, qs, kvpart);
+    if (qs > 1 && Tk > 0) {
+      const int64_t n = Tk * H * (HD / 4);
+      hipLaunchKernelGGL((attn_kv_reduce_kernel<HD>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, kvpart, qs, Tk,
+                         H, ck, (int)B, scale, dk, sdk, dv, sdv);
+    }
     if ((max_k + KB - 1) / KB > 1 && max_q > 0) {
       constexpr int RPB = 256 / (HD / 4);
       const dim3 gr((unsigned)((max_q + RPB - 1) / RPB), (unsigned)H, (unsigned)B);
@@ -2209,6 +2286,13 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   return 0;
 }
 
+int rq_attn_qsplit_set(int n) {
+  fused_qsplit(1, 1, 0, 0);   // resolve the environment default first
+  const int prev = g_attn_qsplit;
+  g_attn_qsplit = n < 0 ? 0 : n;
+  return prev;
+}
+
 int rq_attn_dma_enable(int enable) {
   const int prev = attn_dma_on() ? 1 : 0;
   g_attn_dma = enable ? 1 : 0;
@@ -2220,6 +2304,14 @@ int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, in
   RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_bwd_ws_elems: bad shape");
   *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq);
+  return 0;
+}
+
+int varlen_attn_bwd_ws_elems2(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int64_t Tk,
+                              int64_t* elems) {
+  RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems2: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0 && Tk >= 0, "varlen_attn_bwd_ws_elems2: bad shape");
+  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq, Tk);
   return 0;
 }
 
@@ -2241,7 +2333,7 @@ int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, con
   RQ_CHECK_ARG(ws_elems >= need && (need == 0 || ws), "varlen_attn_bwd2: workspace smaller than varlen_attn_bwd_ws_elems");
   if (B == 0) return 0;
   launch_bwd_fused<64>(B, H, max_q, max_k, (hipStream_t)stream, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q,
-                       cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, ws);
+                       cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, ws, ws_elems);
   RQ_LAUNCH_CHECK("varlen_attn_bwd2");
   return 0;
 }

@@ -529,6 +529,7 @@ struct X3Epilogue {
   uint32_t thr;      // dropout threshold (0 = none) and scale
   float scale;
   uint64_t seed;
+  int acc;           // kEpiStore, unsplit: C += A B^T (an accumulating call without the slab reduction)
 };
 
 // Epilogue SiLU on the hardware exp / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each) instead of
@@ -545,7 +546,13 @@ template <int EPI, bool DROP>
 __device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, float* __restrict__ C,
                                         float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
   if constexpr (EPI == kEpiStore) {
-    *reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n) = v;
+    float4* c = reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n);
+    if (ep.acc) {   // fixed order c + v: bitwise the slab reduction's C[j] + P[0][j]
+      const float4 o = *c;
+      *c = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    } else {
+      *c = v;
+    }
   } else if constexpr (EPI == kEpiAdd) {
     const float4 r = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
     if constexpr (DROP) {   // C = Z + Dropout(A B^T): dropout_add_fwd's mask (element m N + n) and arithmetic
@@ -1405,8 +1412,8 @@ static size_t x3_workspace_bytes(int64_t M, int64_t N, int64_t K, bool accumulat
   X3Plan pw;
   int S = p.S > q.S ? p.S : q.S;   // either tile size may run (rq_gemm_x3s_enable can switch between calls)
   if (x3w_plan(M, N, K, true, &pw) && pw.S > S) S = pw.S;
-  if (accumulate && S < 1) S = 1;
-  return (S > 1 || accumulate) ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
+  (void)accumulate;   // an unsplit accumulating call adds in the GEMM's own epilogue: no slab
+  return S > 1 ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
 }
 
 size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) { return x3_workspace_bytes(M, N, K, false); }
@@ -1443,7 +1450,7 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)A_lo | (uintptr_t)B | (uintptr_t)B_lo) % 16 == 0,
                "rq_gemm_bf16x3: operand pointers must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  X3Epilogue ep{Z, H_hi, H_lo, ldh, 0u, 1.f, seed};
+  X3Epilogue ep{Z, H_hi, H_lo, ldh, 0u, 1.f, seed, 0};
   dropout_params(p, &ep.thr, &ep.scale);
   RQ_CHECK_ARG(!accumulate || epilogue == kEpiStore, "rq_gemm_bf16x3: accumulate needs the plain epilogue");
   if (K == 0) {
@@ -1455,9 +1462,10 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, &pw);
   if (wide) pl = pw;
-  // slab path: split-K partials (or the single product of an accumulating call) go to the workspace
-  // with the plain store, and x3_reduce_kernel applies the real epilogue
-  const bool slab = pl.S > 1 || accumulate;
+  // slab path: split-K partials go to the workspace with the plain store, and x3_reduce_kernel applies
+  // the real epilogue (and the accumulation); an unsplit accumulating call adds in the GEMM's epilogue
+  const bool slab = pl.S > 1;
+  ep.acc = accumulate && !slab;
   float* out = C;
   if (slab) {
     const size_t need = (size_t)pl.S * (size_t)(M * N) * sizeof(float);

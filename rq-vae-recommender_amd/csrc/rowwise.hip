@@ -136,6 +136,14 @@ static int g_l2r_rpw = [] {
 // gw = sum_b gy_b t_b reduced deterministically: each 4-wave workgroup owns kRmsRows rows and writes
 // a [D] partial (waves combined in order through LDS), rms_reduce_kernel sums partials in order.
 constexpr int kRmsRows = 16;   // rows per workgroup: T=11.6k decoder rows -> 725 workgroups
+// Fewer rows per workgroup (8, 4: one row per wave) while 16-row workgroups would leave the chip half
+// empty (ML-32M at 8 sequences per GPU: ~3.2k rows -> 200 workgroups, each wave walking 4 dependent
+// rows); the partials (one [D] row per workgroup) stay small either way.
+static int rms_rows_per_blk(int64_t B) {
+  int r = kRmsRows;
+  while (r > 4 && (B + r - 1) / r < 512) r /= 2;
+  return r;
+}
 
 template <int VPL>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
@@ -177,7 +185,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
                                                           const float* __restrict__ rstd, const float* __restrict__ gy,
                                                           int64_t B, int D, uint32_t thr, float dscale, uint64_t seed,
                                                           const float* __restrict__ gres, float* __restrict__ gx,
-                                                          float* __restrict__ gw_part) {
+                                                          float* __restrict__ gw_part, int rows) {
   seed = epoch_seed(seed);
   __shared__ float4 part[4][VPL * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -189,8 +197,8 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
     gwa[v] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const float invD = 1.f / (float)D;
-  for (int i = wave; i < kRmsRows; i += 4) {
-    const int64_t r = (int64_t)blockIdx.x * kRmsRows + i;
+  for (int i = wave; i < rows; i += 4) {
+    const int64_t r = (int64_t)blockIdx.x * rows + i;
     if (r >= B) break;
     const float rs = rstd[r];
     float4 xv[VPL], gt[VPL];
@@ -486,7 +494,8 @@ int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out,
 
 size_t rq_rmsnorm_bwd_workspace(int64_t B, int64_t D) {
   if (B <= 0 || D <= 0) return 0;
-  return (size_t)((B + kRmsRows - 1) / kRmsRows) * (size_t)D * sizeof(float);
+  const int rows = rms_rows_per_blk(B);
+  return (size_t)((B + rows - 1) / rows) * (size_t)D * sizeof(float);
 }
 
 #define RMS_SWITCH(VPL_EXPR, LAUNCH)                                                                      \
@@ -535,8 +544,9 @@ int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, c
   float dscale;
   dropout_params(p, &thr, &dscale);
   float* part = static_cast<float*>(workspace);
-  const int nblk = (int)((B + kRmsRows - 1) / kRmsRows);
-#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, thr, dscale, seed, gres, gx, part);
+  const int rows = rms_rows_per_blk(B);
+  const int nblk = (int)((B + rows - 1) / rows);
+#define RMS_B(V) hipLaunchKernelGGL((rmsnorm_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w, rstd, gy, B, (int)D, thr, dscale, seed, gres, gx, part, rows);
   RMS_SWITCH((int)((D + 255) / 256), RMS_B)
 #undef RMS_B
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd");

@@ -1,9 +1,12 @@
 """nn.Linear with the MI355X weight-gradient path.
 
 Same parameters, init and state-dict keys as torch.nn.Linear (the reference builds its MLPs from
-nn.Linear, modules/encoder.py:20-31), so checkpoints are interchangeable. On the device the forward
-and data gradient stay on hipBLASLt while grad_weight / grad_bias — a reduction over the whole
-batch — run on rq_linear_wgrad (rqvae_hip.ops.LinearFunction). CPU tensors take torch's path.
+nn.Linear, modules/encoder.py:20-31), so checkpoints are interchangeable. Device fp32 inputs run
+rqvae_hip.ops.LinearFunction: at matmul precision 'high' (the reference's setting) forward, data and
+weight gradients on the split-bf16 MFMA GEMM; at 'highest' forward / data gradient on hipBLASLt and
+grad_weight / grad_bias on rq_linear_wgrad. Module-level CPU use (building a model, loading a
+checkpoint, the reference's own CPU runs) keeps nn.Linear's torch path — that is the module's
+contract, not a fallback of a HIP op: every rqvae_hip op raises RqHipError on CPU tensors.
 """
 import torch
 from torch import nn

@@ -82,9 +82,11 @@ class MultiHeadAttention(nn.Module):
 
     def forward(self, x: AttentionInput, x_kv: Optional[AttentionInput] = None, padding_mask: Optional[Tensor] = None,
                 is_causal: Optional[bool] = True, jagged: bool = False, use_cache: bool = False,
-                residual: Optional[Tensor] = None) -> AttentionInput:
+                residual: Optional[Tensor] = None, kv_values: Optional[Tensor] = None) -> AttentionInput:
         """`residual` (this build's extension, default None = the reference's contract): values
-        (T, d_out) added to the output projection inside its GEMM (out = proj(ctx) + residual)."""
+        (T, d_out) added to the output projection inside its GEMM (out = proj(ctx) + residual).
+        `kv_values` (extension, cross-attention): this layer's `self.kv(x_kv)` already computed by the
+        decoder's hoisted projection of the shared context (TransformerDecoder.forward)."""
         assert not self.cross_attn or x_kv is not None, "Found null x_kv in cross attn. layer"
         if not jagged:
             raise Exception("Unjagged attention currently not supported.")
@@ -93,7 +95,8 @@ class MultiHeadAttention(nn.Module):
         # strides); the backward writes their gradients into one buffer per projection (no cat)
         if self.cross_attn:
             jkv = as_jagged(x_kv)
-            ctx = hip_ops.varlen_attention_packed(self.q(jx.values()), self.kv(jkv.values()), jx.offsets(),
+            kv = self.kv(jkv.values()) if kv_values is None else kv_values
+            ctx = hip_ops.varlen_attention_packed(self.q(jx.values()), kv, jx.offsets(),
                                                   jkv.offsets(), self.num_heads, bool(is_causal), jx.max_len,
                                                   jkv.max_len)
         else:

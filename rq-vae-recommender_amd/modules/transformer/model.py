@@ -28,6 +28,8 @@ from rqvae_hip import ops as hip_ops
 
 # RQ_FF_RESIDUAL=0: keep the feed-forward output as MLP + dropout_add (in-process A/B)
 _FF_RESIDUAL = os.environ.get("RQ_FF_RESIDUAL", "1") != "0"
+# RQ_HOIST_KV=0: per-layer cross-attention K/V projections (in-process A/B: model.transformer._HOIST_KV)
+_HOIST_KV = os.environ.get("RQ_HOIST_KV", "1") != "0"
 
 
 class KVCacheOpsMixin:
@@ -76,17 +78,18 @@ class TransformerBlock(nn.Module):
         return (all(hip_ops.rmsnorm_supported(xv, n.weight) for n in norms) and
                 len({n.eps for n in norms}) == 1)
 
-    def _forward_jagged(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool) -> Jagged:
+    def _forward_jagged(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool, kv=None) -> Jagged:
         use_cache = not self.training and self.enable_kv_cache
         xv = jx.values()
         if self._fork_ok(xv):
-            return self._forward_fork(jx, jkv, is_causal, use_cache)
+            return self._forward_fork(jx, jkv, is_causal, use_cache, kv)
         # residual adds ride in the output-projection GEMMs' epilogue (h = x + MHA(..), h += CrossMHA(..))
         h = self.attention(jx.with_values(self.attn_norm.forward_dropout(xv, self.do)), is_causal=is_causal,
                            jagged=True, use_cache=use_cache, residual=xv).values()
         if self.do_cross_attn:
             h = self.cross_attention(x=jx.with_values(self.cross_attn_norm.forward_dropout(xv, self.do)), x_kv=jkv,
-                                     is_causal=False, jagged=True, use_cache=use_cache, residual=h).values()
+                                     is_causal=False, jagged=True, use_cache=use_cache, residual=h,
+                                     kv_values=kv).values()
         norm, mlp, drop = self.ff
         n3 = norm(h)
         fused = self._ff_residual(mlp, drop, n3, h)
@@ -109,7 +112,8 @@ class TransformerBlock(nn.Module):
             return None
         return hip_ops.mlp_chain_residual(x, chain[0], chain[1], h, drop.p)
 
-    def _forward_fork(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool, use_cache: bool) -> Jagged:
+    def _forward_fork(self, jx: Jagged, jkv: Optional[Jagged], is_causal: bool, use_cache: bool,
+                      kv=None) -> Jagged:
         """Same block, with x's fan-out (norm branches + residual) and h's (ff norm + residual) as
         hip_ops.rmsnorm_fork nodes: the residual gradients are added inside the norm backward kernels."""
         xv = jx.values()
@@ -124,7 +128,7 @@ class TransformerBlock(nn.Module):
                            residual=xr).values()
         if self.do_cross_attn:
             h = self.cross_attention(x=jx.with_values(n2), x_kv=jkv, is_causal=False, jagged=True,
-                                     use_cache=use_cache, residual=h).values()
+                                     use_cache=use_cache, residual=h, kv_values=kv).values()
         n3, hr = hip_ops.rmsnorm_fork(h, norm.eps, norm.weight)
         fused = self._ff_residual(mlp, drop, n3, hr)
         if fused is not None:
@@ -158,9 +162,22 @@ class TransformerDecoder(nn.Module, KVCacheOpsMixin):
             raise Exception("Unjagged attention currently not supported.")
         h = as_jagged(x)
         ctx = as_jagged(context) if context is not None else None
-        for layer in self.layers:
-            h = layer._forward_jagged(h, ctx, is_causal)
+        kvs = self._hoisted_kv(ctx)
+        for i, layer in enumerate(self.layers):
+            h = layer._forward_jagged(h, ctx, is_causal, kvs[i] if kvs is not None else None)
         return h if isinstance(x, Jagged) else _wrap_like(h.values(), x)
+
+    def _hoisted_kv(self, ctx: Optional[Jagged]):
+        """Every layer's cross-attention `kv(context)` as one GEMM over the concatenated K/V weights
+        (they all project the same encoder output): hip_ops.hoisted_projection — one launch instead of
+        one per layer forward, and in the backward one data-gradient GEMM (K = layers x 2 d_out) instead
+        of per-layer GEMMs plus the adds of their context gradients. None when it does not apply."""
+        if not (_HOIST_KV and self.do_cross_attn and ctx is not None and len(self.layers) > 1):
+            return None
+        kvs = [layer.cross_attention.kv for layer in self.layers]
+        if any(m.bias is not None for m in kvs):
+            return None
+        return hip_ops.hoisted_projection(ctx.values(), [m.weight for m in kvs])
 
 
 class TransformerEncoderDecoder(nn.Module, KVCacheOpsMixin):

@@ -57,6 +57,7 @@ _SIGS = {
     "rq_gemm_x3w_enable": ([_I], _I),
     "rq_gemm_x3s_enable": ([_I], _I),
     "rq_attn_dma_enable": ([_I], _I),
+    "rq_attn_qsplit_set": ([_I], _I),
     "rq_split_bf16x3": ([_P, _I64, _P, _P, _P], _I),
     "rq_split_bf16x3_multi": ([_I, _P, _P, _P, _P, _P], _I),
     "rq_unique_workspace": ([_I64], _SZ),
@@ -81,6 +82,7 @@ _SIGS = {
     "varlen_attn_fwd3": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
                           _I64, _P, _I64, _P], _I),
     "varlen_attn_bwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _P], _I),
+    "varlen_attn_bwd_ws_elems2": ([_I64, _I64, _I64, _I64, _I64, _I64, _I64, _P], _I),
     "varlen_attn_bwd2": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
                           _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P, _I64, _P], _I),
     "rq_seed_epoch_advance": ([_P], _I),

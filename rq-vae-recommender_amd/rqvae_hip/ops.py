@@ -391,8 +391,10 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     def desc(t):
         if isinstance(t, Split):
             return t.hi, t.lo, t.hi.shape[-1], 1
-        t = t.contiguous()
-        return t, None, t.shape[-1], 0
+        if not (t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1] and t.stride(0) % 4 == 0 and
+                t.data_ptr() % 16 == 0):
+            t = t.contiguous()   # row-strided 2-D views (column blocks of a wider buffer) are read in place
+        return t, None, t.stride(0) if t.dim() == 2 else t.shape[-1], 0
     ah, al, lda, asp = desc(a)
     bh, bl, ldb, bsp = desc(b)
     dev = ah.device
@@ -412,7 +414,8 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
             M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
             float(p), int(seed), int(accumulate), ptr(ws), nbytes, stream_handle(dev))
     if TIMER.wants("gemm_bf16x3"):
-        TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}", call, *args)
+        TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}{int(accumulate)}",
+                     call, *args)
     else:
         call(*args)
     if epilogue in (EPI_STORE, EPI_ADD):
@@ -1251,7 +1254,7 @@ def _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, s
         return
     import ctypes
     n = ctypes.c_int64(0)
-    call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, ctypes.byref(n))
+    call("varlen_attn_bwd_ws_elems2", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0], ctypes.byref(n))
     ws = torch.empty((int(n.value),), device=q.device, dtype=torch.float32) if n.value else None
     TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd2", *args, ptr(ws) if ws is not None else None,
                  int(n.value), stream_handle(q.device))
@@ -1320,6 +1323,7 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         else:
             ctx.save_for_backward(qsrc, kvsrc, out, lse, cu_q, cu_k)
         ctx.cfg = (self_attn, A, num_heads, bool(causal), int(max_q), int(max_k), float(scale))
+        ctx.kv_sink = None if self_attn else getattr(kvsrc, "_rq_grad_sink", None)
         return out
 
     @staticmethod
@@ -1334,7 +1338,13 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         koff = A if self_attn else 0
         dout = dout.contiguous()
         gq_src = torch.empty_like(qsrc)
-        gkv_src = gq_src if self_attn else torch.empty_like(kvsrc)
+        if self_attn:
+            gkv_src = gq_src
+        elif ctx.kv_sink is not None:   # a column block of the hoisted K/V projection's gradient buffer
+            gkv_src = ctx.kv_sink[0].block(ctx.kv_sink[1])
+        else:
+            gkv_src = torch.empty_like(kvsrc)
+        ctx.kv_sink = None
         q, k, v = qsrc[:, :A], src_kv[:, koff:koff + A], src_kv[:, koff + A:koff + 2 * A]
         dq, dk, dv = gq_src[:, :A], gkv_src[:, koff:koff + A], gkv_src[:, koff + A:koff + 2 * A]
         B = cu_q.shape[0] - 1
@@ -1349,6 +1359,115 @@ def varlen_attention_packed(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, m
     if scale is None:
         scale = 1.0 / math.sqrt(A // num_heads)
     return PackedVarlenAttentionFunction.apply(qsrc, kvsrc, cu_q, cu_k, num_heads, causal, max_q, max_k, scale)
+
+
+class _GradSink:
+    """The (T, n * W) gradient buffer of a hoisted projection, allocated by the first consumer
+    backward that writes its column block (every block is written whole: no zero fill)."""
+
+    def __init__(self, like: torch.Tensor, width: int, n: int):
+        self.like, self.width, self.n, self.buf = like, width, n, None
+
+    def block(self, i: int) -> torch.Tensor:
+        if self.buf is None:
+            self.buf = torch.empty((self.like.shape[0], self.width * self.n), device=self.like.device,
+                                   dtype=torch.float32)
+        return self.buf[:, i * self.width:(i + 1) * self.width]
+
+    def is_block(self, g, i: int) -> bool:
+        return (self.buf is not None and g is not None and g.shape == (self.buf.shape[0], self.width) and
+                g.stride() == self.buf.stride() and
+                g.data_ptr() == self.buf.data_ptr() + i * self.width * self.buf.element_size())
+
+
+class HoistedProjectionFunction(torch.autograd.Function):
+    """[x W_0^T | x W_1^T | ...] for bias-free Linears that read the SAME input — the decoder layers'
+    cross-attention K/V projections of the encoder output (reference modules/transformer/
+    attention.py:186-188 `self.kv(x_kv)` in every decoder layer, transformer/model.py:124-131) — as ONE
+    split-bf16 GEMM over the concatenated weights (bitwise the per-layer products: same k order per
+    output column). Returns one row-strided (T, O_i) column view per weight. Backward: when each
+    consumer wrote its gradient into its block of one shared buffer (PackedVarlenAttentionFunction
+    does for views carrying `_rq_grad_sink`), the data gradient is one GEMM with K = sum O_i (no adds of
+    per-layer input gradients) and the weight gradients one GEMM over the rows."""
+
+    @staticmethod
+    def forward(ctx, x, *weights):
+        O, I = weights[0].shape
+        T = x.shape[0]
+        wsp = split_bf16x3(torch.cat([w.detach() for w in weights], 0))
+        y = gemm_x3(x, True, wsp, True, T, O * len(weights), I)
+        sink = _GradSink(x, O, len(weights))
+        outs = []
+        for i in range(len(weights)):
+            v = y[:, i * O:(i + 1) * O]
+            v._rq_grad_sink = (sink, i)
+            outs.append(v)
+        ctx.save_for_backward(x)
+        ctx.wsp, ctx.weights, ctx.sink = wsp, weights, sink
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        (x,) = ctx.saved_tensors
+        weights, sink, wsp = ctx.weights, ctx.sink, ctx.wsp
+        ctx.wsp = ctx.weights = ctx.sink = None
+        n = len(weights)
+        O, I = weights[0].shape
+        T = x.shape[0]
+        if all(sink.is_block(g, i) for i, g in enumerate(gs)):
+            g = sink.buf
+        else:
+            g = torch.cat([gi if gi is not None else x.new_zeros((T, O)) for gi in gs], 1)
+        sink.buf = None
+        gx = gemm_x3(g, True, wsp, False, T, I, n * O) if ctx.needs_input_grad[0] else None
+        dws = [None] * n
+        if any(ctx.needs_input_grad[1:]):
+            dws = _wgrad_multi_into(weights, g, x, n * O, I, T)
+        return (gx, *dws)
+
+
+def _wgrad_multi_into(weights, g, x, O_all: int, I: int, rows: int):
+    """dW_cat = g^T x (O_all, I) as one GEMM, then each weight's row block added into its flat
+    gradient bucket view (dp.direct_grad; returns None for it) or returned as its gradient."""
+    from . import dp
+    sinks = [dp.direct_grad(w) for w in weights]
+    O = weights[0].shape[0]
+
+    def run():
+        dw = gemm_x3(g, False, x, False, O_all, I, rows)
+        for i, sk in enumerate(sinks):
+            if sk is not None:
+                sk.add_(dw[i * O:(i + 1) * O])
+                dp.direct_grad_done(weights[i])
+        return dw
+    if _SIDE["on"] and any(sk is not None for sk in sinks):
+        main = torch.cuda.current_stream(g.device)
+        side = _side_stream(g.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            dw = run()
+        for t in (g, x):
+            t.record_stream(side)
+        _SIDE["used"] = True
+        if any(sk is None for sk in sinks):   # autograd consumes these on the main stream
+            main.wait_stream(side)
+            dw.record_stream(main)
+    else:
+        dw = run()
+    return [None if sk is not None else dw[i * O:(i + 1) * O] for i, sk in enumerate(sinks)]
+
+
+def hoisted_projection(x: torch.Tensor, weights) -> list:
+    """HoistedProjectionFunction where it applies (matmul precision 'high', fp32 device tensors, equal
+    bias-free weight shapes, both dims % 8), else None (callers keep their per-layer Linears)."""
+    if not (weights and matmul_high() and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and
+            x.shape[0] > 0 and x.is_contiguous()):
+        return None
+    O, I = weights[0].shape
+    if not (all(w.shape == (O, I) and w.dtype == torch.float32 and w.is_cuda for w in weights) and
+            O % 8 == 0 and I % 8 == 0 and x.shape[1] == I):
+        return None
+    return list(HoistedProjectionFunction.apply(x, *weights))
 
 
 def varlen_attention(q, k, v, cu_q, cu_k, num_heads, causal, max_q, max_k, scale=None):

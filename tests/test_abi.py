@@ -48,6 +48,12 @@ def test_library_exports_declared_symbols():
     assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 0, ctypes.byref(n)) == 0 and n.value == 8 + 7 * 500 * 8 * 66
     assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 1, ctypes.byref(n)) == 0 and n.value == 8   # causal
     assert typed.varlen_attn_bwd_ws_elems(4, 8, 48, 5, 5, 500, ctypes.byref(n)) == -22
+    # + the query splits' dK / dV partials when the workgroups cannot fill the chip (ML-32M, 8 sequences:
+    # 8 x 6 x 13 = 624 workgroups -> 3 splits at 256 CUs, the CPU-side default)
+    assert typed.varlen_attn_bwd_ws_elems2(8, 6, 64, 801, 801, 3200, 3200, ctypes.byref(n)) == 0
+    assert n.value == 13 * 3200 * 384 + 8 + 2 * 3 * 3200 * 384
+    assert typed.varlen_attn_bwd_ws_elems2(64, 6, 64, 801, 801, 1000, 1000, ctypes.byref(n)) == 0
+    assert n.value == 13 * 1000 * 384 + 64   # 4,992 workgroups: no split
 
 
 def test_ops_refuse_cpu_tensors():

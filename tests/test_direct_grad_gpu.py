@@ -103,3 +103,59 @@ def test_direct_grad_decoder_model(device):
             assert torch.equal(pa.grad, pb.grad), n
     finally:
         torch.set_float32_matmul_precision("highest")
+
+
+@pytest.mark.parametrize("buckets_on", [False, True])
+def test_hoisted_kv_matches_per_layer(device, buckets_on):
+    """The decoder's cross-attention K/V projections of the shared context as one hoisted GEMM
+    (HoistedProjectionFunction; its backward reads the attention kernels' gradient blocks in place)
+    vs one Linear per layer: same loss and gradients (split-K orders may differ: fp32 tolerances)."""
+    from data.processed import synthetic_tokenized_batch
+    from modules.model import EncoderDecoderRetrievalModel
+    from modules.transformer import model as tm
+    from rqvae_hip import dp, ops
+    torch.set_float32_matmul_precision("high")
+    prev = tm._HOIST_KV
+    try:
+        torch.manual_seed(5)
+        a = EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.0, num_heads=4, n_layers=4,
+                                         num_embeddings=64, sem_id_dim=4, inference_verifier_fn=None,
+                                         max_pos=80).to(device).train()
+        b = copy.deepcopy(a)
+        if buckets_on:
+            buckets = dp.GradBuckets(b.parameters(), overlap=False, flat_views=True)
+            buckets.zero_grad()
+        batch = synthetic_tokenized_batch(48, 20, 4, 64, 11, device)
+        tm._HOIST_KV = False
+        ops._SEED["n"] = 0
+        la = a(batch).loss
+        la.backward()
+        calls = []
+        orig = ops.HoistedProjectionFunction.forward
+
+        def counted(ctx, x, *ws):
+            calls.append(len(ws))
+            return orig(ctx, x, *ws)
+        ops.HoistedProjectionFunction.forward = staticmethod(counted)
+        tm._HOIST_KV = True
+        ops._SEED["n"] = 0
+        try:
+            lb = b(batch).loss
+            lb.backward()
+        finally:
+            ops.HoistedProjectionFunction.forward = staticmethod(orig)
+        if buckets_on:
+            buckets.synchronize()
+        assert calls == [2]   # n_layers=4: two decoder layers, one hoisted launch for both
+        torch.testing.assert_close(lb.detach(), la.detach(), rtol=1e-6, atol=0)
+        for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+            if pa.grad is None:
+                assert pb.grad is None, n
+                continue
+            # split-K orders differ between the hoisted (M = 2 x 2A) and per-layer GEMMs: fp32 rounding only
+            scale = float(pa.grad.abs().max())
+            err = float((pb.grad - pa.grad).abs().max())
+            assert err <= 1e-4 * scale + 1e-7, (n, err, scale)
+    finally:
+        tm._HOIST_KV = prev
+        torch.set_float32_matmul_precision("highest")

@@ -300,3 +300,45 @@ def test_c_abi_entry_points_vs_oracle(device, B, max_q, max_k, H, causal, same):
     chk(dq, rdq, 1e-4, 1e-3, "dq")
     chk(dk, rdk, 1e-4, 1e-3, "dk")
     chk(dv, rdv, 1e-4, 1e-3, "dv")
+
+
+@pytest.mark.parametrize("qsplit", [1, 2, 3, 4])
+def test_fused_backward_query_splits(device, qsplit):
+    """The fused backward with each key block's query range split over `qsplit` workgroups (dK / dV
+    partials summed in split order by attn_kv_reduce_kernel; rq_attn_qsplit_set forces the count) vs
+    the fp64 oracle on ragged long sequences (ML-32M lengths, causal and not) incl. an empty one and
+    zero-padded tail rows; bitwise deterministic run to run."""
+    from rqvae_hip import _lib, ops
+    lib = _lib.load()
+    prev = lib.rq_attn_qsplit_set(qsplit)
+    try:
+        for causal in (False, True):
+            g = gi.rng(77 + qsplit + 5 * causal)
+            H, hd = 6, 64
+            A_ = H * hd
+            ls = [801, 0, 333, 64, 517]
+            cq = np.concatenate([[0], np.cumsum(ls)]).astype(np.int64)
+            T = int(cq[-1]) + 9
+            q = g.standard_normal((T, H, hd), dtype=np.float32)
+            k = g.standard_normal((T, H, hd), dtype=np.float32)
+            v = g.standard_normal((T, H, hd), dtype=np.float32)
+            do = g.standard_normal((T, H, hd), dtype=np.float32)
+            cqt = torch.from_numpy(cq).to(device)
+            runs = []
+            for _ in range(2):
+                qt, kt, vt = (torch.from_numpy(a.reshape(T, A_)).to(device).requires_grad_(True) for a in (q, k, v))
+                o = ops.varlen_attention(qt, kt, vt, cqt, cqt, H, causal, max(ls), max(ls))
+                o.backward(torch.from_numpy(do.reshape(T, A_)).to(device))
+                runs.append((o.detach(), qt.grad, kt.grad, vt.grad))
+            for a, b in zip(*runs):
+                assert torch.equal(a, b)
+            _, dq, dk, dv = runs[0]
+            n = int(cq[-1])
+            for t in (dq, dk, dv):
+                assert torch.count_nonzero(t[n:]) == 0
+            rdq, rdk, rdv = A.attn_bwd(q[:n], k[:n], v[:n], do[:n], cq, cq, causal)
+            for got, ref, what in ((dq, rdq, "dq"), (dk, rdk, "dk"), (dv, rdv, "dv")):
+                a = got[:n].cpu().double().numpy().reshape(ref.shape)
+                assert np.all(np.abs(a - ref) <= 1e-4 + 1e-3 * np.abs(ref)), (what, causal)
+    finally:
+        lib.rq_attn_qsplit_set(prev)

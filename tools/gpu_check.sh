@@ -25,6 +25,22 @@ for s in $steps; do
       run tests 600 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 120 --timeout-method thread \
         > "$O/gpu_tests.log" 2>&1 || exit 1
       tail -3 "$O/gpu_tests.log" ;;
+    gemmtests)   # split-K / accumulate / direct-grad GEMM parity only
+      run gemmtests 300 python -u -m pytest "$R/tests/test_gemm_splitk_epi_gpu.py" "$R/tests/test_gemm_x3s_gpu.py" \
+        "$R/tests/test_direct_grad_gpu.py" "$R/tests/test_gemm_bf16x3_gpu.py" -m gpu -x -q --timeout 120 \
+        --timeout-method thread > "$O/gemmtests.log" 2>&1 || { tail -30 "$O/gemmtests.log"; exit 1; }
+      tail -3 "$O/gemmtests.log" ;;
+    hoisttests)   # hoisted K/V projection + decoder paths it touches
+      run hoisttests 400 python -u -m pytest "$R/tests/test_direct_grad_gpu.py" "$R/tests/test_train_gpu.py" \
+        "$R/tests/test_reference_fixtures_gpu.py" "$R/tests/test_fused_decoder_gpu.py" "$R/tests/test_jagged_attention_gpu.py" -m gpu -x -q --timeout 120 \
+        --timeout-method thread > "$O/hoisttests.log" 2>&1 || { tail -40 "$O/hoisttests.log"; exit 1; }
+      tail -3 "$O/hoisttests.log" ;;
+    abhoist)
+      run abhoist 400 python -u "$R/tools/ab_hoist.py" hoist 2 > "$O/abhoist.jsonl" 2> "$O/abhoist.err"
+      tail -1 "$O/abhoist.jsonl" ;;
+    rqside)
+      run rqside 200 python -u "$R/tools/rq_side_ab.py" 20 3 > "$O/rqside.jsonl" 2> "$O/rqside.err"
+      cat "$O/rqside.jsonl" ;;
     bench)
       run bench 400 python -u "$R/bench.py" > "$O/bench.json" 2> "$O/bench.err"
       cat "$O/bench.json" ;;
@@ -84,6 +100,18 @@ for s in $steps; do
         --kernel-include-regex "rq_fwd|rq_dist" -f csv -d "$O/pmc_sq" -o q -- python3 "$R/tools/pmc_quantize.py" 5 > "$O/pmc_sq.log" 2>&1
       run pmc_sq2 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE \
         --kernel-include-regex "rq_fwd|rq_dist" -f csv -d "$O/pmc_sq2" -o q -- python3 "$R/tools/pmc_quantize.py" 5 > "$O/pmc_sq2.log" 2>&1
+      cd "$R" ;;
+    attnprof)   # kernel-level A/B of the attention forms (attn_ab2 alternates DMA / few-query forms on and off)
+      cd /tmp
+      run attnprof 200 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o attnab -- \
+        python3 "$R/tools/attn_ab2.py" 20 2 > "$O/attnprof.log" 2>&1
+      cd "$R" ;;
+    attnpmc)   # SQ counters of the Amazon-shape attention kernels (tools/attn_ab2.py, DMA forms on)
+      cd /tmp
+      run pmc_attn1 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \
+        --kernel-include-regex "attn_" -f csv -d "$O/pmc_attn1" -o a -- python3 "$R/tools/attn_ab2.py" 2 1 > "$O/pmc_attn1.log" 2>&1
+      run pmc_attn2 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE \
+        --kernel-include-regex "attn_" -f csv -d "$O/pmc_attn2" -o a -- python3 "$R/tools/attn_ab2.py" 2 1 > "$O/pmc_attn2.log" 2>&1
       cd "$R" ;;
     dp2)   # two ranks sharing the one GPU over gloo: exercises every multi-rank code path of bench.py
       RQVAE_DIST_BACKEND=gloo RQVAE_SHARE_DEVICE=1 run dp2 600 python -m torch.distributed.run --nnodes=1 \
