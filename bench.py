@@ -142,7 +142,11 @@ def gemm_launch_stats(timer, steps=1):
         if lay[4] == 0 and (best is None or ms * n > best[0]):
             best = (ms * n, ms, n, M, N, K, *lay[:4])
     _, ms, n, M, N, K, akc, bkc, asp, bsp = best
+    red_ms, red_n = timer.mean_ms("reduce_partials") if "reduce_partials" in timer.events else (0.0, 0)
     return {"shape": [M, N, K, akc, bkc], "operands_split": [asp, bsp], "epilogue": "store",
+            "splitk_reduction": "deferred: the weight-grad slab reductions of a step run batched in "
+                                "rq_reduce_partials launches (%.1f per step, %.4f ms each), not in this launch"
+                                % (red_n / steps, red_ms) if red_n else "in-launch",
             "launch_ms": round(ms, 4), "launches": n,
             "flops_per_launch": 2 * M * N * K, "algorithmic_bytes": 4 * (M * K + N * K + M * N),
             "achieved_tflops": round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 2),
@@ -252,8 +256,10 @@ def main():
     model = build_model(device)
     # grads become ready decoder -> codebooks -> encoder: the first bucket's all-reduce overlaps the
     # encoder MLP backward
+    # flat views even at N=1 (as train_rqvae.py runs it): weight grads accumulate straight into the
+    # buckets (no AccumulateGrad pass) and their split-K reductions share a few deferred launches
     buckets = dp.GradBuckets([list(model.decoder.parameters()) + list(model.layers.parameters()),
-                              list(model.encoder.parameters())])
+                              list(model.encoder.parameters())], flat_views=True)
     buckets.broadcast_params()
     opt = make_adamw(model.parameters(), CFG["lr"], CFG["wd"])
     gen = torch.Generator(device=device).manual_seed(1000 + rk)
@@ -343,8 +349,8 @@ def main():
         if gemm is not None:
             M, N, K, akc, bkc = gemm["shape"]
             asp, bsp = gemm["operands_split"]
-            gtraffic, gtraffic_note = pmc_traffic(
-                regex="gemm_bf16x3_kernel|gemm_x3w_kernel|x3_reduce_kernel", launches=5, script=(
+            gtraffic, gtraffic_note = pmc_traffic(   # the GEMM kernel alone (its slab reduction is deferred)
+                regex="gemm_bf16x3_kernel|gemm_x3w_kernel", launches=5, script=(
                     "pmc_gemm.py", str(M), str(N), str(K), str(akc), str(bkc), "5", str(asp), str(bsp)))
     q_roof = {"kernel": "rq_quantize_fwd", "bound": "mfma", "achieved": round(achieved, 3),
               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),

@@ -117,6 +117,13 @@ int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, co
 int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
                             int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
                             void* workspace, size_t ws_bytes, void* stream);
+/* rq_rmsnorm_dropout_bwd2 with a deferred weight-gradient reduction: defer = 1 leaves gw's per-workgroup
+ * partials (*parts rows of D floats) at the start of the workspace and skips their reduction (*parts = 0
+ * when nothing was deferred); rq_reduce_partials (layout 1) later adds them into gw, batched with other
+ * deferred reductions into one launch. */
+int rq_rmsnorm_dropout_bwd3(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
+                            int defer, int* parts, void* workspace, size_t ws_bytes, void* stream);
 
 /* Elementwise dropout fusions over n fp32 elements (n % 4 == 0, 16-byte aligned), same mask
  * generator as above (element index = position in the buffer):
@@ -193,6 +200,21 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
                        int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
                        const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
                        int accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* rq_gemm_bf16x3_ex2 with a deferred split-K reduction: with accumulate = 1, the plain epilogue and defer =
+ * 1, a split call leaves its *splits partial slabs (M x N fp32 each) at the start of the workspace and
+ * returns without reducing (*splits = 0: the call completed C itself); the caller adds them into C later
+ * with rq_reduce_partials (layout 0). Lets the many small weight-gradient reductions of one backward
+ * share a few launches. */
+int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                       int accumulate, int defer, int* splits, void* workspace, size_t ws_bytes, void* stream);
+/* Deferred partial reductions, up to 48 per launch: for each entry i, out_i[j] = (accumulate_i ? out_i[j] :
+ * 0) + sum_{s < S_i} P_i[s n_i + j], j < n_i (n_i % 4 == 0, 16-B aligned pointers), in the order of the
+ * reduction it replaces (layout 0: rq_gemm_bf16x3_ex3's slab reduction; layout 1: rq_rmsnorm_dropout_bwd3's
+ * weight-gradient partials) — bitwise the immediate result. Entries must not share an output. Host arrays. */
+int rq_reduce_partials(int count, const float* const* P, float* const* out, const int64_t* n, const int* S,
+                       const int* layout, const int* accumulate, void* stream);
 
 /* Which kernel rq_gemm_bf16x3_ex runs for a call: 1 = the wide 256 x 256-tile kernel (both operands
  * split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile kernel, 2 = its 64 x 64-tile form (launches

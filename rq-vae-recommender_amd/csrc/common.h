@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <math.h>
+#include <algorithm>
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4v __attribute__((ext_vector_type(4)));

@@ -1422,10 +1422,11 @@ size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate
   return x3_workspace_bytes(M, N, K, accumulate != 0);
 }
 
-int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
                        int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
                        const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                       int accumulate, void* workspace, size_t ws_bytes, void* stream) {
+                       int accumulate, int defer, int* splits, void* workspace, size_t ws_bytes, void* stream) {
+  if (splits) *splits = 0;
   const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
   RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
                    epilogue <= 3,
@@ -1562,6 +1563,10 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
   RQ_CHECK_ARG(launched, "rq_gemm_bf16x3: operand combination (a_kcontig %d, a_split %d, b_kcontig %d, b_split %d) "
                          "not built for epilogue %d", a_kcontig, (int)asp, b_kcontig, (int)bsp, epilogue);
   RQ_LAUNCH_CHECK("gemm_bf16x3_kernel");
+  if (slab && defer && accumulate && epilogue == kEpiStore && splits) {   // the caller reduces later
+    *splits = pl.S;                                                    // (rq_reduce_partials, layout 0)
+    return 0;
+  }
   if (slab) {
     const int64_t n = M * N;
     const dim3 rg((unsigned)((n / 4 + 63) / 64)), rb(256);
@@ -1575,6 +1580,129 @@ int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcont
     }
 #undef RQ_X3R
     RQ_LAUNCH_CHECK("x3_reduce_kernel");
+  }
+  return 0;
+}
+
+int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                       int accumulate, void* workspace, size_t ws_bytes, void* stream) {
+  return rq_gemm_bf16x3_ex3(A, A_lo, lda, a_kcontig, B, B_lo, ldb, b_kcontig, M, N, K, C, ldc, epilogue, Z, H_hi, H_lo,
+                            ldh, p, seed, accumulate, 0, nullptr, workspace, ws_bytes, stream);
+}
+
+// Deferred partial reductions, many in one launch: out_i[j] (+)= sum_s P_i[s n_i + j] for every entry i,
+// each in the SAME order as the reduction it replaces — layout 0 = x3_reduce_kernel's (4 wave lanes over
+// s, combined in wave order; a workgroup owns 64 float4 columns), layout 1 = rms_reduce_kernel's (64 lanes
+// over s, fixed LDS tree; 4 float4 columns) — so a deferred result is bitwise the immediate one.
+constexpr int kRedSegMax = 48;
+struct RedSegTable {
+  const float* P[kRedSegMax];
+  float* out[kRedSegMax];
+  int64_t n[kRedSegMax];
+  int S[kRedSegMax];
+  int layout[kRedSegMax];
+  int acc[kRedSegMax];
+  int blk0[kRedSegMax + 1];
+  int count;
+};
+
+__global__ void __launch_bounds__(256) reduce_partials_kernel(RedSegTable t) {
+  __shared__ float4 red[256];
+  const int b = blockIdx.x;
+  int e = 0;
+  while (e + 1 < t.count && b >= t.blk0[e + 1]) ++e;
+  const int lb = b - t.blk0[e];
+  const float* __restrict__ P = t.P[e];
+  float* __restrict__ out = t.out[e];
+  const int64_t n = t.n[e];
+  const int S = t.S[e];
+  const int tid = threadIdx.x;
+  if (t.layout[e] == 0) {
+    const int wave = tid >> 6, lane = tid & 63;
+    const int64_t j = ((int64_t)lb * 64 + lane) * 4;
+    const bool ok = j < n;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok)
+      for (int s = wave; s < S; s += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+    red[wave * 64 + lane] = a;
+    __syncthreads();
+    if (wave == 0 && ok) {
+      float4 r = red[lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float4 v = red[w * 64 + lane];
+        r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+      }
+      if (t.acc[e]) {
+        const float4 c = *reinterpret_cast<const float4*>(out + j);
+        r = make_float4(c.x + r.x, c.y + r.y, c.z + r.z, c.w + r.w);
+      }
+      *reinterpret_cast<float4*>(out + j) = r;
+    }
+  } else {
+    constexpr int kC = 4, kQ = 256 / kC;
+    const int c = tid % kC, q = tid / kC;
+    const int64_t j = ((int64_t)lb * kC + c) * 4;
+    const bool ok = j < n;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok)
+      for (int s = q; s < S; s += kQ) {
+        const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+    red[q * kC + c] = a;
+    __syncthreads();
+#pragma unroll
+    for (int h = kQ / 2; h >= 1; h >>= 1) {
+      if (q < h) {
+        const float4 u = red[q * kC + c], v = red[(q + h) * kC + c];
+        red[q * kC + c] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+      }
+      __syncthreads();
+    }
+    if (q == 0 && ok) {
+      float4 r = red[c];
+      if (t.acc[e]) {
+        const float4 o = *reinterpret_cast<const float4*>(out + j);
+        r = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
+      }
+      *reinterpret_cast<float4*>(out + j) = r;
+    }
+  }
+}
+
+int rq_reduce_partials(int count, const float* const* P, float* const* out, const int64_t* n, const int* S,
+                       const int* layout, const int* accumulate, void* stream) {
+  RQ_CHECK_ARG(count >= 0 && (count == 0 || (P && out && n && S && layout && accumulate)),
+               "rq_reduce_partials: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  for (int base = 0; base < count; base += kRedSegMax) {
+    RedSegTable t;
+    t.count = std::min(kRedSegMax, count - base);
+    int blk = 0;
+    for (int i = 0; i < t.count; ++i) {
+      const int k = base + i;
+      RQ_CHECK_ARG(P[k] && out[k] && n[k] > 0 && n[k] % 4 == 0 && S[k] >= 1 && (layout[k] == 0 || layout[k] == 1) &&
+                       ((uintptr_t)P[k] | (uintptr_t)out[k]) % 16 == 0,
+                   "rq_reduce_partials: entry %d: need n %% 4 == 0, S >= 1, layout 0/1, 16-B aligned pointers", k);
+      t.P[i] = P[k];
+      t.out[i] = out[k];
+      t.n[i] = n[k];
+      t.S[i] = S[k];
+      t.layout[i] = layout[k];
+      t.acc[i] = accumulate[k] != 0;
+      t.blk0[i] = blk;
+      blk += (int)((n[k] / 4 + (layout[k] == 0 ? 63 : 3)) / (layout[k] == 0 ? 64 : 4));
+    }
+    t.blk0[t.count] = blk;
+    if (blk == 0) continue;
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)blk), dim3(256), 0, st, t);
+    RQ_LAUNCH_CHECK("reduce_partials_kernel");
   }
   return 0;
 }

@@ -529,9 +529,10 @@ int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float e
   return rq_rmsnorm_dropout_fwd(x, w, B, D, eps, 0.f, 0, y, rstd, stream);
 }
 
-int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+int rq_rmsnorm_dropout_bwd3(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
                             int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
-                            void* workspace, size_t ws_bytes, void* stream) {
+                            int defer, int* parts, void* workspace, size_t ws_bytes, void* stream) {
+  if (parts) *parts = 0;
   RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_bwd: need D %% 4 == 0, D <= 4096");
   RQ_CHECK_ARG(gw && (B == 0 || (x && w && rstd && gy && gx)), "rq_rmsnorm_bwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
@@ -550,10 +551,21 @@ int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, c
   RMS_SWITCH((int)((D + 255) / 256), RMS_B)
 #undef RMS_B
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd");
+  if (defer && parts) {   // gw partials [nblk][D] left in the workspace: rq_reduce_partials (layout 1) sums them
+    *parts = nblk;
+    return 0;
+  }
   hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + kRedCols - 1) / kRedCols)), dim3(256), 0, s, part, nblk, D, gw,
                      accumulate_gw);
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd(reduce)");
   return 0;
+}
+
+int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
+                            void* workspace, size_t ws_bytes, void* stream) {
+  return rq_rmsnorm_dropout_bwd3(x, w, rstd, gy, gres, B, D, p, seed, gx, gw, accumulate_gw, 0, nullptr, workspace,
+                                 ws_bytes, stream);
 }
 
 int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,

@@ -39,6 +39,7 @@ _SIGS = {
     "rq_rmsnorm_dropout_fwd": ([_P, _P, _I64, _I64, _F, _F, _U64, _P, _P, _P], _I),
     "rq_rmsnorm_dropout_bwd": ([_P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _P, _SZ, _P], _I),
     "rq_rmsnorm_dropout_bwd2": ([_P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _I, _P, _SZ, _P], _I),
+    "rq_rmsnorm_dropout_bwd3": ([_P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _I, _I, _P, _P, _SZ, _P], _I),
     "rq_dropout_params": ([_F, _P, _P], _I),
     "rq_silu_dropout_fwd": ([_P, _I64, _F, _U64, _P, _P], _I),
     "rq_silu_dropout_bwd": ([_P, _P, _I64, _F, _U64, _P, _P], _I),
@@ -53,6 +54,9 @@ _SIGS = {
     "rq_gemm_bf16x3_workspace2": ([_I64, _I64, _I64, _I], _SZ),
     "rq_gemm_bf16x3_ex2": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
                             _U64, _I, _P, _SZ, _P], _I),
+    "rq_gemm_bf16x3_ex3": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
+                            _U64, _I, _I, _P, _P, _SZ, _P], _I),
+    "rq_reduce_partials": ([_I, _P, _P, _P, _P, _P, _P, _P], _I),
     "rq_gemm_bf16x3_choice": ([_I64, _I64, _I64, _I, _I, _I, _I, _I, _P], _I),
     "rq_gemm_x3w_enable": ([_I], _I),
     "rq_gemm_x3s_enable": ([_I], _I),

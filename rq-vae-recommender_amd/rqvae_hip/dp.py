@@ -141,6 +141,13 @@ def direct_grad(p) -> Optional[torch.Tensor]:
     return e[0]
 
 
+def defer_ok(p) -> bool:
+    """True when p's owner GradBuckets batches the split-K / RMSNorm weight-gradient reductions into its
+    flat views (ops.flush_reductions at its flush points) instead of reducing per op."""
+    owner = _OWNER.get(id(p))
+    return owner is not None and owner[0].defer
+
+
 def direct_grad_done(p) -> None:
     """The caller has added its contribution into p's flat-bucket view. Nothing to do: the op returns
     None for p to autograd, and the engine still runs p's AccumulateGrad node (with an undefined
@@ -154,7 +161,7 @@ class GradBuckets:
     """Flat gradient buffers + bucketed async all-reduce for a module's parameters."""
 
     def __init__(self, params, bucket_bytes: int = 32 << 20, average: bool = True, overlap: bool = True,
-                 flat_views: bool = False, force_exchange: bool = False):
+                 flat_views: bool = False, force_exchange: bool = False, defer_reductions: bool = True):
         """`params`: an iterable of parameters (buckets follow reverse registration order, ~ the order
         grads become ready), or a list of parameter groups given in the order their grads become
         ready (each group gets its own buckets, so an early group's all-reduce overlaps the rest of
@@ -164,7 +171,10 @@ class GradBuckets:
         `flat_views=True`: gradients live in the flat buffers even with one process, so they sit
         at fixed addresses that several captured graphs can share.
         `overlap=True` is also right for captured steps: GraphedSteps suspends the hooks where the
-        backend cannot be captured (gloo) and exchanges after the replay instead."""
+        backend cannot be captured (gloo) and exchanges after the replay instead.
+        `defer_reductions=True`: weight-gradient partial reductions into the flat views (split-K slabs,
+        RMSNorm partials) are batched (ops.flush_reductions) and run before a bucket's exchange and in
+        finish / synchronize / zero_grad — so gradients are complete only after synchronize()."""
         params = list(params)
         grouped = bool(params) and isinstance(params[0], (list, tuple))
         groups = [list(g) for g in params] if grouped else [list(reversed(params))]
@@ -178,6 +188,7 @@ class GradBuckets:
         # single process without flat_views: no flat views (AccumulateGrad steals, no add_)
         self.active = self.exchange or flat_views
         self.overlap = overlap and self.exchange
+        self.defer = bool(defer_reductions) and self.active
         self.buckets = []
         self._pending = {}
         self._next = 0             # buckets [0, _next) are launched this pass (launch order = index order)
@@ -277,6 +288,7 @@ class GradBuckets:
             return
         from . import ops
         ops.join_wgrad_stream()   # weight grads accumulated on the side stream land before the exchange
+        ops.flush_reductions()    # ... and every deferred reduction into the flat views
         self._pending[bi] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, async_op=True)
 
     def zero_grad(self):
@@ -284,6 +296,9 @@ class GradBuckets:
             for p in self.params:
                 p.grad = None
             return
+        if self.defer:   # a step left unsynchronised: its deferred reductions must not land after the zeroing
+            from . import ops
+            ops.flush_reductions()
         unused = self._unused or ()
         for b in self.buckets:
             b["flat"].zero_()
@@ -317,6 +332,7 @@ class GradBuckets:
         work (no host sync): GraphedSteps captures it at the end of the replayed backward."""
         from . import ops
         ops.join_wgrad_stream()
+        ops.flush_reductions()
         if self.exchange:
             while self._next < len(self.buckets):
                 self._launch(self._next)

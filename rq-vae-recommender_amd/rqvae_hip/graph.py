@@ -149,6 +149,7 @@ class GraphedSteps:
             out.backward()
             out = out.detach()
         ops.join_wgrad_stream()   # side-stream weight grads rejoin inside the capture
+        ops.flush_reductions()    # deferred weight-grad reductions too (their list lives only at capture)
         if exchange and b is not None:
             b.finish()
         if self.capture:   # eager bodies draw their dropout keys from the host counter

@@ -356,12 +356,12 @@ def _wgrad_into(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: 
         side = _side_stream(sink.device)
         side.wait_stream(main)          # operands and the zeroed bucket are ready
         with torch.cuda.stream(side):   # the split-K slab workspace is allocated on the side stream too
-            gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True)
+            gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True, defer=dp.defer_ok(weight))
         for t in _operand_tensors(g) + _operand_tensors(inp):
             t.record_stream(side)       # freed operands are not reused until the side stream is past them
         _SIDE["used"] = True
     else:
-        gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True)
+        gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True, defer=dp.defer_ok(weight))
     dp.direct_grad_done(weight)
     return None
 
@@ -382,12 +382,13 @@ def _x3_workspace(M: int, N: int, K: int, accumulate: bool = False) -> int:
 
 def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
             Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
-            accumulate: bool = False):
+            accumulate: bool = False, defer: bool = False):
     """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex2). a / b: fp32
     tensors or Split. Returns C (EPI_STORE; EPI_ADD: A B^T + Z), (C, H) (EPI_SILU_FWD: C = z,
     H = split(Dropout(SiLU(z)))) or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split
     of shape (M, N). `out`: the (M, N) contiguous fp32 destination of C; `accumulate` (EPI_STORE
-    only): out += A B^T."""
+    only): out += A B^T; with `defer` a split call's slab reduction joins the pending batch
+    (flush_reductions) instead of running now."""
     def desc(t):
         if isinstance(t, Split):
             return t.hi, t.lo, t.hi.shape[-1], 1
@@ -410,17 +411,69 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
     nbytes = _x3_workspace(M, N, K, accumulate)
     ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8) if nbytes else None
-    args = ("rq_gemm_bf16x3_ex2", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
-            M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
-            float(p), int(seed), int(accumulate), ptr(ws), nbytes, stream_handle(dev))
+    defer = bool(defer and accumulate and nbytes)
+    if defer and C.data_ptr() in _DEFER["outs"]:
+        flush_reductions()   # a pending reduction into the same output must land first
+    if defer:
+        import ctypes
+        splits = ctypes.c_int(0)
+        args = ("rq_gemm_bf16x3_ex3", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
+                M, N, K, ptr(C), N, int(epilogue), ptr(Z), None, None, N, float(p), int(seed), 1, 1,
+                ctypes.byref(splits), ptr(ws), nbytes, stream_handle(dev))
+    else:
+        args = ("rq_gemm_bf16x3_ex2", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
+                M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
+                float(p), int(seed), int(accumulate), ptr(ws), nbytes, stream_handle(dev))
     if TIMER.wants("gemm_bf16x3"):
         TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}{int(accumulate)}",
                      call, *args)
     else:
         call(*args)
+    if defer and splits.value > 0:
+        _defer_push(ws, C, M * N, splits.value, 0)
     if epilogue in (EPI_STORE, EPI_ADD):
         return C
     return (C, H) if epilogue == EPI_SILU_FWD else H
+
+
+# Deferred partial reductions (rq_reduce_partials): split-K weight-gradient slabs and RMSNorm weight-
+# gradient partials that accumulate into flat gradient buckets wait here and run as ONE launch (per 48)
+# at the next flush — before a bucket's exchange, in GradBuckets.finish / synchronize / zero_grad, and at
+# the end of a captured step — instead of one reduction launch each (~40 per decoder step).
+_DEFER = {"pending": [], "outs": set()}
+
+
+def _defer_push(ws: torch.Tensor, out: torch.Tensor, n: int, S: int, layout: int):
+    _DEFER["pending"].append((ws, out, int(n), int(S), int(layout), torch.cuda.current_stream(out.device)))
+    _DEFER["outs"].add(out.data_ptr())
+
+
+def flush_reductions() -> None:
+    """Run every pending deferred reduction (stream-ordered after their producers: side-stream weight
+    grads are joined first) and release their partial buffers."""
+    pend = _DEFER["pending"]
+    if not pend:
+        return
+    import ctypes
+    join_wgrad_stream()
+    dev = pend[0][1].device
+    cur = torch.cuda.current_stream(dev)
+    for ws, out, _, _, _, st in pend:
+        if st != cur:
+            cur.wait_stream(st)
+            ws.record_stream(cur)
+    n = len(pend)
+    P = ctypes.c_void_p * n
+    TIMER.around("reduce_partials", call, "rq_reduce_partials", n, P(*[e[0].data_ptr() for e in pend]),
+                 P(*[e[1].data_ptr() for e in pend]), (ctypes.c_int64 * n)(*[e[2] for e in pend]),
+                 (ctypes.c_int * n)(*[e[3] for e in pend]), (ctypes.c_int * n)(*[e[4] for e in pend]),
+                 (ctypes.c_int * n)(*([1] * n)), stream_handle(dev))
+    _DEFER["pending"] = []
+    _DEFER["outs"] = set()
+
+
+def pending_reductions() -> int:
+    return len(_DEFER["pending"])
 
 
 def gemm_x3_choice(M: int, N: int, K: int, a_split: bool, b_split: bool, a_kcontig: bool, b_kcontig: bool,
@@ -785,9 +838,21 @@ def _rmsnorm_bwd(x2, weight, rstd, gy, gres, p: float, seed: int, need_w: bool):
     gw = sink if sink is not None else torch.empty((D,), device=x2.device, dtype=torch.float32)
     nbytes = _lib.load().rq_rmsnorm_bwd_workspace(B, D)
     ws = torch.empty((nbytes,), device=x2.device, dtype=torch.uint8)
-    call("rq_rmsnorm_dropout_bwd2", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
-         ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
-         int(sink is not None), ptr(ws), nbytes, stream_handle(x2.device))
+    defer = sink is not None and dp.defer_ok(weight)
+    if defer and sink.data_ptr() in _DEFER["outs"]:
+        flush_reductions()
+    if defer:
+        import ctypes
+        parts = ctypes.c_int(0)
+        call("rq_rmsnorm_dropout_bwd3", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
+             ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
+             1, 1, ctypes.byref(parts), ptr(ws), nbytes, stream_handle(x2.device))
+        if parts.value > 0:
+            _defer_push(ws, sink, D, parts.value, 1)
+    else:
+        call("rq_rmsnorm_dropout_bwd2", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
+             ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
+             int(sink is not None), ptr(ws), nbytes, stream_handle(x2.device))
     if sink is not None:
         dp.direct_grad_done(weight)
         return gx, None

@@ -225,6 +225,41 @@ def rqvae_fixture(tag, inp, hidden, D, K, L, B, seed, store_grads_full):
     save(f"rqvae_{tag}.npz", **out)
 
 
+def rqvae_ties_fixture(inp=768, hidden=(512, 256, 128), D=64, K=256, L=3, B=512, seed=12, pairs=24, eps=3e-6):
+    """ML-32M dims with near-tied codebooks: at every level, `pairs` codewords get a twin c + eps * |c| u
+    (u a random unit vector), so the items nearest to them sit on a top-2 gap of ~1e-6 — far below the
+    'high' margin (1e-4) — and the margin-unsafe branch of the 'high' contract is exercised against the
+    reference's own ids. Stores the reference eval ids, per-level residuals and margins."""
+    hidden = list(hidden)
+    model = RqVae(input_dim=inp, embed_dim=D, hidden_dims=hidden, codebook_size=K,
+                  codebook_kmeans_init=False, codebook_mode=QuantizeForwardMode.ROTATION_TRICK,
+                  n_layers=L, n_cat_features=0, commitment_weight=0.25)
+    cb_items = gi.items(max(4 * K, 512), inp, seed + 100)
+    model.load_state_dict(rqvae_state((inp, hidden, D), [np.zeros((K, D), F32)] * L, seed))
+    cbs = make_codebooks(model, cb_items, K, L, seed)
+    g = gi.rng(seed + 777)
+    for l in range(L):
+        src = g.permutation(K)[:2 * pairs]
+        for a, b in zip(src[:pairs], src[pairs:]):
+            u = g.standard_normal(D)
+            u /= np.linalg.norm(u)
+            cbs[l][b] = (cbs[l][a].astype(np.float64) + eps * np.linalg.norm(cbs[l][a]) * u).astype(F32)
+    model.load_state_dict(rqvae_state((inp, hidden, D), cbs, seed))
+    x_np = gi.items(B, inp, seed + 300)
+    model.eval()
+    with torch.no_grad():
+        ev = model.get_semantic_ids(torch.from_numpy(x_np))
+        res = model.encode(torch.from_numpy(x_np)).numpy()
+        margins, res_l = [], []
+        for l in range(L):
+            res_l.append(res.copy())
+            margins.append(top2_margin(res, cbs[l]))
+            res = res - cbs[l][ev.sem_ids[:, l].numpy()]
+    save("rqvae_ml32m_ties.npz", inp=inp, hidden=np.array(hidden, np.int64), D=D, K=K, L=L, B=B, seed=seed,
+         x_checksum=gi.checksum(x_np), codebooks=np.stack(cbs), eval_sem_ids=ev.sem_ids.numpy().astype(np.int64),
+         eval_level_residuals=np.stack(res_l).astype(F32), eval_margin=np.stack(margins, 1))
+
+
 # ------------------------------------------------------------------------ jagged
 def jagged_fixture():
     out = {}
@@ -592,6 +627,7 @@ FIXTURES = {
                                          store_grads_full=True),
     "rqvae_ml32m": lambda: rqvae_fixture("ml32m", inp=768, hidden=[512, 256, 128], D=64, K=256, L=3, B=64, seed=12,
                                          store_grads_full=False),
+    "rqvae_ml32m_ties": rqvae_ties_fixture,
     "jagged": jagged_fixture,
     "decoder_small": lambda: decoder_fixture("small", E=32, A=64, H=4, n_layers=4, K=16, L1=4, B=6, n_max=5, seed=21),
     # configs[3] (decoder_ml32m.gin: A=384, H=6, 8 layers, E=128): one sequence of 200 items = 801 ctx tokens

@@ -159,3 +159,49 @@ def test_hoisted_kv_matches_per_layer(device, buckets_on):
     finally:
         tm._HOIST_KV = prev
         torch.set_float32_matmul_precision("highest")
+
+
+@pytest.mark.parametrize("model_kind", ["mlp", "decoder"])
+def test_deferred_reductions_bitwise(device, model_kind):
+    """Deferred weight-gradient reductions (split-K slabs and RMSNorm partials batched into
+    rq_reduce_partials launches at GradBuckets' flush points) give bitwise the gradients of the
+    immediate reductions; they are pending after backward and flushed by synchronize()."""
+    from data.processed import synthetic_tokenized_batch
+    from modules.model import EncoderDecoderRetrievalModel
+    from rqvae_hip import dp, ops
+    torch.set_float32_matmul_precision("high")
+    try:
+        torch.manual_seed(7)
+        if model_kind == "mlp":
+            a = _Net().to(device)
+            gen = torch.Generator(device=device).manual_seed(3)
+            x = torch.randn(8192, 64, generator=gen, device=device)
+            g = torch.randn(8192, 64, generator=gen, device=device)
+
+            def run(m):
+                m(x).backward(g)
+        else:
+            a = EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.0, num_heads=4, n_layers=4,
+                                             num_embeddings=64, sem_id_dim=4, inference_verifier_fn=None,
+                                             max_pos=80).to(device).train()
+            batch = synthetic_tokenized_batch(64, 20, 4, 64, 9, device)
+
+            def run(m):
+                ops._SEED["n"] = 0
+                m(batch).loss.backward()
+        b = copy.deepcopy(a)
+        res = {}
+        for m, defer in ((a, False), (b, True)):
+            buckets = dp.GradBuckets(m.parameters(), overlap=False, flat_views=True, defer_reductions=defer)
+            buckets.zero_grad()
+            run(m)
+            if defer:
+                assert ops.pending_reductions() > 0
+            buckets.synchronize()
+            assert ops.pending_reductions() == 0
+            res[defer] = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        assert res[True].keys() == res[False].keys()
+        for n in res[False]:
+            assert torch.equal(res[True][n], res[False][n]), n
+    finally:
+        torch.set_float32_matmul_precision("highest")

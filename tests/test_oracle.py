@@ -46,6 +46,19 @@ def test_quantize_level(golden, tag):
         _close(gcb[rows], z[f"{mname}_gcb"], 2e-4, 1e-5, f"{mname} grad_cb")
 
 
+def test_quantize_chain_near_ties(golden):
+    """The oracle's argmin on the reference's own level residuals of the near-tie fixture (twin codewords,
+    top-2 gaps ~1e-6): the reference's ids on every row whose fp64 gap exceeds fp32 resolution (1e-6),
+    lowest index among exact ties (torch.min, quantize.py:121)."""
+    z = golden("rqvae_ml32m_ties")
+    res, cbs, ref, margin = z["eval_level_residuals"], z["codebooks"], z["eval_sem_ids"], z["eval_margin"]
+    for l in range(int(z["L"])):
+        ids = Q.argmin_first(Q.l2_dist(res[l], cbs[l]))
+        ok = margin[:, l] > 1e-6
+        assert ok.mean() > 0.8
+        assert np.array_equal(ids[ok], ref[ok, l]), l
+
+
 def _rqvae_state(z):
     inp, hidden, D, L, seed = int(z["inp"]), [int(h) for h in z["hidden"]], int(z["D"]), int(z["L"]), int(z["seed"])
     enc = gi.mlp_weights([inp] + hidden + [D], seed)

@@ -269,6 +269,41 @@ def test_decoder_vs_reference(golden, device, tag, prec):
 
 
 # ------------------------------------------------------------------------------------------- C2
+def test_rqvae_high_precision_near_ties(golden, device):
+    """The 'high' margin contract on its unsafe branch, against the reference's own ids: codebooks with
+    near-duplicate codewords (`rqvae_ml32m_ties.npz`, ~25 % of 512 rows within a 1e-4 top-2 gap at some
+    level). Safe rows: ids exact. Unsafe rows: the first level whose id differs from the reference's must
+    be a near-tie in the REFERENCE's own residual (fp64 distance of our codeword within 1e-4 relative of
+    the reference's minimum), i.e. a flip only ever swaps twins; the flip rate is reported."""
+    from test_quantize_gpu import _rqvae
+    z = golden("rqvae_ml32m_ties")
+    model = _rqvae(z, device)
+    x = torch.from_numpy(gi.items(int(z["B"]), int(z["inp"]), int(z["seed"]) + 300)).to(device)
+    torch.set_float32_matmul_precision("high")
+    try:
+        model.eval()
+        with torch.no_grad():
+            ids = model.get_semantic_ids(x).sem_ids.cpu().numpy()
+    finally:
+        torch.set_float32_matmul_precision("highest")
+    ref, margin, cbs = z["eval_sem_ids"], z["eval_margin"], z["codebooks"].astype(np.float64)
+    res = z["eval_level_residuals"].astype(np.float64)
+    safe = (margin > 1e-4).all(1)
+    assert 0.5 < safe.mean() < 0.95      # both branches populated
+    assert np.array_equal(ids[safe], ref[safe])
+    flips = 0
+    for r in np.nonzero(~safe)[0]:
+        diff = np.nonzero(ids[r] != ref[r])[0]
+        if len(diff) == 0:
+            continue
+        flips += 1
+        l = int(diff[0])
+        d = ((res[l, r][None] - cbs[l]) ** 2).sum(1)
+        assert margin[r, l] <= 1e-4, (r, l)
+        assert d[ids[r, l]] - d[ref[r, l]] <= 1e-4 * abs(d[ref[r, l]]), (r, l)
+    print(f"near-tie flip rate: {flips} / {int((~safe).sum())} unsafe rows")
+
+
 def test_rqvae_high_precision_margin_contract(golden, device):
     """RQ-VAE ML-32M fixture at 'high': ids exact on margin-safe rows (reference top-2 relative gap >
     1e-4 at every level), reported flip rate on the rest; losses rel 1e-4; grads rel 1e-3 in norm."""
