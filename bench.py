@@ -463,7 +463,7 @@ def measure_trainers(iters=30):
                               "wall_s": round(time.perf_counter() - t0, 1)}
         ckpt = sorted(glob.glob(tmp + "/vae/checkpoint_*.pt"))[-1]
         t0 = time.perf_counter()
-        train_decoder.train(iterations=iters, batch_size=DEC["B"], learning_rate=DEC["lr"], weight_decay=DEC["wd"],
+        train_decoder.train(iterations=2 * iters, batch_size=DEC["B"], learning_rate=DEC["lr"], weight_decay=DEC["wd"],
                             dataset=RecDataset.AMAZON, pretrained_rqvae_path=ckpt, decoder_embed_dim=DEC["E"],
                             dropout_p=DEC["dropout"], attn_heads=DEC["H"], attn_embed_dim=DEC["A"],
                             attn_layers=DEC["layers"], save_dir_root=tmp + "/dec/", log_every=10 ** 9, **vae)

@@ -127,10 +127,17 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     t0, hist = time.time(), []
     t_from = start_iter + min(5, (iterations - start_iter) // 2)   # measured span: [t_from, iterations)
     t_mark, toks = None, 0
+    # steady state: the iterations after the last graph capture (a new row bucket's capture costs two
+    # eager warm-up passes + the capture; a long run amortises the few buckets a dataset has)
+    s_mark, s_from, s_toks = None, None, 0
     for it in range(start_iter, iterations):
         if it == t_from:
             torch.cuda.synchronize()
             t_mark = time.perf_counter()
+        if t_mark is not None and s_mark is None:
+            torch.cuda.synchronize()
+            s_mark, s_from, s_toks = time.perf_counter(), it, 0
+        n_graphs = len(graphed.graphs) if graphed is not None else 0
         model.train()
         if graphed is None:
             buckets.zero_grad()
@@ -149,6 +156,7 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
             counts = (data.seq_mask.sum(1) * tokenizer.sem_ids_dim).tolist()
             if t_mark is not None:
                 toks += sum(counts) + len(counts)   # context tokens (+ the user token per sequence)
+                s_toks += sum(counts) + len(counts)
             tok = tokenizer(batch_to(data, device))
             register_row_counts(tok.seq_mask, counts)
             # this rank's shard mean -> share of the GLOBAL-batch mean (unequal, token-balanced shards)
@@ -165,11 +173,19 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
         opt.step()
         sched.step()
         hist.append(total)
+        if graphed is not None and len(graphed.graphs) != n_graphs:
+            s_mark = None   # this iteration captured: the steady span restarts after it
         if it == iterations - 1 and t_mark is not None:
             torch.cuda.synchronize()
-            dt = time.perf_counter() - t_mark
+            t_end = time.perf_counter()
+            dt = t_end - t_mark
+            steady = {}
+            if s_mark is not None and iterations - s_from >= 3:
+                ds = t_end - s_mark
+                steady = dict(steady_iter_ms=ds * 1e3 / (iterations - s_from), steady_iters=iterations - s_from,
+                              steady_ctx_tokens_per_s_rank=s_toks / ds)
             LAST_RUN.update(iter_ms=dt * 1e3 / max(1, iterations - t_from), timed_iters=iterations - t_from,
-                            ctx_tokens_per_s_rank=toks / dt, world=world,
+                            ctx_tokens_per_s_rank=toks / dt, world=world, **steady,
                             step_mode="hipgraph" if graphed is not None else "eager",
                             graphs=len(graphed.graphs) if graphed is not None else 0,
                             eager_steps=graphed.eager_steps if graphed is not None else iterations - start_iter,

@@ -77,6 +77,13 @@ for s in $steps; do
       run attn_dma1 200 python -u "$R/tools/attn_probe.py" > "$O/attn_dma1.jsonl" 2> "$O/attn_dma1.err"
       RQ_ATTN_DMA=0 run attn_dma0 200 python -u "$R/tools/attn_probe.py" > "$O/attn_dma0.jsonl" 2> "$O/attn_dma0.err"
       grep -h amazon "$O/attn_dma1.jsonl" "$O/attn_dma0.jsonl" ;;
+    libprobe)   # library bf16 GEMM over a tripled k vs the split-bf16 kernels at decoder shapes
+      run libprobe 200 python -u "$R/tools/lib_bf16_probe.py" 20 > "$O/libprobe.jsonl" 2> "$O/libprobe.err"
+      cat "$O/libprobe.jsonl" ;;
+    sqdec)   # SQ counter passes on the decoder's qkv forward (fp32 A) and qkv dgrad shapes
+      run sq_qkv 150 bash "$R/tools/pmc_sq_gemm.sh" 11264 1536 512 1 1 0 1 qkv_fwd
+      run sq_dgrad 150 bash "$R/tools/pmc_sq_gemm.sh" 11264 512 1536 1 0 0 1 qkv_dgrad
+      run sq_fc1w 150 bash "$R/tools/pmc_sq_gemm.sh" 11264 1024 512 1 1 1 1 fc1_wide ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
