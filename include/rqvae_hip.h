@@ -232,6 +232,10 @@ int rq_gemm_x3s_enable(int mode);
 /* LDS-DMA staged short attention forms (key ranges <= 128 rows, head dim 64): 1 (default unless
  * RQ_ATTN_DMA=0 is set) on, 0 off (the register-staged kernels). Returns the previous setting. A/B switch. */
 int rq_attn_dma_enable(int enable);
+/* One-pass backward of the few-query attention launches (<= 16 queries per sequence over <= 128 keys, head
+ * dim 64: the decoder's cross-attention and short causal self-attention): 1 (default unless
+ * RQ_ATTN_FEWQ_FUSED=0 is set) on, 0 off (the two-pass dQ + dK/dV kernels). Returns the previous setting. */
+int rq_attn_fewq_fused_enable(int enable);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
 /* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device

@@ -1811,6 +1811,171 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_fewq_kernel(
   }
 }
 
+// ------------------------------------------ fused backward of one query tile over a short key range
+// dQ, dK and dV in ONE pass (the decoder's cross-attention: <= 16 future queries per sequence over <= 128
+// context keys; its causal self-attention over <= 16 tokens). The two-pass form reads every key twice and
+// forms S and dP twice (7 products per tile pair); here each wave owns key tiles (t = wave, wave + NW),
+// forms S and dP once in the dK/dV orientation (queries on the accumulator rows 4 (lane >> 4) + i, keys on
+// the lanes), and from them P, dS -> dV^T += dO^T P, dK^T += Q^T dS (permuted-d products); dS is turned into
+// dS^T by four exact MFMAs against a 0/1 permutation operand (each output is one x * 1 plus zeros), which
+// feeds dQ^T += K^T dS^T. The waves' partial dQ^T sum through LDS in wave order (deterministic). 5 products
+// + the transpose per tile pair; keys are read once. delta = rowsum(dO * O) per query comes in by lane
+// shuffles from the lanes that computed it (lane & 15 = query).
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_fewq_fused_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
+    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
+    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out) {
+  constexpr int HD = 64, TPW = 2;   // key tiles per wave (<= 128 keys over 4 waves)
+  __shared__ __attribute__((aligned(16))) float part[NW][16][HD];
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  if (b == (int)gridDim.z - 1) {   // tail slice: rows past the last sequence
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[b], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[b], Tk, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  const int nkt = (lk + 15) >> 4;   // every key tile gets its dK / dV rows written (zeros past the queries)
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  // this wave's key tiles: K and V in the K pattern (S, dP), K in the V pattern (dQ^T)
+  float4 kp[TPW][4], vk[TPW][4], kv[TPW][4];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    if (t < nkt) {
+      frag_kpat(kb_, sk, t, lk, lane, kp[j]);
+      frag_kpat(vb_, sv, t, lk, lane, vk[j]);
+      frag_vpat(kb_, sk, t, lk, lane, kv[j]);
+    }
+  }
+  // the query tile: Q, dO in the A pattern (row c, d = 16 g + 0..15) and the V pattern (rows 4 g + i,
+  // d = 4 c + 0..3); O (A pattern) only for delta
+  const bool qv = c < lq;
+  const int64_t qrow = q0 + (qv ? c : 0);
+  float qf[HD / 4], dof[HD / 4];
+  load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv && lq > 0, qf);
+  load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv && lq > 0, dof);
+  float4 qvp[4], dvp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qvp[i] = dvp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lq > 0) {
+    frag_vpat(q + q0 * sq + hh * HD, sq, 0, lq, lane, qvp);
+    frag_vpat(dout + q0 * sdo + hh * HD, sdo, 0, lq, lane, dvp);
+  }
+  float delta = 0.f, lse2 = 0.f;
+  if (lq > 0) {
+    float of[HD / 4];
+    load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    if (wave == 0 && qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
+    lse2 = qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f;
+  }
+  // per-lane values of the queries 4 g + i (held by lane 4 g + i)
+  float dl[4], ls[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dl[i] = __shfl(delta, 4 * g + i, 64);
+    ls[i] = __shfl(lse2, 4 * g + i, 64);
+  }
+  // 0/1 permutation operand of the transpose: step s, lane (g, c) = [c == 4 g + s]
+  float pe[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) pe[s] = c == 4 * g + s ? 1.f : 0.f;
+  const float sl2 = scale * kLog2e;
+  f32x4 acc[4];   // partial dQ^T (d permuted) over this wave's key tiles
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + j * NW;
+    if (t < nkt) {
+      // S = Q K^T, dP = dO V^T: rows = queries 4 g + i, columns = keys t * 16 + c
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        st = mfma4(qf[4 * s4], kp[j][s4].x, st);
+        dp = mfma4(dof[4 * s4], vk[j][s4].x, dp);
+        st = mfma4(qf[4 * s4 + 1], kp[j][s4].y, st);
+        dp = mfma4(dof[4 * s4 + 1], vk[j][s4].y, dp);
+        st = mfma4(qf[4 * s4 + 2], kp[j][s4].z, st);
+        dp = mfma4(dof[4 * s4 + 2], vk[j][s4].z, dp);
+        st = mfma4(qf[4 * s4 + 3], kp[j][s4].w, st);
+        dp = mfma4(dof[4 * s4 + 3], vk[j][s4].w, dp);
+      }
+      const int key = t * 16 + c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = 4 * g + i;
+        float p = exp2_fast(__builtin_fmaf(st[i], sl2, -ls[i]));
+        if (!(qr < lq && key < lk && (!causal || key <= qr))) p = 0.f;
+        st[i] = p;
+        dp[i] = p * (dp[i] - dl[i]);   // dS
+      }
+      f32x4 dka[4], dva[4], dst = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {   // dV^T += dO^T P, dK^T += Q^T dS (k = the query index 4 g + i)
+        dva[0] = mfma4(dvp[i].x, st[i], dva[0]);
+        dva[1] = mfma4(dvp[i].y, st[i], dva[1]);
+        dva[2] = mfma4(dvp[i].z, st[i], dva[2]);
+        dva[3] = mfma4(dvp[i].w, st[i], dva[3]);
+        dka[0] = mfma4(qvp[i].x, dp[i], dka[0]);
+        dka[1] = mfma4(qvp[i].y, dp[i], dka[1]);
+        dka[2] = mfma4(qvp[i].z, dp[i], dka[2]);
+        dka[3] = mfma4(qvp[i].w, dp[i], dka[3]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dst = mfma4(dp[s], pe[s], dst);   // dS^T: rows = keys 4 g + i, lanes = queries
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {   // dQ^T += K^T dS^T (k = the key index 4 g + i of the tile)
+        acc[0] = mfma4(kv[j][i].x, dst[i], acc[0]);
+        acc[1] = mfma4(kv[j][i].y, dst[i], acc[1]);
+        acc[2] = mfma4(kv[j][i].z, dst[i], acc[2]);
+        acc[3] = mfma4(kv[j][i].w, dst[i], acc[3]);
+      }
+      if (key < lk) {
+        float* rk = dk + (k0 + key) * sdk + hh * HD + 16 * g;
+        float* rv = dv + (k0 + key) * sdv + hh * HD + 16 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          *reinterpret_cast<float4*>(rk + 4 * i) =
+              make_float4(dka[0][i] * scale, dka[1][i] * scale, dka[2][i] * scale, dka[3][i] * scale);
+          *reinterpret_cast<float4*>(rv + 4 * i) = make_float4(dva[0][i], dva[1][i], dva[2][i], dva[3][i]);
+        }
+      }
+    }
+  }
+  if (lq <= 0) return;   // uniform per workgroup: no dQ rows
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *reinterpret_cast<float4*>(&part[wave][c][16 * g + 4 * i]) = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+  __syncthreads();
+  constexpr int TPR = HD / 4;
+  for (int e = tid; e < 16 * TPR; e += 64 * NW) {
+    const int r = e / TPR, cc = (e % TPR) * 4;
+    if (r >= lq) continue;
+    float4 s4 = *reinterpret_cast<const float4*>(&part[0][r][cc]);
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      const float4 a = *reinterpret_cast<const float4*>(&part[w][r][cc]);
+      s4.x += a.x; s4.y += a.y; s4.z += a.z; s4.w += a.w;
+    }
+    *reinterpret_cast<float4*>(dq + (q0 + r) * sdq + hh * HD + cc) =
+        make_float4(s4.x * scale, s4.y * scale, s4.z * scale, s4.w * scale);
+  }
+}
+
 #ifndef RQ_ATTN_SHORT
 #define RQ_ATTN_SHORT 1   // 0: the chunked kernels for every length (A/B switch)
 #endif
@@ -1901,6 +2066,16 @@ static bool fewq_plan(int64_t hd, int64_t max_q, int64_t max_k) {
   return attn_dma_on() && hd == 64 && max_q <= 16 && max_k <= 128;
 }
 static int fewq_waves(int64_t max_k) { return max_k <= 16 ? 1 : (max_k <= 32 ? 2 : 4); }
+// one-pass backward of the few-query launches (attn_bwd_fewq_fused_kernel); RQ_ATTN_FEWQ_FUSED=0 in the
+// environment or rq_attn_fewq_fused_enable(0) keeps the two-pass fewq dQ + dK/dV kernels (A/B)
+static int g_fewq_fused = -1;
+static bool fewq_fused_on() {
+  if (g_fewq_fused < 0) {
+    const char* e = getenv("RQ_ATTN_FEWQ_FUSED");
+    g_fewq_fused = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_fewq_fused != 0;
+}
 
 template <int HD, int NW>
 static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
@@ -2020,6 +2195,18 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
   if constexpr (HD == 64) {
     int nw = 0, ch = 0;
     const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
+    if (fewq_plan(HD, max_q, max_k) && fewq_fused_on()) {
+#define RQ_FQF(NW_)                                                                                                   \
+  hipLaunchKernelGGL((attn_bwd_fewq_fused_kernel<NW_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, dout, \
+                     sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
+      switch (fewq_waves(max_k)) {
+        case 1: RQ_FQF(1); break;
+        case 2: RQ_FQF(2); break;
+        default: RQ_FQF(4); break;
+      }
+#undef RQ_FQF
+      return;
+    }
     if (fewq_plan(HD, max_q, max_k)) {
 #define RQ_DQF(NW_)                                                                                                   \
   hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<NW_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, \
@@ -2290,6 +2477,12 @@ int rq_attn_qsplit_set(int n) {
   fused_qsplit(1, 1, 0, 0);   // resolve the environment default first
   const int prev = g_attn_qsplit;
   g_attn_qsplit = n < 0 ? 0 : n;
+  return prev;
+}
+
+int rq_attn_fewq_fused_enable(int enable) {
+  const int prev = fewq_fused_on() ? 1 : 0;
+  g_fewq_fused = enable ? 1 : 0;
   return prev;
 }
 

@@ -77,6 +77,9 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (5, 128, 128, 8, 64, True, True),    # short forms: longest staged range (128 rows), causal
     (4, 64, 100, 8, 64, False, False),   # short forms: 64 queries x 100 keys (dQ stages 112 keys)
     (3, 17, 17, 8, 64, True, True),      # short forms: two query tiles per sequence, causal diagonal
+    (5, 16, 128, 8, 64, False, False),   # few-query fused backward: a full query tile, 2 key tiles per wave
+    (4, 16, 16, 8, 64, True, True),      # few-query fused backward: one wave, causal
+    (3, 12, 40, 8, 64, False, False),    # few-query fused backward: two waves
     (4, 70, 70, 4, 32, True, True),
     (2, 40, 90, 2, 128, False, False),
     (5, 30, 30, 4, 16, True, True),      # small head dim (decoder fixtures: A=64, H=4)
@@ -214,6 +217,51 @@ def test_varlen_attention_fused_empty_and_tail(device, lq, lk):
     for b in range(len(lq)):
         if lk[b] == 0:
             assert torch.count_nonzero(dq[int(cq[b]):int(cq[b + 1])]) == 0
+
+
+@pytest.mark.parametrize("lq,lk,causal", [([5, 3, 0, 16], [81, 0, 40, 128], False),
+                                           ([5, 1, 16, 7], [5, 1, 16, 7], True)])
+def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal):
+    """One-pass few-query backward (attn_bwd_fewq_fused_kernel) vs the two-pass fewq dQ + dK/dV kernels on
+    ragged ranges with empty-query / empty-key segments and zero-padded tail rows; each run bitwise
+    deterministic."""
+    from rqvae_hip import _lib, ops
+    g = gi.rng(sum(lq) * 7 + sum(lk))
+    H, hd = 8, 64
+    A_ = H * hd
+    cq = torch.tensor(np.concatenate([[0], np.cumsum(lq)]), device=device)
+    ck = torch.tensor(np.concatenate([[0], np.cumsum(lk)]), device=device)
+    Tq, Tk = int(cq[-1]) + 3, int(ck[-1]) + 5
+    q0 = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
+    k0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
+    v0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
+    do = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
+    lib = _lib.load()
+    res = {}
+    for fused in (True, True, False):
+        prev = lib.rq_attn_fewq_fused_enable(int(fused))
+        try:
+            qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
+            o = ops.varlen_attention(qt, kt, vt, cq, ck, H, causal, max(lq), max(lk))
+            o.backward(do)
+        finally:
+            lib.rq_attn_fewq_fused_enable(prev)
+        r = (qt.grad, kt.grad, vt.grad)
+        if fused in res:
+            for a, b in zip(res[fused], r):
+                assert torch.equal(a, b)
+        res[fused] = r
+    for a, b, what in zip(res[True], res[False], ("dq", "dk", "dv")):
+        assert torch.isfinite(a).all(), what
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5, msg=what)
+    dq, dk, dv = res[True]
+    assert torch.count_nonzero(dq[int(cq[-1]):]) == 0 and torch.count_nonzero(dk[int(ck[-1]):]) == 0
+    assert torch.count_nonzero(dv[int(ck[-1]):]) == 0
+    for b in range(len(lq)):
+        if lk[b] == 0:
+            assert torch.count_nonzero(dq[int(cq[b]):int(cq[b + 1])]) == 0
+        if lq[b] == 0:
+            assert torch.count_nonzero(dk[int(ck[b]):int(ck[b + 1])]) == 0
 
 
 @pytest.mark.parametrize("bucket", [False, True])

@@ -84,6 +84,18 @@ for s in $steps; do
       run sq_qkv 150 bash "$R/tools/pmc_sq_gemm.sh" 11264 1536 512 1 1 0 1 qkv_fwd
       run sq_dgrad 150 bash "$R/tools/pmc_sq_gemm.sh" 11264 512 1536 1 0 0 1 qkv_dgrad
       run sq_fc1w 150 bash "$R/tools/pmc_sq_gemm.sh" 11264 1024 512 1 1 1 1 fc1_wide ;;
+    attntests)   # attention kernels + the decoder fixtures
+      run attntests 400 python -u -m pytest "$R/tests/test_jagged_attention_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" \
+        -m gpu -x -q --timeout 120 --timeout-method thread > "$O/attntests.log" 2>&1 || { tail -40 "$O/attntests.log"; exit 1; }
+      tail -3 "$O/attntests.log" ;;
+    fewqab)   # one-pass few-query backward on / off: attention probe + decoder Amazon step
+      RQ_ATTN_FEWQ_FUSED=1 run fewq1 200 python -u "$R/tools/attn_probe.py" > "$O/fewq1.jsonl" 2> "$O/fewq1.err"
+      RQ_ATTN_FEWQ_FUSED=0 run fewq0 200 python -u "$R/tools/attn_probe.py" > "$O/fewq0.jsonl" 2> "$O/fewq0.err"
+      grep -h cross "$O/fewq1.jsonl" "$O/fewq0.jsonl"
+      RQ_ATTN_FEWQ_FUSED=1 run dec1 200 python -u "$R/bench.py" --decoder-only > "$O/dec_fewq1.json" 2> "$O/dec_fewq1.err"
+      RQ_ATTN_FEWQ_FUSED=0 run dec0 200 python -u "$R/bench.py" --decoder-only > "$O/dec_fewq0.json" 2> "$O/dec_fewq0.err"
+      RQ_ATTN_FEWQ_FUSED=1 run dec1b 200 python -u "$R/bench.py" --decoder-only > "$O/dec_fewq1b.json" 2> "$O/dec_fewq1b.err"
+      cat "$O/dec_fewq1.json" "$O/dec_fewq0.json" "$O/dec_fewq1b.json" | python3 -c "import sys,json; [print(json.loads(l)['decoder_amazon']['ms_per_step']) for l in sys.stdin]" ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
