@@ -236,6 +236,10 @@ int rq_attn_dma_enable(int enable);
  * dim 64: the decoder's cross-attention and short causal self-attention): 1 (default unless
  * RQ_ATTN_FEWQ_FUSED=0 is set) on, 0 off (the two-pass dQ + dK/dV kernels). Returns the previous setting. */
 int rq_attn_fewq_fused_enable(int enable);
+/* The same for self-attention style launches over short ranges (17..128 queries, <= 128 keys, head dim
+ * 64: the encoder's Amazon contexts): 1 (default unless RQ_ATTN_SHORT_FUSED=0 is set) one pass, 0 the
+ * two-pass LDS-DMA dQ + dK/dV kernels. Returns the previous setting. */
+int rq_attn_short_fused_enable(int enable);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
 /* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device

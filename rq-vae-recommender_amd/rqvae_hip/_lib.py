@@ -62,6 +62,7 @@ _SIGS = {
     "rq_gemm_x3s_enable": ([_I], _I),
     "rq_attn_dma_enable": ([_I], _I),
     "rq_attn_fewq_fused_enable": ([_I], _I),
+    "rq_attn_short_fused_enable": ([_I], _I),
     "rq_attn_qsplit_set": ([_I], _I),
     "rq_split_bf16x3": ([_P, _I64, _P, _P, _P], _I),
     "rq_split_bf16x3_multi": ([_I, _P, _P, _P, _P, _P], _I),

@@ -219,12 +219,17 @@ def test_varlen_attention_fused_empty_and_tail(device, lq, lk):
             assert torch.count_nonzero(dq[int(cq[b]):int(cq[b + 1])]) == 0
 
 
-@pytest.mark.parametrize("lq,lk,causal", [([5, 3, 0, 16], [81, 0, 40, 128], False),
-                                           ([5, 1, 16, 7], [5, 1, 16, 7], True)])
-def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal):
-    """One-pass few-query backward (attn_bwd_fewq_fused_kernel) vs the two-pass fewq dQ + dK/dV kernels on
-    ragged ranges with empty-query / empty-key segments and zero-padded tail rows; each run bitwise
-    deterministic."""
+@pytest.mark.parametrize("lq,lk,causal,switch", [
+    ([5, 3, 0, 16], [81, 0, 40, 128], False, "rq_attn_fewq_fused_enable"),
+    ([5, 1, 16, 7], [5, 1, 16, 7], True, "rq_attn_fewq_fused_enable"),
+    ([81, 9, 0, 45, 17], [81, 9, 0, 45, 17], False, "rq_attn_short_fused_enable"),   # encoder (Amazon)
+    ([81, 33, 70, 1, 17], [81, 33, 70, 1, 17], True, "rq_attn_short_fused_enable"),
+    ([40, 0, 128, 20], [100, 30, 128, 0], False, "rq_attn_short_fused_enable"),      # 128 staged rows
+])
+def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal, switch):
+    """One-pass backwards (attn_bwd_fewq_fused_kernel: <= 16 queries; attn_bwd_short_fused_kernel: short
+    self-attention) vs the two-pass kernels on ragged ranges with empty-query / empty-key segments and
+    zero-padded tail rows; each run bitwise deterministic."""
     from rqvae_hip import _lib, ops
     g = gi.rng(sum(lq) * 7 + sum(lk))
     H, hd = 8, 64
@@ -239,13 +244,13 @@ def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal):
     lib = _lib.load()
     res = {}
     for fused in (True, True, False):
-        prev = lib.rq_attn_fewq_fused_enable(int(fused))
+        prev = getattr(lib, switch)(int(fused))
         try:
             qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
             o = ops.varlen_attention(qt, kt, vt, cq, ck, H, causal, max(lq), max(lk))
             o.backward(do)
         finally:
-            lib.rq_attn_fewq_fused_enable(prev)
+            getattr(lib, switch)(prev)
         r = (qt.grad, kt.grad, vt.grad)
         if fused in res:
             for a, b in zip(res[fused], r):

@@ -96,6 +96,11 @@ for s in $steps; do
       RQ_ATTN_FEWQ_FUSED=0 run dec0 200 python -u "$R/bench.py" --decoder-only > "$O/dec_fewq0.json" 2> "$O/dec_fewq0.err"
       RQ_ATTN_FEWQ_FUSED=1 run dec1b 200 python -u "$R/bench.py" --decoder-only > "$O/dec_fewq1b.json" 2> "$O/dec_fewq1b.err"
       cat "$O/dec_fewq1.json" "$O/dec_fewq0.json" "$O/dec_fewq1b.json" | python3 -c "import sys,json; [print(json.loads(l)['decoder_amazon']['ms_per_step']) for l in sys.stdin]" ;;
+    shortab)   # one-pass short self-attention backward on / off: decoder Amazon step (alternating)
+      for v in 1 0 1 0; do
+        RQ_ATTN_SHORT_FUSED=$v run dec_s$v 200 python -u "$R/bench.py" --decoder-only > "$O/dec_short$v.json" 2> "$O/dec_short$v.err"
+        python3 -c "import json; print('short_fused=$v', json.load(open('$O/dec_short$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
