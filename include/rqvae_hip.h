@@ -229,6 +229,10 @@ int rq_gemm_x3w_enable(int enable);
 /* 64 x 64-tile form of the 128-tile kernel: 0 never, 1 (default unless RQ_X3S=0/2 is set) where the
  * time model prefers it, 2 forced wherever the 128-tile kernel would run. Returns the previous mode. */
 int rq_gemm_x3s_enable(int mode);
+/* LDS-DMA form of the 128-tile kernel for fp32 k-contiguous A x split B (bitwise the register-staged
+ * kernel): 0 (default unless RQ_X3D=1/2 is set: slower inside the decoder step) off, 1 for an
+ * n-contiguous B (data gradients), 2 also for a k-contiguous B. Returns the previous setting. A/B switch. */
+int rq_gemm_x3d_enable(int enable);
 /* LDS-DMA staged short attention forms (key ranges <= 128 rows, head dim 64): 1 (default unless
  * RQ_ATTN_DMA=0 is set) on, 0 off (the register-staged kernels). Returns the previous setting. A/B switch. */
 int rq_attn_dma_enable(int enable);

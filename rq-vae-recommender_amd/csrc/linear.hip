@@ -1088,6 +1088,140 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 #undef RQ_W_VM6
 #undef RQ_W_LGKM0
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA form of the 128-tile kernel for an fp32 k-contiguous A and a split B ("x3d"): the decoder's
+// projections and data gradients, whose A (a norm / attention output, an activation gradient) is fp32.
+// The register-staged kernel splits A while staging it and pays the VGPR -> LDS store transfer
+// (ds_write_b128 ~79 B/clk/CU) for every operand byte — at K = 512..1536 that transfer, not the MFMA,
+// bounds it (SQ: MFMA busy 27 %). Here both operands land in LDS by global_load_lds_dwordx4 (no VGPR
+// round trip): A as an fp32 row image (128 rows x 32 k x 4 B: the same bytes as its hi + lo planes; 16-B
+// chunk c of row r at c ^ ((r >> 1) & 1 | (r & 4)), conflict-free for the fragment reads below), B as the
+// wide kernel's half-plane images (x3w_src / wfrag16). A fragments are split to (hi, lo) bf16 right after
+// their ds_read_b128 pair — the same split_bf16x2 as the staging path, so for the same operands this
+// kernel's MFMA inputs, product order (16x16x32, hi.lo + lo.hi + hi.hi per tile) and k order equal
+// gemm_bf16x3_kernel's: the results agree bitwise. Ring: A three k-step slots, B two (80 KiB: two
+// workgroups per CU); per k step each wave issues B(st + 1) then A(st + 2) (4 + 4 DMA instructions) and
+// waits vmcnt(4) + one barrier at the top of the next step (A(st + 1) stays in flight). K % 32 == 0.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDA = 16384;            // A slot: 128 rows x 32 k fp32
+constexpr int kDB = 2 * kWH;          // B slot: hi + lo half-planes
+constexpr int kDLds = 3 * kDA + 2 * kDB;
+static_assert(kDLds == 81920, "x3d LDS");
+
+__device__ __forceinline__ int drow_swz(int r) { return ((r >> 1) & 1) | (r & 4); }
+
+template <bool BKC, int EPI, bool DROP>
+__global__ void __launch_bounds__(256, 2)
+gemm_x3d_kernel(const float* __restrict__ A, int64_t lda, const uint16_t* __restrict__ Bh, const uint16_t* __restrict__ Bl,
+                int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S, int64_t chunk, int per,
+                float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
+  ep.seed = epoch_seed(ep.seed);
+  __shared__ __attribute__((aligned(16))) char lds[kDLds];
+  const int bid = blockIdx.x;
+  const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
+  if (lw >= tiles * S) return;
+  const int s = lw / tiles, t = lw % tiles;
+  const int m0 = (t / tiles_n) * kXT, n0 = (t % tiles_n) * kXT;
+  const int64_t k_lo = (int64_t)s * chunk;
+  const int64_t k_hi = k_lo + chunk < K ? k_lo + chunk : K;
+  const int nk = (int)((k_hi - k_lo) >> 5);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // per-lane DMA sources of this wave's instructions j = wave + 4 u (u = 0..3): A rows 8 j + (lane >> 3)
+  // (128-B rows, position lane & 7 holds chunk (lane & 7) ^ drow_swz(row)); B: x3w_src of 1 KiB block j
+  // (u = 0, 1) per plane
+  int64_t oa[4], ob[2];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = wave + 4 * u, row = 8 * j + (lane >> 3);
+    const int kc = (lane & 7) ^ drow_swz(row);
+    oa[u] = (int64_t)min(m0 + row, M - 1) * lda + k_lo + 4 * kc;
+  }
+  const int64_t kb = BKC ? k_lo : k_lo * ldb, db = BKC ? 32 : 32 * ldb;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) ob[u] = kb + x3w_src<BKC>(ldb, n0, N, wave + 4 * u, lane);
+  auto issue_a = [&](int step, int slot) {
+    const int64_t o = (int64_t)(step < nk ? step : nk - 1) * 32;
+    char* dst = lds + slot * kDA + 1024 * wave;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(A + oa[u] + o),
+                                       (__attribute__((address_space(3))) void*)(dst + 4096 * u), 16, 0, 0);
+  };
+  auto issue_b = [&](int step) {
+    const int64_t o = (int64_t)(step < nk ? step : nk - 1) * db;
+    char* dst = lds + 3 * kDA + (step & 1) * kDB + 1024 * wave;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      glds16(Bh + ob[u] + o, dst + 4096 * u);
+      glds16(Bl + ob[u] + o, dst + kWH + 4096 * u);
+    }
+  };
+
+  floatx4v acc[4][4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = floatx4v{0.f, 0.f, 0.f, 0.f};
+
+  issue_a(0, 0);
+  issue_b(0);
+  issue_a(1, 1);
+  int slot = 0;   // A slot of step st (st % 3)
+  for (int st = 0; st < nk; ++st) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A(st), B(st) landed (A(st + 1) may fly)
+    __builtin_amdgcn_s_barrier();                       // ... for every wave; slots of st - 1 are free
+    issue_b(st + 1);
+    issue_a(st + 2, slot == 0 ? 2 : slot - 1);
+    const char* as = lds + slot * kDA;
+    const char* bh = lds + 3 * kDA + (st & 1) * kDB;
+    const char* bl = bh + kWH;
+    bf16x8_t fa_h[4], fa_l[4], fb_h[4], fb_l[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r = wm * 64 + 16 * p + (lane & 15), c0 = 2 * (lane >> 4), sw = drow_swz(r);
+      const float4 x0 = *reinterpret_cast<const float4*>(as + r * 128 + ((c0 ^ sw) << 4));
+      const float4 x1 = *reinterpret_cast<const float4*>(as + r * 128 + (((c0 + 1) ^ sw) << 4));
+      uint4 h, l;
+      split_bf16x2(x0.x, x0.y, h.x, l.x);
+      split_bf16x2(x0.z, x0.w, h.y, l.y);
+      split_bf16x2(x1.x, x1.y, h.z, l.z);
+      split_bf16x2(x1.z, x1.w, h.w, l.w);
+      fa_h[p] = __builtin_bit_cast(bf16x8_t, h);
+      fa_l[p] = __builtin_bit_cast(bf16x8_t, l);
+      fb_h[p] = wfrag16<BKC>(bh, wn * 64 + 16 * p, lane);
+      fb_l[p] = wfrag16<BKC>(bl, wn * 64 + 16 * p, lane);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);
+      }
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail DMAs drain before the exit
+
+  // 16x16 C/D map of D = B A^T: column (lane & 15) = m, row 4 (lane >> 4) + j = n (gemm_bf16x3_kernel's)
+  float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int m = m0 + wm * 64 + 16 * p + (lane & 15);
+    if (m < M) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * 64 + 16 * q + 4 * (lane >> 4);
+        if (n >= N) continue;
+        x3_epi4<EPI, DROP>(make_float4(acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]), m, n, N, C, Cs, ldc,
+                           ep);
+      }
+    }
+  }
+}
+
 // Split-K slab reduction with the GEMM's epilogue: element j of the (M, N) output (ldc == N) is the
 // fixed-order sum over s of P[s][j] (wave w sums s = w, w + 4, ...; the four wave partials are added
 // in wave order: deterministic, no atomics), then (ACC) plus the current C[j], then the epilogue of
@@ -1358,6 +1492,28 @@ static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool
   return g_x3w == 2 || x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K), M, N, false);   // 2: forced
 }
 
+// RQ_X3D=0 in the environment (or rq_gemm_x3d_enable(0)) keeps the register-staged 128-tile kernel for
+// fp32 k-contiguous A x split B (A/B switch, kernel-vs-kernel tests).
+static int g_x3d = -1;
+static bool x3d_enabled() {
+  if (g_x3d < 0) {
+    const char* e = getenv("RQ_X3D");
+    g_x3d = (e && e[0] == '1') ? 1 : ((e && e[0] == '2') ? 2 : 0);
+  }
+  return g_x3d != 0;
+}
+// The LDS-DMA 128-tile form can run where the 128-tile kernel would, for an fp32 k-contiguous A and a split
+// B, whole 32-deep k steps, and every instantiated epilogue. Measured on MI355X (profiles/r03/x3d_ab.txt):
+// alone (tools/lib_bf16_probe.py: the same launch repeated, A warm in the Infinity Cache) it wins with an
+// n-contiguous B (data gradients dx = g W: 11,264 x 512 x 1,536 87-89 -> 78-81 us, x 4,096 190 -> 161-169
+// us) and loses with a k-contiguous B (11,264 x 1,536 x 512 79 -> 81-84 us); inside the decoder step
+// (cold A, two k steps of DMA lookahead) even the former loses (Amazon step 6.39-6.41 -> 6.46-6.47 ms), so
+// it is OFF by default: RQ_X3D=1 takes the n-contiguous-B shapes, 2 both layouts (A/B, kernel tests).
+static bool x3d_choose(const X3Plan& pl, int64_t N, int64_t K, bool asp, bool bsp, bool a_kc, bool b_kc) {
+  return x3d_enabled() && (!b_kc || g_x3d == 2) && pl.ts == kXT && !asp && bsp && a_kc && K % 32 == 0 &&
+         pl.chunk % 32 == 0 && N >= 8;
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -1496,7 +1652,23 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
       RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
   } while (0)
   bool launched = true;
-  if (wide) {
+  if (!wide && x3d_choose(pl, N, K, asp, bsp, a_kcontig, b_kcontig)) {
+    const float* af = static_cast<const float*>(A);
+    const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
+#define RQ_X3DL(BK, EP, DR)                                                                                       \
+  hipLaunchKernelGGL((gemm_x3d_kernel<BK, EP, DR>), grid, block, 0, s, af, lda, bh, bl, ldb, (int)M, (int)N, K,   \
+                     pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep)
+#define RQ_X3DB(EP, DR) do { if (b_kcontig) RQ_X3DL(true, EP, DR); else RQ_X3DL(false, EP, DR); } while (0)
+    const bool drop = ep.thr != 0;
+    switch (epi_k) {
+      case kEpiStore: RQ_X3DB(kEpiStore, false); break;
+      case kEpiSiluFwd: if (drop) RQ_X3DB(kEpiSiluFwd, true); else RQ_X3DB(kEpiSiluFwd, false); break;
+      case kEpiSiluBwd: if (drop) RQ_X3DB(kEpiSiluBwd, true); else RQ_X3DB(kEpiSiluBwd, false); break;
+      default: if (drop) RQ_X3DB(kEpiAdd, true); else RQ_X3DB(kEpiAdd, false); break;
+    }
+#undef RQ_X3DB
+#undef RQ_X3DL
+  } else if (wide) {
     const uint16_t *ah = static_cast<const uint16_t*>(A), *al = static_cast<const uint16_t*>(A_lo);
     const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
     const dim3 wgrid((unsigned)(pl.tiles * pl.S)), wblock(512);
@@ -1734,7 +1906,13 @@ int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_sp
   const bool wide = x3w_choose(M, N, K, a_split, b_split, a_kcontig, b_kcontig, epilogue, &pw);
   const X3Plan pl = x3_plan(M, N, K);
   if (splits) *splits = wide ? pw.S : pl.S;
-  return wide ? 1 : (pl.ts == 64 ? 2 : 0);
+  return wide ? 1 : (pl.ts == 64 ? 2 : (x3d_choose(pl, N, K, a_split, b_split, a_kcontig, b_kcontig) ? 3 : 0));
+}
+
+int rq_gemm_x3d_enable(int enable) {
+  const int prev = x3d_enabled() ? g_x3d : 0;
+  g_x3d = enable == 2 ? 2 : (enable ? 1 : 0);
+  return prev;
 }
 
 int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,

@@ -60,6 +60,7 @@ _SIGS = {
     "rq_gemm_bf16x3_choice": ([_I64, _I64, _I64, _I, _I, _I, _I, _I, _P], _I),
     "rq_gemm_x3w_enable": ([_I], _I),
     "rq_gemm_x3s_enable": ([_I], _I),
+    "rq_gemm_x3d_enable": ([_I], _I),
     "rq_attn_dma_enable": ([_I], _I),
     "rq_attn_fewq_fused_enable": ([_I], _I),
     "rq_attn_short_fused_enable": ([_I], _I),

@@ -479,18 +479,25 @@ def pending_reductions() -> int:
 def gemm_x3_choice(M: int, N: int, K: int, a_split: bool, b_split: bool, a_kcontig: bool, b_kcontig: bool,
                    epilogue: int = EPI_STORE):
     """(kernel, splits) rq_gemm_bf16x3_ex picks for a call: kernel 'wide' (256 x 256 tiles, LDS-DMA,
-    both operands split), 'x3' (128 x 128 tiles) or 'x3s' (its 64 x 64-tile form); host-only."""
+    both operands split), 'x3' (128 x 128 tiles), 'x3d' (its LDS-DMA form for fp32 k-contiguous A x split B)
+    or 'x3s' (its 64 x 64-tile form); host-only."""
     import ctypes
     s = ctypes.c_int(0)
     k = _lib.load().rq_gemm_bf16x3_choice(M, N, K, int(a_split), int(b_split), int(a_kcontig), int(b_kcontig),
                                           int(epilogue), ctypes.byref(s))
-    return {1: "wide", 2: "x3s"}.get(k, "x3"), int(s.value)
+    return {1: "wide", 2: "x3s", 3: "x3d"}.get(k, "x3"), int(s.value)
 
 
 def gemm_x3w_enable(enable) -> int:
     """Wide split-bf16 GEMM kernel for this process: False off, True on (chosen per shape by the
     round cost model), 2 forced wherever it can run (kernel tests); returns the previous state."""
     return int(_lib.load().rq_gemm_x3w_enable(2 if enable == 2 else int(bool(enable))))
+
+
+def gemm_x3d_enable(enable) -> int:
+    """LDS-DMA form of the 128-tile kernel for fp32 k-contiguous A x split B: False off (register-staged
+    kernel; the default), True on for an n-contiguous B, 2 for every B layout; returns the previous state."""
+    return int(_lib.load().rq_gemm_x3d_enable(2 if enable == 2 else int(bool(enable))))
 
 
 def gemm_x3s_enable(mode) -> int:

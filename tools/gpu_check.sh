@@ -101,6 +101,26 @@ for s in $steps; do
         RQ_ATTN_SHORT_FUSED=$v run dec_s$v 200 python -u "$R/bench.py" --decoder-only > "$O/dec_short$v.json" 2> "$O/dec_short$v.err"
         python3 -c "import json; print('short_fused=$v', json.load(open('$O/dec_short$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    x3dtests)
+      run x3dtests 300 python -u -m pytest "$R/tests/test_gemm_x3d_gpu.py" "$R/tests/test_gemm_bf16x3_gpu.py" "$R/tests/test_gemm_splitk_epi_gpu.py" \
+        -m gpu -x -q --timeout 120 --timeout-method thread > "$O/x3dtests.log" 2>&1 || { tail -40 "$O/x3dtests.log"; exit 1; }
+      tail -3 "$O/x3dtests.log" ;;
+    x3dab)   # LDS-DMA 128-tile form on / off: decoder Amazon step (alternating) + library probe shapes
+      for v in 1 0 1 0; do
+        RQ_X3D=$v run dec_d$v 200 python -u "$R/bench.py" --decoder-only > "$O/dec_x3d$v.json" 2> "$O/dec_x3d$v.err"
+        python3 -c "import json; print('x3d=$v', json.load(open('$O/dec_x3d$v.json'))['decoder_amazon']['ms_per_step'])"
+      done
+      RQ_X3D=1 run libx3d1 200 python -u "$R/tools/lib_bf16_probe.py" 20 > "$O/lib_x3d1.jsonl" 2> "$O/lib_x3d1.err"
+      RQ_X3D=0 run libx3d0 200 python -u "$R/tools/lib_bf16_probe.py" 20 > "$O/lib_x3d0.jsonl" 2> "$O/lib_x3d0.err"
+      python3 - "$O" <<'PY'
+import json, sys
+o = sys.argv[1]
+a = [json.loads(l) for l in open(o + "/lib_x3d1.jsonl")]
+b = [json.loads(l) for l in open(o + "/lib_x3d0.jsonl")]
+for x, y in zip(a, b):
+    print(x["shape"], "fp32A x3d", x["x3_fp32A_splitB_us"], "staged", y["x3_fp32A_splitB_us"], "split", x["x3_split_us"])
+PY
+      ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
