@@ -1452,6 +1452,10 @@ class _GradSink:
                 g.data_ptr() == self.buf.data_ptr() + i * self.width * self.buf.element_size())
 
 
+# RQ_HOIST_SPLIT=0: the hoisted projection reads its fp32 input directly (A/B switch)
+_HOIST_SPLIT = _os.environ.get("RQ_HOIST_SPLIT", "1") != "0"
+
+
 class HoistedProjectionFunction(torch.autograd.Function):
     """[x W_0^T | x W_1^T | ...] for bias-free Linears that read the SAME input — the decoder layers'
     cross-attention K/V projections of the encoder output (reference modules/transformer/
@@ -1467,7 +1471,11 @@ class HoistedProjectionFunction(torch.autograd.Function):
         O, I = weights[0].shape
         T = x.shape[0]
         wsp = split_bf16x3(torch.cat([w.detach() for w in weights], 0))
-        y = gemm_x3(x, True, wsp, True, T, O * len(weights), I)
+        # the shared input split once (4 B read + 4 B written per element): both uses — this forward
+        # (T x n O x I) and the weight-gradient GEMM (its n-contiguous B) — then run on the wide LDS-DMA
+        # kernel instead of splitting x while staging it
+        xs = split_bf16x3(x) if _HOIST_SPLIT else x
+        y = gemm_x3(xs, True, wsp, True, T, O * len(weights), I)
         sink = _GradSink(x, O, len(weights))
         outs = []
         for i in range(len(weights)):
@@ -1475,14 +1483,14 @@ class HoistedProjectionFunction(torch.autograd.Function):
             v._rq_grad_sink = (sink, i)
             outs.append(v)
         ctx.save_for_backward(x)
-        ctx.wsp, ctx.weights, ctx.sink = wsp, weights, sink
+        ctx.wsp, ctx.weights, ctx.sink, ctx.xs = wsp, weights, sink, xs
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *gs):
         (x,) = ctx.saved_tensors
-        weights, sink, wsp = ctx.weights, ctx.sink, ctx.wsp
-        ctx.wsp = ctx.weights = ctx.sink = None
+        weights, sink, wsp, xs = ctx.weights, ctx.sink, ctx.wsp, ctx.xs
+        ctx.wsp = ctx.weights = ctx.sink = ctx.xs = None
         n = len(weights)
         O, I = weights[0].shape
         T = x.shape[0]
@@ -1494,7 +1502,7 @@ class HoistedProjectionFunction(torch.autograd.Function):
         gx = gemm_x3(g, True, wsp, False, T, I, n * O) if ctx.needs_input_grad[0] else None
         dws = [None] * n
         if any(ctx.needs_input_grad[1:]):
-            dws = _wgrad_multi_into(weights, g, x, n * O, I, T)
+            dws = _wgrad_multi_into(weights, g, xs, n * O, I, T)
         return (gx, *dws)
 
 
@@ -1518,7 +1526,7 @@ def _wgrad_multi_into(weights, g, x, O_all: int, I: int, rows: int):
         side.wait_stream(main)
         with torch.cuda.stream(side):
             dw = run()
-        for t in (g, x):
+        for t in [g] + _operand_tensors(x):
             t.record_stream(side)
         _SIDE["used"] = True
         if any(sk is None for sk in sinks):   # autograd consumes these on the main stream

@@ -121,6 +121,22 @@ for x, y in zip(a, b):
     print(x["shape"], "fp32A x3d", x["x3_fp32A_splitB_us"], "staged", y["x3_fp32A_splitB_us"], "split", x["x3_split_us"])
 PY
       ;;
+    redab)   # split-K reduction-launch cost in the GEMM planner: decoder Amazon + ML-32M B=8 steps
+      for v in 4 7 10 4 7 10; do
+        RQ_X3_REDUCE_US=$v run dec_r$v 200 python -u "$R/bench.py" --decoder-only > "$O/dec_red$v.json" 2> "$O/dec_red$v.err"
+        RQ_X3_REDUCE_US=$v run dm8_r$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_red$v.json" 2> "$O/dm8_red$v.err"
+        python3 -c "import json; print('reduce_us=$v amazon', json.load(open('$O/dec_red$v.json'))['decoder_amazon']['ms_per_step'], 'dm8', json.load(open('$O/dm8_red$v.json'))['decoder_ml32m']['ms_per_step'])"
+      done ;;
+    qsplitab)   # fused attention backward query split at the C4 per-rank config (ML-32M, 8 sequences)
+      for v in 0 6 8 4 0 6 8; do
+        RQ_ATTN_QSPLIT=$v run dm8_q$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_q$v.json" 2> "$O/dm8_q$v.err"
+        python3 -c "import json; print('qsplit=$v dm8', json.load(open('$O/dm8_q$v.json'))['decoder_ml32m']['ms_per_step'])"
+      done ;;
+    hoistab)   # hoisted cross K/V projection with its input split once (RQ_HOIST_SPLIT) on / off
+      for v in 1 0 1 0; do
+        RQ_HOIST_SPLIT=$v run dec_h$v 200 python -u "$R/bench.py" --decoder-only > "$O/dec_hs$v.json" 2> "$O/dec_hs$v.err"
+        python3 -c "import json; print('hoist_split=$v', json.load(open('$O/dec_hs$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
