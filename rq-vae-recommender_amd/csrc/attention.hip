@@ -663,6 +663,65 @@ __global__ void __launch_bounds__(64) attn_fwd_split_kernel(const float* __restr
   }
 }
 
+// Key-split form of attn_fwd_kernel for long, few sequences (the C4 per-rank config: 8 sequences of up to
+// 801 keys, 6 heads): with one workgroup per 64-query block walking every key, the launch lasts as long
+// as the longest sequence's chain (51 key tiles). Here grid x = query block x key block (kSplitKB keys,
+// non-causal), each workgroup runs the same staged online softmax over its key block and writes the
+// unnormalised (o, m, l) partial in attn_fwd_split_kernel's layout; attn_fwd_combine_kernel merges them
+// in key-block order (deterministic).
+template <int HD, int NW, int kSplitKB>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, float scale, int64_t Tq,
+    float* __restrict__ part, int nsplit) {
+  constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
+  static_assert(kSplitKB % CH == 0, "key block of whole chunks");
+  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
+  float* K_s = smem;
+  float* V_s = smem + CH * LD;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4;
+  const int j = blockIdx.x % nsplit, qblk = blockIdx.x / nsplit;
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  const int qwg = qblk * 16 * NW, kbeg = j * kSplitKB;
+  if (qwg >= lq || kbeg >= lk) return;        // uniform: no partial for this block (the combine skips it)
+  const int kend = min(lk, kbeg + kSplitKB);
+  const int qb = qwg + wave * 16, qi = qb + (lane & 15);
+  const bool wave_on = qb < lq, qv = qi < lq;
+  float qf[HD / 4];
+  load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float* kb_ = k + k0 * sk + hh * HD;
+  const float* vb_ = v + k0 * sv + hh * HD;
+  RowStage<HD, 64 * NW, CH> stk, stv;
+  FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, kend, qi, 0, scale * kLog2e, &m, &l, o};
+  for (int kc = kbeg; kc < kend; kc += CH) {
+    stk.load(kb_, sk, kc, kend, tid);
+    stv.load(vb_, sv, kc, kend, tid);
+    __syncthreads();                          // the previous chunk's LDS reads are done
+    stk.store(K_s, tid);
+    stv.store(V_s, tid);
+    __syncthreads();
+    const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend - kc + 15) >> 4) : 0);
+    fc.kc = kc;
+    dispatch_tiles<NTL>(nt, kc + CH <= kend, fc);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qv) return;
+  const int64_t H = gridDim.y, row = q0 + qi;
+  store_rowT<HD>(part + (((int64_t)j * Tq + row) * H + hh) * HD, o, 1.f, lane);
+  if (g == 0) {
+    float* ml = part + (int64_t)nsplit * Tq * H * HD;
+    ml[((int64_t)j * H + hh) * Tq + row] = m;
+    ml[((int64_t)(nsplit + j) * H + hh) * Tq + row] = l;
+  }
+}
+
 // one 16-lane group per (query row, head): the split partials' merge, out / lse rows; rows past the last
 // sequence (grid row z == B) get zeros
 template <int HD, int kSplitKB>
@@ -2219,7 +2278,22 @@ static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal) {
   return RQ_ATTN_SPLIT && hd == 64 && !causal && max_q <= 16 && max_k >= RQ_ATTN_SPLIT_MIN_K;
 }
 static int split_kb(int64_t max_k) { return max_k <= 128 ? 32 : 128; }   // 32: RQ_ATTN_SPLIT_MIN_K <= 128 builds
-static int64_t split_ws_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal) {
+// key-split forward for many queries over long keys at low occupancy (attn_fwd_kvsplit_kernel): the C4
+// per-rank config (8 sequences x 6 heads x <= 13 query blocks); RQ_ATTN_KVSPLIT=0 disables (A/B)
+#ifndef RQ_ATTN_KVSPLIT_MAX_WG
+#define RQ_ATTN_KVSPLIT_MAX_WG 1024   // unsplit workgroups (B x H x 64-query blocks) up to which it applies
+#endif
+constexpr int kKvSplitKB = 128;
+static bool kvsplit_plan(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal) {
+  static const bool on = [] {
+    const char* e = getenv("RQ_ATTN_KVSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on && RQ_ATTN_SPLIT && hd == 64 && !causal && max_q > 16 && max_k > 2 * kKvSplitKB &&
+         B * H * ((max_q + 63) / 64) <= RQ_ATTN_KVSPLIT_MAX_WG;
+}
+static int64_t split_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal) {
+  if (kvsplit_plan(B, H, hd, max_q, max_k, causal)) return (max_k + kKvSplitKB - 1) / kKvSplitKB * Tq * H * (hd + 2);
   if (!split_plan(hd, max_q, max_k, causal)) return 0;
   const int kb = split_kb(max_k);
   return (max_k + kb - 1) / kb * Tq * H * (hd + 2);
@@ -2286,6 +2360,17 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
                        float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order, float* split_ws) {
   if constexpr (HD == 64) {
+    if (split_ws && kvsplit_plan(B, H, HD, max_q, max_k, causal)) {
+      const int nsplit = (int)((max_k + kKvSplitKB - 1) / kKvSplitKB);
+      constexpr int RPB = 256 / (HD / 4);
+      const dim3 gs((unsigned)(((max_q + 63) / 64) * nsplit), (unsigned)H, (unsigned)B);
+      const dim3 gc((unsigned)std::max<int64_t>(1, (max_q + RPB - 1) / RPB), (unsigned)H, (unsigned)B + 1);
+      hipLaunchKernelGGL((attn_fwd_kvsplit_kernel<HD, 4, kKvSplitKB>), gs, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck,
+                         scale, Tq, split_ws, nsplit);
+      hipLaunchKernelGGL((attn_fwd_combine_kernel<HD, kKvSplitKB>), gc, dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq, out,
+                         so, lse);
+      return;
+    }
     if (split_ws && split_plan(HD, max_q, max_k, causal)) {
       const int kb = split_kb(max_k);
       const int nsplit = (int)((max_k + kb - 1) / kb);
@@ -2643,7 +2728,7 @@ int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, in
                              int64_t* elems) {
   RQ_CHECK_ARG(elems, "varlen_attn_fwd_ws_elems: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_fwd_ws_elems: bad shape");
-  *elems = ((B + 3) & ~(int64_t)3) + split_ws_elems(H, hd, max_q, max_k, Tq, causal);   // order (B ints, 16-B padded) + split-key partials
+  *elems = ((B + 3) & ~(int64_t)3) + split_ws_elems(B, H, hd, max_q, max_k, Tq, causal);   // order (B ints, 16-B padded) + split-key partials
   return 0;
 }
 
@@ -2651,7 +2736,7 @@ int varlen_attn_fwd3(const float* q, int64_t sq, const float* k, int64_t sk, con
                      const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
                      int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
                      int64_t ws_elems, void* stream) {
-  const int64_t ob = (B + 3) & ~(int64_t)3, sp = split_ws_elems(H, hd, max_q, max_k, Tq, causal);
+  const int64_t ob = (B + 3) & ~(int64_t)3, sp = split_ws_elems(B, H, hd, max_q, max_k, Tq, causal);
   RQ_CHECK_ARG(ws && ws_elems >= ob + sp, "varlen_attn_fwd3: workspace smaller than varlen_attn_fwd_ws_elems");
   return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq,
                        reinterpret_cast<int*>(ws), sp ? ws + ob : nullptr, stream);

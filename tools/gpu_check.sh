@@ -137,6 +137,11 @@ PY
         RQ_HOIST_SPLIT=$v run dec_h$v 200 python -u "$R/bench.py" --decoder-only > "$O/dec_hs$v.json" 2> "$O/dec_hs$v.err"
         python3 -c "import json; print('hoist_split=$v', json.load(open('$O/dec_hs$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    kvsplitab)   # key-split forward (RQ_ATTN_KVSPLIT) on / off at the C4 per-rank config
+      for v in 1 0 1 0; do
+        RQ_ATTN_KVSPLIT=$v run dm8_k$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_k$v.json" 2> "$O/dm8_k$v.err"
+        python3 -c "import json; print('kvsplit=$v dm8', json.load(open('$O/dm8_k$v.json'))['decoder_ml32m']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
