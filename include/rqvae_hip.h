@@ -244,6 +244,19 @@ int rq_attn_fewq_fused_enable(int enable);
  * 64: the encoder's Amazon contexts): 1 (default unless RQ_ATTN_SHORT_FUSED=0 is set) one pass, 0 the
  * two-pass LDS-DMA dQ + dK/dV kernels. Returns the previous setting. */
 int rq_attn_short_fused_enable(int enable);
+/* Decoder loss head (modules/model.py:137-143): X = out_proj output rows (B * npos_x, K), row stride ldx;
+ * logits row r = b * npos + j is X row b * npos_x + j (the reference drops the last position);
+ * u[r] = cross_entropy(logits[r], tgt[r], ignore_index=-1) (NaN for a target >= K), lse[r] saved for the
+ * backward, logits = the contiguous (B * npos, K) copy, loss = sum(u) / B, loss_d[j] = sum_b u[b][j] / B
+ * (fixed-order sums). K <= 1024. */
+int rq_ce_loss_fwd(const float* X, int64_t ldx, int64_t K, const int64_t* tgt, int64_t B, int64_t npos, int64_t npos_x,
+                   float* u, float* lse, float* logits, float* loss, float* loss_d, void* stream);
+/* Its backward: dX (B * npos_x, K, contiguous) from g_loss (scalar), g_loss_d (npos) and g_logits
+ * (B * npos, K), each optional (NULL = zero); rows of the dropped position and ignored targets get only
+ * the g_logits part (or zeros). */
+int rq_ce_loss_bwd(const float* X, int64_t ldx, int64_t K, const int64_t* tgt, const float* lse, int64_t B, int64_t npos,
+                   int64_t npos_x, const float* g_loss, const float* g_loss_d, const float* g_logits, float* dX,
+                   void* stream);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
 /* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device

@@ -377,11 +377,143 @@ __global__ void __launch_bounds__(1024) loss_means_kernel(const float* __restric
   if (t < 3) out[t] = red[t][0] / (float)B;
 }
 
+// ------------------------------------------------------------- decoder output loss (cross-entropy)
+// EncoderDecoderRetrievalModel.forward's loss head (reference modules/model.py:137-143):
+//   logits = out_proj(..).view(B, L + 2, K)[:, :-1, :].flatten(0, 1)       (B * (L + 1), K)
+//   unred  = cross_entropy(logits, sem_ids_fut.flatten(), reduction="none", ignore_index=-1).view(B, -1)
+//   loss   = unred.sum(1).mean();   loss_d = unred.mean(0)
+// as two forward launches (per-row log-sum-exp / loss / the contiguous logits copy; then the two means in
+// one workgroup, fixed-order sums) and one backward launch (every row of the (B * npos_x, K) input
+// gradient, zeros for the dropped last position and ignored targets) instead of ~13 torch kernels.
+// Row r = b * npos + j of the logits is input row b * npos_x + j. One wave per row, K <= 1024.
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) ce_rows_kernel(const float* __restrict__ X, int64_t ldx, int K,
+                                                      const int64_t* __restrict__ tgt, int rows, int npos,
+                                                      int npos_x, float* __restrict__ u, float* __restrict__ lse,
+                                                      float* __restrict__ logits) {
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int b = r / npos, j = r - b * npos;
+  const float* x = X + ((int64_t)b * npos_x + j) * ldx;
+  float* lg = logits + (int64_t)r * K;
+  float m = -INFINITY;
+  for (int k = lane; k < K; k += 64) {
+    const float v = x[k];
+    lg[k] = v;
+    m = fmaxf(m, v);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += expf(x[k] - m);
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float L = m + logf(s);
+    const int64_t t = tgt[r];
+    lse[r] = L;
+    u[r] = t < 0 ? 0.f : (t < K ? L - x[t] : __builtin_nanf(""));   // out-of-range target: NaN, loudly
+  }
+}
+
+// loss = (sum_b sum_j u[b][j]) / B, loss_d[j] = (sum_b u[b][j]) / B: one 256-thread workgroup; per-b row
+// sums in order, then a fixed LDS tree; per-position sums sequential over b (deterministic).
+__global__ void __launch_bounds__(256) ce_means_kernel(const float* __restrict__ u, int B, int npos,
+                                                       float* __restrict__ loss, float* __restrict__ loss_d) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  float a = 0.f;
+  for (int b = t; b < B; b += 256) {
+    float sb = 0.f;
+    for (int j = 0; j < npos; ++j) sb += u[(int64_t)b * npos + j];
+    a += sb;
+  }
+  red[t] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) loss[0] = red[0] / (float)B;
+  for (int j = t; j < npos; j += 256) {
+    float c = 0.f;
+    for (int b = 0; b < B; ++b) c += u[(int64_t)b * npos + j];
+    loss_d[j] = c / (float)B;
+  }
+}
+
+// dX row R = b * npos_x + j: (g_loss + g_loss_d[j]) / B * (softmax(x) - onehot(t)) (+ g_logits row) for
+// j < npos and t >= 0; g_logits only for j < npos and t < 0; zeros otherwise.
+__global__ void __launch_bounds__(256) ce_bwd_kernel(const float* __restrict__ X, int64_t ldx, int K,
+                                                     const int64_t* __restrict__ tgt, const float* __restrict__ lse,
+                                                     int B, int npos, int npos_x, const float* __restrict__ g_loss,
+                                                     const float* __restrict__ g_loss_d,
+                                                     const float* __restrict__ g_logits, float* __restrict__ dX) {
+  const int lane = threadIdx.x & 63, R = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (R >= B * npos_x) return;
+  const int b = R / npos_x, j = R - b * npos_x;
+  float* dx = dX + (int64_t)R * K;
+  if (j >= npos) {
+    for (int k = lane; k < K; k += 64) dx[k] = 0.f;
+    return;
+  }
+  const int r = b * npos + j;
+  const int64_t t = tgt[r];
+  const float* gl = g_logits ? g_logits + (int64_t)r * K : nullptr;
+  if (t < 0) {
+    for (int k = lane; k < K; k += 64) dx[k] = gl ? gl[k] : 0.f;
+    return;
+  }
+  const float g = ((g_loss ? g_loss[0] : 0.f) + (g_loss_d ? g_loss_d[j] : 0.f)) / (float)B;
+  const float L = lse[r];
+  const float* x = X + ((int64_t)b * npos_x + j) * ldx;
+  for (int k = lane; k < K; k += 64) {
+    const float p = expf(x[k] - L);
+    const float v = g * (p - (k == t ? 1.f : 0.f));
+    dx[k] = gl ? v + gl[k] : v;
+  }
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
 
 extern "C" {
+
+int rq_ce_loss_fwd(const float* X, int64_t ldx, int64_t K, const int64_t* tgt, int64_t B, int64_t npos, int64_t npos_x,
+                   float* u, float* lse, float* logits, float* loss, float* loss_d, void* stream) {
+  RQ_CHECK_ARG(B > 0 && K > 0 && K <= 1024 && npos > 0 && npos_x >= npos && ldx >= K && B * npos_x < (1LL << 31),
+               "rq_ce_loss_fwd: bad shape");
+  RQ_CHECK_ARG(X && tgt && u && lse && logits && loss && loss_d, "rq_ce_loss_fwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int rows = (int)(B * npos);
+  hipLaunchKernelGGL(ce_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, ldx, (int)K, tgt, rows,
+                     (int)npos, (int)npos_x, u, lse, logits);
+  hipLaunchKernelGGL(ce_means_kernel, dim3(1), dim3(256), 0, s, u, (int)B, (int)npos, loss, loss_d);
+  RQ_LAUNCH_CHECK("rq_ce_loss_fwd");
+  return 0;
+}
+
+int rq_ce_loss_bwd(const float* X, int64_t ldx, int64_t K, const int64_t* tgt, const float* lse, int64_t B, int64_t npos,
+                   int64_t npos_x, const float* g_loss, const float* g_loss_d, const float* g_logits, float* dX,
+                   void* stream) {
+  RQ_CHECK_ARG(B > 0 && K > 0 && K <= 1024 && npos > 0 && npos_x >= npos && ldx >= K && B * npos_x < (1LL << 31),
+               "rq_ce_loss_bwd: bad shape");
+  RQ_CHECK_ARG(X && tgt && lse && dX, "rq_ce_loss_bwd: null pointer");
+  const int rows = (int)(B * npos_x);
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, X, ldx, (int)K,
+                     tgt, lse, (int)B, (int)npos, (int)npos_x, g_loss, g_loss_d, g_logits, dX);
+  RQ_LAUNCH_CHECK("rq_ce_loss_bwd");
+  return 0;
+}
 
 int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate, void* stream) {
   RQ_CHECK_ARG((P || S == 0) && out, "rq_col_sum: null pointer");

@@ -30,6 +30,8 @@ from rqvae_hip import ops as hip_ops
 
 # RQ_BATCH_SUM=0: torch's broadcast add / repeat (and their reduction backward) in the prologue (A/B)
 _BATCH_SUM = os.environ.get("RQ_BATCH_SUM", "1") != "0"
+# RQ_FUSED_CE=0: the loss head as torch's slice + cross_entropy + means (A/B)
+_FUSED_CE = os.environ.get("RQ_FUSED_CE", "1") != "0"
 
 # As the reference (modules/model.py:27): fp32 matmuls at 'high' precision (split-bf16 GEMM on
 # gfx950, rqvae_hip.ops.gemm_bf16x3); 'highest' restores the exact-fp32 library path.
@@ -133,6 +135,13 @@ class EncoderDecoderRetrievalModel(nn.Module):
         trnsf_out = self._predict(batch)
         if self.training or not self.enable_generation:
             predict_out = self.out_proj(jagged_to_flattened_tensor(trnsf_out))
+            target = batch.sem_ids_fut
+            if _FUSED_CE and hip_ops.ce_loss_supported(predict_out, target, B):
+                # the whole loss head (slice, cross-entropy, both means) in three HIP launches
+                loss, loss_d, logits = hip_ops.cross_entropy_loss(predict_out, target, B)
+                if not self.training:
+                    self.transformer.cached_enc_output = None
+                return ModelOutput(loss=loss, logits=logits, loss_d=loss_d)
             # sem_ids_fut is fixed length, so the jagged values reshape to (B, L+2, K)
             logits = predict_out.view(B, -1, self.num_embeddings)[:, :-1, :].flatten(end_dim=1)
             target = batch.sem_ids_fut.flatten(end_dim=1)

@@ -1156,6 +1156,56 @@ def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     return out
 
 
+class CrossEntropyLossFunction(torch.autograd.Function):
+    """The decoder's loss head (reference modules/model.py:137-143) on rq_ce_loss_fwd / rq_ce_loss_bwd:
+    X = out_proj output (B * npos_x, K) whose last position per sequence is dropped, tgt (B, npos) int64
+    with ignore_index -1 -> (loss = unred.sum(1).mean(), loss_d = unred.mean(0), logits (B * npos, K)),
+    all three differentiable; 3 launches in place of the slice copy, log_softmax / nll_loss, the sums
+    and their backward chain (~13 torch kernels)."""
+
+    @staticmethod
+    def forward(ctx, X, tgt, B: int):
+        K = X.shape[1]
+        npos = tgt.shape[-1]
+        npos_x = X.shape[0] // B
+        dev = X.device
+        t = tgt.reshape(-1).contiguous()
+        u = torch.empty(B * npos, device=dev, dtype=torch.float32)
+        lse = torch.empty_like(u)
+        logits = torch.empty((B * npos, K), device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        loss_d = torch.empty(npos, device=dev, dtype=torch.float32)
+        call("rq_ce_loss_fwd", ptr(X), X.stride(0), K, ptr(t), B, npos, npos_x, ptr(u), ptr(lse), ptr(logits), ptr(loss),
+             ptr(loss_d), stream_handle(dev))
+        ctx.save_for_backward(X, t, lse)
+        ctx.dims = (B, npos, npos_x)
+        return loss, loss_d, logits
+
+    @staticmethod
+    def backward(ctx, g_loss, g_loss_d, g_logits):
+        X, t, lse = ctx.saved_tensors
+        B, npos, npos_x = ctx.dims
+        K = X.shape[1]
+        dX = torch.empty((B * npos_x, K), device=X.device, dtype=torch.float32)
+        gl = g_loss.contiguous() if g_loss is not None else None
+        gd = g_loss_d.contiguous() if g_loss_d is not None else None
+        gg = g_logits.contiguous() if g_logits is not None else None
+        call("rq_ce_loss_bwd", ptr(X), X.stride(0), K, ptr(t), ptr(lse), B, npos, npos_x, ptr(gl), ptr(gd), ptr(gg),
+             ptr(dX), stream_handle(X.device))
+        return dX, None, None
+
+
+def ce_loss_supported(X: torch.Tensor, tgt: torch.Tensor, B: int) -> bool:
+    return (X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.stride(1) == 1 and 0 < X.shape[1] <= 1024
+            and tgt.is_cuda and tgt.dtype == torch.int64 and tgt.dim() == 2 and tgt.shape[0] == B and B > 0 and
+            X.shape[0] % B == 0 and X.shape[0] // B >= tgt.shape[1] > 0)
+
+
+def cross_entropy_loss(X: torch.Tensor, tgt: torch.Tensor, B: int):
+    """(loss, loss_d, logits) of the decoder loss head (CrossEntropyLossFunction)."""
+    return CrossEntropyLossFunction.apply(X, tgt, B)
+
+
 class L2NormReconFunction(torch.autograd.Function):
     """recon_b = sum_c (pre_b / max(|pre_b|, 1e-12) - x_b)^2 — the l2norm that ends the RqVae
     decoder fused with ReconstructionLoss (modules/rqvae.py:145-148). Gradient w.r.t. pre only

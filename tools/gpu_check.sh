@@ -142,6 +142,22 @@ PY
         RQ_ATTN_KVSPLIT=$v run dm8_k$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_k$v.json" 2> "$O/dm8_k$v.err"
         python3 -c "import json; print('kvsplit=$v dm8', json.load(open('$O/dm8_k$v.json'))['decoder_ml32m']['ms_per_step'])"
       done ;;
+    wsab)   # weight gradients on a side stream (--wgrad-stream) at both decoder configs
+      for v in 1 0 1 0; do
+        f=""; [ $v = 1 ] && f="--wgrad-stream"
+        run dm8_ws$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 $f > "$O/dm8_ws$v.json" 2> "$O/dm8_ws$v.err"
+        run am_ws$v 200 python -u "$R/bench.py" --decoder-only $f > "$O/am_ws$v.json" 2> "$O/am_ws$v.err"
+        python3 -c "import json; print('wgrad_stream=$v dm8', json.load(open('$O/dm8_ws$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_ws$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
+    ceab)   # fused loss head (RQ_FUSED_CE) tests + on / off at both decoder configs
+      run cetests 200 python -u -m pytest "$R/tests/test_ce_loss_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" "$R/tests/test_train_gpu.py" \
+        -m gpu -x -q --timeout 120 --timeout-method thread > "$O/cetests.log" 2>&1 || { tail -40 "$O/cetests.log"; exit 1; }
+      tail -1 "$O/cetests.log"
+      for v in 1 0 1 0; do
+        RQ_FUSED_CE=$v run dm8_c$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_c$v.json" 2> "$O/dm8_c$v.err"
+        RQ_FUSED_CE=$v run am_c$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_c$v.json" 2> "$O/am_c$v.err"
+        python3 -c "import json; print('fused_ce=$v dm8', json.load(open('$O/dm8_c$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_c$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
