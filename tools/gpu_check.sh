@@ -158,6 +158,9 @@ PY
         RQ_FUSED_CE=$v run am_c$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_c$v.json" 2> "$O/am_c$v.err"
         python3 -c "import json; print('fused_ce=$v dm8', json.load(open('$O/dm8_c$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_c$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    pairprobe)   # dgrad + wgrad back to back vs concurrent (two streams)
+      run pairprobe 200 python -u "$R/tools/pair_probe.py" 50 > "$O/pairprobe.jsonl" 2> "$O/pairprobe.err"
+      cat "$O/pairprobe.jsonl" ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
