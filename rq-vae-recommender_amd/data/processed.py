@@ -78,8 +78,14 @@ class SeqData(Dataset):
 
     def __init__(self, root: str = "", *args, is_train: bool = True, subsample: bool = False,
                  force_process: bool = False, dataset: RecDataset = RecDataset.ML_1M, data_path: Optional[str] = None,
-                 n_users: Optional[int] = None, n_items: Optional[int] = None, seed: int = 0, **kwargs) -> None:
+                 n_users: Optional[int] = None, n_items: Optional[int] = None, seed: int = 0,
+                 with_features: bool = True, **kwargs) -> None:
+        """`with_features=False` (this build's extension): samples carry empty (., 0) `x` / `x_fut` instead of
+        the items' 768-d features — for consumers that only read ids (the decoder trainer: its tokenizer maps
+        ids to cached semantic ids, reference modules/tokenizer/semids.py:137-153), which saves the per-item
+        feature gather, the collate of (B, M, 768) floats and their host-to-device copy every step."""
         assert (not subsample) or is_train, "Can only subsample on training split."
+        self.with_features = with_features
         self._max_seq_len = DATASET_NAME_TO_MAX_SEQ_LEN[dataset]
         self.subsample = subsample
         self.n_items = n_items or SYNTHETIC_N_ITEMS[dataset]
@@ -110,6 +116,9 @@ class SeqData(Dataset):
         hist = sample[:-1]
         item_ids = torch.tensor(hist + [-1] * (M - len(hist)), dtype=torch.int64)
         fut = torch.tensor([sample[-1]], dtype=torch.int64)
+        if not self.with_features:
+            return SeqBatch(user_ids=torch.tensor([idx]), ids=item_ids, ids_fut=fut, x=torch.empty((M, 0)),
+                            x_fut=torch.empty((1, 0)), seq_mask=item_ids >= 0)
         x = self.item_data[item_ids.clamp_min(0), :768]
         x[item_ids == -1] = -1
         return SeqBatch(user_ids=torch.tensor([idx]), ids=item_ids, ids_fut=fut, x=x,

@@ -137,9 +137,12 @@ class SemanticIdTokenizer(nn.Module):
 
     @torch.no_grad()
     @eval_mode
-    def forward(self, batch: SeqBatch) -> TokenizedSeqBatch:
+    def forward(self, batch: SeqBatch, ids_max: Optional[int] = None) -> TokenizedSeqBatch:
+        """`ids_max` (this build's extension): the batch's largest item id when the caller knows it on the
+        host (a CPU-side loader), so the cache check needs no device read (a sync every step)."""
         B, N = batch.ids.shape
-        if self.cached_ids is None or batch.ids.max() >= self.cached_ids.shape[0]:
+        top = batch.ids.max() if ids_max is None else ids_max
+        if self.cached_ids is None or top >= self.cached_ids.shape[0]:
             sem_ids = self.rq_vae.get_semantic_ids(batch.x).sem_ids
             D = sem_ids.shape[-1]
             seq_mask, sem_ids_fut = None, None

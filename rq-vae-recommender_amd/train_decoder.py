@@ -51,6 +51,53 @@ def token_balanced_shard(seq_mask: torch.Tensor, rank: int, world: int) -> torch
 
 
 
+class _Prefetch:
+    """The host side of the next iterations on a background thread while the GPU runs the current one:
+    the loader's next global batch (the reference's DataLoader, same order), this rank's token-balanced
+    shard, its host-side context row counts and largest item id, pinned for a non-blocking copy. Yields
+    (shard or None, counts, n_glob, ids_max) in loader order; `depth` batches ahead."""
+
+    def __init__(self, loader, rank: int, world: int, sem_ids_dim: int, depth: int = 2):
+        import queue
+        import threading
+        self.q = queue.Queue(maxsize=depth)
+        self.stop = False
+
+        def work():
+            try:
+                while not self.stop:
+                    data = next(loader)
+                    n_glob = data.seq_mask.shape[0]
+                    mine = token_balanced_shard(data.seq_mask, rank, world)
+                    if len(mine) == 0:
+                        self.q.put((None, None, n_glob, None))
+                        continue
+                    data = type(data)(*[v[mine] for v in data])
+                    counts = (data.seq_mask.sum(1) * sem_ids_dim).tolist()
+                    ids_max = int(max(int(data.ids.max()), int(data.ids_fut.max())))
+                    if torch.cuda.is_available():
+                        data = type(data)(*[v.pin_memory() if hasattr(v, "pin_memory") else v for v in data])
+                    self.q.put((data, counts, n_glob, ids_max))
+            except BaseException as e:   # surfaced on the consumer side
+                self.q.put(e)
+        self.thread = threading.Thread(target=work, daemon=True)
+        self.thread.start()
+
+    def next(self):
+        item = self.q.get()
+        if isinstance(item, BaseException):
+            raise item
+        return item
+
+    def close(self):
+        self.stop = True
+        try:
+            while True:
+                self.q.get_nowait()
+        except Exception:
+            pass
+
+
 # Last train() call: steady-state time per iteration (CUDA-synchronised once at the start and once at
 # the end of the measured span, nothing inside it), the step mode and the captured graphs — for the
 # bench's trainer line and the tests.
@@ -78,8 +125,9 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     torch.cuda.set_device(device)
     gemm_tuning.enable()   # fastest measured library GEMM per shape (RQVAE_TUNABLE_GEMM=0: heuristic)
     item_ds = ItemData(root=dataset_folder, dataset=dataset, data_path=data_path, seed=seed)
+    # the decoder reads item ids only (the tokenizer maps them to cached semantic ids): no feature gather
     train_ds = SeqData(root=dataset_folder, dataset=dataset, is_train=True, subsample=train_data_subsample,
-                       data_path=data_path, seed=seed)
+                       data_path=data_path, seed=seed, with_features=False)
     global_batch = batch_size if split_batches else batch_size * world
     g = torch.Generator().manual_seed(seed + 5)
     loader = cycle(DataLoader(train_ds, batch_size=global_batch, shuffle=True, generator=g))
@@ -124,6 +172,8 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     graphed = GraphedSteps(graph_body, lambda inp: model.context_rows(inp[0], bucket), buckets, run_backward=False,
                            prepare=lambda static, inp: copy_row_counts(static[0].seq_mask, inp[0].seq_mask)
                            ) if use_graphs else None
+    feed = _Prefetch(loader, rank, world, tokenizer.sem_ids_dim)
+    w_dev = {}
     t0, hist = time.time(), []
     t_from = start_iter + min(5, (iterations - start_iter) // 2)   # measured span: [t_from, iterations)
     t_mark, toks = None, 0
@@ -143,26 +193,26 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
             buckets.zero_grad()
         total = torch.zeros((), device=device)
         for micro in range(gradient_accumulate_every):
-            data = next(loader)
-            n_glob = data.seq_mask.shape[0]   # the loader's last batch of an epoch may be short
-            mine = token_balanced_shard(data.seq_mask, rank, world)
-            if len(mine) == 0:   # fewer sequences than ranks: zero gradient, exchange in synchronize()
+            # the loader's next global batch, this rank's token-balanced shard (n_glob: the loader's last
+            # batch of an epoch may be short) and its host-side context row counts — no device sync for
+            # the jagged total, and a captured step is keyed by its row bucket — prepared on the feed thread
+            data, counts, n_glob, ids_max = feed.next()
+            if data is None:   # fewer sequences than ranks: zero gradient, exchange in synchronize()
                 if graphed is not None:
                     buckets.zero_grad()
                 continue
-            data = type(data)(*[v[mine] for v in data])
-            # host-side context row counts (the loader's batch is on the CPU): no device sync for the
-            # jagged total, and a captured step can be keyed by its row bucket
-            counts = (data.seq_mask.sum(1) * tokenizer.sem_ids_dim).tolist()
             if t_mark is not None:
                 toks += sum(counts) + len(counts)   # context tokens (+ the user token per sequence)
                 s_toks += sum(counts) + len(counts)
-            tok = tokenizer(batch_to(data, device))
+            tok = tokenizer(batch_to(data, device), ids_max=ids_max)
             register_row_counts(tok.seq_mask, counts)
             # this rank's shard mean -> share of the GLOBAL-batch mean (unequal, token-balanced shards)
-            w = dp.shard_weight(len(mine), n_glob) / gradient_accumulate_every
+            w = dp.shard_weight(len(counts), n_glob) / gradient_accumulate_every
             if graphed is not None:
-                total = total + graphed((tok, torch.tensor(w, device=device)))
+                wt = w_dev.get(w)
+                if wt is None:   # a few distinct weights over a run: one device scalar each, no per-step copy
+                    wt = w_dev[w] = torch.tensor(w, device=device)
+                total = total + graphed((tok, wt))
                 continue
             out = model(tok)
             last = micro == gradient_accumulate_every - 1
@@ -198,6 +248,7 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
             os.makedirs(save_dir_root, exist_ok=True)
             torch.save({"iter": it, "model": model.state_dict(), "optimizer": opt.state_dict(),
                         "scheduler": sched.state_dict()}, os.path.join(save_dir_root, f"checkpoint_{it}.pt"))
+    feed.close()
     return model
 
 

@@ -161,6 +161,12 @@ PY
     pairprobe)   # dgrad + wgrad back to back vs concurrent (two streams)
       run pairprobe 200 python -u "$R/tools/pair_probe.py" 50 > "$O/pairprobe.jsonl" 2> "$O/pairprobe.err"
       cat "$O/pairprobe.jsonl" ;;
+    trainers)   # drop-in trainers: GPU tests + their own steady-state timing
+      run trtests 400 python -u -m pytest "$R/tests/test_train_gpu.py" -m gpu -x -q --timeout 200 --timeout-method thread \
+        > "$O/trtests.log" 2>&1 || { tail -40 "$O/trtests.log"; exit 1; }
+      tail -1 "$O/trtests.log"
+      run trprobe 300 python -u "$R/tools/trainer_probe.py" > "$O/trainers.json" 2> "$O/trainers.err"
+      cat "$O/trainers.json" ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
