@@ -244,6 +244,42 @@ int rq_attn_fewq_fused_enable(int enable);
  * 64: the encoder's Amazon contexts): 1 (default unless RQ_ATTN_SHORT_FUSED=0 is set) one pass, 0 the
  * two-pass LDS-DMA dQ + dK/dV kernels. Returns the previous setting. */
 int rq_attn_short_fused_enable(int enable);
+/* One rq_gemm_bf16x3_ex3 call as a descriptor (the same fields, the same meaning). */
+typedef struct rq_gemm_desc {
+  const void* A;
+  const void* A_lo;
+  int64_t lda;
+  int a_kcontig;
+  const void* B;
+  const void* B_lo;
+  int64_t ldb;
+  int b_kcontig;
+  int64_t M, N, K;
+  float* C;
+  int64_t ldc;
+  int epilogue;
+  const float* Z;
+  uint16_t* H_hi;
+  uint16_t* H_lo;
+  int64_t ldh;
+  float p;
+  uint64_t seed;
+  int accumulate;
+  int defer;
+  void* workspace;
+  size_t ws_bytes;
+} rq_gemm_desc;
+/* Two independent rq_gemm_bf16x3_ex3 calls d[0], d[1] (splits[i] as ex3's `splits`), results identical to the
+ * two calls in a row; where both run on the 128- or 64-tile kernel with the same tile size and a paired
+ * instantiation exists — a Linear's backward: d[0] the data gradient g W (SiLU'-with-dropout epilogue
+ * allowed), d[1] the weight gradient g^T x (modules/encoder.py:7-36, modules/transformer/*: autograd's
+ * grad_input / grad_weight of nn.Linear) — both problems' workgroups run in ONE launch (one launch instead
+ * of two; together they fill the chip where each alone cannot). RQ_X3_PAIR=0 / rq_gemm_pair_enable(0): two
+ * launches. */
+int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream);
+/* 1 when rq_gemm_bf16x3_pair would run d[0], d[1] in one launch (host-only planning), else 0. */
+int rq_gemm_bf16x3_pair_choice(const rq_gemm_desc* d);
+int rq_gemm_pair_enable(int enable);
 /* Decoder loss head (modules/model.py:137-143): X = out_proj output rows (B * npos_x, K), row stride ldx;
  * logits row r = b * npos + j is X row b * npos_x + j (the reference drops the last position);
  * u[r] = cross_entropy(logits[r], tgt[r], ignore_index=-1) (NaN for a target >= K), lse[r] saved for the

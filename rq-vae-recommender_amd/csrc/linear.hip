@@ -18,6 +18,7 @@
 // Workgroups that share a row chunk are placed on the same XCD (blockIdx % 8 selects the XCD)
 // so the tiles re-reading the same g / x rows hit one L2.
 #include "common.h"
+#include "../../include/rqvae_hip.h"
 
 namespace rqhip {
 
@@ -633,18 +634,44 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
   }
 #endif
 
+// One launch's problem (operands, shape, plan, output, epilogue): the kernel argument of the 128-/64-tile
+// kernel and of the paired launch (gemm_x3_pair_kernel) that runs two problems' workgroups in one grid.
+struct X3Args {
+  const void* A;
+  const void* Al;
+  int64_t lda;
+  const void* B;
+  const void* Bl;
+  int64_t ldb;
+  int M, N;
+  int64_t K;
+  int tiles_n, tiles, S;
+  int64_t chunk;
+  int per;
+  float* C;
+  int64_t ldc;
+  X3Epilogue ep;
+};
+
+// LDS bytes of one plane of the TS-tile form (the 64-tile form's compact images: half of every plane)
+template <int TS>
+constexpr int x3_plane_bytes() { return (TS == 64 && RQ_X3S_COMPACT) ? kXPlane / 2 : kXPlane; }
+
 // TS = output tile (128, or 64 for launches whose 128-tiles cannot fill the chip: the decoder's 1,280
 // future-token rows): 4 waves of (TS / 2)^2 outputs, the same k order (so the same result) either way.
-template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false, int TS = 128>
-__global__ void __launch_bounds__(256, TS == 64 ? kXWG64 : kXWG)
-gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int64_t lda, const void* __restrict__ B,
-                   const void* __restrict__ Bl, int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S,
-                   int64_t chunk, int per, float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
+// The body of one workgroup `bid` of problem `a` over the LDS block `lds` (8 planes).
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP, int TS>
+__device__ __forceinline__ void x3_body(const X3Args& a, int bid, char* __restrict__ lds) {
+  const void* __restrict__ A = a.A;
+  const void* __restrict__ Al = a.Al;
+  const void* __restrict__ B = a.B;
+  const void* __restrict__ Bl = a.Bl;
+  const int64_t lda = a.lda, ldb = a.ldb, K = a.K, chunk = a.chunk, ldc = a.ldc;
+  const int M = a.M, N = a.N, tiles_n = a.tiles_n, tiles = a.tiles, S = a.S, per = a.per;
+  float* __restrict__ C = a.C;
+  X3Epilogue ep = a.ep;
   ep.seed = epoch_seed(ep.seed);
-  // the 64-tile form's compact images: half of every plane (row image: 64 rows; column image: 128-B rows)
-  constexpr int kPl = (TS == 64 && RQ_X3S_COMPACT) ? kXPlane / 2 : kXPlane;
-  __shared__ __attribute__((aligned(16))) char lds[8 * kPl];
-  const int bid = blockIdx.x;
+  constexpr int kPl = x3_plane_bytes<TS>();
   const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
   if (lw >= tiles * S) return;
   const int s = lw / tiles, t = lw % tiles;
@@ -799,6 +826,36 @@ gemm_bf16x3_kernel(const void* __restrict__ A, const void* __restrict__ Al, int6
         }
     }
   }
+}
+
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false, int TS = 128>
+__global__ void __launch_bounds__(256, TS == 64 ? kXWG64 : kXWG) gemm_bf16x3_kernel(X3Args a) {
+  __shared__ __attribute__((aligned(16))) char lds[8 * x3_plane_bytes<TS>()];
+  x3_body<AKC, ASP, BKC, BSP, EPI, DROP, TS>(a, blockIdx.x, lds);
+}
+
+// Two problems in ONE launch: workgroups [0, n1) run problem 1, the rest problem 2 (each with its own
+// XCD-major tile order and plan). The backward's data-gradient and weight-gradient GEMMs of a Linear are
+// independent; one launch instead of two saves a launch and lets the pair fill the chip together (the
+// decoder's 1,280-row launches fill 160..480 of 1,024 slots each; the 11,332-row data gradients 356 of 512).
+// P1 / P2: x3_body instantiations (X3Body<form..., TS>); both the same tile size.
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP, int TS>
+struct X3Body {
+  static constexpr int kTS = TS;
+  __device__ __forceinline__ static void run(const X3Args& a, int bid, char* lds) {
+    x3_body<AKC, ASP, BKC, BSP, EPI, DROP, TS>(a, bid, lds);
+  }
+};
+
+template <class P1, class P2>
+__global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pair_kernel(X3Args a1, X3Args a2, int n1) {
+  static_assert(P1::kTS == P2::kTS, "paired problems share the tile size");
+  __shared__ __attribute__((aligned(16))) char lds[8 * x3_plane_bytes<P1::kTS>()];
+  const int bid = blockIdx.x;
+  if (bid < n1)
+    P1::run(a1, bid, lds);
+  else
+    P2::run(a2, bid - n1, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1364,6 +1421,19 @@ static unsigned x3s_pad_lds(const P& pl) {
 #ifndef RQ_X3S_RATE2
 #define RQ_X3S_RATE2 0.35   // 64-tile kernel, kXWG64 workgroups per CU
 #endif
+// Modelled cost (us) of the separate slab-reduction launch of a split-K call: the reduction kernel plus the
+// gap it adds between launches in a replayed step (RQ_X3_REDUCE_US overrides, for A/B runs).
+#ifndef RQ_X3_REDUCE_US
+#define RQ_X3_REDUCE_US 4.0
+#endif
+static double x3_reduce_us() {
+  static double us = -1.0;
+  if (us < 0.0) {
+    const char* e = getenv("RQ_X3_REDUCE_US");
+    us = e ? atof(e) : RQ_X3_REDUCE_US;
+  }
+  return us;
+}
 static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   const int64_t cus = resident_slots() / 2;
   const int64_t wgs = (int64_t)p.tiles * p.S;
@@ -1379,7 +1449,7 @@ static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
     const int64_t rounds = (wgs + slots - 1) / slots;
     t = (double)rounds * per_cu * tile * (double)p.chunk / (rate * 1e6);
   }
-  if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + 4.0;
+  if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + x3_reduce_us();
   return t;
 }
 
@@ -1492,6 +1562,16 @@ static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool
   return g_x3w == 2 || x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K), M, N, false);   // 2: forced
 }
 
+// RQ_X3_PAIR=0 in the environment (or rq_gemm_pair_enable(0)): rq_gemm_bf16x3_pair runs two launches (A/B)
+static int g_x3_pair = -1;
+static bool x3_pair_enabled() {
+  if (g_x3_pair < 0) {
+    const char* e = getenv("RQ_X3_PAIR");
+    g_x3_pair = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_x3_pair != 0;
+}
+
 // RQ_X3D=0 in the environment (or rq_gemm_x3d_enable(0)) keeps the register-staged 128-tile kernel for
 // fp32 k-contiguous A x split B (A/B switch, kernel-vs-kernel tests).
 static int g_x3d = -1;
@@ -1578,11 +1658,27 @@ size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate
   return x3_workspace_bytes(M, N, K, accumulate != 0);
 }
 
-int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                       int accumulate, int defer, int* splits, void* workspace, size_t ws_bytes, void* stream) {
-  if (splits) *splits = 0;
+}  // extern "C"
+
+namespace rqhip {
+
+// One validated and planned rq_gemm_bf16x3 call (x3_prepare), its kernel launch (x3_launch) and its slab
+// reduction or deferral (x3_post): rq_gemm_bf16x3_ex3 runs the three in a row, rq_gemm_bf16x3_pair prepares
+// two calls and, where an instantiation exists, launches both problems in one gemm_x3_pair_kernel.
+struct X3Call {
+  X3Plan pl;
+  bool wide, x3d, slab, asp, bsp, trivial;
+  int a_kc, b_kc, epilogue, epi_k, code, accumulate, defer;
+  int64_t M, N, K;
+  float* C;
+  float* out;
+  X3Args xa;
+};
+
+static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                      int accumulate, int defer, void* workspace, size_t ws_bytes, hipStream_t s, X3Call* c) {
   const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
   RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
                    epilogue <= 3,
@@ -1606,10 +1702,10 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
                "rq_gemm_bf16x3: N and the output leading dims must be multiples of 4 (vector stores), outputs aligned");
   RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)A_lo | (uintptr_t)B | (uintptr_t)B_lo) % 16 == 0,
                "rq_gemm_bf16x3: operand pointers must be 16-byte aligned");
-  hipStream_t s = (hipStream_t)stream;
   X3Epilogue ep{Z, H_hi, H_lo, ldh, 0u, 1.f, seed, 0};
   dropout_params(p, &ep.thr, &ep.scale);
   RQ_CHECK_ARG(!accumulate || epilogue == kEpiStore, "rq_gemm_bf16x3: accumulate needs the plain epilogue");
+  c->trivial = K == 0;
   if (K == 0) {
     RQ_CHECK_ARG(epilogue == kEpiStore, "rq_gemm_bf16x3: K == 0 needs the plain epilogue");
     if (!accumulate) RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
@@ -1630,19 +1726,44 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
                  "rq_gemm_bf16x3: split-K / accumulate needs ldc == N and workspace %zu >= %zu bytes", ws_bytes, need);
     out = static_cast<float*>(workspace);
   }
-  const int epi_k = slab ? (int)kEpiStore : epilogue;   // the epilogue the GEMM kernel itself runs
-  const dim3 grid((unsigned)(pl.per * 8)), block(256);
+  c->pl = pl;
+  c->wide = wide;
+  c->x3d = !wide && x3d_choose(pl, N, K, asp, bsp, a_kcontig, b_kcontig);
+  c->slab = slab;
+  c->asp = asp;
+  c->bsp = bsp;
+  c->a_kc = a_kcontig;
+  c->b_kc = b_kcontig;
+  c->epilogue = epilogue;
+  c->epi_k = slab ? (int)kEpiStore : epilogue;   // the epilogue the GEMM kernel itself runs
+  c->code = (a_kcontig ? 16 : 0) | (asp ? 8 : 0) | (b_kcontig ? 4 : 0) | (bsp ? 2 : 0);
+  c->accumulate = accumulate;
+  c->defer = defer;
+  c->M = M;
+  c->N = N;
+  c->K = K;
+  c->C = C;
+  c->out = out;
   const int64_t ldo = pl.S > 1 ? N : ldc;
-  const int code = (a_kcontig ? 16 : 0) | (asp ? 8 : 0) | (b_kcontig ? 4 : 0) | (bsp ? 2 : 0);
+  c->xa = X3Args{A, A_lo, lda, B, B_lo, ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep};
+  return 0;
+}
+
+static int x3_launch(const X3Call& c, hipStream_t s) {
+  const X3Plan& pl = c.pl;
+  const X3Args& xa = c.xa;
+  const X3Epilogue& ep = xa.ep;
+  const int64_t M = c.M, N = c.N, K = c.K, lda = xa.lda, ldb = xa.ldb, ldo = xa.ldc;
+  const int epi_k = c.epi_k, code = c.code, a_kcontig = c.a_kc, b_kcontig = c.b_kc;
+  const void *A = xa.A, *A_lo = xa.Al, *B = xa.B, *B_lo = xa.Bl;
+  float* out = c.out;
+  const dim3 grid((unsigned)(pl.per * 8)), block(256);
 #define RQ_X3D(AK, AS, BK, BS, EP, DR)                                                                               \
   do {                                                                                                               \
     if (pl.ts == 64)                                                                                                 \
-      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR, 64>), grid, block, x3s_pad_lds(pl), s, A, A_lo,  \
-                         lda, B, B_lo,                                                                               \
-                         ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep);         \
+      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR, 64>), grid, block, x3s_pad_lds(pl), s, xa);     \
     else                                                                                                             \
-      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR>), grid, block, 0, s, A, A_lo, lda, B, B_lo, ldb, \
-                         (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep);              \
+      hipLaunchKernelGGL((gemm_bf16x3_kernel<AK, AS, BK, BS, EP, DR>), grid, block, 0, s, xa);                       \
   } while (0)
 #define RQ_X3(AK, AS, BK, BS, EP)                                                                                    \
   do {                                                                                                               \
@@ -1652,7 +1773,7 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
       RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
   } while (0)
   bool launched = true;
-  if (!wide && x3d_choose(pl, N, K, asp, bsp, a_kcontig, b_kcontig)) {
+  if (c.x3d) {
     const float* af = static_cast<const float*>(A);
     const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
 #define RQ_X3DL(BK, EP, DR)                                                                                       \
@@ -1668,7 +1789,7 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
     }
 #undef RQ_X3DB
 #undef RQ_X3DL
-  } else if (wide) {
+  } else if (c.wide) {
     const uint16_t *ah = static_cast<const uint16_t*>(A), *al = static_cast<const uint16_t*>(A_lo);
     const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
     const dim3 wgrid((unsigned)(pl.tiles * pl.S)), wblock(512);
@@ -1733,27 +1854,144 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
 #undef RQ_X3
 #undef RQ_X3D
   RQ_CHECK_ARG(launched, "rq_gemm_bf16x3: operand combination (a_kcontig %d, a_split %d, b_kcontig %d, b_split %d) "
-                         "not built for epilogue %d", a_kcontig, (int)asp, b_kcontig, (int)bsp, epilogue);
+                         "not built for epilogue %d", a_kcontig, (int)c.asp, b_kcontig, (int)c.bsp, c.epilogue);
   RQ_LAUNCH_CHECK("gemm_bf16x3_kernel");
-  if (slab && defer && accumulate && epilogue == kEpiStore && splits) {   // the caller reduces later
-    *splits = pl.S;                                                    // (rq_reduce_partials, layout 0)
+  return 0;
+}
+
+static int x3_post(const X3Call& c, int* splits, hipStream_t s) {
+  if (!c.slab) return 0;
+  if (c.defer && c.accumulate && c.epilogue == kEpiStore && splits) {   // the caller reduces later
+    *splits = c.pl.S;                                                  // (rq_reduce_partials, layout 0)
     return 0;
   }
-  if (slab) {
-    const int64_t n = M * N;
-    const dim3 rg((unsigned)((n / 4 + 63) / 64)), rb(256);
-    const bool drop = ep.thr != 0 && epilogue != kEpiStore;
-#define RQ_X3R(EP, DR, AC) hipLaunchKernelGGL((x3_reduce_kernel<EP, DR, AC>), rg, rb, 0, s, out, pl.S, n, (int)N, C, ep)
-    switch (epilogue) {
-      case kEpiStore: if (accumulate) RQ_X3R(kEpiStore, false, true); else RQ_X3R(kEpiStore, false, false); break;
-      case kEpiSiluFwd: if (drop) RQ_X3R(kEpiSiluFwd, true, false); else RQ_X3R(kEpiSiluFwd, false, false); break;
-      case kEpiSiluBwd: if (drop) RQ_X3R(kEpiSiluBwd, true, false); else RQ_X3R(kEpiSiluBwd, false, false); break;
-      default: if (drop) RQ_X3R(kEpiAdd, true, false); else RQ_X3R(kEpiAdd, false, false); break;
-    }
+  const int64_t n = c.M * c.N;
+  const int N = (int)c.N;
+  const dim3 rg((unsigned)((n / 4 + 63) / 64)), rb(256);
+  const X3Epilogue& ep = c.xa.ep;
+  const bool drop = ep.thr != 0 && c.epilogue != kEpiStore;
+  float* out = c.out;
+  float* C = c.C;
+  const int S = c.pl.S;
+#define RQ_X3R(EP, DR, AC) hipLaunchKernelGGL((x3_reduce_kernel<EP, DR, AC>), rg, rb, 0, s, out, S, n, N, C, ep)
+  switch (c.epilogue) {
+    case kEpiStore: if (c.accumulate) RQ_X3R(kEpiStore, false, true); else RQ_X3R(kEpiStore, false, false); break;
+    case kEpiSiluFwd: if (drop) RQ_X3R(kEpiSiluFwd, true, false); else RQ_X3R(kEpiSiluFwd, false, false); break;
+    case kEpiSiluBwd: if (drop) RQ_X3R(kEpiSiluBwd, true, false); else RQ_X3R(kEpiSiluBwd, false, false); break;
+    default: if (drop) RQ_X3R(kEpiAdd, true, false); else RQ_X3R(kEpiAdd, false, false); break;
+  }
 #undef RQ_X3R
-    RQ_LAUNCH_CHECK("x3_reduce_kernel");
+  RQ_LAUNCH_CHECK("x3_reduce_kernel");
+  return 0;
+}
+
+template <class P1, class P2>
+static void x3_pair_go(const X3Call& c1, const X3Call& c2, dim3 grid, unsigned pad, hipStream_t s, int n1) {
+  hipLaunchKernelGGL((gemm_x3_pair_kernel<P1, P2>), grid, dim3(256), pad, s, c1.xa, c2.xa, n1);
+}
+template <class P1, int TS>
+static void x3_pair_p2(const X3Call& c1, const X3Call& c2, dim3 grid, unsigned pad, hipStream_t s, int n1) {
+  switch (c2.code) {   // c2: m-contiguous A (fp32 / split) x n-contiguous B (fp32 / split), plain store
+    case 0: x3_pair_go<P1, X3Body<false, false, false, false, kEpiStore, false, TS>>(c1, c2, grid, pad, s, n1); break;
+    case 2: x3_pair_go<P1, X3Body<false, false, false, true, kEpiStore, false, TS>>(c1, c2, grid, pad, s, n1); break;
+    case 8: x3_pair_go<P1, X3Body<false, true, false, false, kEpiStore, false, TS>>(c1, c2, grid, pad, s, n1); break;
+    default: x3_pair_go<P1, X3Body<false, true, false, true, kEpiStore, false, TS>>(c1, c2, grid, pad, s, n1); break;
+  }
+}
+template <int TS>
+static bool x3_pair_ts(int k1, const X3Call& c1, const X3Call& c2, dim3 grid, unsigned pad, hipStream_t s, int n1) {
+  switch (k1) {   // c1: k-contiguous A (fp32 / split) x n-contiguous split B; plain or SiLU' (+ dropout)
+    case 16 | 2: x3_pair_p2<X3Body<true, false, false, true, kEpiStore, false, TS>, TS>(c1, c2, grid, pad, s, n1); return true;
+    case 16 | 8 | 2: x3_pair_p2<X3Body<true, true, false, true, kEpiStore, false, TS>, TS>(c1, c2, grid, pad, s, n1); return true;
+    case 16 | 2 | 32: x3_pair_p2<X3Body<true, false, false, true, kEpiSiluBwd, false, TS>, TS>(c1, c2, grid, pad, s, n1); return true;
+    case 16 | 2 | 64: x3_pair_p2<X3Body<true, false, false, true, kEpiSiluBwd, true, TS>, TS>(c1, c2, grid, pad, s, n1); return true;
+    default: return false;
+  }
+}
+
+// The paired launch of a data-gradient problem c1 and a weight-gradient problem c2 (both on the 128- or
+// 64-tile kernel with the same tile size), for the operand forms of the decoder's backward: c1 = g W
+// (A fp32 or split k-contiguous, B split n-contiguous; plain or SiLU'-with-dropout epilogue), c2 = g^T x
+// (A fp32 or split m-contiguous, B fp32 or split n-contiguous, plain). false: no instantiation.
+static bool x3_pair_launch(const X3Call& c1, const X3Call& c2, hipStream_t s) {
+  if (c1.wide || c2.wide || c1.x3d || c2.x3d || c1.pl.ts != c2.pl.ts) return false;
+  if (c2.epi_k != kEpiStore || c2.code != (c2.code & (8 | 2))) return false;   // c2: m-contig A, n-contig B
+  const bool drop1 = c1.xa.ep.thr != 0 && c1.epi_k != kEpiStore;
+  const int n1 = c1.pl.per * 8, n2 = c2.pl.per * 8;
+  const dim3 grid((unsigned)(n1 + n2));
+  const bool t64 = c1.pl.ts == 64;
+  unsigned pad = 0;
+  if (t64 && RQ_X3S_COMPACT && x3s_resident((int64_t)c1.pl.tiles * c1.pl.S + (int64_t)c2.pl.tiles * c2.pl.S) == kXWG)
+    pad = 32768u;   // few workgroups: spread them 2 per CU (x3s_pad_lds)
+  const int k1 = c1.code | (c1.epi_k == kEpiSiluBwd ? (drop1 ? 64 : 32) : (c1.epi_k == kEpiStore ? 0 : 128));
+  return t64 ? x3_pair_ts<64>(k1, c1, c2, grid, pad, s, n1) : x3_pair_ts<128>(k1, c1, c2, grid, 0u, s, n1);
+}
+
+}  // namespace rqhip
+
+extern "C" {
+
+int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
+                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
+                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
+                       int accumulate, int defer, int* splits, void* workspace, size_t ws_bytes, void* stream) {
+  if (splits) *splits = 0;
+  hipStream_t s = (hipStream_t)stream;
+  X3Call c;
+  const int rc = x3_prepare(A, A_lo, lda, a_kcontig, B, B_lo, ldb, b_kcontig, M, N, K, C, ldc, epilogue, Z, H_hi, H_lo,
+                            ldh, p, seed, accumulate, defer, workspace, ws_bytes, s, &c);
+  if (rc || c.trivial) return rc;
+  const int rl = x3_launch(c, s);
+  if (rl) return rl;
+  return x3_post(c, splits, s);
+}
+
+static_assert(sizeof(rq_gemm_desc) == 184, "rq_gemm_desc layout (the ctypes mirror in rqvae_hip/ops.py)");
+
+static int x3_prepare_desc(const rq_gemm_desc& d, hipStream_t s, X3Call* c) {
+  return x3_prepare(d.A, d.A_lo, d.lda, d.a_kcontig, d.B, d.B_lo, d.ldb, d.b_kcontig, d.M, d.N, d.K, d.C, d.ldc,
+                    d.epilogue, d.Z, d.H_hi, d.H_lo, d.ldh, d.p, d.seed, d.accumulate, d.defer, d.workspace, d.ws_bytes, s,
+                    c);
+}
+
+int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
+  RQ_CHECK_ARG(d != nullptr, "rq_gemm_bf16x3_pair: null descriptors");
+  if (splits) splits[0] = splits[1] = 0;
+  hipStream_t s = (hipStream_t)stream;
+  X3Call c[2];
+  for (int i = 0; i < 2; ++i) {
+    const int rc = x3_prepare_desc(d[i], s, &c[i]);
+    if (rc) return rc;
+  }
+  if (c[0].trivial || c[1].trivial || !x3_pair_enabled() || !x3_pair_launch(c[0], c[1], s)) {
+    for (int i = 0; i < 2; ++i) {
+      if (c[i].trivial) continue;
+      const int rl = x3_launch(c[i], s);
+      if (rl) return rl;
+    }
+  } else {
+    RQ_LAUNCH_CHECK("gemm_x3_pair_kernel");
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (c[i].trivial) continue;
+    const int rp = x3_post(c[i], splits ? splits + i : nullptr, s);
+    if (rp) return rp;
   }
   return 0;
+}
+
+int rq_gemm_bf16x3_pair_choice(const rq_gemm_desc* d) {
+  if (!d) return -1;
+  X3Call c[2];
+  for (int i = 0; i < 2; ++i) {
+    const rq_gemm_desc& e = d[i];
+    if (e.K <= 0 || e.M <= 0 || e.N <= 0) return 0;
+    c[i].pl = x3_plan(e.M, e.N, e.K);
+    X3Plan pw;
+    c[i].wide = x3w_choose(e.M, e.N, e.K, e.A_lo != nullptr, e.B_lo != nullptr, e.a_kcontig, e.b_kcontig, e.epilogue, &pw);
+    c[i].x3d = !c[i].wide && x3d_choose(c[i].pl, e.N, e.K, e.A_lo != nullptr, e.B_lo != nullptr, e.a_kcontig, e.b_kcontig);
+  }
+  return x3_pair_enabled() && !c[0].wide && !c[1].wide && !c[0].x3d && !c[1].x3d && c[0].pl.ts == c[1].pl.ts ? 1 : 0;
 }
 
 int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
@@ -1907,6 +2145,12 @@ int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_sp
   const X3Plan pl = x3_plan(M, N, K);
   if (splits) *splits = wide ? pw.S : pl.S;
   return wide ? 1 : (pl.ts == 64 ? 2 : (x3d_choose(pl, N, K, a_split, b_split, a_kcontig, b_kcontig) ? 3 : 0));
+}
+
+int rq_gemm_pair_enable(int enable) {
+  const int prev = x3_pair_enabled() ? 1 : 0;
+  g_x3_pair = enable ? 1 : 0;
+  return prev;
 }
 
 int rq_gemm_x3d_enable(int enable) {

@@ -63,6 +63,9 @@ _SIGS = {
     "rq_gemm_x3d_enable": ([_I], _I),
     "rq_ce_loss_fwd": ([_P, _I64, _I64, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P], _I),
     "rq_ce_loss_bwd": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
+    "rq_gemm_bf16x3_pair": ([_P, _P, _P], _I),
+    "rq_gemm_bf16x3_pair_choice": ([_P], _I),
+    "rq_gemm_pair_enable": ([_I], _I),
     "rq_attn_dma_enable": ([_I], _I),
     "rq_attn_fewq_fused_enable": ([_I], _I),
     "rq_attn_short_fused_enable": ([_I], _I),

@@ -366,6 +366,33 @@ def _wgrad_into(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: 
     return None
 
 
+def _wgrad_spec(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: int):
+    """gemm_x3 keywords of dW = g^T inp for a paired launch with the data gradient (gemm_x3_pair), added
+    straight into weight's flat gradient bucket when dp.GradBuckets owns one — or None when the side
+    stream is on (the weight gradient then runs there: _wgrad_into)."""
+    from . import dp
+    if _SIDE["on"] or not _PAIR["on"]:
+        return None
+    sink = dp.direct_grad(weight)
+    spec = dict(a=g, a_kcontig=g_kc, b=inp, b_kcontig=inp_kc, M=O, N=I, K=rows)
+    if sink is not None:
+        spec.update(out=sink, accumulate=True, defer=dp.defer_ok(weight))
+    return spec
+
+
+def _wgrad_result(weight, spec, result):
+    """What autograd gets for weight after a paired launch: None when the gradient went into its bucket."""
+    if spec.get("accumulate"):
+        from . import dp
+        dp.direct_grad_done(weight)
+        return None
+    return result
+
+
+# paired data-/weight-gradient launches (gemm_x3_pair); RQ_X3_PAIR=0 in the environment: two launches
+_PAIR = {"on": _os.environ.get("RQ_X3_PAIR", "1") != "0"}
+
+
 EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD, EPI_ADD = 0, 1, 2, 3
 _X3_WS = {}
 
@@ -380,15 +407,23 @@ def _x3_workspace(M: int, N: int, K: int, accumulate: bool = False) -> int:
     return nb
 
 
-def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
-            Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
-            accumulate: bool = False, defer: bool = False):
-    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex2). a / b: fp32
-    tensors or Split. Returns C (EPI_STORE; EPI_ADD: A B^T + Z), (C, H) (EPI_SILU_FWD: C = z,
-    H = split(Dropout(SiLU(z)))) or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split
-    of shape (M, N). `out`: the (M, N) contiguous fp32 destination of C; `accumulate` (EPI_STORE
-    only): out += A B^T; with `defer` a split call's slab reduction joins the pending batch
-    (flush_reductions) instead of running now."""
+class _X3Call(NamedTuple):
+    """One prepared rq_gemm_bf16x3 call: the ex3 argument values, its outputs and what to do after it."""
+    fields: tuple
+    C: torch.Tensor
+    H: "Split"
+    ws: torch.Tensor
+    defer: bool
+    key: str
+    epilogue: int
+    M: int
+    N: int
+    dev: torch.device
+
+
+def _x3_setup(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
+              Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
+              accumulate: bool = False, defer: bool = False) -> _X3Call:
     def desc(t):
         if isinstance(t, Split):
             return t.hi, t.lo, t.hi.shape[-1], 1
@@ -414,26 +449,81 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     defer = bool(defer and accumulate and nbytes)
     if defer and C.data_ptr() in _DEFER["outs"]:
         flush_reductions()   # a pending reduction into the same output must land first
-    if defer:
-        import ctypes
-        splits = ctypes.c_int(0)
-        args = ("rq_gemm_bf16x3_ex3", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
-                M, N, K, ptr(C), N, int(epilogue), ptr(Z), None, None, N, float(p), int(seed), 1, 1,
-                ctypes.byref(splits), ptr(ws), nbytes, stream_handle(dev))
-    else:
-        args = ("rq_gemm_bf16x3_ex2", ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig),
-                M, N, K, ptr(C), N, int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N,
-                float(p), int(seed), int(accumulate), ptr(ws), nbytes, stream_handle(dev))
+    fields = (ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig), M, N, K, ptr(C), N,
+              int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N, float(p), int(seed),
+              int(accumulate), int(defer), ptr(ws), nbytes)
+    key = f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}{int(accumulate)}"
+    return _X3Call(fields, C, H, ws, defer, key, epilogue, M, N, dev)
+
+
+def _x3_result(c: _X3Call, splits: int):
+    if c.defer and splits > 0:
+        _defer_push(c.ws, c.C, c.M * c.N, splits, 0)
+    if c.epilogue in (EPI_STORE, EPI_ADD):
+        return c.C
+    return (c.C, c.H) if c.epilogue == EPI_SILU_FWD else c.H
+
+
+def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
+            Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
+            accumulate: bool = False, defer: bool = False):
+    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex3). a / b: fp32
+    tensors or Split. Returns C (EPI_STORE; EPI_ADD: A B^T + Z), (C, H) (EPI_SILU_FWD: C = z,
+    H = split(Dropout(SiLU(z)))) or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split
+    of shape (M, N). `out`: the (M, N) contiguous fp32 destination of C; `accumulate` (EPI_STORE
+    only): out += A B^T; with `defer` a split call's slab reduction joins the pending batch
+    (flush_reductions) instead of running now."""
+    import ctypes
+    c = _x3_setup(a, a_kcontig, b, b_kcontig, M, N, K, epilogue, Z, p, seed, out, accumulate, defer)
+    splits = ctypes.c_int(0)
+    f = c.fields
+    args = ("rq_gemm_bf16x3_ex3", *f[:21], f[21], ctypes.byref(splits), f[22], f[23], stream_handle(c.dev))
     if TIMER.wants("gemm_bf16x3"):
-        TIMER.around(f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}{int(accumulate)}",
-                     call, *args)
+        TIMER.around(c.key, call, *args)
     else:
         call(*args)
-    if defer and splits.value > 0:
-        _defer_push(ws, C, M * N, splits.value, 0)
-    if epilogue in (EPI_STORE, EPI_ADD):
-        return C
-    return (C, H) if epilogue == EPI_SILU_FWD else H
+    return _x3_result(c, splits.value)
+
+
+_DESC = {}
+
+
+def _desc_type():
+    import ctypes
+    t = _DESC.get("t")
+    if t is None:
+        P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+
+        class Desc(ctypes.Structure):   # rq_gemm_desc (include/rqvae_hip.h)
+            _fields_ = [("A", P), ("A_lo", P), ("lda", I64), ("a_kcontig", I), ("B", P), ("B_lo", P), ("ldb", I64),
+                        ("b_kcontig", I), ("M", I64), ("N", I64), ("K", I64), ("C", P), ("ldc", I64),
+                        ("epilogue", I), ("Z", P), ("H_hi", P), ("H_lo", P), ("ldh", I64), ("p", ctypes.c_float),
+                        ("seed", ctypes.c_uint64), ("accumulate", I), ("defer", I), ("workspace", P),
+                        ("ws_bytes", ctypes.c_size_t)]
+        t = _DESC["t"] = Desc
+    return t
+
+
+def gemm_x3_pair(spec1: dict, spec2: dict):
+    """Two independent gemm_x3 calls (keyword dicts of gemm_x3's arguments: a, a_kcontig, b, b_kcontig, M,
+    N, K, ...) through rq_gemm_bf16x3_pair — one launch where a paired instantiation exists (a Linear's data
+    and weight gradients), results identical to two gemm_x3 calls. Returns (result1, result2)."""
+    import ctypes
+    c1 = _x3_setup(**spec1)
+    c2 = _x3_setup(**spec2)
+    D = _desc_type()
+    arr = (D * 2)(D(*c1.fields), D(*c2.fields))
+    splits = (ctypes.c_int * 2)(0, 0)
+    if TIMER.wants("gemm_bf16x3"):
+        TIMER.around(f"gemm_pair:{c1.key}+{c2.key}", call, "rq_gemm_bf16x3_pair", arr, splits, stream_handle(c1.dev))
+    else:
+        call("rq_gemm_bf16x3_pair", arr, splits, stream_handle(c1.dev))
+    return _x3_result(c1, splits[0]), _x3_result(c2, splits[1])
+
+
+def gemm_pair_enable(enable) -> int:
+    """Paired data-/weight-gradient launches (rq_gemm_bf16x3_pair): False = two launches (A/B)."""
+    return int(_lib.load().rq_gemm_pair_enable(int(bool(enable))))
 
 
 # Deferred partial reductions (rq_reduce_partials): split-K weight-gradient slabs and RMSNorm weight-
@@ -551,12 +641,25 @@ def _mlp_backward(gcur, x_in, wsp, zs, hs, rows: int, p: float, seeds, need_w, n
     for i in reversed(range(n)):
         O, I = wsp[i].hi.shape
         inp = x_in if i == 0 else hs[i - 1]
-        if need_w[i]:
-            dws[i] = _wgrad_into(weights[i], gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
         if i > 0:
-            gcur = gemm_x3(gcur, True, wsp[i], False, rows, I, O, EPI_SILU_BWD, Z=zs[i - 1], p=p, seed=seeds[i - 1])
+            dspec = dict(a=gcur, a_kcontig=True, b=wsp[i], b_kcontig=False, M=rows, N=I, K=O, epilogue=EPI_SILU_BWD,
+                         Z=zs[i - 1], p=p, seed=seeds[i - 1])
         elif need_x:
-            dx = gemm_x3(gcur, True, wsp[0], False, rows, I, O)
+            dspec = dict(a=gcur, a_kcontig=True, b=wsp[0], b_kcontig=False, M=rows, N=I, K=O)
+        else:
+            dspec = None
+        wspec = _wgrad_spec(weights[i], gcur, False, inp, False, O, I, rows) if need_w[i] else None
+        if dspec is not None and wspec is not None:   # dW = g^T h_{i-1} and the data grad in one launch
+            gnext, wres = gemm_x3_pair(dspec, wspec)
+            dws[i] = _wgrad_result(weights[i], wspec, wres)
+        else:
+            if need_w[i]:
+                dws[i] = _wgrad_into(weights[i], gcur, False, inp, False, O, I, rows)   # dW = g^T h_{i-1}
+            gnext = gemm_x3(**dspec) if dspec is not None else None
+        if i > 0:
+            gcur = gnext
+        elif need_x:
+            dx = gnext
     return dx, dws
 
 
@@ -732,6 +835,16 @@ class LinearFunction(torch.autograd.Function):
         g2 = g.reshape(-1, O)
         gx = dW = db = None
         high = ctx.high and g2.shape[0] > 0
+        if (high and ctx.wsp is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and
+                not ctx.has_bias):
+            wspec = _wgrad_spec(ctx.weight, g2.contiguous(), False, x.reshape(-1, I).contiguous(), False, O, I,
+                                g2.shape[0])
+            if wspec is not None:   # data and weight gradient in one launch
+                gx, wres = gemm_x3_pair(dict(a=g2, a_kcontig=True, b=ctx.wsp, b_kcontig=False, M=g2.shape[0], N=I,
+                                             K=O), wspec)
+                dW = _wgrad_result(ctx.weight, wspec, wres)
+                ctx.wsp = ctx.weight = None
+                return gx.view(x.shape), dW, None
         if ctx.needs_input_grad[0]:
             if high and ctx.wsp is not None:
                 gx = gemm_x3(g2, True, ctx.wsp, False, g2.shape[0], I, O).view(x.shape)
@@ -775,6 +888,17 @@ class LinearAddFunction(torch.autograd.Function):
         O, I = weight.shape
         g2 = g.reshape(-1, O)
         gx = dW = None
+        wspec = None
+        if ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:
+            wspec = _wgrad_spec(ctx.weight, g2.contiguous(), False, x.reshape(-1, I).contiguous(), False, O, I,
+                                g2.shape[0])
+        if wspec is not None:   # data and weight gradient in one launch
+            gx, wres = gemm_x3_pair(dict(a=g2, a_kcontig=True, b=ctx.wsp, b_kcontig=False, M=g2.shape[0], N=I, K=O),
+                                    wspec)
+            gx = gx.view(x.shape)
+            dW = _wgrad_result(ctx.weight, wspec, wres)
+            ctx.wsp = ctx.weight = None
+            return gx, dW, g if ctx.needs_input_grad[2] else None
         if ctx.needs_input_grad[0]:
             gx = gemm_x3(g2, True, ctx.wsp, False, g2.shape[0], I, O).view(x.shape)
         ctx.wsp = None
@@ -1549,28 +1673,36 @@ class HoistedProjectionFunction(torch.autograd.Function):
         else:
             g = torch.cat([gi if gi is not None else x.new_zeros((T, O)) for gi in gs], 1)
         sink.buf = None
-        gx = gemm_x3(g, True, wsp, False, T, I, n * O) if ctx.needs_input_grad[0] else None
         dws = [None] * n
+        if ctx.needs_input_grad[0] and any(ctx.needs_input_grad[1:]) and _PAIR["on"] and not _SIDE["on"]:
+            # data gradient and the concatenated weight gradient in one launch
+            gx, dw = gemm_x3_pair(dict(a=g, a_kcontig=True, b=wsp, b_kcontig=False, M=T, N=I, K=n * O),
+                                  dict(a=g, a_kcontig=False, b=xs, b_kcontig=False, M=n * O, N=I, K=T))
+            dws = _wgrad_multi_into(weights, g, xs, n * O, I, T, dw=dw)
+            return (gx, *dws)
+        gx = gemm_x3(g, True, wsp, False, T, I, n * O) if ctx.needs_input_grad[0] else None
         if any(ctx.needs_input_grad[1:]):
             dws = _wgrad_multi_into(weights, g, xs, n * O, I, T)
         return (gx, *dws)
 
 
-def _wgrad_multi_into(weights, g, x, O_all: int, I: int, rows: int):
-    """dW_cat = g^T x (O_all, I) as one GEMM, then each weight's row block added into its flat
-    gradient bucket view (dp.direct_grad; returns None for it) or returned as its gradient."""
+def _wgrad_multi_into(weights, g, x, O_all: int, I: int, rows: int, dw=None):
+    """dW_cat = g^T x (O_all, I) as one GEMM (or `dw` already computed by a paired launch), then each
+    weight's row block added into its flat gradient bucket view (dp.direct_grad; returns None for it) or
+    returned as its gradient."""
     from . import dp
     sinks = [dp.direct_grad(w) for w in weights]
     O = weights[0].shape[0]
+    dw_in = dw
 
     def run():
-        dw = gemm_x3(g, False, x, False, O_all, I, rows)
+        dw = dw_in if dw_in is not None else gemm_x3(g, False, x, False, O_all, I, rows)
         for i, sk in enumerate(sinks):
             if sk is not None:
                 sk.add_(dw[i * O:(i + 1) * O])
                 dp.direct_grad_done(weights[i])
         return dw
-    if _SIDE["on"] and any(sk is not None for sk in sinks):
+    if dw_in is None and _SIDE["on"] and any(sk is not None for sk in sinks):
         main = torch.cuda.current_stream(g.device)
         side = _side_stream(g.device)
         side.wait_stream(main)

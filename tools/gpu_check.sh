@@ -167,6 +167,16 @@ PY
       tail -1 "$O/trtests.log"
       run trprobe 300 python -u "$R/tools/trainer_probe.py" > "$O/trainers.json" 2> "$O/trainers.err"
       cat "$O/trainers.json" ;;
+    pairab)   # paired dgrad/wgrad launches: tests, then on / off at both decoder configs
+      run pairtests 400 python -u -m pytest "$R/tests/test_gemm_pair_gpu.py" "$R/tests/test_direct_grad_gpu.py" "$R/tests/test_fused_decoder_gpu.py" \
+        "$R/tests/test_reference_fixtures_gpu.py" "$R/tests/test_mlp_recon_gpu.py" -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pairtests.log" 2>&1 \
+        || { tail -40 "$O/pairtests.log"; exit 1; }
+      tail -1 "$O/pairtests.log"
+      for v in 1 0 1 0; do
+        RQ_X3_PAIR=$v run dm8_p$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_p$v.json" 2> "$O/dm8_p$v.err"
+        RQ_X3_PAIR=$v run am_p$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_p$v.json" 2> "$O/am_p$v.err"
+        python3 -c "import json; print('pair=$v dm8', json.load(open('$O/dm8_p$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_p$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
