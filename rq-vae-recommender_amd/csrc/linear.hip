@@ -1916,6 +1916,12 @@ static bool x3_pair_ts(int k1, const X3Call& c1, const X3Call& c2, dim3 grid, un
 static bool x3_pair_launch(const X3Call& c1, const X3Call& c2, hipStream_t s) {
   if (c1.wide || c2.wide || c1.x3d || c2.x3d || c1.pl.ts != c2.pl.ts) return false;
   if (c2.epi_k != kEpiStore || c2.code != (c2.code & (8 | 2))) return false;   // c2: m-contig A, n-contig B
+  // pair only where a problem alone leaves resident slots idle (the decoder's 1,280 / 11,332-row launches);
+  // two launches that each fill the chip already (the RQ-VAE's 65,536-row 64-tile layers) gain nothing and
+  // measured 4 us slower paired
+  const int64_t w1 = (int64_t)c1.pl.tiles * c1.pl.S, w2 = (int64_t)c2.pl.tiles * c2.pl.S;
+  const int64_t slots = c1.pl.ts == 64 ? (int64_t)x3s_resident(w1 + w2) * (resident_slots() / 2) : x3_slots();
+  if (w1 >= slots && w2 >= slots) return false;
   const bool drop1 = c1.xa.ep.thr != 0 && c1.epi_k != kEpiStore;
   const int n1 = c1.pl.per * 8, n2 = c2.pl.per * 8;
   const dim3 grid((unsigned)(n1 + n2));
