@@ -2475,14 +2475,21 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     int nw = 0, ch = 0;
     const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
     if (short_fused_plan(HD, max_q, max_k)) {
-#define RQ_SHF(R_)                                                                                                  \
-  hipLaunchKernelGGL((attn_bwd_short_fused_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, out, so, dout, \
-                     sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
+#define RQ_SHF(NW_, R_)                                                                                              \
+  hipLaunchKernelGGL((attn_bwd_short_fused_kernel<NW_, R_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, \
+                     dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
+      // 4 waves with up to two key tiles each, or (RQ_ATTN_SHORT_TPW=1, A/B) one key tile per wave (R / 16
+      // waves: 134 instead of 229 VGPRs, 3 waves per SIMD at R = 96) — measured slower on the Amazon step
+      // (6.20-6.22 vs 6.10-6.15 ms, profiles/r03/short_tpw_ab.txt): more waves idle on short sequences
+      static const bool one_tile = [] {
+        const char* e = getenv("RQ_ATTN_SHORT_TPW");
+        return e && e[0] == '1';
+      }();
       switch (dma_rows_for(std::max(max_q, max_k))) {
-        case 32: RQ_SHF(32); break;
-        case 64: RQ_SHF(64); break;
-        case 96: RQ_SHF(96); break;
-        default: RQ_SHF(128); break;
+        case 32: RQ_SHF(2, 32); break;
+        case 64: RQ_SHF(4, 64); break;
+        case 96: if (one_tile) RQ_SHF(6, 96); else RQ_SHF(4, 96); break;
+        default: if (one_tile) RQ_SHF(8, 128); else RQ_SHF(4, 128); break;
       }
 #undef RQ_SHF
       return;

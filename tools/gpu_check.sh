@@ -177,6 +177,11 @@ PY
         RQ_X3_PAIR=$v run am_p$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_p$v.json" 2> "$O/am_p$v.err"
         python3 -c "import json; print('pair=$v dm8', json.load(open('$O/dm8_p$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_p$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    tpwab)   # short fused attention backward: one key tile per wave (default) vs 4 waves x 2 tiles
+      for v in 1 2 1 2; do
+        RQ_ATTN_SHORT_TPW=$v run am_t$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_t$v.json" 2> "$O/am_t$v.err"
+        python3 -c "import json; print('short_tpw=$v amazon', json.load(open('$O/am_t$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
