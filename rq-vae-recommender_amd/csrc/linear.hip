@@ -1678,7 +1678,8 @@ struct X3Call {
 static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                      int accumulate, int defer, void* workspace, size_t ws_bytes, hipStream_t s, X3Call* c) {
+                      int accumulate, int defer, void* workspace, size_t ws_bytes, hipStream_t s, X3Call* c,
+                      bool unsplit = false) {
   const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
   RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
                    epilogue <= 3,
@@ -1715,6 +1716,7 @@ static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kconti
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, &pw);
   if (wide) pl = pw;
+  else if (unsplit && pl.S > 1) pl = x3_plan_s(M, N, K, 1, false, pl.ts);   // a paired launch's partner fills the chip
   // slab path: split-K partials go to the workspace with the plain store, and x3_reduce_kernel applies
   // the real epilogue (and the accumulation); an unsplit accumulating call adds in the GEMM's epilogue
   const bool slab = pl.S > 1;
@@ -1913,23 +1915,34 @@ static bool x3_pair_ts(int k1, const X3Call& c1, const X3Call& c2, dim3 grid, un
 // 64-tile kernel with the same tile size), for the operand forms of the decoder's backward: c1 = g W
 // (A fp32 or split k-contiguous, B split n-contiguous; plain or SiLU'-with-dropout epilogue), c2 = g^T x
 // (A fp32 or split m-contiguous, B fp32 or split n-contiguous, plain). false: no instantiation.
-static bool x3_pair_launch(const X3Call& c1, const X3Call& c2, hipStream_t s) {
+static int x3_pair_k1(const X3Call& c1) {
+  const bool drop1 = c1.xa.ep.thr != 0 && c1.epi_k != kEpiStore;
+  return c1.code | (c1.epi_k == kEpiSiluBwd ? (drop1 ? 64 : 32) : (c1.epi_k == kEpiStore ? 0 : 128));
+}
+
+// The two problems can share a launch: both on the 128- / 64-tile kernel with one tile size, an instantiated
+// form pair, and at least one of them leaving resident slots idle alone (the decoder's 40..11,332-row
+// launches; two launches that each fill the chip already — the RQ-VAE's 65,536-row 64-tile layers — gain
+// nothing and measured 4 us slower paired).
+static bool x3_pairable(const X3Call& c1, const X3Call& c2) {
   if (c1.wide || c2.wide || c1.x3d || c2.x3d || c1.pl.ts != c2.pl.ts) return false;
   if (c2.epi_k != kEpiStore || c2.code != (c2.code & (8 | 2))) return false;   // c2: m-contig A, n-contig B
-  // pair only where a problem alone leaves resident slots idle (the decoder's 1,280 / 11,332-row launches);
-  // two launches that each fill the chip already (the RQ-VAE's 65,536-row 64-tile layers) gain nothing and
-  // measured 4 us slower paired
+  const int k1 = x3_pair_k1(c1);
+  if (k1 != (16 | 2) && k1 != (16 | 8 | 2) && k1 != (16 | 2 | 32) && k1 != (16 | 2 | 64)) return false;
   const int64_t w1 = (int64_t)c1.pl.tiles * c1.pl.S, w2 = (int64_t)c2.pl.tiles * c2.pl.S;
   const int64_t slots = c1.pl.ts == 64 ? (int64_t)x3s_resident(w1 + w2) * (resident_slots() / 2) : x3_slots();
-  if (w1 >= slots && w2 >= slots) return false;
-  const bool drop1 = c1.xa.ep.thr != 0 && c1.epi_k != kEpiStore;
+  return !(w1 >= slots && w2 >= slots);
+}
+
+static bool x3_pair_launch(const X3Call& c1, const X3Call& c2, hipStream_t s) {
+  if (!x3_pairable(c1, c2)) return false;
+  const int64_t w1 = (int64_t)c1.pl.tiles * c1.pl.S, w2 = (int64_t)c2.pl.tiles * c2.pl.S;
   const int n1 = c1.pl.per * 8, n2 = c2.pl.per * 8;
   const dim3 grid((unsigned)(n1 + n2));
   const bool t64 = c1.pl.ts == 64;
   unsigned pad = 0;
-  if (t64 && RQ_X3S_COMPACT && x3s_resident((int64_t)c1.pl.tiles * c1.pl.S + (int64_t)c2.pl.tiles * c2.pl.S) == kXWG)
-    pad = 32768u;   // few workgroups: spread them 2 per CU (x3s_pad_lds)
-  const int k1 = c1.code | (c1.epi_k == kEpiSiluBwd ? (drop1 ? 64 : 32) : (c1.epi_k == kEpiStore ? 0 : 128));
+  if (t64 && RQ_X3S_COMPACT && x3s_resident(w1 + w2) == kXWG) pad = 32768u;   // few workgroups: 2 per CU (x3s_pad_lds)
+  const int k1 = x3_pair_k1(c1);
   return t64 ? x3_pair_ts<64>(k1, c1, c2, grid, pad, s, n1) : x3_pair_ts<128>(k1, c1, c2, grid, 0u, s, n1);
 }
 
@@ -1954,10 +1967,21 @@ int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcont
 
 static_assert(sizeof(rq_gemm_desc) == 184, "rq_gemm_desc layout (the ctypes mirror in rqvae_hip/ops.py)");
 
-static int x3_prepare_desc(const rq_gemm_desc& d, hipStream_t s, X3Call* c) {
+static int x3_prepare_desc(const rq_gemm_desc& d, hipStream_t s, X3Call* c, bool unsplit = false) {
   return x3_prepare(d.A, d.A_lo, d.lda, d.a_kcontig, d.B, d.B_lo, d.ldb, d.b_kcontig, d.M, d.N, d.K, d.C, d.ldc,
                     d.epilogue, d.Z, d.H_hi, d.H_lo, d.ldh, d.p, d.seed, d.accumulate, d.defer, d.workspace, d.ws_bytes, s,
-                    c);
+                    c, unsplit);
+}
+
+#ifndef RQ_X3_PAIR_UNSPLIT
+#define RQ_X3_PAIR_UNSPLIT 0   // 1: a paired data gradient runs unsplit (no slab reduction launch; measured slower: its chain dominates)
+#endif
+static bool x3_pair_unsplit() {
+  static const bool on = [] {
+    const char* e = getenv("RQ_X3_PAIR_UNSPLIT");
+    return e ? e[0] != '0' : RQ_X3_PAIR_UNSPLIT != 0;
+  }();
+  return on;
 }
 
 int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
@@ -1968,6 +1992,15 @@ int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
   for (int i = 0; i < 2; ++i) {
     const int rc = x3_prepare_desc(d[i], s, &c[i]);
     if (rc) return rc;
+  }
+  // a data gradient split only to fill the chip alone (the decoder's 40..1,280 future-token rows) runs
+  // unsplit next to its weight gradient: no slab, no reduction launch (re-planned when the pair still forms)
+  if (x3_pair_enabled() && x3_pair_unsplit() && !c[0].trivial && !c[1].trivial && c[0].slab && !c[0].wide &&
+      !c[0].x3d) {
+    X3Call u;
+    const int rc = x3_prepare_desc(d[0], s, &u, true);
+    if (rc) return rc;
+    if (x3_pairable(u, c[1])) c[0] = u;
   }
   if (c[0].trivial || c[1].trivial || !x3_pair_enabled() || !x3_pair_launch(c[0], c[1], s)) {
     for (int i = 0; i < 2; ++i) {

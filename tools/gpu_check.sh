@@ -182,6 +182,15 @@ PY
         RQ_ATTN_SHORT_TPW=$v run am_t$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_t$v.json" 2> "$O/am_t$v.err"
         python3 -c "import json; print('short_tpw=$v amazon', json.load(open('$O/am_t$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    unsplitab)   # paired data gradient unsplit (RQ_X3_PAIR_UNSPLIT) on / off
+      run pairtests2 300 python -u -m pytest "$R/tests/test_gemm_pair_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" "$R/tests/test_direct_grad_gpu.py" \
+        -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pairtests2.log" 2>&1 || { tail -40 "$O/pairtests2.log"; exit 1; }
+      tail -1 "$O/pairtests2.log"
+      for v in 1 0 1 0; do
+        RQ_X3_PAIR_UNSPLIT=$v run dm8_u$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_u$v.json" 2> "$O/dm8_u$v.err"
+        RQ_X3_PAIR_UNSPLIT=$v run am_u$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_u$v.json" 2> "$O/am_u$v.err"
+        python3 -c "import json; print('pair_unsplit=$v dm8', json.load(open('$O/dm8_u$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_u$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     keysdm8)   # per-shape device times (and GEMM plans) of one ML-32M decoder step at 8 sequences
       run keys_dm8 200 python -u "$R/tools/dec_gemm_keys.py" 5 dm8 > "$O/keys_dm8.jsonl" 2> "$O/keys_dm8.err"
       tail -1 "$O/keys_dm8.jsonl" ;;
