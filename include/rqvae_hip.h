@@ -244,6 +244,14 @@ int rq_attn_fewq_fused_enable(int enable);
  * 64: the encoder's Amazon contexts): 1 (default unless RQ_ATTN_SHORT_FUSED=0 is set) one pass, 0 the
  * two-pass LDS-DMA dQ + dK/dV kernels. Returns the previous setting. */
 int rq_attn_short_fused_enable(int enable);
+/* rq_segment_sum over up to 16 sources at once (every embedding table of a decoder step: modules/model.py:59-63,
+ * modules/embedding/id_embedder.py): source t's rows (n[t], D) with keys in [0, K[t]) (others and pad[t]
+ * skipped) sum into rows [sum_{u<t} K[u], + K[t]) of out (sum K, D). One pack launch + one segmented-sum
+ * chain instead of one chain per table; sum K <= 4096. */
+size_t rq_segment_sum_multi_workspace(int count, const int64_t* n, const int64_t* K, int64_t D);
+int rq_segment_sum_multi(int count, const float* const* rows, const int64_t* const* keys, const int64_t* n,
+                         const int64_t* K, const int64_t* pad, int64_t D, float* out, void* workspace, size_t ws_bytes,
+                         void* stream);
 /* One rq_gemm_bf16x3_ex3 call as a descriptor (the same fields, the same meaning). */
 typedef struct rq_gemm_desc {
   const void* A;

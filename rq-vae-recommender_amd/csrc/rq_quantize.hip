@@ -1653,6 +1653,93 @@ size_t rq_segment_sum_workspace(int64_t B, int64_t K) {
   return (size_t)(K * nblk + (K + 1) + B) * sizeof(int) + 256 + (size_t)(kSegSplit * K) * 1024 * sizeof(float);
 }
 
+}  // extern "C"
+
+namespace rqhip {
+// Pack of several (rows, keys) sources into one: global row i of source t = i - rowbase[t] (t by a scan over
+// <= kSegMultiMax bases), key -> -1 (skipped) when outside [0, K_t) or the source's padding index, else
+// keybase[t] + key. One thread per float4 of a row; the row's first lane writes the key.
+constexpr int kSegMultiMax = 16;
+struct SegMultiTable {
+  const float* rows[kSegMultiMax];
+  const int64_t* keys[kSegMultiMax];
+  int64_t rowbase[kSegMultiMax + 1];
+  int64_t keybase[kSegMultiMax];
+  int64_t K[kSegMultiMax];
+  int64_t pad[kSegMultiMax];
+  int count;
+};
+__global__ void __launch_bounds__(256) seg_multi_pack_kernel(SegMultiTable t, int D, float* __restrict__ rows_out,
+                                                             int64_t* __restrict__ keys_out) {
+  const int F4 = D / 4;
+  const int64_t total = t.rowbase[t.count];
+  for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < total * F4; f += (int64_t)gridDim.x * 256) {
+    const int64_t i = f / F4;
+    const int c = (int)(f - i * F4);
+    int s = 0;
+    while (s + 1 < t.count && i >= t.rowbase[s + 1]) ++s;
+    const int64_t r = i - t.rowbase[s];
+    reinterpret_cast<float4*>(rows_out + i * D)[c] = reinterpret_cast<const float4*>(t.rows[s] + r * D)[c];
+    if (c == 0) {
+      const int64_t k = t.keys[s][r];
+      keys_out[i] = (k < 0 || k >= t.K[s] || k == t.pad[s]) ? -1 : t.keybase[s] + k;
+    }
+  }
+}
+}  // namespace rqhip
+
+extern "C" {
+
+int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
+                   void* workspace, size_t ws_bytes, void* stream);
+
+size_t rq_segment_sum_multi_workspace(int count, const int64_t* n, const int64_t* K, int64_t D) {
+  if (count <= 0 || !n || !K) return 0;
+  int64_t rows = 0, keys = 0;
+  for (int i = 0; i < count; ++i) {
+    rows += n[i];
+    keys += K[i];
+  }
+  return (size_t)rows * (size_t)D * sizeof(float) + (size_t)rows * sizeof(int64_t) + 256 +
+         rq_segment_sum_workspace(rows, keys);
+}
+
+int rq_segment_sum_multi(int count, const float* const* rows, const int64_t* const* keys, const int64_t* n,
+                         const int64_t* K, const int64_t* pad, int64_t D, float* out, void* workspace, size_t ws_bytes,
+                         void* stream) {
+  RQ_CHECK_ARG(count >= 1 && count <= kSegMultiMax && rows && keys && n && K && pad && out && workspace,
+               "rq_segment_sum_multi: 1 <= count <= %d sources, non-null arrays", kSegMultiMax);
+  SegMultiTable t;
+  t.count = count;
+  t.rowbase[0] = 0;
+  int64_t kb = 0;
+  for (int i = 0; i < count; ++i) {
+    RQ_CHECK_ARG(n[i] >= 0 && K[i] >= 1 && (n[i] == 0 || (rows[i] && keys[i])) && (uintptr_t)rows[i] % 16 == 0,
+                 "rq_segment_sum_multi: source %d: bad rows / keys / K", i);
+    t.rows[i] = rows[i];
+    t.keys[i] = keys[i];
+    t.rowbase[i + 1] = t.rowbase[i] + n[i];
+    t.keybase[i] = kb;
+    t.K[i] = K[i];
+    t.pad[i] = pad[i];
+    kb += K[i];
+  }
+  const int64_t total = t.rowbase[count];
+  RQ_CHECK_ARG(ws_bytes >= rq_segment_sum_multi_workspace(count, n, K, D), "rq_segment_sum_multi: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* prow = static_cast<float*>(workspace);
+  int64_t* pkey = reinterpret_cast<int64_t*>(prow + total * D);
+  char* rest = reinterpret_cast<char*>((((uintptr_t)(pkey + total)) + 255) & ~(uintptr_t)255);
+  const size_t used = (size_t)(rest - static_cast<char*>(workspace));
+  if (total > 0) {
+    const int64_t f4 = total * (D / 4);
+    const unsigned grid = (unsigned)std::min<int64_t>((f4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(seg_multi_pack_kernel, dim3(grid), dim3(256), 0, s, t, (int)D, prow, pkey);
+    RQ_LAUNCH_CHECK("seg_multi_pack_kernel");
+  }
+  return rq_segment_sum(prow, pkey, total, D, kb, out, nullptr, rest, ws_bytes - used, stream);
+}
+
 int rq_segment_sum(const float* rows, const int64_t* keys, int64_t B, int64_t D, int64_t K, float* out, int64_t* counts,
                    void* workspace, size_t ws_bytes, void* stream) {
   RQ_CHECK_ARG(rows && keys && out && workspace, "rq_segment_sum: null pointer");

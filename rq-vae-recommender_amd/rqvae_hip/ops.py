@@ -538,9 +538,82 @@ def _defer_push(ws: torch.Tensor, out: torch.Tensor, n: int, S: int, layout: int
     _DEFER["outs"].add(out.data_ptr())
 
 
+# Deferred embedding-table gradients: each table's (rows, keys) waits here when its weight's gradient lives
+# in a flat bucket; the flush sums every waiting table in ONE segmented-sum chain (rq_segment_sum_multi) and
+# adds each table's slice into its bucket view through the batched reduction above — instead of one
+# 6-launch chain plus an accumulate per table (the decoder's 4-6 tables: ~30 launches a step).
+_EMB = {"pending": [], "on": _os.environ.get("RQ_EMB_DEFER", "1") != "0"}
+_EMB_KMAX = 4096          # rq_segment_sum's key limit, per batch
+_EMB_SRC_MAX = 16         # sources per rq_segment_sum_multi call
+
+
+def emb_defer_enable(enable) -> bool:
+    """Batched (deferred) embedding-table gradients on/off (A/B); returns the previous setting."""
+    prev = _EMB["on"]
+    _EMB["on"] = bool(enable)
+    return prev
+
+
+def _emb_grad(weight, g: torch.Tensor, keys: torch.Tensor, K: int, padding_idx):
+    """An embedding table's gradient: deferred into its flat bucket view (returns None) when the owner
+    GradBuckets batches reductions, else the (K, E) tensor from _table_grad."""
+    from . import dp
+    E = g.shape[-1]
+    if _EMB["on"] and E % 4 == 0 and 4 <= E <= 1024 and K <= _EMB_KMAX and weight is not None \
+            and dp.defer_ok(weight):
+        sink = dp.direct_grad(weight)
+        if sink is not None and sink.is_contiguous() and sink.data_ptr() % 16 == 0 \
+                and sink.dtype == torch.float32 and sink.data_ptr() not in _DEFER["outs"]:
+            pad = -2 if padding_idx is None else int(padding_idx) % K
+            _EMB["pending"].append((g.contiguous().float(), keys.contiguous().to(torch.int64), int(K), pad, sink,
+                                    torch.cuda.current_stream(g.device)))
+            _DEFER["outs"].add(sink.data_ptr())
+            dp.direct_grad_done(weight)
+            return None
+    return _table_grad(g, keys, K, padding_idx)
+
+
+def _flush_embeddings() -> None:
+    """Sum the waiting tables (grouped by row width, <= 16 sources and <= 4096 keys a call) and queue each
+    table's slice as an accumulate-into-sink entry of the batched reduction."""
+    import ctypes
+    pend, _EMB["pending"] = _EMB["pending"], []
+    groups, cur_key = [], None
+    for e in sorted(pend, key=lambda e: e[0].shape[-1]):
+        E = e[0].shape[-1]
+        if not groups or cur_key != E or len(groups[-1]) == _EMB_SRC_MAX or \
+                sum(x[2] for x in groups[-1]) + e[2] > _EMB_KMAX:
+            groups.append([])
+            cur_key = E
+        groups[-1].append(e)
+    L = _lib.load()
+    for grp in groups:
+        dev = grp[0][0].device
+        cs = torch.cuda.current_stream(dev)
+        for e in grp:
+            if e[5] != cs:
+                cs.wait_stream(e[5])
+        n, E = len(grp), grp[0][0].shape[-1]
+        I64, P = ctypes.c_int64 * n, ctypes.c_void_p * n
+        rows_n = I64(*[e[0].shape[0] for e in grp])
+        Ks = I64(*[e[2] for e in grp])
+        nbytes = L.rq_segment_sum_multi_workspace(n, rows_n, Ks, E)
+        ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
+        out = torch.empty((sum(e[2] for e in grp), E), device=dev, dtype=torch.float32)
+        TIMER.around("emb_segsum", call, "rq_segment_sum_multi", n, P(*[e[0].data_ptr() for e in grp]),
+                     P(*[e[1].data_ptr() for e in grp]), rows_n, Ks, I64(*[e[3] for e in grp]), E, ptr(out),
+                     ptr(ws), nbytes, stream_handle(dev))
+        base = 0
+        for e in grp:
+            _defer_push(out[base:base + e[2]], e[4], e[2] * E, 1, 0)
+            base += e[2]
+
+
 def flush_reductions() -> None:
     """Run every pending deferred reduction (stream-ordered after their producers: side-stream weight
     grads are joined first) and release their partial buffers."""
+    if _EMB["pending"]:
+        _flush_embeddings()
     pend = _DEFER["pending"]
     if not pend:
         return
@@ -563,7 +636,7 @@ def flush_reductions() -> None:
 
 
 def pending_reductions() -> int:
-    return len(_DEFER["pending"])
+    return len(_DEFER["pending"]) + len(_EMB["pending"])
 
 
 def gemm_x3_choice(M: int, N: int, K: int, a_split: bool, b_split: bool, a_kcontig: bool, b_kcontig: bool,
@@ -1162,12 +1235,13 @@ class EmbeddingFunction(torch.autograd.Function):
         require_gpu(weight, idx, what="embedding")
         ctx.save_for_backward(idx)
         ctx.K, ctx.padding_idx = weight.shape[0], padding_idx
+        ctx.weight = weight if isinstance(weight, torch.nn.Parameter) else None
         return torch.nn.functional.embedding(idx, weight, padding_idx)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        return _table_grad(g.reshape(-1, g.shape[-1]), idx.reshape(-1), ctx.K, ctx.padding_idx), None, None
+        return _emb_grad(ctx.weight, g.reshape(-1, g.shape[-1]), idx.reshape(-1), ctx.K, ctx.padding_idx), None, None
 
 
 class EmbeddingPairFunction(torch.autograd.Function):
@@ -1181,6 +1255,7 @@ class EmbeddingPairFunction(torch.autograd.Function):
         require_gpu(weight, ia, ib, what="embedding_pair")
         ctx.save_for_backward(ia, ib)
         ctx.K, ctx.padding_idx = weight.shape[0], padding_idx
+        ctx.weight = weight if isinstance(weight, torch.nn.Parameter) else None
         F_ = torch.nn.functional
         return F_.embedding(ia, weight, padding_idx), F_.embedding(ib, weight, padding_idx)
 
@@ -1194,7 +1269,7 @@ class EmbeddingPairFunction(torch.autograd.Function):
         gb = torch.zeros(ib.shape + (E,), device=ib.device) if gb is None else gb
         keys = torch.cat([ia, ib], dim=1).reshape(-1)
         g = torch.cat([ga, gb], dim=1).reshape(-1, E)
-        return _table_grad(g, keys, ctx.K, ctx.padding_idx), None, None, None
+        return _emb_grad(ctx.weight, g, keys, ctx.K, ctx.padding_idx), None, None, None
 
 
 def embedding_pair(ia: torch.Tensor, ib: torch.Tensor, weight: torch.Tensor, padding_idx=None):

@@ -205,3 +205,69 @@ def test_deferred_reductions_bitwise(device, model_kind):
             assert torch.equal(res[True][n], res[False][n]), n
     finally:
         torch.set_float32_matmul_precision("highest")
+
+
+def test_segment_sum_multi_matches_per_table(device):
+    """rq_segment_sum_multi over several sources (padding keys, out-of-range keys, an empty source) is
+    bitwise the per-source rq_segment_sum into the stacked output."""
+    import ctypes
+    from rqvae_hip import _lib, ops
+    gen = torch.Generator(device=device).manual_seed(11)
+    spec = [(700, 257, 256), (0, 33, None), (1500, 1025, 1024), (90, 7, -1), (333, 64, 5)]
+    E = 64
+    rows, keys, pads = [], [], []
+    for n, K, pad in spec:
+        rows.append(torch.randn(n, E, generator=gen, device=device))
+        keys.append(torch.randint(-2, K + 3, (n,), generator=gen, device=device))
+        pads.append(-2 if pad is None else pad % K)
+    n = len(spec)
+    I64, P = ctypes.c_int64 * n, ctypes.c_void_p * n
+    rn, Ks = I64(*[r.shape[0] for r in rows]), I64(*[s[1] for s in spec])
+    L = _lib.load()
+    nbytes = L.rq_segment_sum_multi_workspace(n, rn, Ks, E)
+    ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
+    out = torch.full((sum(s[1] for s in spec), E), float("nan"), device=device)
+    _lib.call("rq_segment_sum_multi", n, P(*[r.data_ptr() for r in rows]), P(*[k.data_ptr() for k in keys]), rn, Ks,
+              I64(*pads), E, out.data_ptr(), ws.data_ptr(), nbytes, _lib.stream_handle(out.device))
+    base = 0
+    for (nr, K, _), r, k, pad in zip(spec, rows, keys, pads):
+        kk = torch.where(k == pad, -1, k)
+        want = ops.segment_sum(r, kk, K, with_counts=False)[0] if nr else torch.zeros(K, E, device=device)
+        assert torch.equal(out[base:base + K], want)
+        base += K
+
+
+def test_deferred_embedding_grads_bitwise(device):
+    """Embedding-table gradients batched at the flush (one rq_segment_sum_multi + the batched reduction)
+    equal the per-table segmented sums bit for bit, and are pending until synchronize()."""
+    from data.processed import synthetic_tokenized_batch
+    from modules.model import EncoderDecoderRetrievalModel
+    from rqvae_hip import dp, ops
+    torch.set_float32_matmul_precision("high")
+    try:
+        torch.manual_seed(9)
+        a = EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.0, num_heads=4, n_layers=2,
+                                         num_embeddings=64, sem_id_dim=4, inference_verifier_fn=None,
+                                         max_pos=80).to(device).train()
+        b = copy.deepcopy(a)
+        batch = synthetic_tokenized_batch(64, 20, 4, 64, 9, device)
+        res = {}
+        for m, on in ((a, False), (b, True)):
+            prev = ops.emb_defer_enable(on)
+            try:
+                buckets = dp.GradBuckets(m.parameters(), overlap=False, flat_views=True, defer_reductions=True)
+                buckets.zero_grad()
+                ops._SEED["n"] = 0
+                m(batch).loss.backward()
+                if on:
+                    assert len(ops._EMB["pending"]) > 0
+                buckets.synchronize()
+                assert ops.pending_reductions() == 0
+            finally:
+                ops.emb_defer_enable(prev)
+            res[on] = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        assert res[True].keys() == res[False].keys()
+        for n in res[False]:
+            assert torch.equal(res[True][n], res[False][n]), n
+    finally:
+        torch.set_float32_matmul_precision("highest")

@@ -182,6 +182,16 @@ PY
         RQ_ATTN_SHORT_TPW=$v run am_t$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_t$v.json" 2> "$O/am_t$v.err"
         python3 -c "import json; print('short_tpw=$v amazon', json.load(open('$O/am_t$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    embab)   # batched (deferred) embedding-table gradients on / off
+      run embtests 400 python -u -m pytest "$R/tests/test_direct_grad_gpu.py" "$R/tests/test_fused_decoder_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" \
+        "$R/tests/test_graph_gpu.py" "$R/tests/test_train_gpu.py" -m gpu -x -q --timeout 120 --timeout-method thread > "$O/embtests.log" 2>&1 \
+        || { tail -40 "$O/embtests.log"; exit 1; }
+      tail -1 "$O/embtests.log"
+      for v in 1 0 1 0; do
+        RQ_EMB_DEFER=$v run dm8_e$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_e$v.json" 2> "$O/dm8_e$v.err"
+        RQ_EMB_DEFER=$v run am_e$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_e$v.json" 2> "$O/am_e$v.err"
+        python3 -c "import json; print('emb_defer=$v dm8', json.load(open('$O/dm8_e$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_e$v.json'))['decoder_amazon']['ms_per_step'])"
+      done ;;
     unsplitab)   # paired data gradient unsplit (RQ_X3_PAIR_UNSPLIT) on / off
       run pairtests2 300 python -u -m pytest "$R/tests/test_gemm_pair_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" "$R/tests/test_direct_grad_gpu.py" \
         -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pairtests2.log" 2>&1 || { tail -40 "$O/pairtests2.log"; exit 1; }
