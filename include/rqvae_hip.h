@@ -233,6 +233,9 @@ int rq_gemm_x3s_enable(int mode);
  * kernel): 0 (default unless RQ_X3D=1/2 is set: slower inside the decoder step) off, 1 for an
  * n-contiguous B (data gradients), 2 also for a k-contiguous B. Returns the previous setting. A/B switch. */
 int rq_gemm_x3d_enable(int enable);
+/* 1 (default): 128-/64-tile launches whose K and split-K chunk are whole 32-deep stages stage operands
+ * without k masks (bitwise the masked path); 0: always masked (A/B). Returns the previous setting. */
+int rq_gemm_kfull_enable(int enable);
 /* LDS-DMA staged short attention forms (key ranges <= 128 rows, head dim 64): 1 (default unless
  * RQ_ATTN_DMA=0 is set) on, 0 off (the register-staged kernels). Returns the previous setting. A/B switch. */
 int rq_attn_dma_enable(int enable);

@@ -302,7 +302,9 @@ __device__ __forceinline__ int row_off(int rr, int c) { return rr * (2 * kXK) + 
 //                       thread, copied to LDS as they are.
 // The LDS images do not depend on TR (a 64-row tile uses the first 64 rows of a row image and the
 // first 64 columns of a column image's 256-B rows, with the same swizzles).
-template <bool KC, bool SP, int TR = 128>
+// KF ("k full"): every stage of the launch lies inside [k_lo, k_hi) (K and the split-K chunk multiples of
+// the stage depth), so no k mask, masked address or zeroing select is emitted.
+template <bool KC, bool SP, int TR = 128, bool KF = false>
 struct XStage {
   static_assert(TR == 128 || (TR == 64 && kXK == 32), "tile rows (64-row tiles need 32-deep k stages)");
   // fp32, k-contig: float4 per thread (two per 16-B bf16 chunk of the row image)
@@ -330,7 +332,7 @@ struct XStage {
         for (int j = 0; j < NJ_FK; ++j) {
           const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * (j >> 1), R - 1);
           const int64_t k = kb + (tid % kXCPR) * 8 + 4 * (j & 1);
-          ok[j] = k < k_hi;
+          ok[j] = KF || k < k_hi;
           v[j] = *reinterpret_cast<const uint4*>(X + row * ld + (ok[j] ? k : k_lo));
         }
       } else {              // thread: 4 consecutive rows 4 (tid % CT), k rows tid / CT + KR j
@@ -338,7 +340,7 @@ struct XStage {
 #pragma unroll
         for (int j = 0; j < NJ_FM; ++j) {
           const int64_t k = kb + (tid / CT_F) + KR_F * j;
-          ok[j] = k < k_hi;
+          ok[j] = KF || k < k_hi;
           v[j] = *reinterpret_cast<const uint4*>(X + (ok[j] ? k : k_lo) * ld + col);
         }
       }
@@ -350,7 +352,7 @@ struct XStage {
         for (int j = 0; j < NJ_SK; ++j) {
           const int64_t row = min(r0 + (tid / kXCPR) + (256 / kXCPR) * j, R - 1);
           const int64_t k = kb + (tid % kXCPR) * 8;
-          ok[j] = k < k_hi;
+          ok[j] = KF || k < k_hi;
           const int64_t o = row * ld + (ok[j] ? k : k_lo);
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
@@ -360,7 +362,7 @@ struct XStage {
 #pragma unroll
         for (int j = 0; j < NJ_SM; ++j) {
           const int64_t k = kb + (tid / CT_S) + KR_S * j;
-          ok[j] = k < k_hi;
+          ok[j] = KF || k < k_hi;
           const int64_t o = (ok[j] ? k : k_lo) * ld + col;
           v[j] = *reinterpret_cast<const uint4*>(Xh + o);
           v[2 + j] = *reinterpret_cast<const uint4*>(Xl + o);
@@ -651,6 +653,7 @@ struct X3Args {
   float* C;
   int64_t ldc;
   X3Epilogue ep;
+  int kf;   // 1: K and chunk are multiples of kXK (the unmasked staging path)
 };
 
 // LDS bytes of one plane of the TS-tile form (the 64-tile form's compact images: half of every plane)
@@ -660,8 +663,8 @@ constexpr int x3_plane_bytes() { return (TS == 64 && RQ_X3S_COMPACT) ? kXPlane /
 // TS = output tile (128, or 64 for launches whose 128-tiles cannot fill the chip: the decoder's 1,280
 // future-token rows): 4 waves of (TS / 2)^2 outputs, the same k order (so the same result) either way.
 // The body of one workgroup `bid` of problem `a` over the LDS block `lds` (8 planes).
-template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP, int TS>
-__device__ __forceinline__ void x3_body(const X3Args& a, int bid, char* __restrict__ lds) {
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP, int TS, bool KF>
+__device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __restrict__ lds) {
   const void* __restrict__ A = a.A;
   const void* __restrict__ Al = a.Al;
   const void* __restrict__ B = a.B;
@@ -707,8 +710,8 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int bid, char* __restri
   // 64-tile stage is 4x less MFMA work, so that form keeps 4 stages in flight).
   constexpr int kDepth = TS == 64 ? RQ_X3S_DEPTH : RQ_X3_DEPTH;
   static_assert(kDepth >= 2 && kDepth <= 4, "stage sets");
-  XStage<AKC, ASP, TS> sa0, sa1, sa2, sa3;
-  XStage<BKC, BSP, TS> sb0, sb1, sb2, sb3;
+  XStage<AKC, ASP, TS, KF> sa0, sa1, sa2, sa3;
+  XStage<BKC, BSP, TS, KF> sb0, sb1, sb2, sb3;
   sa0.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
   sb0.load(B, Bl, ldb, n0, N, k_lo, k_lo, k_hi, tid);
   sa1.load(A, Al, lda, m0, M, k_lo + (int64_t)min(1, nst - 1) * kXK, k_lo, k_hi, tid);
@@ -826,6 +829,15 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int bid, char* __restri
         }
     }
   }
+}
+
+// The body with the staging path picked once per workgroup (uniform): unmasked when every stage is full.
+template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP, int TS>
+__device__ __forceinline__ void x3_body(const X3Args& a, int bid, char* __restrict__ lds) {
+  if (a.kf)
+    x3_body_k<AKC, ASP, BKC, BSP, EPI, DROP, TS, true>(a, bid, lds);
+  else
+    x3_body_k<AKC, ASP, BKC, BSP, EPI, DROP, TS, false>(a, bid, lds);
 }
 
 template <bool AKC, bool ASP, bool BKC, bool BSP, int EPI, bool DROP = false, int TS = 128>
@@ -1572,6 +1584,16 @@ static bool x3_pair_enabled() {
   return g_x3_pair != 0;
 }
 
+// RQ_X3_KFULL=0 (or rq_gemm_kfull_enable(0)): every 128-/64-tile launch stages through the masked path (A/B)
+static int g_x3_kfull = -1;
+static bool x3_kfull_enabled() {
+  if (g_x3_kfull < 0) {
+    const char* e = getenv("RQ_X3_KFULL");
+    g_x3_kfull = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_x3_kfull != 0;
+}
+
 // RQ_X3D=0 in the environment (or rq_gemm_x3d_enable(0)) keeps the register-staged 128-tile kernel for
 // fp32 k-contiguous A x split B (A/B switch, kernel-vs-kernel tests).
 static int g_x3d = -1;
@@ -1747,7 +1769,8 @@ static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kconti
   c->C = C;
   c->out = out;
   const int64_t ldo = pl.S > 1 ? N : ldc;
-  c->xa = X3Args{A, A_lo, lda, B, B_lo, ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep};
+  c->xa = X3Args{A, A_lo, lda, B, B_lo, ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep,
+                 (int)(x3_kfull_enabled() && K % kXK == 0 && pl.chunk % kXK == 0)};
   return 0;
 }
 
@@ -2189,6 +2212,12 @@ int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_sp
 int rq_gemm_pair_enable(int enable) {
   const int prev = x3_pair_enabled() ? 1 : 0;
   g_x3_pair = enable ? 1 : 0;
+  return prev;
+}
+
+int rq_gemm_kfull_enable(int enable) {
+  const int prev = x3_kfull_enabled() ? 1 : 0;
+  g_x3_kfull = enable ? 1 : 0;
   return prev;
 }
 

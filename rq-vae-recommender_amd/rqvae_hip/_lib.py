@@ -68,6 +68,7 @@ _SIGS = {
     "rq_gemm_pair_enable": ([_I], _I),
     "rq_segment_sum_multi_workspace": ([_I, _P, _P, _I64], _SZ),
     "rq_segment_sum_multi": ([_I, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P], _I),
+    "rq_gemm_kfull_enable": ([_I], _I),
     "rq_attn_dma_enable": ([_I], _I),
     "rq_attn_fewq_fused_enable": ([_I], _I),
     "rq_attn_short_fused_enable": ([_I], _I),

@@ -521,6 +521,11 @@ def gemm_x3_pair(spec1: dict, spec2: dict):
     return _x3_result(c1, splits[0]), _x3_result(c2, splits[1])
 
 
+def gemm_kfull_enable(enable) -> int:
+    """Unmasked staging for whole-stage launches (default on); False = the masked path (A/B, tests)."""
+    return int(_lib.load().rq_gemm_kfull_enable(int(bool(enable))))
+
+
 def gemm_pair_enable(enable) -> int:
     """Paired data-/weight-gradient launches (rq_gemm_bf16x3_pair): False = two launches (A/B)."""
     return int(_lib.load().rq_gemm_pair_enable(int(bool(enable))))

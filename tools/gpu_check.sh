@@ -182,6 +182,17 @@ PY
         RQ_ATTN_SHORT_TPW=$v run am_t$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_t$v.json" 2> "$O/am_t$v.err"
         python3 -c "import json; print('short_tpw=$v amazon', json.load(open('$O/am_t$v.json'))['decoder_amazon']['ms_per_step'])"
       done ;;
+    kfullab)   # unmasked GEMM staging (RQ_X3_KFULL) on / off: tests, then the decoder configs and the RQ-VAE line
+      run kftests 500 python -u -m pytest "$R/tests/test_gemm_kfull_gpu.py" "$R/tests/test_gemm_pair_gpu.py" "$R/tests/test_gemm_bf16x3_gpu.py" \
+        "$R/tests/test_gemm_x3s_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" -m gpu -x -q --timeout 120 --timeout-method thread > "$O/kftests.log" 2>&1 \
+        || { tail -40 "$O/kftests.log"; exit 1; }
+      tail -1 "$O/kftests.log"
+      for v in 1 0 1 0; do
+        RQ_X3_KFULL=$v run dm8_k$v 200 python -u "$R/bench.py" --decoder-only --dm-batch 8 > "$O/dm8_k$v.json" 2> "$O/dm8_k$v.err"
+        RQ_X3_KFULL=$v run am_k$v 200 python -u "$R/bench.py" --decoder-only > "$O/am_k$v.json" 2> "$O/am_k$v.err"
+        RQ_X3_KFULL=$v run rq_k$v 200 python -u "$R/bench.py" --no-cpu-baseline --no-pmc --no-extras > "$O/rq_k$v.json" 2> "$O/rq_k$v.err"
+        python3 -c "import json; print('kfull=$v dm8', json.load(open('$O/dm8_k$v.json'))['decoder_ml32m']['ms_per_step'], 'amazon', json.load(open('$O/am_k$v.json'))['decoder_amazon']['ms_per_step'], 'rqvae', json.load(open('$O/rq_k$v.json'))['ms_per_step'])"
+      done ;;
     embab)   # batched (deferred) embedding-table gradients on / off
       run embtests 400 python -u -m pytest "$R/tests/test_direct_grad_gpu.py" "$R/tests/test_fused_decoder_gpu.py" "$R/tests/test_reference_fixtures_gpu.py" \
         "$R/tests/test_graph_gpu.py" "$R/tests/test_train_gpu.py" -m gpu -x -q --timeout 120 --timeout-method thread > "$O/embtests.log" 2>&1 \
