@@ -45,6 +45,20 @@
 #ifndef RQ_ATTN_PREFETCH
 #define RQ_ATTN_PREFETCH 0
 #endif
+#ifndef RQ_ATTN_BWD_PREFETCH
+#define RQ_ATTN_BWD_PREFETCH 0   // 1: fused backward loads the next chunk's Q / dO / lse / delta one chunk ahead (A/B: slower)
+#endif
+#ifndef RQ_ATTN_KVSPLIT_PREFETCH
+#define RQ_ATTN_KVSPLIT_PREFETCH 0   // key-split forward: the block's second chunk loaded during the first
+#endif
+#ifndef RQ_ATTN_BWD_WPE3
+#define RQ_ATTN_BWD_WPE3 0
+#endif
+#if RQ_ATTN_BWD_PREFETCH && RQ_ATTN_BWD_WPE3   // 3 waves per SIMD (what the LDS allows) despite the prefetch registers
+#define RQ_BWD_FUSED_WPE __attribute__((amdgpu_waves_per_eu(3)))
+#else
+#define RQ_BWD_FUSED_WPE
+#endif
 #ifndef RQ_ATTN_BWD_GROUP
 #define RQ_ATTN_BWD_GROUP 2
 #endif
@@ -699,13 +713,23 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
   const float* vb_ = v + k0 * sv + hh * HD;
   RowStage<HD, 64 * NW, CH> stk, stv;
   FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, kend, qi, 0, scale * kLog2e, &m, &l, o};
+  if (RQ_ATTN_KVSPLIT_PREFETCH) {             // next chunk's K / V loaded one chunk ahead (same values)
+    stk.load(kb_, sk, kbeg, kend, tid);
+    stv.load(vb_, sv, kbeg, kend, tid);
+  }
   for (int kc = kbeg; kc < kend; kc += CH) {
-    stk.load(kb_, sk, kc, kend, tid);
-    stv.load(vb_, sv, kc, kend, tid);
+    if (!RQ_ATTN_KVSPLIT_PREFETCH) {
+      stk.load(kb_, sk, kc, kend, tid);
+      stv.load(vb_, sv, kc, kend, tid);
+    }
     __syncthreads();                          // the previous chunk's LDS reads are done
     stk.store(K_s, tid);
     stv.store(V_s, tid);
     __syncthreads();
+    if (RQ_ATTN_KVSPLIT_PREFETCH && kc + CH < kend) {
+      stk.load(kb_, sk, kc + CH, kend, tid);
+      stv.load(vb_, sv, kc + CH, kend, tid);
+    }
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend - kc + 15) >> 4) : 0);
     fc.kc = kc;
     dispatch_tiles<NTL>(nt, kc + CH <= kend, fc);
@@ -852,7 +876,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const float* __restrict
 }
 
 template <int HD, int NW, int CH>
-__global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
+__global__ void __launch_bounds__(64 * NW) RQ_BWD_FUSED_WPE attn_bwd_fused_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
     const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
@@ -920,12 +944,20 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
   RowStage<HD, 64 * NW, CH> stq, sto;
   FusedChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, dS_s, lane, 0, 0, lq, kj, causal, wave * 16 + (lane & 15), LDS_, kv,
                     scale * kLog2e, dka, dva};
-  for (int qc = c_lo; qc < c_hi; qc += CH) {
+  // Q / dO / lse / delta of a chunk are loaded into registers one chunk ahead (RQ_ATTN_BWD_PREFETCH):
+  // the next chunk's global loads are in flight while this chunk's products run (a long sequence's
+  // workgroup walks up to ~9 chunks back to back at 8 sequences per GPU); same values, same order.
+  float lse_r = 0.f, dl_r = 0.f;
+  auto load_chunk = [&](int qc) {
     stq.load(qb_, sq, qc, lq, tid);
     sto.load(ob_, sdo, qc, lq, tid);
     const bool ok = tid < CH && qc + tid < lq;
-    const float lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
-    const float dl_r = ok ? dl_h[qc + tid] : 0.f;
+    lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
+    dl_r = ok ? dl_h[qc + tid] : 0.f;
+  };
+  if (RQ_ATTN_BWD_PREFETCH && c_lo < c_hi) load_chunk(c_lo);
+  for (int qc = c_lo; qc < c_hi; qc += CH) {
+    if (!RQ_ATTN_BWD_PREFETCH) load_chunk(qc);
     __syncthreads();                          // previous chunk's Q/dO/dS reads are done
     stq.store(Q_s, tid);
     sto.store(O_s, tid);
@@ -934,6 +966,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
       dl_s[tid] = dl_r;
     }
     __syncthreads();
+    if (RQ_ATTN_BWD_PREFETCH && qc + CH < c_hi) load_chunk(qc + CH);
     const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? max(0, min(NTL, (lq - qc + 15) >> 4) - t0) : 0);
     // dS columns of tiles this wave does not compute are zero (K_s rows past lk are zero too, but

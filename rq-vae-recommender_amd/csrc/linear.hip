@@ -160,6 +160,13 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
     int s = wave;
+    for (; s + 28 < S; s += 32) {   // 8 slab loads in flight; adds in s order (same bits)
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+    }
     for (; s + 12 < S; s += 16) {
       float4 v[4];
 #pragma unroll
@@ -1308,6 +1315,13 @@ __global__ void __launch_bounds__(256) x3_reduce_kernel(const float* __restrict_
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
     int s = wave;
+    for (; s + 28 < S; s += 32) {   // 8 slab loads in flight; adds in s order (same bits)
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+    }
     for (; s + 12 < S; s += 16) {
       float4 v[4];
 #pragma unroll
@@ -2096,11 +2110,29 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(RedSegTable t) {
     const int64_t j = ((int64_t)lb * 64 + lane) * 4;
     const bool ok = j < n;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok)
-      for (int s = wave; s < S; s += 4) {
+    if (ok) {
+      // 8 slab loads in flight per lane (a deferred batch has S ~ 10..42: one load at a time left the
+      // launch latency-bound at ~2.6 TB/s); the adds stay in s order, so the sum is the same bits.
+      int s = wave;
+      for (; s + 28 < S; s += 32) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+      }
+      for (; s + 12 < S; s += 16) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+      }
+      for (; s < S; s += 4) {
         const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
+    }
     red[wave * 64 + lane] = a;
     __syncthreads();
     if (wave == 0 && ok) {

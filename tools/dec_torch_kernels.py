@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Which Python call sites launch the torch (non-rqhip) GPU kernels of one eager decoder train step
 at the bench's Amazon config (same model, GradBuckets with flat views, HIP AdamW): torch.profiler
-with stacks, device time per (kernel, top user frame).   python tools/dec_torch_kernels.py"""
+with stacks, device time per (kernel, top user frame).   python tools/dec_torch_kernels.py [dm B]
+(`dm 8`: the ML-32M config at 8 sequences, the C4 per-rank shape)."""
 import collections
 import os
 import sys
@@ -19,7 +20,9 @@ def main():
     from rqvae_hip import dp, gemm_tuning
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel
-    cfg = bench.DEC
+    cfg = dict(bench.DEC)
+    if len(sys.argv) > 2 and sys.argv[1] == "dm":
+        cfg = dict(bench.DEC_DM, B=int(sys.argv[2]))
     dev = torch.device("cuda", 0)
     gemm_tuning.enable()
     torch.manual_seed(3)
