@@ -116,3 +116,31 @@ def test_train_decoder_graphed(tmp_path, device, capsys):
     assert all(np.isfinite(t["loss"]) for t in traces[True])
     # step 0 is eager in both modes (same seed, same batch, same dropout keys)
     assert traces[True][0]["loss"] == pytest.approx(traces[False][0]["loss"], rel=1e-6)
+
+
+def test_train_rqvae_amp_flag(tmp_path, device, capsys):
+    """amp=True (the reference's accelerate fp16 autocast switch, train_rqvae.py:36,62,147) is accepted with a
+    warning: every op of the step is an fp32 HIP kernel autocast leaves alone, so the per-step losses are the
+    amp=False ones."""
+    import numpy as np
+    import train_rqvae
+    from data.processed import RecDataset
+    from modules.quantize import QuantizeForwardMode
+    kw = dict(iterations=6, batch_size=64, learning_rate=0.0005, dataset=RecDataset.AMAZON, vae_input_dim=768,
+              vae_n_cat_feats=0, vae_hidden_dims=[512, 256, 128], vae_embed_dim=32, vae_codebook_size=256,
+              vae_codebook_mode=QuantizeForwardMode.ROTATION_TRICK, vae_n_layers=3, do_eval=False,
+              save_dir_root=str(tmp_path) + "/", save_model_every=10 ** 9, log_every=1, seed=3)
+    traces = {}
+    for amp in (False, True):
+        np.random.seed(0)
+        capsys.readouterr()
+        if amp:
+            with pytest.warns(UserWarning, match="amp=True"):
+                train_rqvae.train(amp=True, **kw)
+        else:
+            train_rqvae.train(**kw)
+        traces[amp] = _trace(capsys)
+    assert len(traces[True]) == len(traces[False]) > 0
+    for a, b in zip(traces[False], traces[True]):
+        for k in ("loss", "rl", "vl"):
+            assert a[k] == pytest.approx(b[k], rel=1e-6, abs=1e-9), (k, a, b)
