@@ -51,6 +51,14 @@
 #ifndef RQ_ATTN_KVSPLIT_PREFETCH
 #define RQ_ATTN_KVSPLIT_PREFETCH 0   // key-split forward: the block's second chunk loaded during the first
 #endif
+// The few-query / short kernels' per-wave partial tiles (part / part_o [NW][16][HD]) are written by lane
+// (row c = lane % 16, columns 16 (lane / 16) + 4 i): with 256-byte rows all 16 rows hit the same banks
+// (16-way conflicts on every ds_write_b128: 8-17 conflict cycles per LDS instruction in the Amazon SQ
+// pass). 4 floats of row padding put the 16 rows on disjoint 4-bank groups; same values, same order.
+#ifndef RQ_ATTN_PART_PAD
+#define RQ_ATTN_PART_PAD 1
+#endif
+constexpr int kPartPad = RQ_ATTN_PART_PAD ? 4 : 0;
 #ifndef RQ_ATTN_BWD_WPE3
 #define RQ_ATTN_BWD_WPE3 0
 #endif
@@ -1685,7 +1693,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_fewq_kernel(
     int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
     float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
   constexpr int HD = 64, TPW = 2;   // key tiles per wave (<= 128 keys over 4 waves)
-  __shared__ __attribute__((aligned(16))) float part_o[NW][16][HD];
+  __shared__ __attribute__((aligned(16))) float part_o[NW][16][HD + kPartPad];
   __shared__ float part_m[NW][16], part_l[NW][16];
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1807,7 +1815,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_fewq_kernel(
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ delta_out) {
   constexpr int HD = 64, TPW = 2;
-  __shared__ __attribute__((aligned(16))) float part[NW][16][HD];
+  __shared__ __attribute__((aligned(16))) float part[NW][16][HD + kPartPad];
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
@@ -1921,7 +1929,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fewq_fused_kernel(
     int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
     float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out) {
   constexpr int HD = 64, TPW = 2;   // key tiles per wave (<= 128 keys over 4 waves)
-  __shared__ __attribute__((aligned(16))) float part[NW][16][HD];
+  __shared__ __attribute__((aligned(16))) float part[NW][16][HD + kPartPad];
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
@@ -2088,7 +2096,7 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_bwd_short_fused_kernel(
   constexpr int HD = 64, NT = R / 16, TPW = (NT + NW - 1) / NW;
   static_assert(R % 16 == 0 && R <= 128 && TPW <= 2, "staged rows");
   __shared__ __attribute__((aligned(16))) char lds[2 * R * 256];
-  __shared__ __attribute__((aligned(16))) float part[NW][16][HD];
+  __shared__ __attribute__((aligned(16))) float part[NW][16][HD + kPartPad];
   __shared__ float lse_s[R], dl_s[R];
   char* Q_s = lds;
   char* O_s = lds + R * 256;
