@@ -353,6 +353,18 @@ int rq_l2norm_recon_bwd_split(const float* pre, const float* x, const float* nor
 int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream);
 int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out, void* stream);
 
+/* Gumbel-softmax quantize, training (replaces modules/quantize.py:107-112,121,124-129 with
+ * distributions/gumbel.py:14-18 for GUMBEL_SOFTMAX + L2): per row b, dist_k = |x|^2 + |c_k|^2 - 2 x.c_k,
+ * ids[b] = argmin_k dist (lowest index on ties), weights = softmax((noise - dist) / temperature) over the K
+ * codes (noise: (B, K) Gumbel samples drawn by the caller, as the reference's sample_gumbel), emb = weights @
+ * codebook. x (B, D), codebook (K, D), weights (B, K), emb (B, D), all contiguous fp32; D <= 256, K <= 4096.
+ * rq_gumbel_softmax_bwd: g_emb (B, D) -> dx (B, D) and ddist (B, K) = d loss / d dist; the codebook gradient
+ * weights^T g_emb + 2 colsum(ddist) (.) codebook - 2 ddist^T x is the caller's GEMMs. */
+int rq_gumbel_softmax_fwd(const float* x, int64_t B, int64_t D, const float* codebook, int64_t K, const float* noise,
+                          float temperature, float* weights, float* emb, int64_t* ids, void* stream);
+int rq_gumbel_softmax_bwd(const float* x, const float* codebook, const float* weights, const float* g_emb, int64_t B,
+                          int64_t D, int64_t K, float temperature, float* dx, float* ddist, void* stream);
+
 /* Jagged (NJT) conversion — ops/triton/jagged.py. dtype: 0 fp32, 1 bf16, 2 fp16.
  * jagged_offsets: offsets (B+1) int64 = [0, cumsum(clamp(lengths, 0, N))]   (jagged.py:30-33)
  * jagged_from_padded: values[offsets[b]+t] = x[b,t] (+1-1 rounding when add_one_sub_one, as

@@ -482,6 +482,121 @@ __global__ void __launch_bounds__(256) ce_bwd_kernel(const float* __restrict__ X
   }
 }
 
+
+// ------------------------------------------------------------------------ Gumbel-softmax quantize
+// Reference: modules/quantize.py:107-112,121,124-129 (training, GUMBEL_SOFTMAX, L2 distance) with
+// distributions/gumbel.py:8-18: dist_k = |x|^2 + |c_k|^2 - 2 x.c_k; ids = argmin_k dist (lowest index on
+// ties); w = softmax((-dist + g) / T) over the K codes (g: the Gumbel noise the caller sampled, as the
+// reference's sample_gumbel does); emb = w @ codebook. One wave per row: lanes over codes for the
+// distances / softmax (y and w staged in the wave's LDS slice), lanes over dims for the w @ codebook sum.
+// Backward (rows independent): dw_k = g_emb . c_k; dy = w (dw - sum_j w_j dw_j) / T; ddist = -dy;
+// dx = 2 x sum_k ddist_k - 2 sum_k ddist_k c_k. The codebook gradient (a K x B x D contraction:
+// w^T g_emb + 2 colsum(ddist) c - 2 ddist^T x) is left to the caller's GEMMs, so ddist is written out.
+constexpr int kGsMaxK = 4096, kGsMaxD = 256, kGsWaves = 4;
+
+__device__ __forceinline__ float gs_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(64 * kGsWaves) gumbel_softmax_fwd_kernel(
+    const float* __restrict__ x, int64_t B, int D, const float* __restrict__ cb, int K, const float* __restrict__ noise,
+    float inv_t, float* __restrict__ w_out, float* __restrict__ emb, int64_t* __restrict__ ids) {
+  __shared__ float ys[kGsWaves][kGsMaxK];
+  __shared__ float xs[kGsWaves][kGsMaxD];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kGsWaves + wave;
+  if (b >= B) return;   // uniform per wave; no workgroup barrier below
+  const float* xr = x + b * D;
+  float xx = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float v = xr[d];
+    xs[wave][d] = v;
+    xx += v * v;
+  }
+  xx = gs_wave_sum(xx);
+  __builtin_amdgcn_wave_barrier();   // xs of every lane visible to the wave
+  float best = INFINITY, ymax = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int k = lane; k < K; k += 64) {
+    const float* c = cb + (int64_t)k * D;
+    float dot = 0.f, cc = 0.f;
+    for (int d = 0; d < D; ++d) {
+      const float cv = c[d];
+      dot += xs[wave][d] * cv;
+      cc += cv * cv;
+    }
+    const float dist = xx + cc - 2.f * dot;
+    if (dist < best) { best = dist; bi = k; }   // k ascending per lane: first minimum kept
+    const float y = (noise[b * K + k] - dist) * inv_t;
+    ys[wave][k] = y;
+    ymax = fmaxf(ymax, y);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    ymax = fmaxf(ymax, __shfl_xor(ymax, o, 64));
+  }
+  float se = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float e = expf(ys[wave][k] - ymax);
+    ys[wave][k] = e;
+    se += e;
+  }
+  se = gs_wave_sum(se);
+  const float inv = 1.f / se;
+  for (int k = lane; k < K; k += 64) {
+    const float wk = ys[wave][k] * inv;
+    ys[wave][k] = wk;
+    w_out[b * K + k] = wk;
+  }
+  if (lane == 0) ids[b] = bi;
+  __builtin_amdgcn_wave_barrier();   // ys of every lane visible to the wave (LDS, same wave)
+  for (int d = lane; d < D; d += 64) {
+    float a = 0.f;
+    for (int k = 0; k < K; ++k) a += ys[wave][k] * cb[(int64_t)k * D + d];
+    emb[b * D + d] = a;
+  }
+}
+
+__global__ void __launch_bounds__(64 * kGsWaves) gumbel_softmax_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ cb, const float* __restrict__ w, const float* __restrict__ g,
+    int64_t B, int D, int K, float inv_t, float* __restrict__ dx, float* __restrict__ ddist) {
+  __shared__ float ds[kGsWaves][kGsMaxK];
+  __shared__ float gs[kGsWaves][kGsMaxD];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kGsWaves + wave;
+  if (b >= B) return;
+  for (int d = lane; d < D; d += 64) gs[wave][d] = g[b * D + d];
+  __builtin_amdgcn_wave_barrier();
+  float swd = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float* c = cb + (int64_t)k * D;
+    float dw = 0.f;
+    for (int d = 0; d < D; ++d) dw += gs[wave][d] * c[d];
+    ds[wave][k] = dw;
+    swd += w[b * K + k] * dw;
+  }
+  swd = gs_wave_sum(swd);
+  float s1 = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float dd = -w[b * K + k] * (ds[wave][k] - swd) * inv_t;
+    ds[wave][k] = dd;
+    ddist[b * K + k] = dd;
+    s1 += dd;
+  }
+  s1 = gs_wave_sum(s1);
+  __builtin_amdgcn_wave_barrier();
+  for (int d = lane; d < D; d += 64) {
+    float a = 0.f;
+    for (int k = 0; k < K; ++k) a += ds[wave][k] * cb[(int64_t)k * D + d];
+    dx[b * D + d] = 2.f * x[b * D + d] * s1 - 2.f * a;
+  }
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -712,5 +827,34 @@ int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const floa
 }
 
 int rq_seed_epoch_addr_rowwise(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }
+
+
+int rq_gumbel_softmax_fwd(const float* x, int64_t B, int64_t D, const float* codebook, int64_t K, const float* noise,
+                          float temperature, float* weights, float* emb, int64_t* ids, void* stream) {
+  RQ_CHECK_ARG(B >= 0 && D > 0 && D <= rqhip::kGsMaxD && K > 0 && K <= rqhip::kGsMaxK && temperature > 0.f,
+               "rq_gumbel_softmax_fwd: need 0 < D <= %d, 0 < K <= %d, temperature > 0", rqhip::kGsMaxD,
+               rqhip::kGsMaxK);
+  if (B == 0) return 0;
+  RQ_CHECK_ARG(x && codebook && noise && weights && emb && ids, "rq_gumbel_softmax_fwd: null pointer");
+  const dim3 g((unsigned)((B + rqhip::kGsWaves - 1) / rqhip::kGsWaves));
+  hipLaunchKernelGGL(rqhip::gumbel_softmax_fwd_kernel, g, dim3(64 * rqhip::kGsWaves), 0, (hipStream_t)stream, x, B,
+                     (int)D, codebook, (int)K, noise, 1.f / temperature, weights, emb, ids);
+  RQ_LAUNCH_CHECK("rq_gumbel_softmax_fwd");
+  return 0;
+}
+
+int rq_gumbel_softmax_bwd(const float* x, const float* codebook, const float* weights, const float* g_emb, int64_t B,
+                          int64_t D, int64_t K, float temperature, float* dx, float* ddist, void* stream) {
+  RQ_CHECK_ARG(B >= 0 && D > 0 && D <= rqhip::kGsMaxD && K > 0 && K <= rqhip::kGsMaxK && temperature > 0.f,
+               "rq_gumbel_softmax_bwd: need 0 < D <= %d, 0 < K <= %d, temperature > 0", rqhip::kGsMaxD,
+               rqhip::kGsMaxK);
+  if (B == 0) return 0;
+  RQ_CHECK_ARG(x && codebook && weights && g_emb && dx && ddist, "rq_gumbel_softmax_bwd: null pointer");
+  const dim3 g((unsigned)((B + rqhip::kGsWaves - 1) / rqhip::kGsWaves));
+  hipLaunchKernelGGL(rqhip::gumbel_softmax_bwd_kernel, g, dim3(64 * rqhip::kGsWaves), 0, (hipStream_t)stream, x,
+                     codebook, weights, g_emb, B, (int)D, (int)K, 1.f / temperature, dx, ddist);
+  RQ_LAUNCH_CHECK("rq_gumbel_softmax_bwd");
+  return 0;
+}
 
 }  // extern "C"

@@ -8,9 +8,12 @@ Public surface kept from the reference (names, argument meaning, return types, s
 Execution: the L2-distance path (every config) runs the fused HIP kernel
 ``rqvae_hip.ops.rq_quantize`` — MFMA fp32 distance + argmin + codeword gather + rotation trick /
 STE / eval output + VQ loss in one launch, and the matching VJP with a deterministic codebook
-gradient. GUMBEL_SOFTMAX (differentiable through the full distance matrix) and the COSINE
-distance have no config and run as GPU torch composites of the same math.
+gradient. GUMBEL_SOFTMAX training with the L2 distance (the reference's default codebook mode, differentiable
+through the full distance matrix) runs on rq_gumbel_softmax_fwd / _bwd (distances, ids, softmax of the noised
+logits and weights @ codebook per row; the codebook gradient as three torch ops); the COSINE distance and
+Gumbel outside the kernel's shapes (D <= 256, K <= 4096) run as GPU torch composites of the same math.
 """
+import os
 from enum import Enum
 from typing import NamedTuple
 
@@ -19,6 +22,7 @@ from torch import nn
 from torch import Tensor
 from torch.nn import functional as F
 
+import distributions.gumbel as _gumbel
 from distributions.gumbel import gumbel_softmax_sample
 from init.kmeans import kmeans_init_
 from modules.loss import QuantizeLoss
@@ -26,6 +30,11 @@ from modules.normalize import L2NormalizationLayer
 from rqvae_hip import ops as hip_ops
 
 from modules.ginlite import gin as _gin   # gin-config, or the built-in subset when gin is absent
+
+
+# RQ_GUMBEL_HIP=1: the training-mode Gumbel-softmax quantize on rq_gumbel_softmax_fwd / _bwd;
+# default (until its GPU parity run): the torch composite.
+GUMBEL_HIP = os.environ.get("RQ_GUMBEL_HIP", "0") == "1"
 
 
 class QuantizeForwardMode(Enum):
@@ -133,6 +142,12 @@ class Quantize(nn.Module):
             if mode is not None:
                 emb, _, ids, qloss, _ = hip_ops.rq_quantize(x, codebook.unsqueeze(0), mode, self.commitment_weight)
                 return QuantizeOutput(embeddings=emb[0], ids=ids[:, 0], loss=qloss)
+            if (self.training and self.forward_mode == QuantizeForwardMode.GUMBEL_SOFTMAX and GUMBEL_HIP
+                    and hip_ops.gumbel_softmax_supported(x, codebook)):
+                # the noise is drawn exactly as the reference's gumbel_softmax_sample draws it (torch.rand)
+                noise = _gumbel.sample_gumbel((x.shape[0], codebook.shape[0]), x.device)
+                emb, ids = hip_ops.gumbel_softmax_quantize(x, codebook, noise, temperature)
+                return QuantizeOutput(embeddings=emb, ids=ids, loss=self.quantize_loss(query=x, value=emb))
         elif self.distance_mode != QuantizeDistance.COSINE:
             raise Exception("Unsupported Quantize distance mode.")
         return self._composite_forward(x, codebook, temperature)

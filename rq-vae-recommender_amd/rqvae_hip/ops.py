@@ -1440,6 +1440,53 @@ def l2norm_recon_loss(pre, x):
     return L2NormReconFunction.apply(pre, x)
 
 
+class GumbelSoftmaxQuantizeFunction(torch.autograd.Function):
+    """Training-mode GUMBEL_SOFTMAX + L2 quantize (modules/quantize.py:107-129, distributions/gumbel.py:14-18):
+    (x, codebook, noise, T) -> (emb = softmax((noise - dist) / T) @ codebook, ids = argmin dist) on
+    rq_gumbel_softmax_fwd; backward: dx and d/d dist on rq_gumbel_softmax_bwd, the codebook gradient
+    w^T g + 2 colsum(ddist) (.) c - 2 ddist^T x as three torch GEMM / reduction ops."""
+
+    @staticmethod
+    def forward(ctx, x, codebook, noise, temperature):
+        require_gpu(x, codebook, noise, what="gumbel_softmax_quantize")
+        x, cb, noise = x.detach().contiguous(), codebook.detach().contiguous(), noise.detach().contiguous()
+        B, D = x.shape
+        K = cb.shape[0]
+        w = torch.empty((B, K), device=x.device, dtype=torch.float32)
+        emb = torch.empty((B, D), device=x.device, dtype=torch.float32)
+        ids = torch.empty((B,), device=x.device, dtype=torch.int64)
+        call("rq_gumbel_softmax_fwd", ptr(x), B, D, ptr(cb), K, ptr(noise), float(temperature), ptr(w), ptr(emb),
+             ptr(ids), stream_handle(x.device))
+        ctx.save_for_backward(x, cb, w)
+        ctx.temperature = float(temperature)
+        ctx.mark_non_differentiable(ids)
+        return emb, ids
+
+    @staticmethod
+    def backward(ctx, g_emb, _g_ids):
+        x, cb, w = ctx.saved_tensors
+        B, D = x.shape
+        K = cb.shape[0]
+        g = g_emb.contiguous()
+        dx = torch.empty_like(x)
+        ddist = torch.empty((B, K), device=x.device, dtype=torch.float32)
+        call("rq_gumbel_softmax_bwd", ptr(x), ptr(cb), ptr(w), ptr(g), B, D, K, ctx.temperature, ptr(dx), ptr(ddist),
+             stream_handle(x.device))
+        dcb = None
+        if ctx.needs_input_grad[1]:
+            dcb = w.t() @ g - 2.0 * (ddist.t() @ x) + 2.0 * ddist.sum(dim=0).unsqueeze(1) * cb
+        return dx, dcb, None, None
+
+
+def gumbel_softmax_supported(x: torch.Tensor, codebook: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and codebook.dtype == torch.float32 and x.dim() == 2
+            and 0 < x.shape[1] <= 256 and 0 < codebook.shape[0] <= 4096)
+
+
+def gumbel_softmax_quantize(x, codebook, noise, temperature):
+    return GumbelSoftmaxQuantizeFunction.apply(x, codebook, noise, temperature)
+
+
 def row_norms(x: torch.Tensor) -> torch.Tensor:
     """|x_r|_2 over the last axis (no grad): one HBM pass (rq_row_norms)."""
     require_gpu(x, what="row_norms")
