@@ -32,9 +32,9 @@ from rqvae_hip import ops as hip_ops
 from modules.ginlite import gin as _gin   # gin-config, or the built-in subset when gin is absent
 
 
-# RQ_GUMBEL_HIP=1: the training-mode Gumbel-softmax quantize on rq_gumbel_softmax_fwd / _bwd;
-# default (until its GPU parity run): the torch composite.
-GUMBEL_HIP = os.environ.get("RQ_GUMBEL_HIP", "0") == "1"
+# RQ_GUMBEL_HIP=0: the training-mode Gumbel-softmax quantize as the torch composite (A/B, cross-checks);
+# default: rq_gumbel_softmax_fwd / _bwd (GPU parity: tests/test_gumbel_gpu.py and the reference fixtures).
+GUMBEL_HIP = os.environ.get("RQ_GUMBEL_HIP", "1") != "0"
 
 
 class QuantizeForwardMode(Enum):
