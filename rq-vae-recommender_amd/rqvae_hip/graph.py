@@ -181,7 +181,10 @@ class GraphedSteps:
         g = torch.cuda.CUDAGraph()
         try:
             if in_graph:
-                with torch.cuda.graph(g, pool=self.pool):
+                # thread_local: the process group's watchdog thread polls the events of earlier (eager)
+                # collectives; under the default global capture mode such a poll landing inside this capture
+                # fails the capture ("operation not permitted when stream is capturing", seen on MI355X)
+                with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                     out = self._body(exchange=True)
             else:
                 with torch.cuda.graph(g, pool=self.pool), self.buckets.suspended():
