@@ -91,6 +91,10 @@ def copy_row_counts(dst: Tensor, src: Tensor) -> None:
     e = _HOST_ROWS.get(id(src))
     if e is not None and e[0]() is src:
         key = id(dst)
+        d = _HOST_ROWS.get(key)
+        if d is not None and d[0]() is dst:   # dst already tracked (a static input): update, no new finalizer
+            _HOST_ROWS[key] = (d[0], e[1])
+            return
         _HOST_ROWS[key] = (weakref.ref(dst), e[1])
         weakref.finalize(dst, _HOST_ROWS.pop, key, None)
 

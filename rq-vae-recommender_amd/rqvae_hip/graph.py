@@ -177,42 +177,66 @@ class GraphedSteps:
         if not self.capture:
             self.graphs[key] = (None, None)
             return self.graphs[key]
-        in_graph = self.in_graph
-        g = torch.cuda.CUDAGraph()
-        try:
-            if in_graph:
-                # thread_local: the process group's watchdog thread polls the events of earlier (eager)
-                # collectives; under the default global capture mode such a poll landing inside this capture
-                # fails the capture ("operation not permitted when stream is capturing", seen on MI355X)
-                with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
-                    out = self._body(exchange=True)
-            else:
-                with torch.cuda.graph(g, pool=self.pool), self.buckets.suspended():
-                    out = self._body(exchange=False)
-        except Exception as e:   # capturing the collectives failed: exchange after the replay instead
-            if not in_graph:
-                raise
-            self.capture_error = repr(e)[:300]
+        # thread_local capture mode everywhere: other threads of the process keep making HIP calls while
+        # the step is captured — the process group's watchdog polls the events of earlier (eager)
+        # collectives, a trainer's feed thread pins host memory (the caching host allocator queries and
+        # records events) — and under the default global mode any such call fails the capture ("operation
+        # not permitted when stream is capturing", seen on MI355X with the watchdog)
+        g, out, err = self._try_capture(self.in_graph)
+        if self.in_graph and self._world() > 1:
+            # one decision for all ranks: if any rank failed to capture its collectives, every rank
+            # exchanges after the replay (a mixed in-graph / post-replay world would still issue the same
+            # all-reduces, but nothing would test it)
+            ok = torch.tensor([0.0 if err is not None else 1.0], device=self._device())
+            import torch.distributed as dist
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if float(ok.item()) == 0.0:
+                err = err or "capture of the exchange failed on another rank"
+        if err is not None:
+            if not self.in_graph:
+                raise err if isinstance(err, BaseException) else RuntimeError(err)
+            self.capture_error = repr(err)[:300]
             self.in_graph = False
             torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool), self.buckets.suspended():
-                out = self._body(exchange=False)
+            g, out, err2 = self._try_capture(False)
+            if err2 is not None:
+                raise err2
         if self.pool is None:
             self.pool = g.pool()
         self.graphs[key] = (g, out)
         return self.graphs[key]
 
+    def _try_capture(self, in_graph: bool):
+        """Capture one step body: (graph, its output, None) or (None, None, the exception)."""
+        import contextlib
+        g = torch.cuda.CUDAGraph()
+        susp = contextlib.nullcontext() if in_graph else self.buckets.suspended()
+        try:
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"), susp:
+                out = self._body(exchange=in_graph)
+        except Exception as e:
+            return None, None, e
+        return g, out, None
+
+    @staticmethod
+    def _world() -> int:
+        import torch.distributed as dist
+        return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+    def _device(self):
+        b = self.buckets
+        if b is not None and b.buckets:
+            return b.buckets[0]["flat"].device
+        return torch.device("cuda", torch.cuda.current_device())
+
     def _eager(self, batch):
-        """One ordinary eager step on the static inputs (the exchange from the hooks; the caller's
+        """One ordinary eager step on the batch itself (the exchange from the hooks; the caller's
         synchronize() finishes it)."""
         self.eager_steps += 1
-        if self.prepare is not None:
-            self.prepare(self.static, batch)
         b = self.buckets
         if b is not None:
             b.zero_grad()
-        out = self.loss_fn(self.static)
+        out = self.loss_fn(batch)
         if self.run_backward:
             out.backward()
             out = out.detach()
@@ -221,17 +245,19 @@ class GraphedSteps:
     def __call__(self, batch):
         sig = self._signature(batch)
         key = (sig, self.key_fn(batch))
-        self._copy_in(batch, sig)
         entry = self.graphs.get(key)
         if not self._probed or (entry is None and len(self.graphs) >= self.max_graphs):
             # first step: eager on every rank (settles the unused parameters before anything is
-            # captured); past max_graphs: eager
+            # captured); past max_graphs: eager. Neither touches the static inputs.
             self._probed = True
             return self._eager(batch)
+        self._copy_in(batch, sig)
         if entry is None:
             entry = self._capture(key, batch)
         g, out = entry
         if g is None:   # capture=False: the body runs eagerly, with the captured form's exchange
+            if self.prepare is not None:
+                self.prepare(self.static, batch)
             out = self._body(exchange=self.in_graph)
         else:
             g.replay()

@@ -26,9 +26,8 @@ import time
 import warnings
 
 import torch
-from torch.utils.data import DataLoader
 
-from data.processed import ItemData, RecDataset, SeqData
+from data.processed import ItemData, RecDataset, SeqData, batch_loader
 from data.utils import batch_to, cycle
 from modules.ginlite import gin
 from modules.model import EncoderDecoderRetrievalModel
@@ -63,20 +62,22 @@ class _Prefetch:
         import threading
         self.q = queue.Queue(maxsize=depth)
         self.stop = False
+        pin = torch.cuda.is_available()
 
         def work():
             try:
                 while not self.stop:
                     data = next(loader)
                     n_glob = data.seq_mask.shape[0]
-                    mine = token_balanced_shard(data.seq_mask, rank, world)
-                    if len(mine) == 0:
-                        self.q.put((None, None, n_glob, None))
-                        continue
-                    data = type(data)(*[v[mine] for v in data])
+                    if world > 1:
+                        mine = token_balanced_shard(data.seq_mask, rank, world)
+                        if len(mine) == 0:
+                            self.q.put((None, None, n_glob, None))
+                            continue
+                        data = type(data)(*[v[mine] for v in data])
                     counts = (data.seq_mask.sum(1) * sem_ids_dim).tolist()
                     ids_max = int(max(int(data.ids.max()), int(data.ids_fut.max())))
-                    if torch.cuda.is_available():
+                    if pin:
                         data = type(data)(*[v.pin_memory() if hasattr(v, "pin_memory") else v for v in data])
                     self.q.put((data, counts, n_glob, ids_max))
             except BaseException as e:   # surfaced on the consumer side
@@ -91,12 +92,16 @@ class _Prefetch:
         return item
 
     def close(self):
+        """Stop the feed thread and join it (it may be blocked on a full queue: keep draining)."""
+        import queue
         self.stop = True
-        try:
-            while True:
-                self.q.get_nowait()
-        except Exception:
-            pass
+        while self.thread.is_alive():
+            try:
+                while True:
+                    self.q.get_nowait()
+            except queue.Empty:
+                pass
+            self.thread.join(timeout=0.01)
 
 
 # Last train() call: steady-state time per iteration (CUDA-synchronised once at the start and once at
@@ -117,12 +122,13 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
           train_data_subsample=True, model_jagged_mode=True, vae_hf_model_name="edobotta/rqvae-amazon-beauty",
           data_path=None, log_every=100, seed=0, cuda_graphs=True):
     if amp:
-        # The reference's amp=True wraps the forward in accelerate's fp16 autocast. Every matmul-shaped op of
-        # the decoder hot path is a HIP kernel on fp32 tensors at the 'high' split-bf16 precision (finer than fp16), which
-        # autocast does not touch, so the flag is accepted and the step runs unchanged (no GradScaler needed:
-        # gradients are fp32). mixed_precision_type is recorded for the log only.
-        warnings.warn(f"amp=True ({mixed_precision_type}): the decoder hot path computes fp32 (split-bf16 'high' MFMA GEMMs); "
-                      "autocast has no op to cast, the step is unchanged", stacklevel=2)
+        # The reference's amp=True wraps the step in accelerate's fp16 autocast. This build does not enable
+        # autocast: the flag is accepted and the step runs in fp32 — the decoder hot path's matmul-shaped ops are
+        # HIP kernels at the 'high' split-bf16 precision (finer than fp16); any remaining torch ops (e.g. the
+        # Gumbel-softmax composite) also stay fp32, where the reference would cast them to fp16. No
+        # GradScaler is needed (gradients are fp32); mixed_precision_type is recorded for the log only.
+        warnings.warn(f"amp=True ({mixed_precision_type}): accepted, but the step runs in fp32 with no autocast "
+                      "(the decoder hot path is split-bf16 'high' MFMA GEMMs + fp32 kernels)", stacklevel=2)
     if push_vae_to_hf:
         raise NotImplementedError("HF hub upload is out of scope (network)")
     LAST_RUN.clear()
@@ -136,7 +142,8 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
                        data_path=data_path, seed=seed, with_features=False)
     global_batch = batch_size if split_batches else batch_size * world
     g = torch.Generator().manual_seed(seed + 5)
-    loader = cycle(DataLoader(train_ds, batch_size=global_batch, shuffle=True, generator=g))
+    # the reference DataLoader's shuffled order, batches fetched whole (SeqData list indexing)
+    loader = cycle(batch_loader(train_ds, global_batch, g))
 
     tokenizer = SemanticIdTokenizer(input_dim=vae_input_dim, hidden_dims=vae_hidden_dims, output_dim=vae_embed_dim,
                                     codebook_size=vae_codebook_size, n_layers=vae_n_layers, n_cat_feats=vae_n_cat_feats,
@@ -179,6 +186,22 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
                            prepare=lambda static, inp: copy_row_counts(static[0].seq_mask, inp[0].seq_mask)
                            ) if use_graphs else None
     feed = _Prefetch(loader, rank, world, tokenizer.sem_ids_dim)
+    try:
+        _train_loop(feed, model, tokenizer, graphed, buckets, opt, sched, device, rank, world, start_iter, iterations,
+                    gradient_accumulate_every, log_every, save_model_every, save_dir_root)
+    finally:
+        feed.close()
+    return model
+
+
+_PHASES = ("feed_wait", "tokenize", "step", "exchange", "optimizer", "log_save")
+
+
+def _train_loop(feed, model, tokenizer, graphed, buckets, opt, sched, device, rank, world, start_iter, iterations,
+                gradient_accumulate_every, log_every, save_model_every, save_dir_root):
+    """The reference's loop (train_decoder.py:180-204) over the prefetched batches. Host time per phase
+    is accumulated over the steady span (LAST_RUN["host_ms_per_iter"]): the loop must stay ahead of the
+    GPU, so these are the numbers to read when the trainer is slower than its bench step."""
     w_dev = {}
     t0, hist = time.time(), []
     t_from = start_iter + min(5, (iterations - start_iter) // 2)   # measured span: [t_from, iterations)
@@ -186,23 +209,29 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     # steady state: the iterations after the last graph capture (a new row bucket's capture costs two
     # eager warm-up passes + the capture; a long run amortises the few buckets a dataset has)
     s_mark, s_from, s_toks = None, None, 0
+    phase = dict.fromkeys(_PHASES, 0.0)
+    clock = time.perf_counter
     for it in range(start_iter, iterations):
         if it == t_from:
             torch.cuda.synchronize()
-            t_mark = time.perf_counter()
+            t_mark = clock()
         if t_mark is not None and s_mark is None:
             torch.cuda.synchronize()
-            s_mark, s_from, s_toks = time.perf_counter(), it, 0
+            s_mark, s_from, s_toks = clock(), it, 0
+            phase = dict.fromkeys(_PHASES, 0.0)
         n_graphs = len(graphed.graphs) if graphed is not None else 0
         model.train()
         if graphed is None:
             buckets.zero_grad()
-        total = torch.zeros((), device=device)
+        total = None
         for micro in range(gradient_accumulate_every):
             # the loader's next global batch, this rank's token-balanced shard (n_glob: the loader's last
             # batch of an epoch may be short) and its host-side context row counts — no device sync for
             # the jagged total, and a captured step is keyed by its row bucket — prepared on the feed thread
+            c0 = clock()
             data, counts, n_glob, ids_max = feed.next()
+            c1 = clock()
+            phase["feed_wait"] += c1 - c0
             if data is None:   # fewer sequences than ranks: zero gradient, exchange in synchronize()
                 if graphed is not None:
                     buckets.zero_grad()
@@ -214,38 +243,50 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
             register_row_counts(tok.seq_mask, counts)
             # this rank's shard mean -> share of the GLOBAL-batch mean (unequal, token-balanced shards)
             w = dp.shard_weight(len(counts), n_glob) / gradient_accumulate_every
+            c2 = clock()
+            phase["tokenize"] += c2 - c1
             if graphed is not None:
                 wt = w_dev.get(w)
                 if wt is None:   # a few distinct weights over a run: one device scalar each, no per-step copy
                     wt = w_dev[w] = torch.tensor(w, device=device)
-                total = total + graphed((tok, wt))
-                continue
-            out = model(tok)
-            last = micro == gradient_accumulate_every - 1
-            with (contextlib.nullcontext() if last else buckets.no_sync()):
-                (out.loss * w).backward()
-            total = total + out.loss.detach() / gradient_accumulate_every
+                loss = graphed((tok, wt)).clone()   # the graph's output buffer is overwritten by the next replay
+            else:
+                out = model(tok)
+                last = micro == gradient_accumulate_every - 1
+                with (contextlib.nullcontext() if last else buckets.no_sync()):
+                    (out.loss * w).backward()
+                loss = out.loss.detach() / gradient_accumulate_every
+            total = loss if total is None else total + loss
+            phase["step"] += clock() - c2
+        c3 = clock()
         buckets.synchronize()
+        c4 = clock()
         opt.step()
         sched.step()
-        hist.append(total)
+        c5 = clock()
+        phase["exchange"] += c4 - c3
+        phase["optimizer"] += c5 - c4
+        hist.append(total if total is not None else torch.zeros((), device=device))
         if graphed is not None and len(graphed.graphs) != n_graphs:
             s_mark = None   # this iteration captured: the steady span restarts after it
         if it == iterations - 1 and t_mark is not None:
             torch.cuda.synchronize()
-            t_end = time.perf_counter()
+            t_end = clock()
             dt = t_end - t_mark
             steady = {}
             if s_mark is not None and iterations - s_from >= 3:
                 ds = t_end - s_mark
-                steady = dict(steady_iter_ms=ds * 1e3 / (iterations - s_from), steady_iters=iterations - s_from,
-                              steady_ctx_tokens_per_s_rank=s_toks / ds)
+                n_s = iterations - s_from
+                steady = dict(steady_iter_ms=ds * 1e3 / n_s, steady_iters=n_s,
+                              steady_ctx_tokens_per_s_rank=s_toks / ds,
+                              host_ms_per_iter={k: round(v * 1e3 / n_s, 4) for k, v in phase.items()})
             LAST_RUN.update(iter_ms=dt * 1e3 / max(1, iterations - t_from), timed_iters=iterations - t_from,
                             ctx_tokens_per_s_rank=toks / dt, world=world, **steady,
                             step_mode="hipgraph" if graphed is not None else "eager",
                             graphs=len(graphed.graphs) if graphed is not None else 0,
                             eager_steps=graphed.eager_steps if graphed is not None else iterations - start_iter,
                             exchange="in-graph" if graphed is not None and graphed.in_graph else "hooks + synchronize")
+        c6 = clock()
         if rank == 0 and (it % log_every == 0 or it + 1 == iterations):
             print(json.dumps({"iter": it, "loss": float(torch.stack(hist).mean()), "lr": opt.param_groups[0]["lr"],
                               "elapsed_s": round(time.time() - t0, 2)}), flush=True)
@@ -254,8 +295,8 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
             os.makedirs(save_dir_root, exist_ok=True)
             torch.save({"iter": it, "model": model.state_dict(), "optimizer": opt.state_dict(),
                         "scheduler": sched.state_dict()}, os.path.join(save_dir_root, f"checkpoint_{it}.pt"))
-    feed.close()
-    return model
+        phase["log_save"] += clock() - c6
+
 
 
 if __name__ == "__main__":

@@ -64,12 +64,13 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
           vae_sim_vq=False, vae_n_layers=3, dataset_split="beauty", data_path=None, log_every=100, seed=0,
           cuda_graphs=True):
     if amp:
-        # The reference's amp=True wraps the forward in accelerate's fp16 autocast. Every matmul-shaped op of
-        # the RQ-VAE hot path is a HIP kernel on fp32 tensors at the 'high' split-bf16 precision (finer than fp16), which
-        # autocast does not touch, so the flag is accepted and the step runs unchanged (no GradScaler needed:
-        # gradients are fp32). mixed_precision_type is recorded for the log only.
-        warnings.warn(f"amp=True ({mixed_precision_type}): the RQ-VAE hot path computes fp32 (split-bf16 'high' MFMA GEMMs); "
-                      "autocast has no op to cast, the step is unchanged", stacklevel=2)
+        # The reference's amp=True wraps the step in accelerate's fp16 autocast. This build does not enable
+        # autocast: the flag is accepted and the step runs in fp32 — the RQ-VAE hot path's matmul-shaped ops are
+        # HIP kernels at the 'high' split-bf16 precision (finer than fp16); any remaining torch ops (e.g. the
+        # Gumbel-softmax composite) also stay fp32, where the reference would cast them to fp16. No
+        # GradScaler is needed (gradients are fp32); mixed_precision_type is recorded for the log only.
+        warnings.warn(f"amp=True ({mixed_precision_type}): accepted, but the step runs in fp32 with no autocast "
+                      "(the RQ-VAE hot path is split-bf16 'high' MFMA GEMMs + fp32 kernels)", stacklevel=2)
     LAST_RUN.clear()
     rank, world, local_rank = dp.init_from_env()
     device = torch.device("cuda", local_rank)

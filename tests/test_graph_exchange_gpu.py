@@ -27,9 +27,13 @@ def _port():
     return p
 
 
-def test_in_graph_exchange_matches_eager():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "graph_exchange_probe.py"), str(_port())],
-                       capture_output=True, text=True, timeout=100)
+@pytest.mark.parametrize("race", [False, True])
+def test_in_graph_exchange_matches_eager(race):
+    """race: the capture runs while a second thread polls an eager all-reduce's Work and pins host memory
+    (the watchdog / feed-thread calls that aborted a global-mode capture in round 3): it must capture the
+    exchange and replay it exactly."""
+    args = [sys.executable, os.path.join(ROOT, "tools", "graph_exchange_probe.py"), str(_port())] + (["race"] if race else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
@@ -37,5 +41,7 @@ def test_in_graph_exchange_matches_eager():
     assert res["in_graph_default"], "RCCL group: the exchange should be captured in the graph"
     assert res["capture_error"] is None and res["in_graph"], res["capture_error"]
     assert res["steps"][-1]["graphs"] == 1
+    if race:
+        assert res["race_polls"] > 0
     for s in res["steps"]:
         assert s["max_abs_grad_diff"] == 0.0, res

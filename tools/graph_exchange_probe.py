@@ -5,7 +5,12 @@ One process, a world-1 RCCL group, dp.GradBuckets(force_exchange=True) with seve
 decoder model's forward + backward replayed from GraphedSteps with the buckets' all-reduces captured
 inside the graph (in_graph_exchange). Prints one JSON line: whether the collectives were captured,
 and the max |grad| difference of each replayed step against an eager step of an identical model
-copy (a one-rank all-reduce is the identity, so the gradients must match bit for bit)."""
+copy (a one-rank all-reduce is the identity, so the gradients must match bit for bit).
+
+`race` (argv[2]): the capture runs while another thread keeps making HIP calls — it polls
+is_completed() of an eager all-reduce Work kept alive across the capture (what the process group's
+watchdog does) and pins host memory (what a trainer's feed thread does). Under the global capture mode
+such calls fail the capture (the round-3 watchdog abort); every capture here is thread-local."""
 import copy
 import json
 import os
@@ -20,6 +25,10 @@ import torch.distributed as dist  # noqa: E402
 
 def main():
     port = sys.argv[1] if len(sys.argv) > 1 else "29533"
+    mode = sys.argv[2] if len(sys.argv) > 2 else ""
+    race = mode.startswith("race")
+    do_poll = race and mode in ("race", "race_poll", "race_poll_waited")
+    do_pin = race and mode in ("race", "race_pin")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -39,8 +48,33 @@ def main():
                       prepare=lambda static, b: copy_row_counts(static.seq_mask, b.seq_mask))
     res = {"buckets": len(buckets.buckets), "in_graph_default": gs.in_graph, "steps": []}
     batch = synthetic_tokenized_batch(8, 20, 4, 64, 11, dev)
+    import threading
+    stop = threading.Event()
+    polls = [0]
+    poller = None
     for step in range(4):
+        if race and step == 1:   # step 1 captures: an eager collective in flight + a thread polling it
+            side = torch.ones(1 << 20, device=dev)
+            work = dist.all_reduce(side, async_op=True) if do_poll else None
+            if mode == "race_poll_waited":
+                work.wait()
+                torch.cuda.synchronize()
+
+            def poll():
+                while not stop.is_set():
+                    if work is not None:
+                        work.is_completed()
+                    if do_pin:
+                        torch.empty(4096).pin_memory()
+                    polls[0] += 1
+            poller = threading.Thread(target=poll, daemon=True)
+            poller.start()
         gs(batch)
+        if poller is not None and step == 1:
+            stop.set()
+            poller.join()
+            if work is not None:
+                work.wait()
         buckets.synchronize()
         for p in ref.parameters():
             p.grad = None
@@ -59,6 +93,7 @@ def main():
     torch.cuda.synchronize()
     res["in_graph"] = gs.in_graph
     res["capture_error"] = gs.capture_error
+    res["race_polls"] = polls[0]
     print(json.dumps(res), flush=True)
     dist.destroy_process_group()
 
