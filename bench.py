@@ -79,14 +79,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--decoder-only", action="store_true", help="profile helper: run only the decoder extra")
     ap.add_argument("--no-graph", action="store_true", help="decoder steps eager instead of hipGraph replays")
-    ap.add_argument("--wgrad-stream", action="store_true",
-                    help="decoder weight grads on a side stream (A/B: measured 7.59 vs 7.24 ms main-stream, off)")
     ap.add_argument("--no-dm", action="store_true", help="skip the ML-32M decoder lines")
     ap.add_argument("--dm-batch", type=int, default=0, help="with --decoder-only: the ML-32M config at this batch")
     return ap.parse_args()
-
-
-WGRAD_STREAM = [False]
 
 
 def make_items(n, dim, gen, device):
@@ -232,7 +227,6 @@ def cpu_baseline(budget_s, B=2048):
 
 def main():
     args = parse()
-    WGRAD_STREAM[0] = args.wgrad_stream
     from rqvae_hip import dp, ops
     from data.schemas import SeqBatch
     rk, ws, lr = dp.init_from_env()
@@ -360,7 +354,7 @@ def main():
               "hbm_GBps_at_algorithmic_bytes": round(alg_bytes / (q_ms * 1e-3) / 1e9, 1)}
     roof = q_roof
     if gemm is not None:   # the split-bf16 GEMM is the dominant kernel at 'high' precision
-        roof = {"kernel": "gemm_bf16x3 (rq_gemm_bf16x3_ex: the step's largest-time plain-epilogue launch, M x N x K)",
+        roof = {"kernel": "gemm_bf16x3 (rq_gemm_bf16x3_run: the step's largest-time plain-epilogue launch, M x N x K)",
                 "bound": "mfma",
                 "achieved": gemm["achieved_tflops"], "peak": round(BF16_MFMA_PEAK_TFLOPS / 3, 1), "unit": "TFLOP/s",
                 "frac": round(gemm["achieved_tflops"] / (BF16_MFMA_PEAK_TFLOPS / 3), 4),
@@ -698,9 +692,6 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
     # inside each replayed graph with RCCL (GraphedSteps in-graph exchange), eager otherwise
     buckets = dp.GradBuckets(m.parameters(), overlap=True, flat_views=graphs)
     buckets.broadcast_params()
-    # optional: weight grads accumulate into the flat buckets on a side stream (overlapping the
-    # data-grad chain) — measured slower on MI355X (7.59 vs 7.24 ms per Amazon step), so off by default
-    ops.wgrad_stream_enable(graphs and WGRAD_STREAM[0])
     opt = make_adamw(m.parameters(), cfg["lr"], cfg["wd"])
     batches = [synthetic_tokenized_batch(B, cfg["max_items"], cfg["sem_id_dim"], cfg["K"], 50 + 97 * rk + i, device)
                for i in range(4)]

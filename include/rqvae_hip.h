@@ -45,29 +45,20 @@ int rq_codebook_sqnorm(const float* rows, int64_t n, int64_t D, float* out, void
  *   x (B,D) fp32 encoder output; codebooks (L,K,D); cb_sqnorm (L,K) from rq_codebook_sqnorm.
  *   mode RQ_MODE_ROTATION / RQ_MODE_STE (training) or RQ_MODE_EVAL; beta = commitment weight.
  * Outputs: ids (B,L) int64; emb_out (L,B,D); residuals (L,B,D) with residuals[0] = x;
- *   qloss (B,) = sum_l loss_l; emb_sum (B,D) = sum_l emb_out_l, or NULL.
+ *   qloss (B,) = sum_l loss_l; emb_sum (B,D) = sum_l emb_out_l, or NULL; emb_norms (L,B) =
+ *   |emb_out[l][b]|_2, the embs_norm diagnostic of RqVae.forward (modules/rqvae.py:151), or NULL (the
+ *   16x16 kernel writes them from its level epilogue; every other kernel adds one row-norm pass).
  * Requires D a power of two in [8, 1024], 1 <= K <= 2^20, 1 <= L <= 64. Ids are the lowest
- * index among equal minimum distances (torch.min semantics, quantize.py:121). */
+ * index among equal minimum distances (torch.min semantics, quantize.py:121).
+ * impl: the kernel (0 = auto: 4 for D == 64, K <= 288, B >= 32768; else 2 for D <= 64; else 3 when
+ * allowed; else 1), 1 = fused LDS-tiled kernel (any D), 2 = register-resident 32x32x2 kernel (D <= 64),
+ * 3 = split path for D >= 128 with 2*ceil(K/128)+1 <= D (per level: distance GEMM + partial argmin over
+ * 128x128 tiles, then a row epilogue; emb_out doubles as the level's scratch before it is written),
+ * 4 = register-resident 16x16x4 kernel (D == 64, K <= 288; 4 waves per SIMD). Every kernel gives the
+ * same ids and the same outputs within fp32 summation order (kernel-vs-kernel tests). */
 int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
-                    float* emb_sum, void* stream);
-
-/* Same as rq_quantize_fwd with an explicit kernel choice (benchmarking / A-B testing):
- * impl 0 = auto (4 for D == 64, K <= 288, B >= 32768; else 2 for D <= 64; else 3 when allowed;
- * else 1), 1 = fused LDS-tiled kernel (any D), 2 = register-resident 32x32x2 kernel (D <= 64),
- * 3 = split path for D >= 128 with 2*ceil(K/128)+1 <= D (per level: distance GEMM + partial argmin
- * over 128x128 tiles, then a row epilogue; emb_out doubles as the level's scratch before it is
- * written), 4 = register-resident 16x16x4 kernel (D == 64, K <= 288; 4 waves per SIMD). */
-int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
-                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
-                         float* qloss, float* emb_sum, int impl, void* stream);
-
-/* rq_quantize_fwd plus emb_norms (L,B) = |emb_out[l][b]|_2, the embs_norm diagnostic of
- * RqVae.forward (modules/rqvae.py:151). The 16x16 kernel (impl 4 under auto) writes the norms from
- * its level epilogue; every other kernel is followed by one rq_row_norms pass over emb_out. */
-int rq_quantize_fwd2(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
-                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
-                     float* emb_sum, float* emb_norms, void* stream);
+                    float* emb_sum, float* emb_norms, int impl, void* stream);
 
 /* Backward of rq_quantize_fwd (the autograd graph of modules/quantize.py:99-156 chained by
  * modules/rqvae.py:129): grads of emb_out (g_emb, (L,B,D) or NULL), of sum_l emb_out
@@ -107,24 +98,16 @@ int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const floa
  * (seed, e) instead of storing it. p = 0 is plain RMSNorm. */
 int rq_rmsnorm_dropout_fwd(const float* x, const float* w, int64_t B, int64_t D, float eps, float p, uint64_t seed,
                            float* y, float* rstd, void* stream);
-int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
-                           float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
-                           void* stream);
-/* rq_rmsnorm_dropout_bwd with two fusions: gres (NULL or B x D) is added to gx — the gradient that
- * reaches x along the residual stream (modules/transformer/model.py:75-82: x feeds both the norm and
- * the residual add; autograd would sum the two in a separate pass) — and accumulate_gw = 1 adds the
- * weight gradient into gw instead of overwriting it (a flat data-parallel gradient bucket). */
-int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
-                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
-                            void* workspace, size_t ws_bytes, void* stream);
-/* rq_rmsnorm_dropout_bwd2 with a deferred weight-gradient reduction: defer = 1 leaves gw's per-workgroup
- * partials (*parts rows of D floats) at the start of the workspace and skips their reduction (*parts = 0
- * when nothing was deferred); rq_reduce_partials (layout 1) later adds them into gw, batched with other
- * deferred reductions into one launch. */
-int rq_rmsnorm_dropout_bwd3(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
-                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
-                            int defer, int* parts, void* workspace, size_t ws_bytes, void* stream);
-
+/* Its backward, with two fusions and a deferral: gres (NULL or B x D) is added to gx — the gradient that
+ * reaches x along the residual stream (modules/transformer/model.py:75-82: x feeds both the norm and the
+ * residual add; autograd would sum the two in a separate pass) — and accumulate_gw = 1 adds the weight
+ * gradient into gw instead of overwriting it (a flat data-parallel gradient bucket). defer = 1 leaves gw's
+ * per-workgroup partials (*parts rows of D floats) at the start of the workspace and skips their reduction
+ * (*parts = 0 when nothing was deferred); rq_reduce_partials (layout 1) later adds them into gw, batched
+ * with other deferred reductions into one launch. workspace >= rq_rmsnorm_bwd_workspace(B, D) bytes. */
+int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+                           int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
+                           int defer, int* parts, void* workspace, size_t ws_bytes, void* stream);
 /* Elementwise dropout fusions over n fp32 elements (n % 4 == 0, 16-byte aligned), same mask
  * generator as above (element index = position in the buffer):
  *   rq_silu_dropout_fwd  h = Dropout(SiLU(z))         the MLP hidden layer (modules/encoder.py:20-28)
@@ -139,7 +122,7 @@ int rq_dropout_add_fwd(const float* h, const float* y, int64_t n, float p, uint6
 int rq_dropout_bwd(const float* g, int64_t n, float p, uint64_t seed, float* gy, void* stream);
 
 /* Dropout epoch: a device-side word mixed into every mask key of the functions above and of
- * rq_gemm_bf16x3_ex (key = seed + epoch * C). 0 by default (keys = the host seeds). A train step
+ * rq_gemm_bf16x3_run (key = seed + epoch * C). 0 by default (keys = the host seeds). A train step
  * captured into a hipGraph ends with rq_seed_epoch_advance, so every replay draws fresh masks while
  * the forward and backward of one step share the epoch (replaces the per-step host RNG state that
  * torch.compile's cudagraphs trees manage for the reference's nn.Dropout, modules/model.py:247).
@@ -160,102 +143,44 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
  * (modules/rqvae.py:19, modules/model.py:27): each operand split as a = hi + lo in bf16, products
  * hi.hi + hi.lo + lo.hi accumulated in fp32 on bf16 MFMA (per-product relative error <= ~2^-17;
  * TF32's is 2^-11). Replaces the nn.Linear matmuls of modules/encoder.py:7-36 and
- * modules/transformer/* (forward x W^T, data grad g W, weight grad g^T x).
+ * modules/transformer (forward x W^T, data grad g W, weight grad g^T x).
  *   C[m*ldc + n] = sum_k A(m,k) B(n,k),  A(m,k) = a_kcontig ? A[m*lda + k] : A[k*lda + m],
  *                                         B(n,k) = b_kcontig ? B[n*ldb + k] : B[k*ldb + n].
  * The contiguous axis of each operand (K for a k-contiguous one, else M or N) and lda, ldb % 4 == 0,
- * 16-byte aligned pointers. When the output tiles cannot fill
- * the GPU, K is split across workgroups with a fixed-order reduction (deterministic); that case
- * needs ldc == N and workspace >= rq_gemm_bf16x3_workspace(M, N, K) bytes (0 = no split). */
+ * 16-byte aligned pointers. When the output tiles cannot fill the GPU, K is split across workgroups
+ * with a fixed-order reduction (deterministic); that case needs ldc == N and workspace >=
+ * rq_gemm_bf16x3_workspace(M, N, K) bytes (0 = the shape never splits). */
 size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K);
 int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
                    int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream);
 
-/* General form of rq_gemm_bf16x3 for the fused MLP chain (modules/encoder.py:7-36 — Linear, SiLU,
- * [Dropout], ..., Linear): an operand is fp32 (X_lo == NULL) or pre-split, two bf16 planes
- * (X = hi, X_lo = lo) of the operand's shape; split operands need their contiguous axis and ld
- * % 8 == 0. The epilogue turns the tile into:
- *   0  C = A B^T
- *   3  C = A B^T + Z                                             (a residual add after a projection);
+/* Kernel policy of one call (rq_gemm_desc.flags; 0 = the time model picks per shape). For kernel-vs-kernel
+ * tests and A/B measurements; every policy gives the same bits for the same split operands. */
+#define RQ_GEMM_ONLY_128 1    /* the 128 x 128-tile kernel only (no wide kernel, no 64-tile form) */
+#define RQ_GEMM_ONLY_64 2     /* the 64 x 64-tile form wherever the 128-tile kernel would run */
+#define RQ_GEMM_FORCE_WIDE 4  /* the wide 256 x 256-tile kernel wherever it can run */
+#define RQ_GEMM_NO_WIDE 8     /* never the wide kernel (128- / 64-tile chosen by the model) */
+#define RQ_GEMM_MASKED 16     /* masked k staging even for whole 32-deep stages (bitwise the unmasked path) */
+#define RQ_GEMM_NO_PAIR 32    /* rq_gemm_bf16x3_pair: two launches */
+
+/* One general split-bf16 GEMM call (the fused MLP chain, modules/encoder.py:7-36 — Linear, SiLU,
+ * [Dropout], ..., Linear — and every decoder Linear). An operand is fp32 (X_lo == NULL) or pre-split:
+ * two bf16 planes (X = hi, X_lo = lo) of the operand's shape; split operands need their contiguous axis
+ * and ld % 8 == 0. The epilogue turns the tile into:
+ *   0  C = A B^T                                                  (accumulate = 1: C += A B^T)
+ *   3  C = A B^T + Z                                              (a residual add after a projection);
  *      with p > 0: C = Z + Dropout_p(A B^T), the mask of rq_dropout_add_fwd (element m N + n), so
  *      rq_dropout_bwd regenerates it — the transformer block's h + Dropout(MLP(..)) in the MLP's last GEMM
  *   1  C = z = A B^T, and H = split(Dropout_p(SiLU(z)))          (a hidden layer's forward)
  *   2  H = split(SiLU'(Z) * Dropout_p(A B^T)), C unused          (its pre-activation grad)
- * H_hi / H_lo: bf16 planes (M, N) of row stride ldh; Z: (M, N) of stride ldc. The dropout mask is
- * element e = m N + n of the same counter-based mask as rq_silu_dropout_fwd (seed). */
-int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                      void* workspace, size_t ws_bytes, void* stream);
-/* rq_gemm_bf16x3_ex with split-K for every epilogue and accumulation. When the output tiles cannot
- * fill the GPU (e.g. the decoder's 1,280 future-token rows), K is split for any epilogue: the partials
- * go to the workspace and a fixed-order reduction applies the epilogue (deterministic). accumulate = 1
- * (plain epilogue only): C += A B^T — a weight gradient added straight into an existing .grad buffer
- * (replaces autograd's AccumulateGrad add into data-parallel flat gradient buckets; an unsplit call
- * adds in the GEMM's own epilogue, a split one in the reduction, both as C + (A B^T) in fp32). Split-K
- * calls need ldc == N and workspace >= rq_gemm_bf16x3_workspace2(M, N, K, accumulate) bytes (0 when
- * the shape never splits). */
-size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate);
-int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                       int accumulate, void* workspace, size_t ws_bytes, void* stream);
-/* rq_gemm_bf16x3_ex2 with a deferred split-K reduction: with accumulate = 1, the plain epilogue and defer =
- * 1, a split call leaves its *splits partial slabs (M x N fp32 each) at the start of the workspace and
- * returns without reducing (*splits = 0: the call completed C itself); the caller adds them into C later
- * with rq_reduce_partials (layout 0). Lets the many small weight-gradient reductions of one backward
- * share a few launches. */
-int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                       int accumulate, int defer, int* splits, void* workspace, size_t ws_bytes, void* stream);
-/* Deferred partial reductions, up to 48 per launch: for each entry i, out_i[j] = (accumulate_i ? out_i[j] :
- * 0) + sum_{s < S_i} P_i[s n_i + j], j < n_i (n_i % 4 == 0, 16-B aligned pointers), in the order of the
- * reduction it replaces (layout 0: rq_gemm_bf16x3_ex3's slab reduction; layout 1: rq_rmsnorm_dropout_bwd3's
- * weight-gradient partials) — bitwise the immediate result. Entries must not share an output. Host arrays. */
-int rq_reduce_partials(int count, const float* const* P, float* const* out, const int64_t* n, const int* S,
-                       const int* layout, const int* accumulate, void* stream);
-
-/* Which kernel rq_gemm_bf16x3_ex runs for a call: 1 = the wide 256 x 256-tile kernel (both operands
- * split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile kernel, 2 = its 64 x 64-tile form (launches
- * whose 128-tiles cannot fill the chip); *splits (optional) = its split-K factor. -1 for an empty
- * shape. Host-only. */
-int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_split, int a_kcontig, int b_kcontig,
-                          int epilogue, int* splits);
-/* Enable (1) / disable (0) the wide kernel for this process (default: on unless RQ_X3W=0 is set; when on,
- * a cost model of resident-workgroup rounds picks it per shape); 2 = force it wherever it can run.
- * Returns the previous setting. For A/B measurements and kernel-vs-kernel tests. */
-int rq_gemm_x3w_enable(int enable);
-/* 64 x 64-tile form of the 128-tile kernel: 0 never, 1 (default unless RQ_X3S=0/2 is set) where the
- * time model prefers it, 2 forced wherever the 128-tile kernel would run. Returns the previous mode. */
-int rq_gemm_x3s_enable(int mode);
-/* LDS-DMA form of the 128-tile kernel for fp32 k-contiguous A x split B (bitwise the register-staged
- * kernel): 0 (default unless RQ_X3D=1/2 is set: slower inside the decoder step) off, 1 for an
- * n-contiguous B (data gradients), 2 also for a k-contiguous B. Returns the previous setting. A/B switch. */
-int rq_gemm_x3d_enable(int enable);
-/* 1 (default): 128-/64-tile launches whose K and split-K chunk are whole 32-deep stages stage operands
- * without k masks (bitwise the masked path); 0: always masked (A/B). Returns the previous setting. */
-int rq_gemm_kfull_enable(int enable);
-/* LDS-DMA staged short attention forms (key ranges <= 128 rows, head dim 64): 1 (default unless
- * RQ_ATTN_DMA=0 is set) on, 0 off (the register-staged kernels). Returns the previous setting. A/B switch. */
-int rq_attn_dma_enable(int enable);
-/* One-pass backward of the few-query attention launches (<= 16 queries per sequence over <= 128 keys, head
- * dim 64: the decoder's cross-attention and short causal self-attention): 1 (default unless
- * RQ_ATTN_FEWQ_FUSED=0 is set) on, 0 off (the two-pass dQ + dK/dV kernels). Returns the previous setting. */
-int rq_attn_fewq_fused_enable(int enable);
-/* The same for self-attention style launches over short ranges (17..128 queries, <= 128 keys, head dim
- * 64: the encoder's Amazon contexts): 1 (default unless RQ_ATTN_SHORT_FUSED=0 is set) one pass, 0 the
- * two-pass LDS-DMA dQ + dK/dV kernels. Returns the previous setting. */
-int rq_attn_short_fused_enable(int enable);
-/* rq_segment_sum over up to 16 sources at once (every embedding table of a decoder step: modules/model.py:59-63,
- * modules/embedding/id_embedder.py): source t's rows (n[t], D) with keys in [0, K[t]) (others and pad[t]
- * skipped) sum into rows [sum_{u<t} K[u], + K[t]) of out (sum K, D). One pack launch + one segmented-sum
- * chain instead of one chain per table; sum K <= 4096. */
-size_t rq_segment_sum_multi_workspace(int count, const int64_t* n, const int64_t* K, int64_t D);
-int rq_segment_sum_multi(int count, const float* const* rows, const int64_t* const* keys, const int64_t* n,
-                         const int64_t* K, const int64_t* pad, int64_t D, float* out, void* workspace, size_t ws_bytes,
-                         void* stream);
-/* One rq_gemm_bf16x3_ex3 call as a descriptor (the same fields, the same meaning). */
+ * H_hi / H_lo: bf16 planes (M, N) of row stride ldh; Z: (M, N) of stride ldc. The dropout mask is element
+ * e = m N + n of the same counter-based mask as rq_silu_dropout_fwd (seed). Split-K applies to every
+ * epilogue (partials in the workspace, a fixed-order reduction applies the epilogue). accumulate = 1
+ * (plain epilogue only): C += A B^T — a weight gradient added straight into a flat data-parallel
+ * gradient bucket (replaces autograd's AccumulateGrad add). defer = 1 (with accumulate): a split call
+ * leaves its *splits partial slabs (M x N fp32 each) at the start of the workspace and does not reduce
+ * them (*splits = 0: the call completed C itself); the caller adds them into C later with
+ * rq_reduce_partials (layout 0), batched with other deferred reductions. */
 typedef struct rq_gemm_desc {
   const void* A;
   const void* A_lo;
@@ -279,18 +204,38 @@ typedef struct rq_gemm_desc {
   int defer;
   void* workspace;
   size_t ws_bytes;
+  int flags;     /* RQ_GEMM_* kernel policy, 0 = automatic */
+  int reserved;  /* 0 */
 } rq_gemm_desc;
-/* Two independent rq_gemm_bf16x3_ex3 calls d[0], d[1] (splits[i] as ex3's `splits`), results identical to the
+int rq_gemm_bf16x3_run(const rq_gemm_desc* d, int* splits, void* stream);
+/* Two independent calls d[0], d[1] (splits[i] as rq_gemm_bf16x3_run's `splits`), results identical to the
  * two calls in a row; where both run on the 128- or 64-tile kernel with the same tile size and a paired
  * instantiation exists — a Linear's backward: d[0] the data gradient g W (SiLU'-with-dropout epilogue
- * allowed), d[1] the weight gradient g^T x (modules/encoder.py:7-36, modules/transformer/*: autograd's
+ * allowed), d[1] the weight gradient g^T x (modules/encoder.py:7-36, modules/transformer: autograd's
  * grad_input / grad_weight of nn.Linear) — both problems' workgroups run in ONE launch (one launch instead
- * of two; together they fill the chip where each alone cannot). RQ_X3_PAIR=0 / rq_gemm_pair_enable(0): two
- * launches. */
+ * of two; together they fill the chip where each alone cannot). RQ_GEMM_NO_PAIR in either: two launches. */
 int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream);
+/* Host-only planning of a descriptor (pointers may be NULL): the kernel rq_gemm_bf16x3_run would launch —
+ * 1 = the wide 256 x 256-tile kernel (both operands split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile
+ * kernel, 2 = its 64 x 64-tile form, -1 = empty shape / invalid — and *splits its split-K factor. */
+int rq_gemm_bf16x3_plan(const rq_gemm_desc* d, int* splits);
 /* 1 when rq_gemm_bf16x3_pair would run d[0], d[1] in one launch (host-only planning), else 0. */
-int rq_gemm_bf16x3_pair_choice(const rq_gemm_desc* d);
-int rq_gemm_pair_enable(int enable);
+int rq_gemm_bf16x3_pair_plan(const rq_gemm_desc* d);
+/* Deferred partial reductions, up to 48 per launch: for each entry i, out_i[j] = (accumulate_i ? out_i[j] :
+ * 0) + sum_{s < S_i} P_i[s n_i + j], j < n_i (n_i % 4 == 0, 16-B aligned pointers), in the order of the
+ * reduction it replaces (layout 0: rq_gemm_bf16x3_run's slab reduction; layout 1: rq_rmsnorm_dropout_bwd's
+ * weight-gradient partials) — bitwise the immediate result. Entries must not share an output. Host arrays. */
+int rq_reduce_partials(int count, const float* const* P, float* const* out, const int64_t* n, const int* S,
+                       const int* layout, const int* accumulate, void* stream);
+
+/* rq_segment_sum over up to 16 sources at once (every embedding table of a decoder step: modules/model.py:59-63,
+ * modules/embedding/id_embedder.py): source t's rows (n[t], D) with keys in [0, K[t]) (others and pad[t]
+ * skipped) sum into rows [sum_{u<t} K[u], + K[t]) of out (sum K, D). One pack launch + one segmented-sum
+ * chain instead of one chain per table; sum K <= 4096. */
+size_t rq_segment_sum_multi_workspace(int count, const int64_t* n, const int64_t* K, int64_t D);
+int rq_segment_sum_multi(int count, const float* const* rows, const int64_t* const* keys, const int64_t* n,
+                         const int64_t* K, const int64_t* pad, int64_t D, float* out, void* workspace, size_t ws_bytes,
+                         void* stream);
 /* Decoder loss head (modules/model.py:137-143): X = out_proj output rows (B * npos_x, K), row stride ldx;
  * logits row r = b * npos + j is X row b * npos_x + j (the reference drops the last position);
  * u[r] = cross_entropy(logits[r], tgt[r], ignore_index=-1) (NaN for a target >= K), lse[r] saved for the
@@ -313,12 +258,9 @@ int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, ui
 
 /* Number of distinct L-tuples among the B rows of ids (B,L) -> *out_count (device int64).
  * p_unique_ids = count / B (modules/rqvae.py:152-157, which computes it in O(B^2 L)).
- * Requires K^L < 2^63. workspace >= rq_unique_workspace(B) bytes. */
-size_t rq_unique_workspace(int64_t B);
-/* Workspace for these (B, L, K): where K^L <= 2^24 a byte map of K^L bytes (counted in one pass, no
- * scattered atomics), else the hash table of rq_unique_workspace(B). rq_unique_count uses the map when
- * K^L <= 2^24 and ws_bytes covers it. */
-size_t rq_unique_workspace2(int64_t B, int64_t L, int64_t K);
+ * Requires K^L < 2^63. workspace >= rq_unique_workspace(B, L, K) bytes: where K^L <= 2^24 a byte map
+ * of K^L bytes (counted in one pass, no scattered atomics), else a hash table of ~2B slots. */
+size_t rq_unique_workspace(int64_t B, int64_t L, int64_t K);
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
                     size_t ws_bytes, void* stream);
 
@@ -327,11 +269,6 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
  * `bos_emb.repeat(B, 1, 1)` of EncoderDecoderRetrievalModel._predict (modules/model.py:91-95).
  * n % 4 == 0; P and out 16-byte aligned. accumulate != 0: out += sum. */
 int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate, void* stream);
-
-/* Rows per wave of the l2norm + reconstruction kernels (1, 2 or 4; other values leave it unchanged);
- * returns the previous setting. Results are bitwise independent of it (per-row arithmetic is the same);
- * the initial value comes from the environment variable RQ_L2R_RPW (default 1). */
-int rq_l2norm_recon_rows_per_wave(int rpw);
 
 /* Fused decoder head of RqVae.forward (modules/rqvae.py:145-150): x_hat = l2norm(pre) (decoder MLP's
  * final L2NormalizationLayer, F.normalize eps 1e-12) and recon[b] = sum_c (x_hat - x)^2
@@ -389,52 +326,40 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
  *   lse (H, Tq) fp32 log-sum-exp per query (written by fwd, read by bwd). hd in {16, 32, 64, 128}.
  *   Tq / Tk: ALLOCATED rows of the q-side / kv-side buffers (>= cu_q[B] / cu_k[B]); rows past the
  *   last sequence get zero out / dq / dk / dv (written by the kernels: graph-capturable per bucket).
- * Backward is deterministic (no atomics): dq per query block (also writes delta (H, Tq) = rowsum(dO*O),
- * caller-provided scratch), then dk/dv per key block. B < 65535. */
+ *   ws / ws_elems: caller-provided fp32 scratch of at least varlen_attn_{fwd,bwd}_ws_elems(...) floats, or
+ *   NULL / 0 (the forms that need none).
+ *   flags: RQ_ATTN_* kernel policy, 0 = the measured-best forms (kernel-vs-kernel tests / A/B runs; every
+ *   policy computes the same function within fp32 summation order).
+ * Forward: with scratch, long ranges (max_k > 128, 2 <= B <= 4096) rank the sequences longest-first and
+ * dispatch their workgroups in that order (no straggler tail); <= 16 queries per sequence over > 128 keys
+ * (non-causal: the decoder's cross-attention) run split-key partials (one one-wave workgroup per 128-key
+ * block) merged per query in block order (deterministic); many queries over long keys at low occupancy run
+ * the key-split form. Backward is deterministic (no atomics): short ranges run one-pass forms (dQ, dK, dV
+ * from S and dP formed once per tile pair); with scratch, longer ranges (hd == 64) run ONE fused launch
+ * per key block (after a delta = rowsum(dO*O) pre-pass) whose dQ partials are summed in block order by a
+ * reduction launch, and — when varlen_attn_bwd_ws_elems was given Tk >= 0 — may split each key block's
+ * query range over up to 4 workgroups when the grid cannot fill the GPU (few long sequences per GPU),
+ * their dK / dV partials summed in split order. Without scratch those ranges run the two-pass form (dQ per
+ * query block, writing delta (H, Tq) to the caller's `delta`, then dK / dV per key block). */
+#define RQ_ATTN_NO_DMA 1          /* register-staged short forms instead of the LDS-DMA ones */
+#define RQ_ATTN_TWO_PASS 2        /* two-pass backward everywhere (no one-pass / fused forms) */
+#define RQ_ATTN_NO_SPLIT 4        /* no split-key / key-split forward */
+#define RQ_ATTN_QSPLIT_SHIFT 8
+#define RQ_ATTN_QSPLIT(n) ((n) << RQ_ATTN_QSPLIT_SHIFT)   /* fused backward query splits forced to n (1..8; 1 = off) */
+int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
+                             int flags, int64_t* elems);
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream);
-/* varlen_attn_fwd with one float scratch `ws` of varlen_attn_fwd_ws_elems(...) floats (the product's entry,
- * rqvae_hip/ops.py): for long ranges (max_k > 128, 2 <= B <= 4096) the launch first ranks the sequences
- * longest-first into ws (B ints, padded to 16 B) and dispatches their workgroups in that order (no straggler
- * tail), and for <= 16 queries per sequence over > 128 keys (non-causal: the decoder's cross-attention) it
- * runs split-key partials in ws — one one-wave workgroup per 128-key block, merged per query in block order
- * by a combine launch (deterministic). Same results as varlen_attn_fwd within fp32 summation order;
- * varlen_attn_fwd itself (no scratch) is tested against the oracle at the same shapes
- * (tests/test_jagged_attention_gpu.py::test_c_abi_entry_points_vs_oracle). */
-int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
-                             int64_t* elems);
-int varlen_attn_fwd3(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
-                     int64_t ws_elems, void* stream);
+                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
+                    int64_t ws_elems, int flags, void* stream);
+/* Tk < 0: scratch without the query splits' dK / dV partials. */
+int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int64_t Tk,
+                             int flags, int64_t* elems);
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
-                    float* delta, void* stream);
-/* Same contract as varlen_attn_bwd; where hd == 64 and the key / query ranges are longer than the short
- * forms serve (the decoder's encoder self-attention), ONE fused launch computes dQ, dK and dV per key
- * block with S and dP formed once per tile pair (after a delta = rowsum(dO*O) pre-pass); dQ of
- * sequences longer than one key block is summed from per-block partials in block order by a reduction
- * launch (deterministic, no atomics). ws: caller-provided scratch of at least
- * varlen_attn_bwd_ws_elems(...) floats (0 -> ws may be NULL; it also holds the longest-first sequence
- * order of the fused launch, as varlen_attn_fwd3). Other shapes run varlen_attn_bwd. With a workspace
- * of varlen_attn_bwd_ws_elems2(..., Tk, ...) floats the fused launch may also split each key block's
- * query range over up to 4 workgroups when the grid cannot fill the GPU (few long sequences per GPU);
- * their dK / dV partials are summed in split order by one more launch (deterministic). */
-int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
-                             int64_t* elems);
-/* Query splits of the fused backward: n > 0 forces n (1 = off), 0 = automatic (the default;
- * RQ_ATTN_QSPLIT in the environment sets the initial value). Returns the previous setting. */
-int rq_attn_qsplit_set(int n);
-int varlen_attn_bwd_ws_elems2(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int64_t Tk,
-                              int64_t* elems);
-int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
-                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
-                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
-                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
-                     float* delta, float* ws, int64_t ws_elems, void* stream);
+                    float* delta, float* ws, int64_t ws_elems, int flags, void* stream);
 
 /* AdamW step (torch.optim.AdamW as stepped by train_rqvae.py:168-172 / train_decoder.py:203) over
  * every fp32 parameter of a group, one launch per 64 tensors. segs: HOST array of nseg records of 5

@@ -37,20 +37,11 @@
 
 #include <algorithm>
 
-// Build switches (A/B-measured on MI355X, tools/attn_ab.sh, profiles/r02/attn_ab.txt): register
-// prefetch of the next staged chunk (off: +33-64 VGPRs cost more occupancy than the overlap gains),
-// and the number of 16-row tiles whose S / dP chains the backward passes interleave (2: 4 would
+// Build switches (A/B-measured on MI355X, profiles/r02/attn_ab.txt; register prefetch of the next
+// staged chunk was measured slower everywhere — +33-64 VGPRs cost more occupancy than the overlap gains —
+// and is not built): the number of 16-row tiles whose S / dP chains the backward passes interleave (2: 4 would
 // drop the dK/dV pass to one wave per SIMD). The Makefile builds this file with
 // -mllvm -amdgpu-mfma-vgpr-form (accumulators in VGPRs: no accvgpr moves around the softmax).
-#ifndef RQ_ATTN_PREFETCH
-#define RQ_ATTN_PREFETCH 0
-#endif
-#ifndef RQ_ATTN_BWD_PREFETCH
-#define RQ_ATTN_BWD_PREFETCH 0   // 1: fused backward loads the next chunk's Q / dO / lse / delta one chunk ahead (A/B: slower)
-#endif
-#ifndef RQ_ATTN_KVSPLIT_PREFETCH
-#define RQ_ATTN_KVSPLIT_PREFETCH 0   // key-split forward: the block's second chunk loaded during the first
-#endif
 // The few-query / short kernels' per-wave partial tiles (part / part_o [NW][16][HD]) are written by lane
 // (row c = lane % 16, columns 16 (lane / 16) + 4 i): with 256-byte rows all 16 rows hit the same banks
 // (16-way conflicts on every ds_write_b128: 8-17 conflict cycles per LDS instruction in the Amazon SQ
@@ -59,14 +50,6 @@
 #define RQ_ATTN_PART_PAD 1
 #endif
 constexpr int kPartPad = RQ_ATTN_PART_PAD ? 4 : 0;
-#ifndef RQ_ATTN_BWD_WPE3
-#define RQ_ATTN_BWD_WPE3 0
-#endif
-#if RQ_ATTN_BWD_PREFETCH && RQ_ATTN_BWD_WPE3   // 3 waves per SIMD (what the LDS allows) despite the prefetch registers
-#define RQ_BWD_FUSED_WPE __attribute__((amdgpu_waves_per_eu(3)))
-#else
-#define RQ_BWD_FUSED_WPE
-#endif
 #ifndef RQ_ATTN_BWD_GROUP
 #define RQ_ATTN_BWD_GROUP 2
 #endif
@@ -331,24 +314,14 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restri
   const float* kb_ = k + k0 * sk + hh * HD;
   const float* vb_ = v + k0 * sv + hh * HD;
   RowStage<HD, 64 * NW, CH> stk, stv;
-  if (RQ_ATTN_PREFETCH && kend > 0) {
-    stk.load(kb_, sk, 0, lk, tid);
-    stv.load(vb_, sv, 0, lk, tid);
-  }
   FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, lk, qi, causal, scale * kLog2e, &m, &l, o};
   for (int kc = 0; kc < kend; kc += CH) {
-    if (!RQ_ATTN_PREFETCH) {
-      stk.load(kb_, sk, kc, lk, tid);
-      stv.load(vb_, sv, kc, lk, tid);
-    }
+    stk.load(kb_, sk, kc, lk, tid);
+    stv.load(vb_, sv, kc, lk, tid);
     __syncthreads();                          // the previous chunk's LDS reads are done
     stk.store(K_s, tid);
     stv.store(V_s, tid);
     __syncthreads();
-    if (RQ_ATTN_PREFETCH && kc + CH < kend) {   // next chunk's loads fly while this one is multiplied
-      stk.load(kb_, sk, kc + CH, lk, tid);
-      stv.load(vb_, sv, kc + CH, lk, tid);
-    }
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend_w - kc + 15) >> 4) : 0);
     fc.kc = kc;
     dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fc);
@@ -449,25 +422,15 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
   const float* kb_ = k + k0 * sk + hh * HD;
   const float* vb_ = v + k0 * sv + hh * HD;
   RowStage<HD, 64 * NW, CH> stk, stv;
-  if (RQ_ATTN_PREFETCH && kend > 0) {
-    stk.load(kb_, sk, 0, lk, tid);
-    stv.load(vb_, sv, 0, lk, tid);
-  }
   DqChunk<HD> fc{K_s, V_s, qf, dof, lane, 0, lk, qi, causal, scale * kLog2e,
                  qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f, delta, acc};
   for (int kc = 0; kc < kend; kc += CH) {
-    if (!RQ_ATTN_PREFETCH) {
-      stk.load(kb_, sk, kc, lk, tid);
-      stv.load(vb_, sv, kc, lk, tid);
-    }
+    stk.load(kb_, sk, kc, lk, tid);
+    stv.load(vb_, sv, kc, lk, tid);
     __syncthreads();
     stk.store(K_s, tid);
     stv.store(V_s, tid);
     __syncthreads();
-    if (RQ_ATTN_PREFETCH && kc + CH < kend) {
-      stk.load(kb_, sk, kc + CH, lk, tid);
-      stv.load(vb_, sv, kc + CH, lk, tid);
-    }
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend_w - kc + 15) >> 4) : 0);
     fc.kc = kc;
     dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fc);
@@ -578,10 +541,9 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
     lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
     dl_r = ok ? dl_h[qc + tid] : 0.f;
   };
-  if (RQ_ATTN_PREFETCH && qstart < lq) load_chunk(qstart);
   DkdvChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, lane, 0, 0, lq, kj, causal, scale * kLog2e, dka, dva};
   for (int qc = qstart; qc < lq; qc += CH) {
-    if (!RQ_ATTN_PREFETCH) load_chunk(qc);
+    load_chunk(qc);
     __syncthreads();
     stq.store(Q_s, tid);
     sto.store(O_s, tid);
@@ -590,7 +552,6 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkdv_kernel(
       dl_s[tid] = dl_r;
     }
     __syncthreads();
-    if (RQ_ATTN_PREFETCH && qc + CH < lq) load_chunk(qc + CH);
     const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);   // tiles wholly before the keys
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (lq - qc + 15) >> 4) - t0 : 0);
     fc.qc = qc;
@@ -721,23 +682,13 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
   const float* vb_ = v + k0 * sv + hh * HD;
   RowStage<HD, 64 * NW, CH> stk, stv;
   FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, kend, qi, 0, scale * kLog2e, &m, &l, o};
-  if (RQ_ATTN_KVSPLIT_PREFETCH) {             // next chunk's K / V loaded one chunk ahead (same values)
-    stk.load(kb_, sk, kbeg, kend, tid);
-    stv.load(vb_, sv, kbeg, kend, tid);
-  }
   for (int kc = kbeg; kc < kend; kc += CH) {
-    if (!RQ_ATTN_KVSPLIT_PREFETCH) {
-      stk.load(kb_, sk, kc, kend, tid);
-      stv.load(vb_, sv, kc, kend, tid);
-    }
+    stk.load(kb_, sk, kc, kend, tid);
+    stv.load(vb_, sv, kc, kend, tid);
     __syncthreads();                          // the previous chunk's LDS reads are done
     stk.store(K_s, tid);
     stv.store(V_s, tid);
     __syncthreads();
-    if (RQ_ATTN_KVSPLIT_PREFETCH && kc + CH < kend) {
-      stk.load(kb_, sk, kc + CH, kend, tid);
-      stv.load(vb_, sv, kc + CH, kend, tid);
-    }
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend - kc + 15) >> 4) : 0);
     fc.kc = kc;
     dispatch_tiles<NTL>(nt, kc + CH <= kend, fc);
@@ -884,7 +835,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const float* __restrict
 }
 
 template <int HD, int NW, int CH>
-__global__ void __launch_bounds__(64 * NW) RQ_BWD_FUSED_WPE attn_bwd_fused_kernel(
+__global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
     const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
@@ -952,9 +903,8 @@ __global__ void __launch_bounds__(64 * NW) RQ_BWD_FUSED_WPE attn_bwd_fused_kerne
   RowStage<HD, 64 * NW, CH> stq, sto;
   FusedChunk<HD> fc{Q_s, O_s, lse_s, dl_s, kf, vf, dS_s, lane, 0, 0, lq, kj, causal, wave * 16 + (lane & 15), LDS_, kv,
                     scale * kLog2e, dka, dva};
-  // Q / dO / lse / delta of a chunk are loaded into registers one chunk ahead (RQ_ATTN_BWD_PREFETCH):
-  // the next chunk's global loads are in flight while this chunk's products run (a long sequence's
-  // workgroup walks up to ~9 chunks back to back at 8 sequences per GPU); same values, same order.
+  // Q / dO / lse / delta of a chunk: global -> registers, then LDS (prefetching the next chunk into
+  // registers measured slower: 158 -> 177 VGPRs, 3 -> 2 waves per SIMD, profiles/r03/attn_bwd_prefetch_ab.txt)
   float lse_r = 0.f, dl_r = 0.f;
   auto load_chunk = [&](int qc) {
     stq.load(qb_, sq, qc, lq, tid);
@@ -963,9 +913,8 @@ __global__ void __launch_bounds__(64 * NW) RQ_BWD_FUSED_WPE attn_bwd_fused_kerne
     lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
     dl_r = ok ? dl_h[qc + tid] : 0.f;
   };
-  if (RQ_ATTN_BWD_PREFETCH && c_lo < c_hi) load_chunk(c_lo);
   for (int qc = c_lo; qc < c_hi; qc += CH) {
-    if (!RQ_ATTN_BWD_PREFETCH) load_chunk(qc);
+    load_chunk(qc);
     __syncthreads();                          // previous chunk's Q/dO/dS reads are done
     stq.store(Q_s, tid);
     sto.store(O_s, tid);
@@ -974,7 +923,6 @@ __global__ void __launch_bounds__(64 * NW) RQ_BWD_FUSED_WPE attn_bwd_fused_kerne
       dl_s[tid] = dl_r;
     }
     __syncthreads();
-    if (RQ_ATTN_BWD_PREFETCH && qc + CH < c_hi) load_chunk(qc + CH);
     const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? max(0, min(NTL, (lq - qc + 15) >> 4) - t0) : 0);
     // dS columns of tiles this wave does not compute are zero (K_s rows past lk are zero too, but
@@ -2315,75 +2263,60 @@ static bool lpt_plan(int64_t B, int64_t max_len) { return RQ_ATTN_LPT && B >= 2 
 #ifndef RQ_ATTN_SPLIT_MIN_K
 #define RQ_ATTN_SPLIT_MIN_K 129   // key ranges from here use the split-key forward (A/B: at the Amazon
 #endif                            // contexts, <= 81 keys in 32-key blocks, it ties the chunked form)
-static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal) {
-  return RQ_ATTN_SPLIT && hd == 64 && !causal && max_q <= 16 && max_k >= RQ_ATTN_SPLIT_MIN_K;
+// The kernel policy of one call, from its `flags` argument (RQ_ATTN_* in include/rqvae_hip.h; 0 = the
+// measured-best forms): LDS-DMA short forms, one-pass backwards, split-key / key-split forwards, and the
+// fused backward's query splits (0 = automatic).
+struct AttnPolicy {
+  bool dma, fused, split;
+  int qsplit;
+};
+static AttnPolicy attn_policy(int flags) {
+  return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
+                    (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15};
+}
+
+static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal, const AttnPolicy& pol) {
+  return RQ_ATTN_SPLIT && pol.split && hd == 64 && !causal && max_q <= 16 && max_k >= RQ_ATTN_SPLIT_MIN_K;
 }
 static int split_kb(int64_t max_k) { return max_k <= 128 ? 32 : 128; }   // 32: RQ_ATTN_SPLIT_MIN_K <= 128 builds
 // key-split forward for many queries over long keys at low occupancy (attn_fwd_kvsplit_kernel): the C4
-// per-rank config (8 sequences x 6 heads x <= 13 query blocks); RQ_ATTN_KVSPLIT=0 disables (A/B)
+// per-rank config (8 sequences x 6 heads x <= 13 query blocks); RQ_ATTN_NO_SPLIT disables it (A/B)
 #ifndef RQ_ATTN_KVSPLIT_MAX_WG
 #define RQ_ATTN_KVSPLIT_MAX_WG 1024   // unsplit workgroups (B x H x 64-query blocks) up to which it applies
 #endif
 constexpr int kKvSplitKB = 128;
-static bool kvsplit_plan(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal) {
-  static const bool on = [] {
-    const char* e = getenv("RQ_ATTN_KVSPLIT");
-    return !(e && e[0] == '0');
-  }();
-  return on && RQ_ATTN_SPLIT && hd == 64 && !causal && max_q > 16 && max_k > 2 * kKvSplitKB &&
+static bool kvsplit_plan(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
+                         const AttnPolicy& pol) {
+  return pol.split && RQ_ATTN_SPLIT && hd == 64 && !causal && max_q > 16 && max_k > 2 * kKvSplitKB &&
          B * H * ((max_q + 63) / 64) <= RQ_ATTN_KVSPLIT_MAX_WG;
 }
-static int64_t split_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal) {
-  if (kvsplit_plan(B, H, hd, max_q, max_k, causal)) return (max_k + kKvSplitKB - 1) / kKvSplitKB * Tq * H * (hd + 2);
-  if (!split_plan(hd, max_q, max_k, causal)) return 0;
+static int64_t split_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
+                              const AttnPolicy& pol) {
+  if (kvsplit_plan(B, H, hd, max_q, max_k, causal, pol)) return (max_k + kKvSplitKB - 1) / kKvSplitKB * Tq * H * (hd + 2);
+  if (!split_plan(hd, max_q, max_k, causal, pol)) return 0;
   const int kb = split_kb(max_k);
   return (max_k + kb - 1) / kb * Tq * H * (hd + 2);
 }
 
 // LDS-DMA short forms (attn_fwd_dma_kernel): self-attention style launches (more than one query tile)
-// whose key range fits 128 staged rows. RQ_ATTN_DMA=0 in the environment or rq_attn_dma_enable(0)
-// keeps the register-staged kernels (A/B).
-static int g_attn_dma = -1;
-static bool attn_dma_on() {
-  if (g_attn_dma < 0) {
-    const char* e = getenv("RQ_ATTN_DMA");
-    g_attn_dma = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_attn_dma != 0;
-}
+// whose key range fits 128 staged rows; RQ_ATTN_NO_DMA keeps the register-staged kernels (A/B).
 static int dma_rows_for(int64_t max_k) { return max_k <= 32 ? 32 : (max_k <= 64 ? 64 : (max_k <= 96 ? 96 : 128)); }
-static bool dma_fwd_plan(int64_t hd, int64_t max_q, int64_t max_k) {   // also the dQ pass
-  return attn_dma_on() && hd == 64 && max_q > 16 && max_k <= 128;
+static bool dma_fwd_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {   // also the dQ pass
+  return pol.dma && hd == 64 && max_q > 16 && max_k <= 128;
 }
-static bool dma_kv_plan(int64_t hd, int64_t max_q, int64_t max_k) {    // dK / dV pass: queries staged
-  return attn_dma_on() && hd == 64 && max_k > 16 && max_q <= 128;
+static bool dma_kv_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {    // dK / dV: queries staged
+  return pol.dma && hd == 64 && max_k > 16 && max_q <= 128;
 }
 // one query tile over <= 128 keys (cross-attention, the decoder's short causal self-attention): forward and
 // dQ with the key tiles split over the waves (attn_fwd_fewq_kernel / attn_bwd_dq_fewq_kernel)
-static bool fewq_plan(int64_t hd, int64_t max_q, int64_t max_k) {
-  return attn_dma_on() && hd == 64 && max_q <= 16 && max_k <= 128;
+static bool fewq_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {
+  return pol.dma && hd == 64 && max_q <= 16 && max_k <= 128;
 }
 static int fewq_waves(int64_t max_k) { return max_k <= 16 ? 1 : (max_k <= 32 ? 2 : 4); }
-// one-pass backward of the few-query launches (attn_bwd_fewq_fused_kernel); RQ_ATTN_FEWQ_FUSED=0 in the
-// environment or rq_attn_fewq_fused_enable(0) keeps the two-pass fewq dQ + dK/dV kernels (A/B)
-static int g_short_fused = -1;   // the same for self-attention style launches (attn_bwd_short_fused_kernel)
-static bool short_fused_on() {
-  if (g_short_fused < 0) {
-    const char* e = getenv("RQ_ATTN_SHORT_FUSED");
-    g_short_fused = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_short_fused != 0;
-}
-static bool short_fused_plan(int64_t hd, int64_t max_q, int64_t max_k) {
-  return attn_dma_on() && short_fused_on() && hd == 64 && max_q > 16 && max_q <= 128 && max_k <= 128;
-}
-static int g_fewq_fused = -1;
-static bool fewq_fused_on() {
-  if (g_fewq_fused < 0) {
-    const char* e = getenv("RQ_ATTN_FEWQ_FUSED");
-    g_fewq_fused = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_fewq_fused != 0;
+// one-pass backward of the self-attention style short launches (attn_bwd_short_fused_kernel) and of the
+// few-query launches (attn_bwd_fewq_fused_kernel); RQ_ATTN_TWO_PASS keeps the two-pass dQ + dK/dV kernels
+static bool short_fused_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {
+  return pol.dma && pol.fused && hd == 64 && max_q > 16 && max_q <= 128 && max_k <= 128;
 }
 
 template <int HD, int NW>
@@ -2399,9 +2332,10 @@ template <int HD>
 static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q, int64_t sq,
                        const float* k,
                        int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal,
-                       float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order, float* split_ws) {
+                       float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order, float* split_ws,
+                       const AttnPolicy& pol) {
   if constexpr (HD == 64) {
-    if (split_ws && kvsplit_plan(B, H, HD, max_q, max_k, causal)) {
+    if (split_ws && kvsplit_plan(B, H, HD, max_q, max_k, causal, pol)) {
       const int nsplit = (int)((max_k + kKvSplitKB - 1) / kKvSplitKB);
       constexpr int RPB = 256 / (HD / 4);
       const dim3 gs((unsigned)(((max_q + 63) / 64) * nsplit), (unsigned)H, (unsigned)B);
@@ -2412,7 +2346,7 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                          so, lse);
       return;
     }
-    if (split_ws && split_plan(HD, max_q, max_k, causal)) {
+    if (split_ws && split_plan(HD, max_q, max_k, causal, pol)) {
       const int kb = split_kb(max_k);
       const int nsplit = (int)((max_k + kb - 1) / kb);
       constexpr int RPB = 256 / (HD / 4);
@@ -2426,7 +2360,7 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #undef RQ_SPL
       return;
     }
-    if (fewq_plan(HD, max_q, max_k)) {
+    if (fewq_plan(HD, max_q, max_k, pol)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
       switch (fewq_waves(max_k)) {
         case 1: hipLaunchKernelGGL((attn_fwd_fewq_kernel<1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
@@ -2435,7 +2369,7 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
       }
       return;
     }
-    if (dma_fwd_plan(HD, max_q, max_k)) {
+    if (dma_fwd_plan(HD, max_q, max_k, pol)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
 #define RQ_FD(R_)                                                                                              \
   hipLaunchKernelGGL((attn_fwd_dma_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, \
@@ -2509,33 +2443,29 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                        const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
                        const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck,
                        int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv,
-                       int64_t Tk, float* delta) {
+                       int64_t Tk, float* delta, const AttnPolicy& pol) {
   // dQ pass first: it also writes delta_q = dO.O, which the dK/dV pass reads per query chunk
   bool dq_done = false, kv_done = false;
   if constexpr (HD == 64) {
     int nw = 0, ch = 0;
     const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
-    if (short_fused_plan(HD, max_q, max_k)) {
+    if (short_fused_plan(HD, max_q, max_k, pol)) {
 #define RQ_SHF(NW_, R_)                                                                                              \
   hipLaunchKernelGGL((attn_bwd_short_fused_kernel<NW_, R_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, \
                      dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
-      // 4 waves with up to two key tiles each, or (RQ_ATTN_SHORT_TPW=1, A/B) one key tile per wave (R / 16
-      // waves: 134 instead of 229 VGPRs, 3 waves per SIMD at R = 96) — measured slower on the Amazon step
-      // (6.20-6.22 vs 6.10-6.15 ms, profiles/r03/short_tpw_ab.txt): more waves idle on short sequences
-      static const bool one_tile = [] {
-        const char* e = getenv("RQ_ATTN_SHORT_TPW");
-        return e && e[0] == '1';
-      }();
+      // 4 waves with up to two key tiles each (one key tile per wave, R / 16 waves, measured slower on the
+      // Amazon step: 6.20-6.22 vs 6.10-6.15 ms, profiles/r03/short_tpw_ab.txt — more waves idle on short
+      // sequences)
       switch (dma_rows_for(std::max(max_q, max_k))) {
         case 32: RQ_SHF(2, 32); break;
         case 64: RQ_SHF(4, 64); break;
-        case 96: if (one_tile) RQ_SHF(6, 96); else RQ_SHF(4, 96); break;
-        default: if (one_tile) RQ_SHF(8, 128); else RQ_SHF(4, 128); break;
+        case 96: RQ_SHF(4, 96); break;
+        default: RQ_SHF(4, 128); break;
       }
 #undef RQ_SHF
       return;
     }
-    if (fewq_plan(HD, max_q, max_k) && fewq_fused_on()) {
+    if (fewq_plan(HD, max_q, max_k, pol) && pol.fused) {
 #define RQ_FQF(NW_)                                                                                                   \
   hipLaunchKernelGGL((attn_bwd_fewq_fused_kernel<NW_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, dout, \
                      sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
@@ -2547,7 +2477,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #undef RQ_FQF
       return;
     }
-    if (fewq_plan(HD, max_q, max_k)) {
+    if (fewq_plan(HD, max_q, max_k, pol)) {
 #define RQ_DQF(NW_)                                                                                                   \
   hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<NW_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, \
                      lse, Tq, cq, ck, causal, scale, dq, sdq, delta)
@@ -2558,7 +2488,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
       }
 #undef RQ_DQF
       dq_done = true;
-    } else if (dma_fwd_plan(HD, max_q, max_k)) {
+    } else if (dma_fwd_plan(HD, max_q, max_k, pol)) {
 #define RQ_DQD(R_)                                                                                                  \
   hipLaunchKernelGGL((attn_bwd_dq_dma_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, \
                      Tq, cq, ck, causal, scale, dq, sdq, delta)
@@ -2578,7 +2508,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #undef RQ_DQS
       dq_done = true;
     }
-    if (dma_kv_plan(HD, max_q, max_k)) {
+    if (dma_kv_plan(HD, max_q, max_k, pol)) {
       if (!dq_done) {   // the dK/dV pass reads delta: chunked dQ first
         launch_dq_chunked<HD>(B, H, max_q, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cq, ck, causal, scale, dq,
                               sdq, delta);
@@ -2639,15 +2569,9 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #endif                                 // A/B from 33 keys: Amazon decoder step 6.53 -> 6.60 ms, fewq_ab.txt)
 constexpr int kFusedKB = 16 * RQ_ATTN_FUSED_NW;
 
-static bool fused_plan(int64_t hd, int64_t max_q, int64_t max_k) {
-  if (!RQ_ATTN_FUSED || hd != 64) return false;
-  // few queries (cross-attention): their own threshold
-  // (RQ_ATTN_FEWQ_MIN_K in the environment overrides the threshold: in-process A/B of the decoder step)
-  static const int64_t fewq_min = [] {
-    const char* e = getenv("RQ_ATTN_FEWQ_MIN_K");
-    return e ? (int64_t)atoll(e) : (int64_t)RQ_ATTN_FUSED_MIN_K_FEWQ;
-  }();
-  if (max_q <= 16) return max_k >= fewq_min;
+static bool fused_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {
+  if (!RQ_ATTN_FUSED || !pol.fused || hd != 64) return false;
+  if (max_q <= 16) return max_k >= RQ_ATTN_FUSED_MIN_K_FEWQ;   // few queries (cross-attention): own threshold
   if (max_k < RQ_ATTN_FUSED_MIN_K) return false;
   int nw = 0, ch = 0;
   return !short_plan(max_k, max_q, &nw, &ch);
@@ -2656,14 +2580,9 @@ static bool fused_plan(int64_t hd, int64_t max_q, int64_t max_k) {
 // Query splits of the fused backward: when (sequences x heads x key blocks) workgroups cannot fill the
 // chip twice over (ML-32M at 8 sequences per GPU: ~300 workgroups, each walking up to 801 queries), each
 // key block's query range is split over up to 4 workgroups (whole 32-query chunks, >= 2 per split);
-// their dK / dV partials are summed by attn_kv_reduce_kernel. RQ_ATTN_QSPLIT=n forces n (1 = off).
-static int g_attn_qsplit = -1;   // -1: RQ_ATTN_QSPLIT from the environment (0 = auto); rq_attn_qsplit_set
-static int fused_qsplit(int64_t B, int64_t H, int64_t max_q, int64_t max_k) {
-  if (g_attn_qsplit < 0) {
-    const char* e = getenv("RQ_ATTN_QSPLIT");
-    g_attn_qsplit = e ? std::max(0, atoi(e)) : 0;
-  }
-  const int forced = g_attn_qsplit;
+// their dK / dV partials are summed by attn_kv_reduce_kernel. A call's RQ_ATTN_QSPLIT(n) forces n (1 = off).
+static int fused_qsplit(int64_t B, int64_t H, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {
+  const int forced = pol.qsplit;
   if (max_q <= 16) return 1;
   const int64_t max_by_len = std::max<int64_t>(1, max_q / (2 * RQ_ATTN_FUSED_CH));
   if (forced > 0) return (int)std::min<int64_t>(std::min(forced, 8), max_by_len);
@@ -2681,17 +2600,18 @@ static int fused_qsplit(int64_t B, int64_t H, int64_t max_q, int64_t max_k) {
 
 // floats of dQ partials the fused backward needs: one (Tq, H*hd) slab per key block when a sequence may
 // span more than one block
-static int64_t fused_part_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq) {
-  if (!fused_plan(hd, max_q, max_k)) return 0;
+static int64_t fused_part_elems(int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, const AttnPolicy& pol) {
+  if (!fused_plan(hd, max_q, max_k, pol)) return 0;
   const int64_t nkb = (max_k + kFusedKB - 1) / kFusedKB;
   return nkb > 1 ? nkb * Tq * H * hd : 0;
 }
 // + B ints of LPT order (float slots, padded to 16 B) [+ the query splits' dK / dV partials, Tk >= 0]
 static int64_t fused_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
-                              int64_t Tk = -1) {
-  if (!fused_plan(hd, max_q, max_k)) return 0;
-  const int64_t base = fused_part_elems(H, hd, max_q, max_k, Tq) + (lpt_plan(B, max_q) ? ((B + 3) & ~(int64_t)3) : 0);
-  const int qs = Tk >= 0 ? fused_qsplit(B, H, max_q, max_k) : 1;
+                              const AttnPolicy& pol, int64_t Tk = -1) {
+  if (!fused_plan(hd, max_q, max_k, pol)) return 0;
+  const int64_t base =
+      fused_part_elems(H, hd, max_q, max_k, Tq, pol) + (lpt_plan(B, max_q) ? ((B + 3) & ~(int64_t)3) : 0);
+  const int qs = Tk >= 0 ? fused_qsplit(B, H, max_q, max_k, pol) : 1;
   return base + (qs > 1 ? 2 * qs * Tk * H * hd : 0);
 }
 
@@ -2700,12 +2620,13 @@ static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k,
                              int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                              int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq,
                              const int64_t* ck, int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk,
-                             float* dv, int64_t sdv, int64_t Tk, float* delta, float* ws, int64_t ws_elems) {
+                             float* dv, int64_t sdv, int64_t Tk, float* delta, float* ws, int64_t ws_elems,
+                             const AttnPolicy& pol) {
   if constexpr (HD == 64) {
     constexpr int NW = RQ_ATTN_FUSED_NW, CH = RQ_ATTN_FUSED_CH, KB = 16 * NW;
     const int* ord = nullptr;
     if (lpt_plan(B, max_q)) {   // the order lives after the dQ partials in ws
-      int* o = reinterpret_cast<int*>(ws + fused_part_elems(H, HD, max_q, max_k, Tq));
+      int* o = reinterpret_cast<int*>(ws + fused_part_elems(H, HD, max_q, max_k, Tq, pol));
       hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, cq, (int)B, o);
       ord = o;
     }
@@ -2714,10 +2635,10 @@ static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k,
     if (threads > 0)
       hipLaunchKernelGGL((attn_delta_kernel<HD>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, out, so, dout,
                          sdo, Tq, H, delta);
-    // query splits only when the caller sized the workspace for them (varlen_attn_bwd_ws_elems2)
-    int qs = fused_qsplit(B, H, max_q, max_k);
-    if (qs > 1 && ws_elems < fused_ws_elems(B, H, HD, max_q, max_k, Tq, Tk)) qs = 1;
-    float* kvpart = qs > 1 ? ws + fused_ws_elems(B, H, HD, max_q, max_k, Tq) : nullptr;
+    // query splits only when the caller sized the workspace for them (varlen_attn_bwd_ws_elems with Tk)
+    int qs = fused_qsplit(B, H, max_q, max_k, pol);
+    if (qs > 1 && ws_elems < fused_ws_elems(B, H, HD, max_q, max_k, Tq, pol, Tk)) qs = 1;
+    float* kvpart = qs > 1 ? ws + fused_ws_elems(B, H, HD, max_q, max_k, Tq, pol) : nullptr;
     const dim3 g((unsigned)(std::max<int64_t>(1, (max_k + KB - 1) / KB) * qs), (unsigned)H, (unsigned)B + 1);   // + tail
     hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, NW, CH>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse,
                        delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord, qs, kvpart);
@@ -2746,134 +2667,86 @@ using namespace rqhip;
 
 extern "C" {
 
-static int attn_fwd_impl(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                         const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                         int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, int* order,
-                         float* split_ws, void* stream) {
-  RQ_CHECK_ARG(q && k && v && cu_q && cu_k && out && lse, "varlen_attn_fwd: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<65535)");
-  RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
-  if (B == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  switch (hd) {
-    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
-    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
-    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
-    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws); break;
-  }
-  RQ_LAUNCH_CHECK("varlen_attn_fwd");
+int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
+                             int flags, int64_t* elems) {
+  RQ_CHECK_ARG(elems, "varlen_attn_fwd_ws_elems: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_fwd_ws_elems: bad shape");
+  // order (B ints, 16-B padded) + split-key partials
+  *elems = ((B + 3) & ~(int64_t)3) + split_ws_elems(B, H, hd, max_q, max_k, Tq, causal, attn_policy(flags));
   return 0;
 }
 
 int varlen_attn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, void* stream) {
-  return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq, nullptr,
-                       nullptr, stream);
-}
-
-int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,
-                             int64_t* elems) {
-  RQ_CHECK_ARG(elems, "varlen_attn_fwd_ws_elems: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_fwd_ws_elems: bad shape");
-  *elems = ((B + 3) & ~(int64_t)3) + split_ws_elems(B, H, hd, max_q, max_k, Tq, causal);   // order (B ints, 16-B padded) + split-key partials
+                    int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
+                    int64_t ws_elems, int flags, void* stream) {
+  RQ_CHECK_ARG(q && k && v && cu_q && cu_k && out && lse, "varlen_attn_fwd: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_fwd: bad shape (hd must be 16/32/64/128, B<65535)");
+  RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0, "varlen_attn_fwd: row strides must be x4");
+  const AttnPolicy pol = attn_policy(flags);
+  int* order = nullptr;
+  float* split_ws = nullptr;
+  if (ws != nullptr) {   // no scratch (ws NULL): natural sequence order, no split-key / key-split forms
+    const int64_t ob = (B + 3) & ~(int64_t)3, sp = split_ws_elems(B, H, hd, max_q, max_k, Tq, causal, pol);
+    RQ_CHECK_ARG(ws_elems >= ob + sp, "varlen_attn_fwd: workspace %lld < varlen_attn_fwd_ws_elems %lld floats",
+                 (long long)ws_elems, (long long)(ob + sp));
+    order = reinterpret_cast<int*>(ws);
+    split_ws = sp ? ws + ob : nullptr;
+  }
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (hd) {
+    case 16: launch_fwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws, pol); break;
+    case 32: launch_fwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws, pol); break;
+    case 64: launch_fwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws, pol); break;
+    case 128: launch_fwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, cu_q, cu_k, causal, scale, out, so, lse, Tq, order, split_ws, pol); break;
+  }
+  RQ_LAUNCH_CHECK("varlen_attn_fwd");
   return 0;
 }
 
-int varlen_attn_fwd3(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv,
-                     const int64_t* cu_q, const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q,
-                     int64_t max_k, int causal, float scale, float* out, int64_t so, float* lse, int64_t Tq, float* ws,
-                     int64_t ws_elems, void* stream) {
-  const int64_t ob = (B + 3) & ~(int64_t)3, sp = split_ws_elems(B, H, hd, max_q, max_k, Tq, causal);
-  RQ_CHECK_ARG(ws && ws_elems >= ob + sp, "varlen_attn_fwd3: workspace smaller than varlen_attn_fwd_ws_elems");
-  return attn_fwd_impl(q, sq, k, sk, v, sv, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, so, lse, Tq,
-                       reinterpret_cast<int*>(ws), sp ? ws + ob : nullptr, stream);
+int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int64_t Tk,
+                             int flags, int64_t* elems) {
+  RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems: null pointer");
+  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_bwd_ws_elems: bad shape");
+  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq, attn_policy(flags), Tk);
+  return 0;
 }
 
 int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
-                    float* delta, void* stream) {
+                    float* delta, float* ws, int64_t ws_elems, int flags, void* stream) {
   RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv && delta,
                "varlen_attn_bwd: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd: bad shape (hd must be 16/32/64/128, B<65535)");
   RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0 && sdo % 4 == 0 && sdq % 4 == 0 &&
                    sdk % 4 == 0 && sdv % 4 == 0,
                "varlen_attn_bwd: row strides must be x4");
+  const AttnPolicy pol = attn_policy(flags);
+  // the fused long-range form needs its scratch; a call without one (ws NULL) runs the two-pass form there
+  const bool fused = fused_plan(hd, max_q, max_k, pol) && ws != nullptr;
+  if (fused) {
+    const int64_t need = fused_ws_elems(B, H, hd, max_q, max_k, Tq, pol);
+    RQ_CHECK_ARG(ws_elems >= need, "varlen_attn_bwd: workspace %lld < varlen_attn_bwd_ws_elems %lld floats",
+                 (long long)ws_elems, (long long)need);
+  }
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (fused) {
+    launch_bwd_fused<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal,
+                         scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, ws, ws_elems, pol);
+    RQ_LAUNCH_CHECK("varlen_attn_bwd");
+    return 0;
+  }
   switch (hd) {
-    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
-    case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
-    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
-    case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta); break;
+    case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
+    case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
+    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
+    case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_bwd");
-  return 0;
-}
-
-int rq_attn_qsplit_set(int n) {
-  fused_qsplit(1, 1, 0, 0);   // resolve the environment default first
-  const int prev = g_attn_qsplit;
-  g_attn_qsplit = n < 0 ? 0 : n;
-  return prev;
-}
-
-int rq_attn_short_fused_enable(int enable) {
-  const int prev = short_fused_on() ? 1 : 0;
-  g_short_fused = enable ? 1 : 0;
-  return prev;
-}
-
-int rq_attn_fewq_fused_enable(int enable) {
-  const int prev = fewq_fused_on() ? 1 : 0;
-  g_fewq_fused = enable ? 1 : 0;
-  return prev;
-}
-
-int rq_attn_dma_enable(int enable) {
-  const int prev = attn_dma_on() ? 1 : 0;
-  g_attn_dma = enable ? 1 : 0;
-  return prev;
-}
-
-int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq,
-                             int64_t* elems) {
-  RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_bwd_ws_elems: bad shape");
-  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq);
-  return 0;
-}
-
-int varlen_attn_bwd_ws_elems2(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int64_t Tk,
-                              int64_t* elems) {
-  RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems2: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0 && Tk >= 0, "varlen_attn_bwd_ws_elems2: bad shape");
-  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq, Tk);
-  return 0;
-}
-
-int varlen_attn_bwd2(const float* q, int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
-                     int64_t so, const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cu_q,
-                     const int64_t* cu_k, int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int causal,
-                     float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv, int64_t Tk,
-                     float* delta, float* ws, int64_t ws_elems, void* stream) {
-  if (!fused_plan(hd, max_q, max_k))
-    return varlen_attn_bwd(q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, B, H, hd, max_q, max_k, causal,
-                           scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, stream);
-  RQ_CHECK_ARG(q && k && v && out && dout && lse && cu_q && cu_k && dq && dk && dv && delta,
-               "varlen_attn_bwd2: null pointer");
-  RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k), "varlen_attn_bwd2: bad shape (hd must be 16/32/64/128, B<65535)");
-  RQ_CHECK_ARG(sq % 4 == 0 && sk % 4 == 0 && sv % 4 == 0 && so % 4 == 0 && sdo % 4 == 0 && sdq % 4 == 0 &&
-                   sdk % 4 == 0 && sdv % 4 == 0,
-               "varlen_attn_bwd2: row strides must be x4");
-  const int64_t need = fused_ws_elems(B, H, hd, max_q, max_k, Tq);
-  RQ_CHECK_ARG(ws_elems >= need && (need == 0 || ws), "varlen_attn_bwd2: workspace smaller than varlen_attn_bwd_ws_elems");
-  if (B == 0) return 0;
-  launch_bwd_fused<64>(B, H, max_q, max_k, (hipStream_t)stream, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q,
-                       cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, ws, ws_elems);
-  RQ_LAUNCH_CHECK("varlen_attn_bwd2");
   return 0;
 }
 

@@ -7,6 +7,8 @@
 #include <math.h>
 #include <algorithm>
 
+#include "../../include/rqvae_hip.h"   // every extern "C" definition is checked against its declaration
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4v __attribute__((ext_vector_type(4)));
 
@@ -142,6 +144,11 @@ static __device__ uint64_t rq_seed_epoch = 0;
 __device__ __forceinline__ uint64_t epoch_seed(uint64_t seed) {
   return seed + rq_seed_epoch * 0xD6E8FEB86659FD93ull;
 }
+// the three copies' device addresses (current device) and their update launch (c_abi.cpp's callers)
+int seed_epoch_addr_dropout(void** out);
+int seed_epoch_addr_rowwise(void** out);
+int seed_epoch_addr_linear(void** out);
+int seed_epoch_update(void* a, void* b, void* c, uint64_t value, int add, void* stream);
 // thr / scale of nn.Dropout(p) for the kernels below (dropout.hip).
 void dropout_params(float p, uint32_t* thr, float* scale);
 struct Keep4 {

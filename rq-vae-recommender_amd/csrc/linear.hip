@@ -18,7 +18,6 @@
 // Workgroups that share a row chunk are placed on the same XCD (blockIdx % 8 selects the XCD)
 // so the tiles re-reading the same g / x rows hit one L2.
 #include "common.h"
-#include "../../include/rqvae_hip.h"
 
 namespace rqhip {
 
@@ -1164,140 +1163,6 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 #undef RQ_W_VM6
 #undef RQ_W_LGKM0
 
-// ---------------------------------------------------------------------------------------------
-// LDS-DMA form of the 128-tile kernel for an fp32 k-contiguous A and a split B ("x3d"): the decoder's
-// projections and data gradients, whose A (a norm / attention output, an activation gradient) is fp32.
-// The register-staged kernel splits A while staging it and pays the VGPR -> LDS store transfer
-// (ds_write_b128 ~79 B/clk/CU) for every operand byte — at K = 512..1536 that transfer, not the MFMA,
-// bounds it (SQ: MFMA busy 27 %). Here both operands land in LDS by global_load_lds_dwordx4 (no VGPR
-// round trip): A as an fp32 row image (128 rows x 32 k x 4 B: the same bytes as its hi + lo planes; 16-B
-// chunk c of row r at c ^ ((r >> 1) & 1 | (r & 4)), conflict-free for the fragment reads below), B as the
-// wide kernel's half-plane images (x3w_src / wfrag16). A fragments are split to (hi, lo) bf16 right after
-// their ds_read_b128 pair — the same split_bf16x2 as the staging path, so for the same operands this
-// kernel's MFMA inputs, product order (16x16x32, hi.lo + lo.hi + hi.hi per tile) and k order equal
-// gemm_bf16x3_kernel's: the results agree bitwise. Ring: A three k-step slots, B two (80 KiB: two
-// workgroups per CU); per k step each wave issues B(st + 1) then A(st + 2) (4 + 4 DMA instructions) and
-// waits vmcnt(4) + one barrier at the top of the next step (A(st + 1) stays in flight). K % 32 == 0.
-// ---------------------------------------------------------------------------------------------
-constexpr int kDA = 16384;            // A slot: 128 rows x 32 k fp32
-constexpr int kDB = 2 * kWH;          // B slot: hi + lo half-planes
-constexpr int kDLds = 3 * kDA + 2 * kDB;
-static_assert(kDLds == 81920, "x3d LDS");
-
-__device__ __forceinline__ int drow_swz(int r) { return ((r >> 1) & 1) | (r & 4); }
-
-template <bool BKC, int EPI, bool DROP>
-__global__ void __launch_bounds__(256, 2)
-gemm_x3d_kernel(const float* __restrict__ A, int64_t lda, const uint16_t* __restrict__ Bh, const uint16_t* __restrict__ Bl,
-                int64_t ldb, int M, int N, int64_t K, int tiles_n, int tiles, int S, int64_t chunk, int per,
-                float* __restrict__ C, int64_t ldc, X3Epilogue ep) {
-  ep.seed = epoch_seed(ep.seed);
-  __shared__ __attribute__((aligned(16))) char lds[kDLds];
-  const int bid = blockIdx.x;
-  const int lw = (bid & 7) * per + (bid >> 3);   // XCD-major: neighbours (same A rows / same k chunk) share an L2
-  if (lw >= tiles * S) return;
-  const int s = lw / tiles, t = lw % tiles;
-  const int m0 = (t / tiles_n) * kXT, n0 = (t % tiles_n) * kXT;
-  const int64_t k_lo = (int64_t)s * chunk;
-  const int64_t k_hi = k_lo + chunk < K ? k_lo + chunk : K;
-  const int nk = (int)((k_hi - k_lo) >> 5);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  // per-lane DMA sources of this wave's instructions j = wave + 4 u (u = 0..3): A rows 8 j + (lane >> 3)
-  // (128-B rows, position lane & 7 holds chunk (lane & 7) ^ drow_swz(row)); B: x3w_src of 1 KiB block j
-  // (u = 0, 1) per plane
-  int64_t oa[4], ob[2];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = wave + 4 * u, row = 8 * j + (lane >> 3);
-    const int kc = (lane & 7) ^ drow_swz(row);
-    oa[u] = (int64_t)min(m0 + row, M - 1) * lda + k_lo + 4 * kc;
-  }
-  const int64_t kb = BKC ? k_lo : k_lo * ldb, db = BKC ? 32 : 32 * ldb;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) ob[u] = kb + x3w_src<BKC>(ldb, n0, N, wave + 4 * u, lane);
-  auto issue_a = [&](int step, int slot) {
-    const int64_t o = (int64_t)(step < nk ? step : nk - 1) * 32;
-    char* dst = lds + slot * kDA + 1024 * wave;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(A + oa[u] + o),
-                                       (__attribute__((address_space(3))) void*)(dst + 4096 * u), 16, 0, 0);
-  };
-  auto issue_b = [&](int step) {
-    const int64_t o = (int64_t)(step < nk ? step : nk - 1) * db;
-    char* dst = lds + 3 * kDA + (step & 1) * kDB + 1024 * wave;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      glds16(Bh + ob[u] + o, dst + 4096 * u);
-      glds16(Bl + ob[u] + o, dst + kWH + 4096 * u);
-    }
-  };
-
-  floatx4v acc[4][4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[p][q] = floatx4v{0.f, 0.f, 0.f, 0.f};
-
-  issue_a(0, 0);
-  issue_b(0);
-  issue_a(1, 1);
-  int slot = 0;   // A slot of step st (st % 3)
-  for (int st = 0; st < nk; ++st) {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A(st), B(st) landed (A(st + 1) may fly)
-    __builtin_amdgcn_s_barrier();                       // ... for every wave; slots of st - 1 are free
-    issue_b(st + 1);
-    issue_a(st + 2, slot == 0 ? 2 : slot - 1);
-    const char* as = lds + slot * kDA;
-    const char* bh = lds + 3 * kDA + (st & 1) * kDB;
-    const char* bl = bh + kWH;
-    bf16x8_t fa_h[4], fa_l[4], fb_h[4], fb_l[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int r = wm * 64 + 16 * p + (lane & 15), c0 = 2 * (lane >> 4), sw = drow_swz(r);
-      const float4 x0 = *reinterpret_cast<const float4*>(as + r * 128 + ((c0 ^ sw) << 4));
-      const float4 x1 = *reinterpret_cast<const float4*>(as + r * 128 + (((c0 + 1) ^ sw) << 4));
-      uint4 h, l;
-      split_bf16x2(x0.x, x0.y, h.x, l.x);
-      split_bf16x2(x0.z, x0.w, h.y, l.y);
-      split_bf16x2(x1.x, x1.y, h.z, l.z);
-      split_bf16x2(x1.z, x1.w, h.w, l.w);
-      fa_h[p] = __builtin_bit_cast(bf16x8_t, h);
-      fa_l[p] = __builtin_bit_cast(bf16x8_t, l);
-      fb_h[p] = wfrag16<BKC>(bh, wn * 64 + 16 * p, lane);
-      fb_l[p] = wfrag16<BKC>(bl, wn * 64 + 16 * p, lane);
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);
-        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);
-        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);
-      }
-    slot = slot == 2 ? 0 : slot + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail DMAs drain before the exit
-
-  // 16x16 C/D map of D = B A^T: column (lane & 15) = m, row 4 (lane >> 4) + j = n (gemm_bf16x3_kernel's)
-  float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int m = m0 + wm * 64 + 16 * p + (lane & 15);
-    if (m < M) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = n0 + wn * 64 + 16 * q + 4 * (lane >> 4);
-        if (n >= N) continue;
-        x3_epi4<EPI, DROP>(make_float4(acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]), m, n, N, C, Cs, ldc,
-                           ep);
-      }
-    }
-  }
-}
-
 // Split-K slab reduction with the GEMM's epilogue: element j of the (M, N) output (ldc == N) is the
 // fixed-order sum over s of P[s][j] (wave w sums s = w, w + 4, ...; the four wave partials are added
 // in wave order: deterministic, no atomics), then (ACC) plus the current C[j], then the epilogue of
@@ -1448,18 +1313,9 @@ static unsigned x3s_pad_lds(const P& pl) {
 #define RQ_X3S_RATE2 0.35   // 64-tile kernel, kXWG64 workgroups per CU
 #endif
 // Modelled cost (us) of the separate slab-reduction launch of a split-K call: the reduction kernel plus the
-// gap it adds between launches in a replayed step (RQ_X3_REDUCE_US overrides, for A/B runs).
-#ifndef RQ_X3_REDUCE_US
-#define RQ_X3_REDUCE_US 4.0
-#endif
-static double x3_reduce_us() {
-  static double us = -1.0;
-  if (us < 0.0) {
-    const char* e = getenv("RQ_X3_REDUCE_US");
-    us = e ? atof(e) : RQ_X3_REDUCE_US;
-  }
-  return us;
-}
+// gap it adds between launches in a replayed step (4 us measured best of 4 / 8 / 16 at both decoder
+// configs, profiles/r03/reduce_us_ab.txt).
+constexpr double kX3ReduceUs = 4.0;
 static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   const int64_t cus = resident_slots() / 2;
   const int64_t wgs = (int64_t)p.tiles * p.S;
@@ -1475,7 +1331,7 @@ static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
     const int64_t rounds = (wgs + slots - 1) / slots;
     t = (double)rounds * per_cu * tile * (double)p.chunk / (rate * 1e6);
   }
-  if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + x3_reduce_us();
+  if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + kX3ReduceUs;
   return t;
 }
 
@@ -1492,17 +1348,6 @@ static X3Plan x3_plan_s(int64_t M, int64_t N, int64_t K, int64_t S, bool wide, i
   if (p.S < 1) p.S = 1;
   p.per = wide ? 0 : (p.tiles * p.S + 7) / 8;
   return p;
-}
-
-// RQ_X3S=0 in the environment (or rq_gemm_x3s_enable(0)) keeps the 128-tile kernel for every shape,
-// 2 forces the 64-tile kernel (A/B runs, kernel tests); 1 (default) lets the time model choose.
-static int g_x3s = -1;
-static int x3s_mode() {
-  if (g_x3s < 0) {
-    const char* e = getenv("RQ_X3S");
-    g_x3s = (e && e[0] == '0') ? 0 : ((e && e[0] == '2') ? 2 : 1);
-  }
-  return g_x3s;
 }
 
 // Best split-K plan of one tile size: split K when the output tiles cannot fill the chip (weight
@@ -1531,12 +1376,12 @@ static X3Plan x3_plan_t(int64_t M, int64_t N, int64_t K, bool allow_split, int t
 
 // 128-tile kernel, or its 64-tile form where the time model prefers it (the 128-tiles of a
 // 1,280-row operand are 40 workgroups: split-K slabs and their reduction cost more than the GEMM).
-static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) {
+// flags (the call's rq_gemm_desc.flags): RQ_GEMM_ONLY_128 / RQ_GEMM_ONLY_64 pin one tile size.
+static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, int flags, bool allow_split = true) {
   const X3Plan p = x3_plan_t(M, N, K, allow_split, kXT);
-  const int mode = x3s_mode();
-  if (mode == 0) return p;
+  if (flags & RQ_GEMM_ONLY_128) return p;
   const X3Plan q = x3_plan_t(M, N, K, allow_split, 64);
-  if (mode == 2) return q;
+  if (flags & RQ_GEMM_ONLY_64) return q;
   return x3_plan_time(q, M, N, false) < x3_plan_time(p, M, N, false) ? q : p;
 }
 
@@ -1544,22 +1389,11 @@ static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, bool allow_split = true) 
 #define RQ_X3W_MIN_STEPS 8   // split-K of the wide kernel: k steps per workgroup at least
 #endif
 
-// RQ_X3W=0 in the environment (or rq_gemm_x3w_enable(0)) disables the wide kernel: A/B runs and
-// kernel-vs-kernel tests in one build.
-static int g_x3w = -1;
-static bool x3w_enabled() {
-  if (g_x3w < 0) {
-    const char* e = getenv("RQ_X3W");
-    g_x3w = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_x3w >= 1;
-}
-
 // Plan of the wide kernel, or false when the 128-tile kernel serves the shape better: k steps
 // must be whole (K % 32), padding of a partial 256-row tile must stay small (R % 256 == 0 or
 // R >= 2048), and the launch must cover at least a quarter of the CUs (split-K when allowed).
 static bool x3w_plan(int64_t M, int64_t N, int64_t K, bool allow_split, X3Plan* p) {
-  if (!x3w_enabled() || K % 32 != 0 || K <= 0) return false;
+  if (K % 32 != 0 || K <= 0) return false;
   auto fits = [](int64_t R) { return R % kWT2 == 0 || R >= 2048; };
   if (!fits(M) || !fits(N)) return false;
   const int cus = resident_slots() / 2;
@@ -1578,56 +1412,16 @@ static bool x3w_plan(int64_t M, int64_t N, int64_t K, bool allow_split, X3Plan* 
 }
 
 // The wide kernel runs when both operands are split planes, the (layout, epilogue) pair is
-// instantiated (every layout for the plain store; the fused MLP chain's layouts otherwise) and the
-// shape plans (x3w_plan).
+// instantiated (every layout for the plain store; the fused MLP chain's layouts otherwise), the shape
+// plans (x3w_plan) and the time model prefers it — or wherever it can run under RQ_GEMM_FORCE_WIDE;
+// never under RQ_GEMM_NO_WIDE / RQ_GEMM_ONLY_128 / RQ_GEMM_ONLY_64.
 static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool a_kc, bool b_kc, int epilogue,
-                       X3Plan* p) {
+                       int flags, X3Plan* p) {
+  if (flags & (RQ_GEMM_NO_WIDE | RQ_GEMM_ONLY_128 | RQ_GEMM_ONLY_64)) return false;
   const bool combo = epilogue == kEpiStore || (epilogue == kEpiSiluFwd && a_kc && b_kc) ||
                      (epilogue == kEpiSiluBwd && a_kc && !b_kc) || (epilogue == kEpiAdd && a_kc && b_kc);
   if (!(asp && bsp && combo && x3w_plan(M, N, K, true, p))) return false;
-  return g_x3w == 2 || x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K), M, N, false);   // 2: forced
-}
-
-// RQ_X3_PAIR=0 in the environment (or rq_gemm_pair_enable(0)): rq_gemm_bf16x3_pair runs two launches (A/B)
-static int g_x3_pair = -1;
-static bool x3_pair_enabled() {
-  if (g_x3_pair < 0) {
-    const char* e = getenv("RQ_X3_PAIR");
-    g_x3_pair = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_x3_pair != 0;
-}
-
-// RQ_X3_KFULL=0 (or rq_gemm_kfull_enable(0)): every 128-/64-tile launch stages through the masked path (A/B)
-static int g_x3_kfull = -1;
-static bool x3_kfull_enabled() {
-  if (g_x3_kfull < 0) {
-    const char* e = getenv("RQ_X3_KFULL");
-    g_x3_kfull = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_x3_kfull != 0;
-}
-
-// RQ_X3D=0 in the environment (or rq_gemm_x3d_enable(0)) keeps the register-staged 128-tile kernel for
-// fp32 k-contiguous A x split B (A/B switch, kernel-vs-kernel tests).
-static int g_x3d = -1;
-static bool x3d_enabled() {
-  if (g_x3d < 0) {
-    const char* e = getenv("RQ_X3D");
-    g_x3d = (e && e[0] == '1') ? 1 : ((e && e[0] == '2') ? 2 : 0);
-  }
-  return g_x3d != 0;
-}
-// The LDS-DMA 128-tile form can run where the 128-tile kernel would, for an fp32 k-contiguous A and a split
-// B, whole 32-deep k steps, and every instantiated epilogue. Measured on MI355X (profiles/r03/x3d_ab.txt):
-// alone (tools/lib_bf16_probe.py: the same launch repeated, A warm in the Infinity Cache) it wins with an
-// n-contiguous B (data gradients dx = g W: 11,264 x 512 x 1,536 87-89 -> 78-81 us, x 4,096 190 -> 161-169
-// us) and loses with a k-contiguous B (11,264 x 1,536 x 512 79 -> 81-84 us); inside the decoder step
-// (cold A, two k steps of DMA lookahead) even the former loses (Amazon step 6.39-6.41 -> 6.46-6.47 ms), so
-// it is OFF by default: RQ_X3D=1 takes the n-contiguous-B shapes, 2 both layouts (A/B, kernel tests).
-static bool x3d_choose(const X3Plan& pl, int64_t N, int64_t K, bool asp, bool bsp, bool a_kc, bool b_kc) {
-  return x3d_enabled() && (!b_kc || g_x3d == 2) && pl.ts == kXT && !asp && bsp && a_kc && K % 32 == 0 &&
-         pl.chunk % 32 == 0 && N >= 8;
+  return (flags & RQ_GEMM_FORCE_WIDE) || x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K, flags), M, N, false);
 }
 
 }  // namespace rqhip
@@ -1675,54 +1469,50 @@ int rq_linear_wgrad(const float* g, int64_t ldg, const float* x, int64_t ldx, in
 }
 
 
-// Slab bytes of a call: split-K slabs (S > 1), or one slab for an accumulating call (C += A B^T runs
-// through the slab reduction even unsplit).
-static size_t x3_workspace_bytes(int64_t M, int64_t N, int64_t K, bool accumulate) {
+// Slab bytes of a call: split-K slabs (S > 1) of whichever kernel may run for the shape (the largest of
+// the 128-tile, 64-tile and wide plans, so one workspace serves every rq_gemm_desc.flags policy). An
+// unsplit accumulating call adds in the GEMM's own epilogue: no slab.
+static size_t x3_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  // the larger of the two kernels' split-K slabs (which one runs depends on the operand formats)
   const X3Plan p = x3_plan_t(M, N, K, true, kXT), q = x3_plan_t(M, N, K, true, 64);
   X3Plan pw;
-  int S = p.S > q.S ? p.S : q.S;   // either tile size may run (rq_gemm_x3s_enable can switch between calls)
+  int S = p.S > q.S ? p.S : q.S;
   if (x3w_plan(M, N, K, true, &pw) && pw.S > S) S = pw.S;
-  (void)accumulate;   // an unsplit accumulating call adds in the GEMM's own epilogue: no slab
   return S > 1 ? (size_t)S * (size_t)(M * N) * sizeof(float) : 0;
 }
 
-size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) { return x3_workspace_bytes(M, N, K, false); }
-
-size_t rq_gemm_bf16x3_workspace2(int64_t M, int64_t N, int64_t K, int accumulate) {
-  return x3_workspace_bytes(M, N, K, accumulate != 0);
-}
+size_t rq_gemm_bf16x3_workspace(int64_t M, int64_t N, int64_t K) { return x3_workspace_bytes(M, N, K); }
 
 }  // extern "C"
 
 namespace rqhip {
 
 // One validated and planned rq_gemm_bf16x3 call (x3_prepare), its kernel launch (x3_launch) and its slab
-// reduction or deferral (x3_post): rq_gemm_bf16x3_ex3 runs the three in a row, rq_gemm_bf16x3_pair prepares
+// reduction or deferral (x3_post): rq_gemm_bf16x3_run runs the three in a row, rq_gemm_bf16x3_pair prepares
 // two calls and, where an instantiation exists, launches both problems in one gemm_x3_pair_kernel.
 struct X3Call {
   X3Plan pl;
-  bool wide, x3d, slab, asp, bsp, trivial;
-  int a_kc, b_kc, epilogue, epi_k, code, accumulate, defer;
+  bool wide, slab, asp, bsp, trivial;
+  int a_kc, b_kc, epilogue, epi_k, code, accumulate, defer, flags;
   int64_t M, N, K;
   float* C;
   float* out;
   X3Args xa;
 };
 
-static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                      int accumulate, int defer, void* workspace, size_t ws_bytes, hipStream_t s, X3Call* c,
-                      bool unsplit = false) {
+// Validate and plan one call. dry = planning only (rq_gemm_bf16x3_plan): no stream work, no workspace check.
+static int x3_prepare(const rq_gemm_desc& d, hipStream_t s, X3Call* c, bool dry = false) {
+  const void *A = d.A, *A_lo = d.A_lo, *B = d.B, *B_lo = d.B_lo;
+  const int64_t lda = d.lda, ldb = d.ldb, M = d.M, N = d.N, K = d.K, ldc = d.ldc, ldh = d.ldh;
+  const int a_kcontig = d.a_kcontig, b_kcontig = d.b_kcontig, epilogue = d.epilogue, accumulate = d.accumulate;
+  float* C = d.C;
   const bool asp = A_lo != nullptr, bsp = B_lo != nullptr;
-  RQ_CHECK_ARG(((A && B) || K == 0) && M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 &&
-                   epilogue <= 3,
+  RQ_CHECK_ARG(dry || (((A && B) || K == 0) && M > 0 && N > 0), "rq_gemm_bf16x3: bad arguments");
+  RQ_CHECK_ARG(K >= 0 && M > 0 && N > 0 && M < (1 << 30) && N < (1 << 30) && epilogue >= 0 && epilogue <= 3,
                "rq_gemm_bf16x3: bad arguments");
   const bool needs_h = epilogue == kEpiSiluFwd || epilogue == kEpiSiluBwd;
-  RQ_CHECK_ARG((epilogue == kEpiSiluBwd || C) && (!needs_h || (H_hi && H_lo && ldh >= N)) &&
-                   ((epilogue != kEpiSiluBwd && epilogue != kEpiAdd) || Z),
+  RQ_CHECK_ARG(dry || ((epilogue == kEpiSiluBwd || C) && (!needs_h || (d.H_hi && d.H_lo && ldh >= N)) &&
+                       ((epilogue != kEpiSiluBwd && epilogue != kEpiAdd) || d.Z)),
                "rq_gemm_bf16x3: epilogue %d needs %s", epilogue,
                epilogue == kEpiSiluBwd ? "Z and H planes"
                                        : (epilogue == kEpiSiluFwd ? "C and H planes" : (epilogue ? "C and Z" : "C")));
@@ -1734,39 +1524,39 @@ static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kconti
                "(fp32) / 8 (split)", 4);
   RQ_CHECK_ARG(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && (epilogue == kEpiSiluBwd || ldc >= N),
                "rq_gemm_bf16x3: leading dimension too small");
-  RQ_CHECK_ARG(N % 4 == 0 && ldc % 4 == 0 && ldh % 4 == 0 && ((uintptr_t)C | (uintptr_t)Z) % 16 == 0 &&
-                   ((uintptr_t)H_hi | (uintptr_t)H_lo) % 8 == 0,
+  RQ_CHECK_ARG(N % 4 == 0 && ldc % 4 == 0 && ldh % 4 == 0 && ((uintptr_t)C | (uintptr_t)d.Z) % 16 == 0 &&
+                   ((uintptr_t)d.H_hi | (uintptr_t)d.H_lo) % 8 == 0,
                "rq_gemm_bf16x3: N and the output leading dims must be multiples of 4 (vector stores), outputs aligned");
   RQ_CHECK_ARG(((uintptr_t)A | (uintptr_t)A_lo | (uintptr_t)B | (uintptr_t)B_lo) % 16 == 0,
                "rq_gemm_bf16x3: operand pointers must be 16-byte aligned");
-  X3Epilogue ep{Z, H_hi, H_lo, ldh, 0u, 1.f, seed, 0};
-  dropout_params(p, &ep.thr, &ep.scale);
+  X3Epilogue ep{d.Z, d.H_hi, d.H_lo, ldh, 0u, 1.f, d.seed, 0};
+  dropout_params(d.p, &ep.thr, &ep.scale);
   RQ_CHECK_ARG(!accumulate || epilogue == kEpiStore, "rq_gemm_bf16x3: accumulate needs the plain epilogue");
   c->trivial = K == 0;
   if (K == 0) {
     RQ_CHECK_ARG(epilogue == kEpiStore, "rq_gemm_bf16x3: K == 0 needs the plain epilogue");
-    if (!accumulate) RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
+    if (!accumulate && !dry)
+      RQ_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M, s));
     return 0;
   }
-  X3Plan pl = x3_plan(M, N, K);
+  const int flags = d.flags;
+  X3Plan pl = x3_plan(M, N, K, flags);
   X3Plan pw;
-  const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, &pw);
+  const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, flags, &pw);
   if (wide) pl = pw;
-  else if (unsplit && pl.S > 1) pl = x3_plan_s(M, N, K, 1, false, pl.ts);   // a paired launch's partner fills the chip
   // slab path: split-K partials go to the workspace with the plain store, and x3_reduce_kernel applies
   // the real epilogue (and the accumulation); an unsplit accumulating call adds in the GEMM's epilogue
   const bool slab = pl.S > 1;
   ep.acc = accumulate && !slab;
   float* out = C;
-  if (slab) {
+  if (slab && !dry) {
     const size_t need = (size_t)pl.S * (size_t)(M * N) * sizeof(float);
-    RQ_CHECK_ARG(workspace != nullptr && ws_bytes >= need && ldc == N,
-                 "rq_gemm_bf16x3: split-K / accumulate needs ldc == N and workspace %zu >= %zu bytes", ws_bytes, need);
-    out = static_cast<float*>(workspace);
+    RQ_CHECK_ARG(d.workspace != nullptr && d.ws_bytes >= need && ldc == N,
+                 "rq_gemm_bf16x3: split-K / accumulate needs ldc == N and workspace %zu >= %zu bytes", d.ws_bytes, need);
+    out = static_cast<float*>(d.workspace);
   }
   c->pl = pl;
   c->wide = wide;
-  c->x3d = !wide && x3d_choose(pl, N, K, asp, bsp, a_kcontig, b_kcontig);
   c->slab = slab;
   c->asp = asp;
   c->bsp = bsp;
@@ -1776,15 +1566,18 @@ static int x3_prepare(const void* A, const void* A_lo, int64_t lda, int a_kconti
   c->epi_k = slab ? (int)kEpiStore : epilogue;   // the epilogue the GEMM kernel itself runs
   c->code = (a_kcontig ? 16 : 0) | (asp ? 8 : 0) | (b_kcontig ? 4 : 0) | (bsp ? 2 : 0);
   c->accumulate = accumulate;
-  c->defer = defer;
+  c->defer = d.defer;
+  c->flags = flags;
   c->M = M;
   c->N = N;
   c->K = K;
   c->C = C;
   c->out = out;
   const int64_t ldo = pl.S > 1 ? N : ldc;
+  // whole 32-deep stages: unmasked staging (bitwise the masked path; RQ_GEMM_MASKED keeps the masked one)
+  const int kfull = !(flags & RQ_GEMM_MASKED) && K % kXK == 0 && pl.chunk % kXK == 0;
   c->xa = X3Args{A, A_lo, lda, B, B_lo, ldb, (int)M, (int)N, K, pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep,
-                 (int)(x3_kfull_enabled() && K % kXK == 0 && pl.chunk % kXK == 0)};
+                 kfull};
   return 0;
 }
 
@@ -1812,23 +1605,7 @@ static int x3_launch(const X3Call& c, hipStream_t s) {
       RQ_X3D(AK, AS, BK, BS, EP, false);                                                                             \
   } while (0)
   bool launched = true;
-  if (c.x3d) {
-    const float* af = static_cast<const float*>(A);
-    const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
-#define RQ_X3DL(BK, EP, DR)                                                                                       \
-  hipLaunchKernelGGL((gemm_x3d_kernel<BK, EP, DR>), grid, block, 0, s, af, lda, bh, bl, ldb, (int)M, (int)N, K,   \
-                     pl.tiles_n, pl.tiles, pl.S, pl.chunk, pl.per, out, ldo, ep)
-#define RQ_X3DB(EP, DR) do { if (b_kcontig) RQ_X3DL(true, EP, DR); else RQ_X3DL(false, EP, DR); } while (0)
-    const bool drop = ep.thr != 0;
-    switch (epi_k) {
-      case kEpiStore: RQ_X3DB(kEpiStore, false); break;
-      case kEpiSiluFwd: if (drop) RQ_X3DB(kEpiSiluFwd, true); else RQ_X3DB(kEpiSiluFwd, false); break;
-      case kEpiSiluBwd: if (drop) RQ_X3DB(kEpiSiluBwd, true); else RQ_X3DB(kEpiSiluBwd, false); break;
-      default: if (drop) RQ_X3DB(kEpiAdd, true); else RQ_X3DB(kEpiAdd, false); break;
-    }
-#undef RQ_X3DB
-#undef RQ_X3DL
-  } else if (c.wide) {
+  if (c.wide) {
     const uint16_t *ah = static_cast<const uint16_t*>(A), *al = static_cast<const uint16_t*>(A_lo);
     const uint16_t *bh = static_cast<const uint16_t*>(B), *bl = static_cast<const uint16_t*>(B_lo);
     const dim3 wgrid((unsigned)(pl.tiles * pl.S)), wblock(512);
@@ -1962,7 +1739,7 @@ static int x3_pair_k1(const X3Call& c1) {
 // launches; two launches that each fill the chip already — the RQ-VAE's 65,536-row 64-tile layers — gain
 // nothing and measured 4 us slower paired).
 static bool x3_pairable(const X3Call& c1, const X3Call& c2) {
-  if (c1.wide || c2.wide || c1.x3d || c2.x3d || c1.pl.ts != c2.pl.ts) return false;
+  if (c1.wide || c2.wide || c1.pl.ts != c2.pl.ts) return false;
   if (c2.epi_k != kEpiStore || c2.code != (c2.code & (8 | 2))) return false;   // c2: m-contig A, n-contig B
   const int k1 = x3_pair_k1(c1);
   if (k1 != (16 | 2) && k1 != (16 | 8 | 2) && k1 != (16 | 2 | 32) && k1 != (16 | 2 | 64)) return false;
@@ -1987,38 +1764,18 @@ static bool x3_pair_launch(const X3Call& c1, const X3Call& c2, hipStream_t s) {
 
 extern "C" {
 
-int rq_gemm_bf16x3_ex3(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                       int accumulate, int defer, int* splits, void* workspace, size_t ws_bytes, void* stream) {
+static_assert(sizeof(rq_gemm_desc) == 192, "rq_gemm_desc layout (the ctypes mirror in rqvae_hip/ops.py)");
+
+int rq_gemm_bf16x3_run(const rq_gemm_desc* d, int* splits, void* stream) {
+  RQ_CHECK_ARG(d != nullptr, "rq_gemm_bf16x3_run: null descriptor");
   if (splits) *splits = 0;
   hipStream_t s = (hipStream_t)stream;
   X3Call c;
-  const int rc = x3_prepare(A, A_lo, lda, a_kcontig, B, B_lo, ldb, b_kcontig, M, N, K, C, ldc, epilogue, Z, H_hi, H_lo,
-                            ldh, p, seed, accumulate, defer, workspace, ws_bytes, s, &c);
+  const int rc = x3_prepare(*d, s, &c);
   if (rc || c.trivial) return rc;
   const int rl = x3_launch(c, s);
   if (rl) return rl;
   return x3_post(c, splits, s);
-}
-
-static_assert(sizeof(rq_gemm_desc) == 184, "rq_gemm_desc layout (the ctypes mirror in rqvae_hip/ops.py)");
-
-static int x3_prepare_desc(const rq_gemm_desc& d, hipStream_t s, X3Call* c, bool unsplit = false) {
-  return x3_prepare(d.A, d.A_lo, d.lda, d.a_kcontig, d.B, d.B_lo, d.ldb, d.b_kcontig, d.M, d.N, d.K, d.C, d.ldc,
-                    d.epilogue, d.Z, d.H_hi, d.H_lo, d.ldh, d.p, d.seed, d.accumulate, d.defer, d.workspace, d.ws_bytes, s,
-                    c, unsplit);
-}
-
-#ifndef RQ_X3_PAIR_UNSPLIT
-#define RQ_X3_PAIR_UNSPLIT 0   // 1: a paired data gradient runs unsplit (no slab reduction launch; measured slower: its chain dominates)
-#endif
-static bool x3_pair_unsplit() {
-  static const bool on = [] {
-    const char* e = getenv("RQ_X3_PAIR_UNSPLIT");
-    return e ? e[0] != '0' : RQ_X3_PAIR_UNSPLIT != 0;
-  }();
-  return on;
 }
 
 int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
@@ -2027,19 +1784,11 @@ int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   X3Call c[2];
   for (int i = 0; i < 2; ++i) {
-    const int rc = x3_prepare_desc(d[i], s, &c[i]);
+    const int rc = x3_prepare(d[i], s, &c[i]);
     if (rc) return rc;
   }
-  // a data gradient split only to fill the chip alone (the decoder's 40..1,280 future-token rows) runs
-  // unsplit next to its weight gradient: no slab, no reduction launch (re-planned when the pair still forms)
-  if (x3_pair_enabled() && x3_pair_unsplit() && !c[0].trivial && !c[1].trivial && c[0].slab && !c[0].wide &&
-      !c[0].x3d) {
-    X3Call u;
-    const int rc = x3_prepare_desc(d[0], s, &u, true);
-    if (rc) return rc;
-    if (x3_pairable(u, c[1])) c[0] = u;
-  }
-  if (c[0].trivial || c[1].trivial || !x3_pair_enabled() || !x3_pair_launch(c[0], c[1], s)) {
+  const bool no_pair = ((d[0].flags | d[1].flags) & RQ_GEMM_NO_PAIR) != 0;
+  if (c[0].trivial || c[1].trivial || no_pair || !x3_pair_launch(c[0], c[1], s)) {
     for (int i = 0; i < 2; ++i) {
       if (c[i].trivial) continue;
       const int rl = x3_launch(c[i], s);
@@ -2056,26 +1805,23 @@ int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
   return 0;
 }
 
-int rq_gemm_bf16x3_pair_choice(const rq_gemm_desc* d) {
-  if (!d) return -1;
-  X3Call c[2];
-  for (int i = 0; i < 2; ++i) {
-    const rq_gemm_desc& e = d[i];
-    if (e.K <= 0 || e.M <= 0 || e.N <= 0) return 0;
-    c[i].pl = x3_plan(e.M, e.N, e.K);
-    X3Plan pw;
-    c[i].wide = x3w_choose(e.M, e.N, e.K, e.A_lo != nullptr, e.B_lo != nullptr, e.a_kcontig, e.b_kcontig, e.epilogue, &pw);
-    c[i].x3d = !c[i].wide && x3d_choose(c[i].pl, e.N, e.K, e.A_lo != nullptr, e.B_lo != nullptr, e.a_kcontig, e.b_kcontig);
-  }
-  return x3_pair_enabled() && !c[0].wide && !c[1].wide && !c[0].x3d && !c[1].x3d && c[0].pl.ts == c[1].pl.ts ? 1 : 0;
+int rq_gemm_bf16x3_plan(const rq_gemm_desc* d, int* splits) {
+  if (splits) *splits = 0;
+  if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0) return -1;
+  X3Call c;
+  if (x3_prepare(*d, nullptr, &c, true) != 0) return -1;
+  if (splits) *splits = c.pl.S;
+  return c.wide ? 1 : (c.pl.ts == 64 ? 2 : 0);
 }
 
-int rq_gemm_bf16x3_ex2(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                       int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                       const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                       int accumulate, void* workspace, size_t ws_bytes, void* stream) {
-  return rq_gemm_bf16x3_ex3(A, A_lo, lda, a_kcontig, B, B_lo, ldb, b_kcontig, M, N, K, C, ldc, epilogue, Z, H_hi, H_lo,
-                            ldh, p, seed, accumulate, 0, nullptr, workspace, ws_bytes, stream);
+int rq_gemm_bf16x3_pair_plan(const rq_gemm_desc* d) {
+  if (!d || ((d[0].flags | d[1].flags) & RQ_GEMM_NO_PAIR)) return 0;
+  X3Call c[2];
+  for (int i = 0; i < 2; ++i) {
+    if (d[i].M <= 0 || d[i].N <= 0 || d[i].K <= 0) return 0;
+    if (x3_prepare(d[i], nullptr, &c[i], true) != 0) return 0;
+  }
+  return x3_pairable(c[0], c[1]) ? 1 : 0;
 }
 
 // Deferred partial reductions, many in one launch: out_i[j] (+)= sum_s P_i[s n_i + j] for every entry i,
@@ -2211,58 +1957,24 @@ int rq_reduce_partials(int count, const float* const* P, float* const* out, cons
   return 0;
 }
 
-int rq_gemm_bf16x3_ex(const void* A, const void* A_lo, int64_t lda, int a_kcontig, const void* B, const void* B_lo,
-                      int64_t ldb, int b_kcontig, int64_t M, int64_t N, int64_t K, float* C, int64_t ldc, int epilogue,
-                      const float* Z, uint16_t* H_hi, uint16_t* H_lo, int64_t ldh, float p, uint64_t seed,
-                      void* workspace, size_t ws_bytes, void* stream) {
-  return rq_gemm_bf16x3_ex2(A, A_lo, lda, a_kcontig, B, B_lo, ldb, b_kcontig, M, N, K, C, ldc, epilogue, Z, H_hi, H_lo,
-                            ldh, p, seed, 0, workspace, ws_bytes, stream);
-}
-
-int rq_gemm_x3s_enable(int mode) {
-  const int prev = x3s_mode();
-  g_x3s = mode == 2 ? 2 : (mode ? 1 : 0);
-  return prev;
-}
-
-int rq_gemm_x3w_enable(int enable) {
-  const int prev = x3w_enabled() ? g_x3w : 0;
-  g_x3w = enable == 2 ? 2 : (enable ? 1 : 0);
-  return prev;
-}
-
-int rq_gemm_bf16x3_choice(int64_t M, int64_t N, int64_t K, int a_split, int b_split, int a_kcontig, int b_kcontig,
-                          int epilogue, int* splits) {
-  if (M <= 0 || N <= 0 || K <= 0) return -1;
-  X3Plan pw;
-  const bool wide = x3w_choose(M, N, K, a_split, b_split, a_kcontig, b_kcontig, epilogue, &pw);
-  const X3Plan pl = x3_plan(M, N, K);
-  if (splits) *splits = wide ? pw.S : pl.S;
-  return wide ? 1 : (pl.ts == 64 ? 2 : (x3d_choose(pl, N, K, a_split, b_split, a_kcontig, b_kcontig) ? 3 : 0));
-}
-
-int rq_gemm_pair_enable(int enable) {
-  const int prev = x3_pair_enabled() ? 1 : 0;
-  g_x3_pair = enable ? 1 : 0;
-  return prev;
-}
-
-int rq_gemm_kfull_enable(int enable) {
-  const int prev = x3_kfull_enabled() ? 1 : 0;
-  g_x3_kfull = enable ? 1 : 0;
-  return prev;
-}
-
-int rq_gemm_x3d_enable(int enable) {
-  const int prev = x3d_enabled() ? g_x3d : 0;
-  g_x3d = enable == 2 ? 2 : (enable ? 1 : 0);
-  return prev;
-}
-
 int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, int64_t M,
                    int64_t N, int64_t K, float* C, int64_t ldc, void* workspace, size_t ws_bytes, void* stream) {
-  return rq_gemm_bf16x3_ex(A, nullptr, lda, a_kcontig, B, nullptr, ldb, b_kcontig, M, N, K, C, ldc, kEpiStore, nullptr,
-                           nullptr, nullptr, 0, 0.f, 0, workspace, ws_bytes, stream);
+  rq_gemm_desc d{};
+  d.A = A;
+  d.lda = lda;
+  d.a_kcontig = a_kcontig;
+  d.B = B;
+  d.ldb = ldb;
+  d.b_kcontig = b_kcontig;
+  d.M = M;
+  d.N = N;
+  d.K = K;
+  d.C = C;
+  d.ldc = ldc;
+  d.epilogue = kEpiStore;
+  d.workspace = workspace;
+  d.ws_bytes = ws_bytes;
+  return rq_gemm_bf16x3_run(&d, nullptr, stream);
 }
 
 int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, uint16_t* const* hi,
@@ -2310,6 +2022,7 @@ int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void*
   return 0;
 }
 
-int rq_seed_epoch_addr_linear(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }
 
 }  // extern "C"
+
+int rqhip::seed_epoch_addr_linear(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }

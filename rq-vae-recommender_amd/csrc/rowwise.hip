@@ -122,13 +122,8 @@ __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __re
   }
 }
 
-// Rows per wave of the two kernels above (1 = one row per wave; 2 / 4 keep more bytes in flight per
-// wave with fewer workgroups). rq_l2norm_recon_rows_per_wave() sets it (A/B); RQ_L2R_RPW at load.
-static int g_l2r_rpw = [] {
-  const char* e = getenv("RQ_L2R_RPW");
-  const int v = e ? atoi(e) : 1;
-  return (v == 2 || v == 4) ? v : 1;
-}();
+// The launches run one row per wave (the kernels' RPW = 1): 2 or 4 rows per wave were no faster at
+// 65,536 x 768 (profiles/r02/l2r_rpw_ab.txt).
 
 // ---------------------------------------------------------------------------------------
 // RMSNorm (modules/normalize.py:22-32): t = x * rsqrt(mean(x^2) + eps), y = t * w.
@@ -645,12 +640,6 @@ int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate,
   return 0;
 }
 
-int rq_l2norm_recon_rows_per_wave(int rpw) {
-  const int prev = g_l2r_rpw;
-  if (rpw == 1 || rpw == 2 || rpw == 4) g_l2r_rpw = rpw;
-  return prev;
-}
-
 int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
                         void* stream) {
   RQ_CHECK_ARG(pre && x && recon && norms, "rq_l2norm_recon_fwd: null pointer");
@@ -658,16 +647,13 @@ int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, 
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int vpl = (int)((C + 255) / 256);
-  const int rpw = vpl <= 4 ? g_l2r_rpw : 1;   // register budget: RPW * VPL * 8 floats of loads per lane
-  const dim3 g((unsigned)((B + 4 * rpw - 1) / (4 * rpw)));
+  const dim3 g((unsigned)((B + 3) / 4));
 #define L2R_LAUNCH(V, R) hipLaunchKernelGGL((l2norm_recon_fwd_kernel<V, R>), g, dim3(256), 0, s, pre, x, B, (int)C, recon, norms)
-#define L2R_CASE(V) case V: if (rpw == 4) L2R_LAUNCH(V, 4); else if (rpw == 2) L2R_LAUNCH(V, 2); else L2R_LAUNCH(V, 1); break;
 #define L2R_CASE1(V) case V: L2R_LAUNCH(V, 1); break;
   switch (vpl) {
-    L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
+    L2R_CASE1(1) L2R_CASE1(2) L2R_CASE1(3) L2R_CASE1(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
     L2R_CASE1(9) L2R_CASE1(10) L2R_CASE1(11) L2R_CASE1(12) L2R_CASE1(13) L2R_CASE1(14) L2R_CASE1(15) L2R_CASE1(16)
   }
-#undef L2R_CASE
 #undef L2R_CASE1
 #undef L2R_LAUNCH
   RQ_LAUNCH_CHECK("rq_l2norm_recon_fwd");
@@ -680,22 +666,17 @@ static int l2norm_recon_bwd_launch(const float* pre, const float* x, const float
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int vpl = (int)((C + 255) / 256);
-  const int rpw = vpl <= 4 ? g_l2r_rpw : 1;
-  const dim3 g((unsigned)((B + 4 * rpw - 1) / (4 * rpw)));
+  const dim3 g((unsigned)((B + 3) / 4));
   const bool sp = g_hi != nullptr;
 #define L2R_LAUNCH(V, SP, R)                                                                                     \
   hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, SP, R>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, \
                      g_pre, g_hi, g_lo)
-#define L2R_R(V, SP) if (rpw == 4) L2R_LAUNCH(V, SP, 4); else if (rpw == 2) L2R_LAUNCH(V, SP, 2); else L2R_LAUNCH(V, SP, 1);
-#define L2R_CASE(V) case V: if (sp) { L2R_R(V, true) } else { L2R_R(V, false) } break;
 #define L2R_CASE1(V) case V: if (sp) L2R_LAUNCH(V, true, 1); else L2R_LAUNCH(V, false, 1); break;
   switch (vpl) {
-    L2R_CASE(1) L2R_CASE(2) L2R_CASE(3) L2R_CASE(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
+    L2R_CASE1(1) L2R_CASE1(2) L2R_CASE1(3) L2R_CASE1(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
     L2R_CASE1(9) L2R_CASE1(10) L2R_CASE1(11) L2R_CASE1(12) L2R_CASE1(13) L2R_CASE1(14) L2R_CASE1(15) L2R_CASE1(16)
   }
-#undef L2R_CASE
 #undef L2R_CASE1
-#undef L2R_R
 #undef L2R_LAUNCH
   RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd");
   return 0;
@@ -776,9 +757,9 @@ int rq_rmsnorm_fwd(const float* x, const float* w, int64_t B, int64_t D, float e
   return rq_rmsnorm_dropout_fwd(x, w, B, D, eps, 0.f, 0, y, rstd, stream);
 }
 
-int rq_rmsnorm_dropout_bwd3(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
-                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
-                            int defer, int* parts, void* workspace, size_t ws_bytes, void* stream) {
+int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
+                           int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
+                           int defer, int* parts, void* workspace, size_t ws_bytes, void* stream) {
   if (parts) *parts = 0;
   RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm_bwd: need D %% 4 == 0, D <= 4096");
   RQ_CHECK_ARG(gw && (B == 0 || (x && w && rstd && gy && gx)), "rq_rmsnorm_bwd: null pointer");
@@ -808,25 +789,12 @@ int rq_rmsnorm_dropout_bwd3(const float* x, const float* w, const float* rstd, c
   return 0;
 }
 
-int rq_rmsnorm_dropout_bwd2(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
-                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
-                            void* workspace, size_t ws_bytes, void* stream) {
-  return rq_rmsnorm_dropout_bwd3(x, w, rstd, gy, gres, B, D, p, seed, gx, gw, accumulate_gw, 0, nullptr, workspace,
-                                 ws_bytes, stream);
-}
-
-int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
-                           float p, uint64_t seed, float* gx, float* gw, void* workspace, size_t ws_bytes,
-                           void* stream) {
-  return rq_rmsnorm_dropout_bwd2(x, w, rstd, gy, nullptr, B, D, p, seed, gx, gw, 0, workspace, ws_bytes, stream);
-}
-
 int rq_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* gy, int64_t B, int64_t D,
                    float* gx, float* gw, void* workspace, size_t ws_bytes, void* stream) {
-  return rq_rmsnorm_dropout_bwd(x, w, rstd, gy, B, D, 0.f, 0, gx, gw, workspace, ws_bytes, stream);
+  return rq_rmsnorm_dropout_bwd(x, w, rstd, gy, nullptr, B, D, 0.f, 0, gx, gw, 0, 0, nullptr, workspace, ws_bytes,
+                                stream);
 }
 
-int rq_seed_epoch_addr_rowwise(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }
 
 
 int rq_gumbel_softmax_fwd(const float* x, int64_t B, int64_t D, const float* codebook, int64_t K, const float* noise,
@@ -858,3 +826,5 @@ int rq_gumbel_softmax_bwd(const float* x, const float* codebook, const float* we
 }
 
 }  // extern "C"
+
+int rqhip::seed_epoch_addr_rowwise(void** out) { return (int)hipGetSymbolAddress(out, HIP_SYMBOL(rqhip::rq_seed_epoch)); }

@@ -1479,33 +1479,14 @@ int rq_codebook_sqnorm(const float* rows, int64_t n, int64_t D, float* out, void
   return 0;
 }
 
-int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
-                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
-                         float* qloss, float* emb_sum, int impl, void* stream);
-
-int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
-                    int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
-                    float* emb_sum, void* stream) {
-  return rq_quantize_fwd_impl(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss, emb_sum,
-                              0, stream);
-}
-
-int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream);   // rowwise.hip
 static int quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
                         float* qloss, float* emb_sum, int impl, float* emb_norms, void* stream);
 
-int rq_quantize_fwd_impl(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm,
-                         int64_t K, int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals,
-                         float* qloss, float* emb_sum, int impl, void* stream) {
+int rq_quantize_fwd(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
+                    int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
+                    float* emb_sum, float* emb_norms, int impl, void* stream) {
   return quantize_fwd(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss, emb_sum, impl,
-                      nullptr, stream);
-}
-
-int rq_quantize_fwd2(const float* x, int64_t B, int64_t D, const float* codebooks, const float* cb_sqnorm, int64_t K,
-                     int64_t L, int mode, float beta, int64_t* ids, float* emb_out, float* residuals, float* qloss,
-                     float* emb_sum, float* emb_norms, void* stream) {
-  return quantize_fwd(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss, emb_sum, 0,
                       emb_norms, stream);
 }
 
@@ -1525,11 +1506,11 @@ static int quantize_fwd(const float* x, int64_t B, int64_t D, const float* codeb
   dim3 g((unsigned)((B + kTB - 1) / kTB));
   const int b = (int)B, d = (int)D, k = (int)K, l = (int)L;
   RQ_CHECK_ARG(impl >= 0 && impl <= 4,
-               "rq_quantize_fwd_impl: impl must be 0 (auto), 1 (tiled), 2 (register), 3 (split) or 4 (register 16x16)");
+               "rq_quantize_fwd: impl must be 0 (auto), 1 (tiled), 2 (register), 3 (split) or 4 (register 16x16)");
   const bool split_ok = D >= 128 && 2 * ((K + kSN - 1) / kSN) + 1 <= D;
   const bool r16_ok = D == 64 && K <= 288;   // two 65 * K * 4-byte images per CU
   if (impl == 0) impl = (r16_ok && B >= 32768) ? 4 : D <= 64 ? 2 : (split_ok ? 3 : 1);
-  RQ_CHECK_ARG(impl != 4 || r16_ok, "rq_quantize_fwd_impl: 16x16 register kernel needs D == 64 and K <= 288");
+  RQ_CHECK_ARG(impl != 4 || r16_ok, "rq_quantize_fwd: 16x16 register kernel needs D == 64 and K <= 288");
   if (emb_norms != nullptr && impl != 4) {   // only the 16x16 kernel fuses the norms: one extra row pass otherwise
     const int rc = quantize_fwd(x, B, D, codebooks, cb_sqnorm, K, L, mode, beta, ids, emb_out, residuals, qloss,
                                 emb_sum, impl, nullptr, stream);

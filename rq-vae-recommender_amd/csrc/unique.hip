@@ -112,14 +112,14 @@ static int64_t table_slots(int64_t B) {
   return t < 64 ? 64 : t;
 }
 
-size_t rq_unique_workspace(int64_t B) { return (size_t)table_slots(B) * sizeof(unsigned long long); }
+static size_t table_bytes(int64_t B) { return (size_t)table_slots(B) * sizeof(unsigned long long); }
 
 // workspace of rq_unique_count for these K, L: the byte map where K^L <= 2^24, else the hash table
-size_t rq_unique_workspace2(int64_t B, int64_t L, int64_t K) {
+size_t rq_unique_workspace(int64_t B, int64_t L, int64_t K) {
   double keys = 1;
   for (int64_t l = 0; l < L; ++l) keys *= (double)K;
   // the map (rounded to 16 B) + the out-of-range row counter
-  return use_byte_map(B, keys) ? (size_t)(((int64_t)keys + 15) / 16 * 16 + 16) : rq_unique_workspace(B);
+  return use_byte_map(B, keys) ? (size_t)(((int64_t)keys + 15) / 16 * 16 + 16) : table_bytes(B);
 }
 
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
@@ -132,7 +132,7 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
   hipStream_t s = (hipStream_t)stream;
   double keys = 1;
   for (int64_t l = 0; l < L; ++l) keys *= (double)K;
-  if (use_byte_map(B, keys) && ws_bytes >= rq_unique_workspace2(B, L, K)) {
+  if (use_byte_map(B, keys) && ws_bytes >= rq_unique_workspace(B, L, K)) {
     const int64_t nb = ((int64_t)keys + 15) / 16 * 16;
     unsigned long long* bad = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + nb);
     RQ_HIP(zero_async(workspace, (size_t)nb + 16, s));
@@ -145,7 +145,7 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
     RQ_LAUNCH_CHECK("rq_unique_count");
     return 0;
   }
-  RQ_CHECK_ARG(ws_bytes >= rq_unique_workspace(B), "rq_unique_count: workspace too small");
+  RQ_CHECK_ARG(ws_bytes >= table_bytes(B), "rq_unique_count: workspace too small");
   const int64_t slots = table_slots(B);
   hipLaunchKernelGGL(unique_table_init_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s,
                      (unsigned long long*)workspace, slots, (unsigned long long*)out_count);

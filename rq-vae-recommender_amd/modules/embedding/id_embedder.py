@@ -4,7 +4,6 @@ SemIdEmbedder: one table of sem_ids_dim*K + 1 rows; token (type t, id s) -> row 
 padded positions (seq_mask False) -> the padding row (index sem_ids_dim*K, padding_idx).
 UserIdEmbedder: user_id mod num_buckets -> row of a num_buckets table.
 """
-import os
 from typing import NamedTuple
 
 import torch
@@ -13,8 +12,8 @@ from torch import Tensor
 
 from rqvae_hip import ops as hip_ops
 
-# RQ_EMB_PAIR=0: gather cat([seq, fut]) and slice (in-process A/B of the paired embedding)
-_EMB_PAIR = os.environ.get("RQ_EMB_PAIR", "1") != "0"
+# False: gather cat([seq, fut]) and slice (the unpaired form; tests / A-B probes set the attribute)
+_EMB_PAIR = True
 
 
 class Embedding(nn.Embedding):

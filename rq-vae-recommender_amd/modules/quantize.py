@@ -13,7 +13,6 @@ through the full distance matrix) and the COSINE distance run as GPU torch compo
 Gumbel row kernels rq_gumbel_softmax_fwd / _bwd are parity-tested and opt-in (RQ_GUMBEL_HIP=1: slower than
 the composite's library GEMMs as measured).
 """
-import os
 from enum import Enum
 from typing import NamedTuple
 
@@ -32,10 +31,10 @@ from rqvae_hip import ops as hip_ops
 from modules.ginlite import gin as _gin   # gin-config, or the built-in subset when gin is absent
 
 
-# RQ_GUMBEL_HIP=1: the training-mode Gumbel-softmax quantize on rq_gumbel_softmax_fwd / _bwd (parity-tested);
+# GUMBEL_HIP = True: the training-mode Gumbel-softmax quantize on rq_gumbel_softmax_fwd / _bwd (parity-tested);
 # default: the GPU torch composite — measured faster (ML-32M level shape fwd+bwd 1.31 vs 2.35 ms: the row
-# kernels' per-lane K x D dot loops lose to the library GEMMs; an MFMA distance / w @ codebook form is next).
-GUMBEL_HIP = os.environ.get("RQ_GUMBEL_HIP", "0") == "1"
+# kernels' per-lane K x D dot loops lose to the library GEMMs). Tests set the attribute.
+GUMBEL_HIP = False
 
 
 class QuantizeForwardMode(Enum):

@@ -13,7 +13,6 @@ Jagged inputs may be torch NJTs (drop-in) or dense ``ops.jagged.Jagged`` views; 
 unwrapped once at the module boundary and every row-wise op (RMSNorm, dropout, Linear, residual
 adds) runs on the dense (T, C) values, avoiding NJT's per-op Python dispatch.
 """
-import os
 from typing import List, Optional
 
 import torch
@@ -26,10 +25,9 @@ from modules.transformer.attention import AttentionInput, MultiHeadAttention, _w
 from ops.jagged import Jagged, as_jagged
 from rqvae_hip import ops as hip_ops
 
-# RQ_FF_RESIDUAL=0: keep the feed-forward output as MLP + dropout_add (in-process A/B)
-_FF_RESIDUAL = os.environ.get("RQ_FF_RESIDUAL", "1") != "0"
-# RQ_HOIST_KV=0: per-layer cross-attention K/V projections (in-process A/B: model.transformer._HOIST_KV)
-_HOIST_KV = os.environ.get("RQ_HOIST_KV", "1") != "0"
+# False selects the unfused form (tests / A-B probes set these module attributes):
+_FF_RESIDUAL = True   # False: the feed-forward output as MLP + dropout_add
+_HOIST_KV = True      # False: per-layer cross-attention K/V projections
 
 
 class KVCacheOpsMixin:

@@ -26,9 +26,7 @@ _SIGS = {
     "rq_abi_version": ([], _I),
     "rq_last_error": ([], ctypes.c_char_p),
     "rq_codebook_sqnorm": ([_P, _I64, _I64, _P, _P], _I),
-    "rq_quantize_fwd": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P], _I),
-    "rq_quantize_fwd_impl": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _I, _P], _I),
-    "rq_quantize_fwd2": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P, _P], _I),
+    "rq_quantize_fwd": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P, _I, _P], _I),
     "rq_quantize_bwd_workspace": ([_I64, _I64, _I64, _I64], _SZ),
     "rq_quantize_bwd": ([_P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I),
     "rq_segment_sum_workspace": ([_I64, _I64], _SZ),
@@ -37,9 +35,7 @@ _SIGS = {
     "rq_rmsnorm_bwd_workspace": ([_I64, _I64], _SZ),
     "rq_rmsnorm_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_rmsnorm_dropout_fwd": ([_P, _P, _I64, _I64, _F, _F, _U64, _P, _P, _P], _I),
-    "rq_rmsnorm_dropout_bwd": ([_P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _P, _SZ, _P], _I),
-    "rq_rmsnorm_dropout_bwd2": ([_P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _I, _P, _SZ, _P], _I),
-    "rq_rmsnorm_dropout_bwd3": ([_P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _I, _I, _P, _P, _SZ, _P], _I),
+    "rq_rmsnorm_dropout_bwd": ([_P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _I, _I, _P, _P, _SZ, _P], _I),
     "rq_dropout_params": ([_F, _P, _P], _I),
     "rq_silu_dropout_fwd": ([_P, _I64, _F, _U64, _P, _P], _I),
     "rq_silu_dropout_bwd": ([_P, _P, _I64, _F, _U64, _P, _P], _I),
@@ -49,37 +45,20 @@ _SIGS = {
     "rq_linear_wgrad": ([_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_gemm_bf16x3_workspace": ([_I64, _I64, _I64], _SZ),
     "rq_gemm_bf16x3": ([_P, _I64, _I, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I),
-    "rq_gemm_bf16x3_ex": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
-                           _U64, _P, _SZ, _P], _I),
-    "rq_gemm_bf16x3_workspace2": ([_I64, _I64, _I64, _I], _SZ),
-    "rq_gemm_bf16x3_ex2": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
-                            _U64, _I, _P, _SZ, _P], _I),
-    "rq_gemm_bf16x3_ex3": ([_P, _P, _I64, _I, _P, _P, _I64, _I, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _P, _I64, _F,
-                            _U64, _I, _I, _P, _P, _SZ, _P], _I),
+    "rq_gemm_bf16x3_run": ([_P, _P, _P], _I),
+    "rq_gemm_bf16x3_plan": ([_P, _P], _I),
     "rq_reduce_partials": ([_I, _P, _P, _P, _P, _P, _P, _P], _I),
-    "rq_gemm_bf16x3_choice": ([_I64, _I64, _I64, _I, _I, _I, _I, _I, _P], _I),
-    "rq_gemm_x3w_enable": ([_I], _I),
-    "rq_gemm_x3s_enable": ([_I], _I),
-    "rq_gemm_x3d_enable": ([_I], _I),
     "rq_ce_loss_fwd": ([_P, _I64, _I64, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P], _I),
     "rq_ce_loss_bwd": ([_P, _I64, _I64, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "rq_gemm_bf16x3_pair": ([_P, _P, _P], _I),
-    "rq_gemm_bf16x3_pair_choice": ([_P], _I),
-    "rq_gemm_pair_enable": ([_I], _I),
+    "rq_gemm_bf16x3_pair_plan": ([_P], _I),
     "rq_segment_sum_multi_workspace": ([_I, _P, _P, _I64], _SZ),
     "rq_segment_sum_multi": ([_I, _P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P], _I),
-    "rq_gemm_kfull_enable": ([_I], _I),
-    "rq_attn_dma_enable": ([_I], _I),
-    "rq_attn_fewq_fused_enable": ([_I], _I),
-    "rq_attn_short_fused_enable": ([_I], _I),
-    "rq_attn_qsplit_set": ([_I], _I),
     "rq_split_bf16x3": ([_P, _I64, _P, _P, _P], _I),
     "rq_split_bf16x3_multi": ([_I, _P, _P, _P, _P, _P], _I),
-    "rq_unique_workspace": ([_I64], _SZ),
-    "rq_unique_workspace2": ([_I64, _I64, _I64], _SZ),
+    "rq_unique_workspace": ([_I64, _I64, _I64], _SZ),
     "rq_unique_count": ([_P, _I64, _I64, _I64, _P, _P, _SZ, _P], _I),
     "rq_l2norm_recon_fwd": ([_P, _P, _I64, _I64, _P, _P, _P], _I),
-    "rq_l2norm_recon_rows_per_wave": ([_I], _I),
     "rq_col_sum": ([_P, _I64, _I64, _P, _I, _P], _I),
     "rq_row_norms": ([_P, _I64, _I64, _P, _P], _I),
     "rq_loss_means": ([_P, _P, _I64, _P, _P], _I),
@@ -91,17 +70,12 @@ _SIGS = {
     "jagged_from_padded": ([_P, _I64, _I64, _I64, _P, _P, _I, _I, _P], _I),
     "jagged_from_padded_rows": ([_P, _I64, _I64, _I64, _P, _P, _I64, _I, _I, _P], _I),
     "jagged_to_padded": ([_P, _P, _I64, _I64, _I64, _P, _I, _P], _I),
+    "varlen_attn_fwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P], _I),
     "varlen_attn_fwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
-                         _I64, _P], _I),
+                         _I64, _P, _I64, _I, _P], _I),
+    "varlen_attn_bwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P], _I),
     "varlen_attn_bwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
-                         _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I),
-    "varlen_attn_fwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _I, _P], _I),
-    "varlen_attn_fwd3": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
-                          _I64, _P, _I64, _P], _I),
-    "varlen_attn_bwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _P], _I),
-    "varlen_attn_bwd_ws_elems2": ([_I64, _I64, _I64, _I64, _I64, _I64, _I64, _P], _I),
-    "varlen_attn_bwd2": ([_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
-                          _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P, _I64, _P], _I),
+                         _I64, _I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P, _I64, _I, _P], _I),
     "rq_seed_epoch_advance": ([_P], _I),
     "rq_seed_epoch_set": ([_U64, _P], _I),
     "rq_adamw_step": ([_P, _I64, _F, _F, _F, _F, _F, _F, _F, _P], _I),

@@ -287,8 +287,7 @@ class GradBuckets:
         if b["expect"] == 0:   # every parameter of the bucket is unused on every rank
             return
         from . import ops
-        ops.join_wgrad_stream()   # weight grads accumulated on the side stream land before the exchange
-        ops.flush_reductions()    # ... and every deferred reduction into the flat views
+        ops.flush_reductions()    # every deferred reduction into the flat views lands before the exchange
         self._pending[bi] = dist.all_reduce(b["flat"], op=dist.ReduceOp.SUM, async_op=True)
 
     def zero_grad(self):
@@ -331,7 +330,6 @@ class GradBuckets:
         """Launch what is left (in index order) and wait for every bucket, then average. Pure stream
         work (no host sync): GraphedSteps captures it at the end of the replayed backward."""
         from . import ops
-        ops.join_wgrad_stream()
         ops.flush_reductions()
         if self.exchange:
             while self._next < len(self.buckets):

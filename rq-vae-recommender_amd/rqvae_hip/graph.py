@@ -148,8 +148,7 @@ class GraphedSteps:
         if self.run_backward:
             out.backward()
             out = out.detach()
-        ops.join_wgrad_stream()   # side-stream weight grads rejoin inside the capture
-        ops.flush_reductions()    # deferred weight-grad reductions too (their list lives only at capture)
+        ops.flush_reductions()    # deferred weight-grad reductions (their list lives only at capture)
         if exchange and b is not None:
             b.finish()
         if self.capture:   # eager bodies draw their dropout keys from the host counter
@@ -182,6 +181,8 @@ class GraphedSteps:
         # collectives, a trainer's feed thread pins host memory (the caching host allocator queries and
         # records events) — and under the default global mode any such call fails the capture ("operation
         # not permitted when stream is capturing", seen on MI355X with the watchdog)
+        if self.in_graph:
+            self._quiesce()
         g, out, err = self._try_capture(self.in_graph)
         if self.in_graph and self._world() > 1:
             # one decision for all ranks: if any rank failed to capture its collectives, every rank
@@ -205,6 +206,19 @@ class GraphedSteps:
             self.pool = g.pool()
         self.graphs[key] = (g, out)
         return self.graphs[key]
+
+    # ProcessGroupNCCL's watchdog thread wakes every 100 ms and queries the end events of the collectives
+    # it tracks until it sees them complete. On ROCm a query of such an event from another thread while
+    # the exchange is being captured fails the capture even in thread-local mode ("dependency created on
+    # uncaptured work in another stream", tools/graph_exchange_probe.py race_forever), so before an
+    # in-graph capture every earlier collective is completed on the device and the watchdog is given
+    # more than two of its polling periods to retire them.
+    QUIESCE_S = 0.3
+
+    def _quiesce(self):
+        import time
+        torch.cuda.synchronize()
+        time.sleep(self.QUIESCE_S)
 
     def _try_capture(self, in_graph: bool):
         """Capture one step body: (graph, its output, None) or (None, None, the exception)."""

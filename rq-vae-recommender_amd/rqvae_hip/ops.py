@@ -93,13 +93,9 @@ class RqQuantizeFunction(torch.autograd.Function):
         es = torch.empty((B, D), device=dev, dtype=torch.float32)
         s = stream_handle(dev)
         call("rq_codebook_sqnorm", ptr(cbs), L * K, D, ptr(csq), s)
-        if with_norms:
-            norms = torch.empty((L, B), device=dev, dtype=torch.float32)
-            TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd2", ptr(x), B, D, ptr(cbs), ptr(csq), K, L,
-                         int(mode), float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), ptr(norms), s)
-        else:
-            TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L,
-                         int(mode), float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), s)
+        norms = torch.empty((L, B), device=dev, dtype=torch.float32) if with_norms else None
+        TIMER.around("rq_quantize_fwd", call, "rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L,
+                     int(mode), float(beta), ptr(ids), ptr(emb), ptr(res), ptr(ql), ptr(es), ptr(norms), 0, s)
         ctx.save_for_backward(res, ids, cbs)
         ctx.mode, ctx.beta = int(mode), float(beta)
         ctx.mark_non_differentiable(ids)
@@ -166,10 +162,9 @@ def linear_wgrad(g: torch.Tensor, x: torch.Tensor, with_bias: bool):
     return dW, db
 
 
-import os as _os
 
 # weight grads over fewer rows than this go to the library GEMM (one launch beats split-K + reduce)
-WGRAD_MIN_ROWS = int(_os.environ.get("RQVAE_WGRAD_MIN_ROWS", "1024"))
+WGRAD_MIN_ROWS = 1024
 
 
 def wgrad_supported(weight: torch.Tensor) -> bool:
@@ -180,7 +175,7 @@ def wgrad_supported(weight: torch.Tensor) -> bool:
 # With tuned library GEMMs (rqvae_hip.gemm_tuning) the library's g^T x beats the split-K kernel
 # up to this many rows (measured: decoder weight grads over ~11k rows 2.8 -> ~2.0 ms/step on the
 # tuned library path, RQ-VAE grads over 65,536 rows 1.29 ms on the split-K kernel vs 1.45 ms).
-WGRAD_TUNED_LIB_MAX_ROWS = int(_os.environ.get("RQVAE_WGRAD_TUNED_LIB_MAX_ROWS", "32768"))
+WGRAD_TUNED_LIB_MAX_ROWS = 32768
 
 
 def _wgrad_choice(g2: torch.Tensor, x2: torch.Tensor, with_bias: bool) -> str:
@@ -310,68 +305,30 @@ def split_weights(weights) -> list:
     return res
 
 
-_SIDE = {"on": False, "streams": {}, "used": False}
-
-
-def wgrad_stream_enable(on: bool) -> bool:
-    """Run the weight-grad GEMMs that accumulate into flat gradient buckets (_wgrad_into's direct path)
-    on a side stream: they depend on nothing downstream in the backward, so they overlap the data-grad
-    chain, attention and norm backward kernels (a parallel branch of a captured graph). Consumers of
-    the gradients must call join_wgrad_stream() first (GradBuckets.synchronize / _launch and
-    graph.GraphedSteps do). Returns the previous setting."""
-    prev = _SIDE["on"]
-    _SIDE["on"] = bool(on)
-    return prev
-
-
-def _side_stream(device):
-    s = _SIDE["streams"].get(device.index)
-    if s is None:
-        s = _SIDE["streams"][device.index] = torch.cuda.Stream(device=device)
-    return s
-
-
-def join_wgrad_stream() -> None:
-    """Make the current stream wait for every weight grad launched on the side stream."""
-    if _SIDE["used"]:
-        for s in _SIDE["streams"].values():
-            torch.cuda.current_stream(s.device).wait_stream(s)
-        _SIDE["used"] = False
-
-
 def _operand_tensors(t):
     return [t.hi, t.lo] if isinstance(t, Split) else [t]
 
 
 def _wgrad_into(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: int):
     """dW = g^T inp for `weight` (split-bf16 GEMM): added straight into weight's flat gradient bucket
-    when dp.GradBuckets owns one (returns None: autograd must not accumulate it again) — on the side
-    stream when wgrad_stream_enable(True) — else a new (O, I) tensor for autograd."""
+    when dp.GradBuckets owns one (returns None: autograd must not accumulate it again), else a new
+    (O, I) tensor for autograd. (A side stream for these was measured slower inside the captured steps:
+    Amazon 6.16 -> 6.38-6.43 ms, profiles/r03 — one stream it is.)"""
     from . import dp
     sink = dp.direct_grad(weight)
     if sink is None:
         return gemm_x3(g, g_kc, inp, inp_kc, O, I, rows)
-    if _SIDE["on"]:
-        main = torch.cuda.current_stream(sink.device)
-        side = _side_stream(sink.device)
-        side.wait_stream(main)          # operands and the zeroed bucket are ready
-        with torch.cuda.stream(side):   # the split-K slab workspace is allocated on the side stream too
-            gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True, defer=dp.defer_ok(weight))
-        for t in _operand_tensors(g) + _operand_tensors(inp):
-            t.record_stream(side)       # freed operands are not reused until the side stream is past them
-        _SIDE["used"] = True
-    else:
-        gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True, defer=dp.defer_ok(weight))
+    gemm_x3(g, g_kc, inp, inp_kc, O, I, rows, out=sink, accumulate=True, defer=dp.defer_ok(weight))
     dp.direct_grad_done(weight)
     return None
 
 
 def _wgrad_spec(weight, g, g_kc: bool, inp, inp_kc: bool, O: int, I: int, rows: int):
     """gemm_x3 keywords of dW = g^T inp for a paired launch with the data gradient (gemm_x3_pair), added
-    straight into weight's flat gradient bucket when dp.GradBuckets owns one — or None when the side
-    stream is on (the weight gradient then runs there: _wgrad_into)."""
+    straight into weight's flat gradient bucket when dp.GradBuckets owns one — or None when the GEMM
+    policy asks for separate launches (GEMM_NO_PAIR: _wgrad_into)."""
     from . import dp
-    if _SIDE["on"] or not _PAIR["on"]:
+    if not _pairing():
         return None
     sink = dp.direct_grad(weight)
     spec = dict(a=g, a_kcontig=g_kc, b=inp, b_kcontig=inp_kc, M=O, N=I, K=rows)
@@ -389,26 +346,52 @@ def _wgrad_result(weight, spec, result):
     return result
 
 
-# paired data-/weight-gradient launches (gemm_x3_pair); RQ_X3_PAIR=0 in the environment: two launches
-_PAIR = {"on": _os.environ.get("RQ_X3_PAIR", "1") != "0"}
+# Kernel policy of the split-bf16 GEMM calls (rq_gemm_desc.flags, RQ_GEMM_* in include/rqvae_hip.h; 0 = the
+# time model's choice): set only by kernel-vs-kernel tests and A/B probes through gemm_policy(); the library
+# itself keeps no state — the flags travel in every descriptor.
+GEMM_ONLY_128, GEMM_ONLY_64, GEMM_FORCE_WIDE, GEMM_NO_WIDE, GEMM_MASKED, GEMM_NO_PAIR = 1, 2, 4, 8, 16, 32
+_GEMM_POLICY = {"flags": 0}
+
+
+class _Policy:
+    def __init__(self, store, flags):
+        self.store, self.flags = store, int(flags)
+
+    def __enter__(self):
+        self.prev = self.store["flags"]
+        self.store["flags"] = self.flags
+        return self
+
+    def __exit__(self, *exc):
+        self.store["flags"] = self.prev
+        return False
+
+
+def gemm_policy(flags: int) -> _Policy:
+    """`with ops.gemm_policy(ops.GEMM_ONLY_64): ...` — every split-bf16 GEMM launched inside (forward and
+    the backward run inside the block) carries these RQ_GEMM_* flags."""
+    return _Policy(_GEMM_POLICY, flags)
+
+
+def _pairing() -> bool:
+    return not (_GEMM_POLICY["flags"] & GEMM_NO_PAIR)
 
 
 EPI_STORE, EPI_SILU_FWD, EPI_SILU_BWD, EPI_ADD = 0, 1, 2, 3
 _X3_WS = {}
 
 
-def _x3_workspace(M: int, N: int, K: int, accumulate: bool = False) -> int:
-    """Slab bytes of rq_gemm_bf16x3_ex2 for a shape (split-K partials, or the single slab of an
-    accumulating call; host-only plan, memoised per shape)."""
-    key = (M, N, K, accumulate)
+def _x3_workspace(M: int, N: int, K: int) -> int:
+    """Split-K slab bytes of rq_gemm_bf16x3_run for a shape (host-only plan, memoised per shape)."""
+    key = (M, N, K)
     nb = _X3_WS.get(key)
     if nb is None:
-        nb = _X3_WS[key] = int(_lib.load().rq_gemm_bf16x3_workspace2(M, N, K, int(accumulate)))
+        nb = _X3_WS[key] = int(_lib.load().rq_gemm_bf16x3_workspace(M, N, K))
     return nb
 
 
 class _X3Call(NamedTuple):
-    """One prepared rq_gemm_bf16x3 call: the ex3 argument values, its outputs and what to do after it."""
+    """One prepared rq_gemm_bf16x3 call: its rq_gemm_desc field values, outputs and what to do after it."""
     fields: tuple
     C: torch.Tensor
     H: "Split"
@@ -444,14 +427,14 @@ def _x3_setup(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, ep
     if epilogue in (EPI_SILU_FWD, EPI_SILU_BWD):
         H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
-    nbytes = _x3_workspace(M, N, K, accumulate)
+    nbytes = _x3_workspace(M, N, K)
     ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8) if nbytes else None
     defer = bool(defer and accumulate and nbytes)
     if defer and C.data_ptr() in _DEFER["outs"]:
         flush_reductions()   # a pending reduction into the same output must land first
     fields = (ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig), M, N, K, ptr(C), N,
               int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N, float(p), int(seed),
-              int(accumulate), int(defer), ptr(ws), nbytes)
+              int(accumulate), int(defer), ptr(ws), nbytes, _GEMM_POLICY["flags"], 0)
     key = f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}{int(accumulate)}"
     return _X3Call(fields, C, H, ws, defer, key, epilogue, M, N, dev)
 
@@ -467,7 +450,7 @@ def _x3_result(c: _X3Call, splits: int):
 def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
             Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
             accumulate: bool = False, defer: bool = False):
-    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_ex3). a / b: fp32
+    """Split-bf16 GEMM with pre-split operands and fused epilogues (rq_gemm_bf16x3_run). a / b: fp32
     tensors or Split. Returns C (EPI_STORE; EPI_ADD: A B^T + Z), (C, H) (EPI_SILU_FWD: C = z,
     H = split(Dropout(SiLU(z)))) or H (EPI_SILU_BWD: split(SiLU'(Z) * Dropout(A B^T))); H is a Split
     of shape (M, N). `out`: the (M, N) contiguous fp32 destination of C; `accumulate` (EPI_STORE
@@ -476,8 +459,8 @@ def gemm_x3(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epil
     import ctypes
     c = _x3_setup(a, a_kcontig, b, b_kcontig, M, N, K, epilogue, Z, p, seed, out, accumulate, defer)
     splits = ctypes.c_int(0)
-    f = c.fields
-    args = ("rq_gemm_bf16x3_ex3", *f[:21], f[21], ctypes.byref(splits), f[22], f[23], stream_handle(c.dev))
+    d = _desc_type()(*c.fields)
+    args = ("rq_gemm_bf16x3_run", ctypes.byref(d), ctypes.byref(splits), stream_handle(c.dev))
     if TIMER.wants("gemm_bf16x3"):
         TIMER.around(c.key, call, *args)
     else:
@@ -499,7 +482,7 @@ def _desc_type():
                         ("b_kcontig", I), ("M", I64), ("N", I64), ("K", I64), ("C", P), ("ldc", I64),
                         ("epilogue", I), ("Z", P), ("H_hi", P), ("H_lo", P), ("ldh", I64), ("p", ctypes.c_float),
                         ("seed", ctypes.c_uint64), ("accumulate", I), ("defer", I), ("workspace", P),
-                        ("ws_bytes", ctypes.c_size_t)]
+                        ("ws_bytes", ctypes.c_size_t), ("flags", I), ("reserved", I)]
         t = _DESC["t"] = Desc
     return t
 
@@ -521,16 +504,6 @@ def gemm_x3_pair(spec1: dict, spec2: dict):
     return _x3_result(c1, splits[0]), _x3_result(c2, splits[1])
 
 
-def gemm_kfull_enable(enable) -> int:
-    """Unmasked staging for whole-stage launches (default on); False = the masked path (A/B, tests)."""
-    return int(_lib.load().rq_gemm_kfull_enable(int(bool(enable))))
-
-
-def gemm_pair_enable(enable) -> int:
-    """Paired data-/weight-gradient launches (rq_gemm_bf16x3_pair): False = two launches (A/B)."""
-    return int(_lib.load().rq_gemm_pair_enable(int(bool(enable))))
-
-
 # Deferred partial reductions (rq_reduce_partials): split-K weight-gradient slabs and RMSNorm weight-
 # gradient partials that accumulate into flat gradient buckets wait here and run as ONE launch (per 48)
 # at the next flush — before a bucket's exchange, in GradBuckets.finish / synchronize / zero_grad, and at
@@ -547,7 +520,7 @@ def _defer_push(ws: torch.Tensor, out: torch.Tensor, n: int, S: int, layout: int
 # in a flat bucket; the flush sums every waiting table in ONE segmented-sum chain (rq_segment_sum_multi) and
 # adds each table's slice into its bucket view through the batched reduction above — instead of one
 # 6-launch chain plus an accumulate per table (the decoder's 4-6 tables: ~30 launches a step).
-_EMB = {"pending": [], "on": _os.environ.get("RQ_EMB_DEFER", "1") != "0"}
+_EMB = {"pending": [], "on": True}
 _EMB_KMAX = 4096          # rq_segment_sum's key limit, per batch
 _EMB_SRC_MAX = 16         # sources per rq_segment_sum_multi call
 
@@ -623,7 +596,6 @@ def flush_reductions() -> None:
     if not pend:
         return
     import ctypes
-    join_wgrad_stream()
     dev = pend[0][1].device
     cur = torch.cuda.current_stream(dev)
     for ws, out, _, _, _, st in pend:
@@ -646,32 +618,16 @@ def pending_reductions() -> int:
 
 def gemm_x3_choice(M: int, N: int, K: int, a_split: bool, b_split: bool, a_kcontig: bool, b_kcontig: bool,
                    epilogue: int = EPI_STORE):
-    """(kernel, splits) rq_gemm_bf16x3_ex picks for a call: kernel 'wide' (256 x 256 tiles, LDS-DMA,
-    both operands split), 'x3' (128 x 128 tiles), 'x3d' (its LDS-DMA form for fp32 k-contiguous A x split B)
-    or 'x3s' (its 64 x 64-tile form); host-only."""
+    """(kernel, splits) rq_gemm_bf16x3_run picks for a call under the current gemm_policy: kernel 'wide'
+    (256 x 256 tiles, LDS-DMA, both operands split), 'x3' (128 x 128 tiles) or 'x3s' (its 64 x 64-tile
+    form); 'none' for an empty or invalid shape. Host-only (rq_gemm_bf16x3_plan)."""
     import ctypes
-    s = ctypes.c_int(0)
-    k = _lib.load().rq_gemm_bf16x3_choice(M, N, K, int(a_split), int(b_split), int(a_kcontig), int(b_kcontig),
-                                          int(epilogue), ctypes.byref(s))
-    return {1: "wide", 2: "x3s", 3: "x3d"}.get(k, "x3"), int(s.value)
-
-
-def gemm_x3w_enable(enable) -> int:
-    """Wide split-bf16 GEMM kernel for this process: False off, True on (chosen per shape by the
-    round cost model), 2 forced wherever it can run (kernel tests); returns the previous state."""
-    return int(_lib.load().rq_gemm_x3w_enable(2 if enable == 2 else int(bool(enable))))
-
-
-def gemm_x3d_enable(enable) -> int:
-    """LDS-DMA form of the 128-tile kernel for fp32 k-contiguous A x split B: False off (register-staged
-    kernel; the default), True on for an n-contiguous B, 2 for every B layout; returns the previous state."""
-    return int(_lib.load().rq_gemm_x3d_enable(2 if enable == 2 else int(bool(enable))))
-
-
-def gemm_x3s_enable(mode) -> int:
-    """64 x 64-tile form of the 128-tile split-bf16 kernel: 0 off, 1 chosen per shape by the time model
-    (default), 2 forced wherever the 128-tile kernel would run; returns the previous mode."""
-    return int(_lib.load().rq_gemm_x3s_enable(2 if mode == 2 else int(bool(mode))))
+    d = _desc_type()(A_lo=16 if a_split else None, lda=K if a_kcontig else M, a_kcontig=int(a_kcontig),
+                     B_lo=16 if b_split else None, ldb=K if b_kcontig else N, b_kcontig=int(b_kcontig), M=M, N=N, K=K,
+                     ldc=N, epilogue=int(epilogue), ldh=N, flags=_GEMM_POLICY["flags"])
+    s_ = ctypes.c_int(0)
+    k = _lib.load().rq_gemm_bf16x3_plan(ctypes.byref(d), ctypes.byref(s_))
+    return {1: "wide", 2: "x3s", 0: "x3"}.get(k, "none"), int(s_.value)
 
 
 def mlp_fusable(x: torch.Tensor, weights) -> bool:
@@ -1038,7 +994,7 @@ class RMSNormFunction(torch.autograd.Function):
 
 def _rmsnorm_bwd(x2, weight, rstd, gy, gres, p: float, seed: int, need_w: bool):
     """(gx [+ gres], gw) of one RMSNorm(+dropout) — gw added straight into the parameter's flat
-    gradient bucket when dp.GradBuckets owns one (then returned as None), rq_rmsnorm_dropout_bwd2."""
+    gradient bucket when dp.GradBuckets owns one (then returned as None), rq_rmsnorm_dropout_bwd."""
     from . import dp
     B, D = x2.shape
     gy2 = gy.contiguous().view(B, D)
@@ -1050,18 +1006,13 @@ def _rmsnorm_bwd(x2, weight, rstd, gy, gres, p: float, seed: int, need_w: bool):
     defer = sink is not None and dp.defer_ok(weight)
     if defer and sink.data_ptr() in _DEFER["outs"]:
         flush_reductions()
-    if defer:
-        import ctypes
-        parts = ctypes.c_int(0)
-        call("rq_rmsnorm_dropout_bwd3", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
-             ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
-             1, 1, ctypes.byref(parts), ptr(ws), nbytes, stream_handle(x2.device))
-        if parts.value > 0:
-            _defer_push(ws, sink, D, parts.value, 1)
-    else:
-        call("rq_rmsnorm_dropout_bwd2", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
-             ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
-             int(sink is not None), ptr(ws), nbytes, stream_handle(x2.device))
+    import ctypes
+    parts = ctypes.c_int(0)
+    call("rq_rmsnorm_dropout_bwd", ptr(x2), ptr(weight), ptr(rstd), ptr(gy2),
+         ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(p), int(seed), ptr(gx), ptr(gw),
+         int(sink is not None), int(defer), ctypes.byref(parts), ptr(ws), nbytes, stream_handle(x2.device))
+    if defer and parts.value > 0:
+        _defer_push(ws, sink, D, parts.value, 1)
     if sink is not None:
         dp.direct_grad_done(weight)
         return gx, None
@@ -1073,7 +1024,7 @@ class RMSNormForkFunction(torch.autograd.Function):
     its norm branches and to the residual stream (modules/transformer/model.py:75-82: h = x +
     SelfAttn(Dropout(attn_norm(x))) [+ CrossAttn(Dropout(cross_attn_norm(x)))]; out = h +
     Dropout(MLP(RMSNorm(h)))) as one node, so the backward adds the residual gradient inside the norm
-    backward kernels (rq_rmsnorm_dropout_bwd2 gres) instead of autograd summing the three branch
+    backward kernels (rq_rmsnorm_dropout_bwd gres) instead of autograd summing the three branch
     gradients with separate add kernels. Forward = the RMSNormFunction kernels."""
 
     @staticmethod
@@ -1354,7 +1305,7 @@ def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     ids = ids.contiguous().to(torch.int64)
     B, L = ids.shape
     out = torch.empty((), device=ids.device, dtype=torch.int64)
-    nbytes = _lib.load().rq_unique_workspace2(B, L, int(K))
+    nbytes = _lib.load().rq_unique_workspace(B, L, int(K))
     ws = torch.empty((nbytes,), device=ids.device, dtype=torch.uint8)
     call("rq_unique_count", ptr(ids), B, L, int(K), ptr(out), ptr(ws), nbytes, stream_handle(ids.device))
     return out
@@ -1600,37 +1551,50 @@ class JaggedToPaddedValues(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------ attention
+# Kernel policy of the attention calls (the `flags` argument, RQ_ATTN_* in include/rqvae_hip.h; 0 = the
+# measured-best forms): set only by kernel-vs-kernel tests and A/B probes through attn_policy().
+ATTN_NO_DMA, ATTN_TWO_PASS, ATTN_NO_SPLIT = 1, 2, 4
+_ATTN_POLICY = {"flags": 0}
+
+
+def ATTN_QSPLIT(n: int) -> int:
+    return int(n) << 8
+
+
+def attn_policy(flags: int) -> _Policy:
+    """`with ops.attn_policy(ops.ATTN_TWO_PASS): ...` — every varlen attention launch inside (forward and
+    the backward run inside the block) carries these RQ_ATTN_* flags."""
+    return _Policy(_ATTN_POLICY, flags)
+
+
 def _attn_fwd(q, k, v, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, lse):
-    """Forward launch(es) (varlen_attn_fwd3: scratch for the LPT order and split-key partials)."""
+    """Forward launch(es) (varlen_attn_fwd with scratch for the LPT order and split-key partials)."""
     import ctypes
     Tq = q.shape[0]
+    flags = _ATTN_POLICY["flags"]
     n = ctypes.c_int64(0)
-    call("varlen_attn_fwd_ws_elems", B, H, hd, int(max_q), int(max_k), Tq, int(causal), ctypes.byref(n))
+    call("varlen_attn_fwd_ws_elems", B, H, hd, int(max_q), int(max_k), Tq, int(causal), flags, ctypes.byref(n))
     ws = torch.empty((max(1, int(n.value)),), device=q.device, dtype=torch.float32)
-    TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd3", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+    TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
                  v.stride(0), ptr(cu_q), ptr(cu_k), B, H, hd, int(max_q), int(max_k), int(causal), float(scale),
-                 ptr(out), out.stride(0), ptr(lse), Tq, ptr(ws), ws.numel(), stream_handle(q.device))
-
-
-ATTN_FUSED_BWD = True   # varlen_attn_bwd2 (fused dQ/dK/dV where it applies); False: the two-pass form (A/B)
+                 ptr(out), out.stride(0), ptr(lse), Tq, ptr(ws), ws.numel(), flags, stream_handle(q.device))
 
 
 def _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv):
-    """Backward launch(es) of varlen attention into dq / dk / dv (row-strided views)."""
-    Tq, A = q.shape
-    delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
-    args = (ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out), out.stride(0), ptr(dout),
-            dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B, H, A // H, int(max_q), int(max_k), int(causal),
-            float(scale), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), k.shape[0], ptr(delta))
-    if not ATTN_FUSED_BWD:
-        TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd", *args, stream_handle(q.device))
-        return
+    """Backward launch(es) of varlen attention into dq / dk / dv (row-strided views); scratch sized for
+    the fused form's query splits (Tk given)."""
     import ctypes
+    Tq, A = q.shape
+    flags = _ATTN_POLICY["flags"]
+    delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
     n = ctypes.c_int64(0)
-    call("varlen_attn_bwd_ws_elems2", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0], ctypes.byref(n))
+    call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0], flags, ctypes.byref(n))
     ws = torch.empty((int(n.value),), device=q.device, dtype=torch.float32) if n.value else None
-    TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd2", *args, ptr(ws) if ws is not None else None,
-                 int(n.value), stream_handle(q.device))
+    TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+                 v.stride(0), ptr(out), out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B,
+                 H, A // H, int(max_q), int(max_k), int(causal), float(scale), ptr(dq), dq.stride(0), ptr(dk),
+                 dk.stride(0), ptr(dv), dv.stride(0), k.shape[0], ptr(delta), ptr(ws), int(n.value), flags,
+                 stream_handle(q.device))
 
 
 class VarlenAttentionFunction(torch.autograd.Function):
@@ -1753,8 +1717,8 @@ class _GradSink:
                 g.data_ptr() == self.buf.data_ptr() + i * self.width * self.buf.element_size())
 
 
-# RQ_HOIST_SPLIT=0: the hoisted projection reads its fp32 input directly (A/B switch)
-_HOIST_SPLIT = _os.environ.get("RQ_HOIST_SPLIT", "1") != "0"
+# False: the hoisted projection reads its fp32 input directly (A/B probes set the attribute)
+_HOIST_SPLIT = True
 
 
 class HoistedProjectionFunction(torch.autograd.Function):
@@ -1801,7 +1765,7 @@ class HoistedProjectionFunction(torch.autograd.Function):
             g = torch.cat([gi if gi is not None else x.new_zeros((T, O)) for gi in gs], 1)
         sink.buf = None
         dws = [None] * n
-        if ctx.needs_input_grad[0] and any(ctx.needs_input_grad[1:]) and _PAIR["on"] and not _SIDE["on"]:
+        if ctx.needs_input_grad[0] and any(ctx.needs_input_grad[1:]) and _pairing():
             # data gradient and the concatenated weight gradient in one launch
             gx, dw = gemm_x3_pair(dict(a=g, a_kcontig=True, b=wsp, b_kcontig=False, M=T, N=I, K=n * O),
                                   dict(a=g, a_kcontig=False, b=xs, b_kcontig=False, M=n * O, N=I, K=T))
@@ -1822,27 +1786,11 @@ def _wgrad_multi_into(weights, g, x, O_all: int, I: int, rows: int, dw=None):
     O = weights[0].shape[0]
     dw_in = dw
 
-    def run():
-        dw = dw_in if dw_in is not None else gemm_x3(g, False, x, False, O_all, I, rows)
-        for i, sk in enumerate(sinks):
-            if sk is not None:
-                sk.add_(dw[i * O:(i + 1) * O])
-                dp.direct_grad_done(weights[i])
-        return dw
-    if dw_in is None and _SIDE["on"] and any(sk is not None for sk in sinks):
-        main = torch.cuda.current_stream(g.device)
-        side = _side_stream(g.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            dw = run()
-        for t in [g] + _operand_tensors(x):
-            t.record_stream(side)
-        _SIDE["used"] = True
-        if any(sk is None for sk in sinks):   # autograd consumes these on the main stream
-            main.wait_stream(side)
-            dw.record_stream(main)
-    else:
-        dw = run()
+    dw = dw_in if dw_in is not None else gemm_x3(g, False, x, False, O_all, I, rows)
+    for i, sk in enumerate(sinks):
+        if sk is not None:
+            sk.add_(dw[i * O:(i + 1) * O])
+            dp.direct_grad_done(weights[i])
     return [None if sk is not None else dw[i * O:(i + 1) * O] for i, sk in enumerate(sinks)]
 
 

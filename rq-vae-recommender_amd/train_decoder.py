@@ -256,6 +256,8 @@ def _train_loop(feed, model, tokenizer, graphed, buckets, opt, sched, device, ra
                 with (contextlib.nullcontext() if last else buckets.no_sync()):
                     (out.loss * w).backward()
                 loss = out.loss.detach() / gradient_accumulate_every
+            if world > 1:   # the global-batch mean is the shard means weighted by their shares (logged below)
+                loss = loss * (len(counts) / n_glob)
             total = loss if total is None else total + loss
             phase["step"] += clock() - c2
         c3 = clock()
@@ -287,10 +289,14 @@ def _train_loop(feed, model, tokenizer, graphed, buckets, opt, sched, device, ra
                             eager_steps=graphed.eager_steps if graphed is not None else iterations - start_iter,
                             exchange="in-graph" if graphed is not None and graphed.in_graph else "hooks + synchronize")
         c6 = clock()
-        if rank == 0 and (it % log_every == 0 or it + 1 == iterations):
-            print(json.dumps({"iter": it, "loss": float(torch.stack(hist).mean()), "lr": opt.param_groups[0]["lr"],
-                              "elapsed_s": round(time.time() - t0, 2)}), flush=True)
+        if it % log_every == 0 or it + 1 == iterations:
+            mean = torch.stack(hist).mean()
             hist = []
+            if world > 1:   # global-batch loss, as the reference logs it (its ranks all see the whole batch, A-5)
+                torch.distributed.all_reduce(mean)
+            if rank == 0:
+                print(json.dumps({"iter": it, "loss": float(mean), "lr": opt.param_groups[0]["lr"],
+                                  "elapsed_s": round(time.time() - t0, 2)}), flush=True)
         if rank == 0 and ((it + 1) % save_model_every == 0 or it + 1 == iterations):
             os.makedirs(save_dir_root, exist_ok=True)
             torch.save({"iter": it, "model": model.state_dict(), "optimizer": opt.state_dict(),

@@ -164,9 +164,17 @@ def train(iterations=50000, batch_size=64, learning_rate=0.0001, weight_decay=0.
                             graphs=len(graphed.graphs) if graphed is not None else 0,
                             eager_steps=graphed.eager_steps if graphed is not None else iterations + 1,
                             exchange="in-graph" if graphed is not None and graphed.in_graph else "hooks + synchronize")
-        if rank == 0 and (it % log_every == 0 or it == start_iter + iterations):
-            vals = torch.stack(hist).mean(0).tolist()
+        if it % log_every == 0 or it == start_iter + iterations:
+            vals = torch.stack(hist).mean(0)
             hist = []
+            if world > 1:
+                # global-batch means, as the reference logs them (its ranks all see the whole batch, SURVEY A-5):
+                # each rank's shard means weighted by its share; p_unique_ids stays this rank's shard value
+                g = vals[:3] * ((hi - lo) / global_batch)
+                torch.distributed.all_reduce(g)
+                vals = torch.cat([g, vals[3:]])
+            vals = vals.tolist()
+        if rank == 0 and (it % log_every == 0 or it == start_iter + iterations):
             print(json.dumps({"iter": it, "loss": vals[0], "rl": vals[1], "vl": vals[2], "p_unique_ids": vals[3],
                               "elapsed_s": round(time.time() - t0, 2)}), flush=True)
         if do_eval and ((it + 1) % eval_every == 0 or it + 1 == iterations) and rank == 0:

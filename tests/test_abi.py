@@ -32,27 +32,32 @@ def test_library_exports_declared_symbols():
     assert not missing, missing
     assert set(_declared()) == set(_lib.EXPORTED_SYMBOLS)
     typed = _lib.load()
-    assert typed.rq_abi_version() == 2
+    assert typed.rq_abi_version() == 3
     # argument checks run on the host and never touch the device
-    rc = typed.rq_quantize_fwd(None, 4, 48, None, None, 8, 1, 3, 0.25, None, None, None, None, None, None)
+    rc = typed.rq_quantize_fwd(None, 4, 48, None, None, 8, 1, 3, 0.25, None, None, None, None, None, None, 0, None)
     assert rc == -22 and b"null pointer" in typed.rq_last_error()
     assert typed.rq_quantize_bwd_workspace(1024, 64, 256, 3) > 1024 * 64 * 3 * 4
     # fused attention backward scratch: one dQ partial slab per 64-key block when sequences span several
     n = ctypes.c_int64(-1)
-    assert typed.varlen_attn_bwd_ws_elems(64, 6, 64, 801, 801, 1000, ctypes.byref(n)) == 0 and n.value == 13 * 1000 * 384 + 64
-    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 64, 64, 500, ctypes.byref(n)) == 0 and n.value == 0   # one block
-    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 5, 500, ctypes.byref(n)) == 0 and n.value == 0     # short forms
-    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 81, 500, ctypes.byref(n)) == 0 and n.value == 0   # short cross
-    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 801, 500, ctypes.byref(n)) == 0 and n.value == 13 * 500 * 512
+    assert typed.varlen_attn_bwd_ws_elems(64, 6, 64, 801, 801, 1000, -1, 0, ctypes.byref(n)) == 0 \
+        and n.value == 13 * 1000 * 384 + 64
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 64, 64, 500, -1, 0, ctypes.byref(n)) == 0 and n.value == 0   # one block
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 5, 500, -1, 0, ctypes.byref(n)) == 0 and n.value == 0   # short forms
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 81, 500, -1, 0, ctypes.byref(n)) == 0 and n.value == 0  # short cross
+    # the two-pass policy needs no scratch; a forced query split adds the dK / dV partials (Tk >= 0)
+    assert typed.varlen_attn_bwd_ws_elems(64, 6, 64, 801, 801, 1000, -1, 2, ctypes.byref(n)) == 0 and n.value == 0
+    assert typed.varlen_attn_bwd_ws_elems(8, 6, 64, 801, 801, 1000, 1000, 4 << 8, ctypes.byref(n)) == 0 \
+        and n.value == 13 * 1000 * 384 + 8 + 2 * 4 * 1000 * 384
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 64, 5, 801, 500, -1, 0, ctypes.byref(n)) == 0 and n.value == 13 * 500 * 512
     # forward scratch: LPT order (16-B padded) + split-key partials for few queries over > 128 keys
-    assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 0, ctypes.byref(n)) == 0 and n.value == 8 + 7 * 500 * 8 * 66
-    assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 1, ctypes.byref(n)) == 0 and n.value == 8   # causal
-    assert typed.varlen_attn_bwd_ws_elems(4, 8, 48, 5, 5, 500, ctypes.byref(n)) == -22
+    assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 0, 0, ctypes.byref(n)) == 0 and n.value == 8 + 7 * 500 * 8 * 66
+    assert typed.varlen_attn_fwd_ws_elems(5, 8, 64, 6, 801, 500, 1, 0, ctypes.byref(n)) == 0 and n.value == 8   # causal
+    assert typed.varlen_attn_bwd_ws_elems(4, 8, 48, 5, 5, 500, -1, 0, ctypes.byref(n)) == -22
     # + the query splits' dK / dV partials when the workgroups cannot fill the chip (ML-32M, 8 sequences:
     # 8 x 6 x 13 = 624 workgroups -> 3 splits at 256 CUs, the CPU-side default)
-    assert typed.varlen_attn_bwd_ws_elems2(8, 6, 64, 801, 801, 3200, 3200, ctypes.byref(n)) == 0
+    assert typed.varlen_attn_bwd_ws_elems(8, 6, 64, 801, 801, 3200, 3200, 0, ctypes.byref(n)) == 0
     assert n.value == 13 * 3200 * 384 + 8 + 2 * 3 * 3200 * 384
-    assert typed.varlen_attn_bwd_ws_elems2(64, 6, 64, 801, 801, 1000, 1000, ctypes.byref(n)) == 0
+    assert typed.varlen_attn_bwd_ws_elems(64, 6, 64, 801, 801, 1000, 1000, 0, ctypes.byref(n)) == 0
     assert n.value == 13 * 1000 * 384 + 64   # 4,992 workgroups: no split
 
 
@@ -63,3 +68,17 @@ def test_ops_refuse_cpu_tensors():
     cb = torch.zeros(1, 8, 16)
     with pytest.raises(RqHipError, match="no CPU fallback"):
         ops.rq_quantize(x, cb)
+
+
+def test_library_exports_nothing_undeclared():
+    """The C ABI is exactly the header: no internal helper or retired entry point is exported."""
+    import shutil
+    import subprocess
+    from rqvae_hip import _lib
+    if not os.path.exists(_lib.LIB_PATH) or shutil.which("nm") is None:
+        pytest.skip("library not built or nm missing")
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if len(l.split()) == 3 and l.split()[1] == "T"}
+    c_names = {n for n in exported if not n.startswith("_")}   # C++ (mangled) symbols are not the ABI
+    assert c_names == set(_declared()), sorted(c_names ^ set(_declared()))
+

@@ -1,4 +1,4 @@
-"""Unmasked staging of the 128-/64-tile split-bf16 GEMM (rq_gemm_kfull_enable: launches whose K and split-K
+"""Unmasked staging of the 128-/64-tile split-bf16 GEMM (the default; RQ_GEMM_MASKED keeps the masked path: launches whose K and split-K
 chunk are whole 32-deep stages drop the k masks, masked addresses and zeroing selects) against the masked
 path — bitwise, for every operand layout / split form, both tile sizes, split-K slabs, fused epilogues and
 the paired launch; shapes whose K is not a whole number of stages keep the masked path either way."""
@@ -15,13 +15,9 @@ def _ops():
 
 def _both(fn):
     ops = _ops()
-    prev = ops.gemm_kfull_enable(True)
-    try:
-        a = fn()
-        ops.gemm_kfull_enable(False)
+    a = fn()
+    with ops.gemm_policy(ops.GEMM_MASKED):
         b = fn()
-    finally:
-        ops.gemm_kfull_enable(prev)
     return a, b
 
 

@@ -1,4 +1,4 @@
-"""Split-K for every epilogue of the split-bf16 GEMM (rq_gemm_bf16x3_ex2): when the output tiles cannot
+"""Split-K for every epilogue of the split-bf16 GEMM (rq_gemm_bf16x3_run): when the output tiles cannot
 fill the chip (the decoder's 1,280 future-token rows: 40 tiles of 128 x 128) the partial products go
 to slabs and a fixed-order reduction applies the epilogue (SiLU fwd / bwd with dropout, residual add)
 — and accumulation into an existing buffer (C += A B^T, the weight gradient added into a flat
@@ -26,9 +26,8 @@ def _x3_tiles_only():
     """These tests are about the 128-tile kernel's split-K path: keep the 64-tile form (which serves
     1,280-row launches unsplit) out of the way."""
     ops = _ops()
-    prev = ops.gemm_x3s_enable(0)
-    yield
-    ops.gemm_x3s_enable(prev)
+    with ops.gemm_policy(ops.GEMM_ONLY_128):
+        yield
 
 
 def _close(a, b, tol):

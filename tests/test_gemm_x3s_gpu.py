@@ -27,11 +27,8 @@ def _ops():
 @pytest.fixture
 def small_on():
     ops = _ops()
-    prev_w = ops.gemm_x3w_enable(False)   # the wide kernel would take some split-operand shapes
-    prev = ops.gemm_x3s_enable(2)
-    yield ops
-    ops.gemm_x3s_enable(prev)
-    ops.gemm_x3w_enable(prev_w)
+    with ops.gemm_policy(ops.GEMM_ONLY_64):   # forced (and never the wide kernel) for every call inside
+        yield ops
 
 
 def _mk(M, N, K, a_kc, b_kc, gen, device, integer):
@@ -44,7 +41,7 @@ def _mk(M, N, K, a_kc, b_kc, gen, device, integer):
     return a, b
 
 
-# operand formats the plain-store dispatch builds (rq_gemm_bf16x3_ex2): every fp32 layout, and the
+# operand formats the plain-store dispatch builds (rq_gemm_bf16x3_run): every fp32 layout, and the
 # split / mixed layouts the fused chains use
 BUILT = {(ak, bk, False, False) for ak in (True, False) for bk in (True, False)} | {
     (True, True, True, True), (True, True, False, True), (True, False, True, True), (True, False, False, True),
@@ -72,13 +69,10 @@ def test_x3s_exact_on_integers(device, small_on, a_kc, b_kc, M, N, K, split):
 
 def _both(ops, fn):
     """fn() under the 64-tile kernel and under the 128-tile kernel."""
-    ops.gemm_x3s_enable(2)
-    s = fn()
-    ops.gemm_x3s_enable(0)
-    try:
+    with ops.gemm_policy(ops.GEMM_ONLY_64):
+        s = fn()
+    with ops.gemm_policy(ops.GEMM_ONLY_128):
         o = fn()
-    finally:
-        ops.gemm_x3s_enable(2)
     return s, o
 
 
@@ -89,9 +83,8 @@ def test_x3s_random_bitwise_equal_x3(device, small_on, a_kc, b_kc):
     ops = small_on
     M, N, K = 4096, 512, 256
     assert ops.gemm_x3_choice(M, N, K, False, False, a_kc, b_kc)[1] == 1
-    ops.gemm_x3s_enable(0)
-    assert ops.gemm_x3_choice(M, N, K, False, False, a_kc, b_kc)[1] == 1
-    ops.gemm_x3s_enable(2)
+    with ops.gemm_policy(ops.GEMM_ONLY_128):
+        assert ops.gemm_x3_choice(M, N, K, False, False, a_kc, b_kc)[1] == 1
     gen = torch.Generator(device=device).manual_seed(7 + 2 * a_kc + b_kc)
     a, b = _mk(M, N, K, a_kc, b_kc, gen, device, False)
     cs, co = _both(ops, lambda: ops.gemm_x3(a, a_kc, b, b_kc, M, N, K))
@@ -137,15 +130,11 @@ def test_x3s_split_k_epilogue_and_accumulate(device, small_on):
 
 
 def test_x3s_planner_picks_small_for_decoder_future_rows():
-    ops = _ops()
-    prev = ops.gemm_x3s_enable(1)
-    try:
-        for (M, N, K, akc, bkc, asp, bsp) in [(1280, 512, 512, True, True, False, True),
-                                              (512, 512, 1280, False, False, False, False)]:
-            assert ops.gemm_x3_choice(M, N, K, asp, bsp, akc, bkc)[0] == "x3s", (M, N, K)
-        assert ops.gemm_x3_choice(65536, 512, 768, False, True, True, True)[0] == "x3"
-    finally:
-        ops.gemm_x3s_enable(prev)
+    ops = _ops()   # the default policy: the time model chooses
+    for (M, N, K, akc, bkc, asp, bsp) in [(1280, 512, 512, True, True, False, True),
+                                          (512, 512, 1280, False, False, False, False)]:
+        assert ops.gemm_x3_choice(M, N, K, asp, bsp, akc, bkc)[0] == "x3s", (M, N, K)
+    assert ops.gemm_x3_choice(65536, 512, 768, False, True, True, True)[0] == "x3"
 
 
 def test_x3s_split_k_accumulate_many_launches(device, small_on):

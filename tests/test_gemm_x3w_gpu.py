@@ -7,7 +7,8 @@ staggered groups) against fp64 and against the 128-tile kernel it replaces for l
 * random operands: the two kernels agree BITWISE whenever they use the same split (same 32-deep k
   steps, same product order) — the fused epilogues (SiLU fwd / bwd with dropout, residual add)
   never split; the split-K store within the split-bf16 bound of fp64;
-* rq_gemm_bf16x3_choice really selects the wide kernel for the shapes tested here.
+* rq_gemm_bf16x3_plan really selects the wide kernel for the shapes tested here (RQ_GEMM_FORCE_WIDE /
+  RQ_GEMM_NO_WIDE descriptor flags pick the kernel per call: the library keeps no switch).
 """
 import pytest
 import torch
@@ -38,9 +39,8 @@ def _mk(M, N, K, a_kc, b_kc, gen, device, integer):
 @pytest.fixture
 def wide_on():
     ops = _ops()
-    prev = ops.gemm_x3w_enable(2)   # forced: these tests are about the wide kernel itself
-    yield ops
-    ops.gemm_x3w_enable(prev)
+    with ops.gemm_policy(ops.GEMM_FORCE_WIDE):   # forced: these tests are about the wide kernel itself
+        yield ops
 
 
 @pytest.mark.parametrize("a_kc,b_kc", LAYOUTS)
@@ -77,13 +77,10 @@ def test_x3w_random_within_bound_and_repeatable(device, wide_on, a_kc, b_kc, M, 
 
 def _both(ops, fn):
     """fn() under the wide kernel and under the 128-tile kernel."""
-    ops.gemm_x3w_enable(2)
-    w = fn()
-    ops.gemm_x3w_enable(False)
-    try:
+    with ops.gemm_policy(ops.GEMM_FORCE_WIDE):
+        w = fn()
+    with ops.gemm_policy(ops.GEMM_NO_WIDE):
         o = fn()
-    finally:
-        ops.gemm_x3w_enable(2)
     return w, o
 
 
@@ -112,9 +109,8 @@ def test_x3w_fused_epilogues_equal_x3_kernel(device, wide_on, p):
     r = torch.randn(M, N, generator=gen, device=device)
     assert ops.gemm_x3_choice(M, N, K, True, True, True, True, ops.EPI_ADD)[0] == "wide"
     aw = ops.gemm_x3(x, True, W, True, M, N, K, ops.EPI_ADD, Z=r)
-    ops.gemm_x3w_enable(False)
-    ao = ops.gemm_x3(x32, True, W, True, M, N, K, ops.EPI_ADD, Z=r)
-    ops.gemm_x3w_enable(2)
+    with ops.gemm_policy(ops.GEMM_NO_WIDE):
+        ao = ops.gemm_x3(x32, True, W, True, M, N, K, ops.EPI_ADD, Z=r)
     assert torch.equal(aw, ao)
 
 
@@ -124,5 +120,5 @@ def test_x3w_not_chosen_for_fp32_or_small(device, wide_on):
     assert ops.gemm_x3_choice(65536, 128, 256, True, True, True, True)[0] != "wide"       # N = 128: half tile
     assert ops.gemm_x3_choice(64, 64, 64, True, True, True, True)[0] != "wide"
     assert ops.gemm_x3_choice(65536, 512, 100, True, True, True, True)[0] != "wide"       # K % 32
-    ops.gemm_x3w_enable(False)
-    assert ops.gemm_x3_choice(65536, 512, 768, True, True, True, True)[0] != "wide"
+    with ops.gemm_policy(ops.GEMM_NO_WIDE):
+        assert ops.gemm_x3_choice(65536, 512, 768, True, True, True, True)[0] != "wide"

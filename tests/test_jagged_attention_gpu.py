@@ -89,16 +89,13 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
 ])
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("dma", [True, False])
-def test_varlen_attention_vs_oracle(device, monkeypatch, B, max_q, max_k, H, hd, causal, same, fused, dma):
-    """Both backward forms, and the LDS-DMA short forms (key ranges <= 128, hd 64) on and off."""
-    from rqvae_hip import _lib, ops
-    monkeypatch.setattr(ops, "ATTN_FUSED_BWD", fused)
-    lib = _lib.load()
-    prev = lib.rq_attn_dma_enable(int(dma))
-    try:
+def test_varlen_attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same, fused, dma):
+    """One-pass (fused) and two-pass backwards, and the LDS-DMA short forms (key ranges <= 128, hd 64) on
+    and off: the per-call RQ_ATTN_* policy flags."""
+    from rqvae_hip import ops
+    flags = (0 if fused else ops.ATTN_TWO_PASS) | (0 if dma else ops.ATTN_NO_DMA)
+    with ops.attn_policy(flags):
         _attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same)
-    finally:
-        lib.rq_attn_dma_enable(prev)
 
 
 def _attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
@@ -200,13 +197,10 @@ def test_varlen_attention_fused_empty_and_tail(device, lq, lk):
     do = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
     res = {}
     for fused in (True, False):
-        ops.ATTN_FUSED_BWD = fused
-        try:
+        with ops.attn_policy(0 if fused else ops.ATTN_TWO_PASS):
             qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
             o = ops.varlen_attention(qt, kt, vt, cq, ck, H, False, max(lq), max(lk))
             o.backward(do)
-        finally:
-            ops.ATTN_FUSED_BWD = True
         res[fused] = (o.detach(), qt.grad, kt.grad, vt.grad)
     for a, b, what in zip(res[True], res[False], ("out", "dq", "dk", "dv")):
         assert torch.isfinite(a).all(), what
@@ -219,18 +213,18 @@ def test_varlen_attention_fused_empty_and_tail(device, lq, lk):
             assert torch.count_nonzero(dq[int(cq[b]):int(cq[b + 1])]) == 0
 
 
-@pytest.mark.parametrize("lq,lk,causal,switch", [
-    ([5, 3, 0, 16], [81, 0, 40, 128], False, "rq_attn_fewq_fused_enable"),
-    ([5, 1, 16, 7], [5, 1, 16, 7], True, "rq_attn_fewq_fused_enable"),
-    ([81, 9, 0, 45, 17], [81, 9, 0, 45, 17], False, "rq_attn_short_fused_enable"),   # encoder (Amazon)
-    ([81, 33, 70, 1, 17], [81, 33, 70, 1, 17], True, "rq_attn_short_fused_enable"),
-    ([40, 0, 128, 20], [100, 30, 128, 0], False, "rq_attn_short_fused_enable"),      # 128 staged rows
+@pytest.mark.parametrize("lq,lk,causal", [
+    ([5, 3, 0, 16], [81, 0, 40, 128], False),    # few queries (cross-attention)
+    ([5, 1, 16, 7], [5, 1, 16, 7], True),        # few queries, causal
+    ([81, 9, 0, 45, 17], [81, 9, 0, 45, 17], False),   # short self-attention (the Amazon encoder)
+    ([81, 33, 70, 1, 17], [81, 33, 70, 1, 17], True),
+    ([40, 0, 128, 20], [100, 30, 128, 0], False),      # 128 staged rows
 ])
-def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal, switch):
+def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal):
     """One-pass backwards (attn_bwd_fewq_fused_kernel: <= 16 queries; attn_bwd_short_fused_kernel: short
     self-attention) vs the two-pass kernels on ragged ranges with empty-query / empty-key segments and
     zero-padded tail rows; each run bitwise deterministic."""
-    from rqvae_hip import _lib, ops
+    from rqvae_hip import ops
     g = gi.rng(sum(lq) * 7 + sum(lk))
     H, hd = 8, 64
     A_ = H * hd
@@ -241,16 +235,12 @@ def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal, switch)
     k0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
     v0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
     do = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
-    lib = _lib.load()
     res = {}
     for fused in (True, True, False):
-        prev = getattr(lib, switch)(int(fused))
-        try:
+        with ops.attn_policy(0 if fused else ops.ATTN_TWO_PASS):
             qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
             o = ops.varlen_attention(qt, kt, vt, cq, ck, H, causal, max(lq), max(lk))
             o.backward(do)
-        finally:
-            getattr(lib, switch)(prev)
         r = (qt.grad, kt.grad, vt.grad)
         if fused in res:
             for a, b in zip(res[fused], r):
@@ -336,11 +326,12 @@ def test_c_abi_entry_points_vs_oracle(device, B, max_q, max_k, H, causal, same):
     lse = torch.empty((H, Tq), device=device)
     st = stream_handle(device)
     call("varlen_attn_fwd", ptr(qt), A_, ptr(kt), A_, ptr(vt), A_, ptr(cqt), ptr(ckt), B, H, hd, mq, mk, int(causal),
-         float(scale), ptr(out), A_, ptr(lse), Tq, st)
+         float(scale), ptr(out), A_, ptr(lse), Tq, None, 0, 0, st)
     dq, dk, dv = (torch.empty((n, A_), device=device) for n in (Tq, Tk, Tk))
     delta = torch.empty((H, Tq), device=device)
     call("varlen_attn_bwd", ptr(qt), A_, ptr(kt), A_, ptr(vt), A_, ptr(out), A_, ptr(dot), A_, ptr(lse), Tq, ptr(cqt),
-         ptr(ckt), B, H, hd, mq, mk, int(causal), float(scale), ptr(dq), A_, ptr(dk), A_, ptr(dv), A_, Tk, ptr(delta), st)
+         ptr(ckt), B, H, hd, mq, mk, int(causal), float(scale), ptr(dq), A_, ptr(dk), A_, ptr(dv), A_, Tk, ptr(delta),
+         None, 0, 0, st)
     torch.cuda.synchronize()
     ref, _ = A.attn_fwd(q, k, v, cq, ck, causal)
     rdq, rdk, rdv = A.attn_bwd(q, k, v, do, cq, ck, causal)
@@ -358,13 +349,11 @@ def test_c_abi_entry_points_vs_oracle(device, B, max_q, max_k, H, causal, same):
 @pytest.mark.parametrize("qsplit", [1, 2, 3, 4])
 def test_fused_backward_query_splits(device, qsplit):
     """The fused backward with each key block's query range split over `qsplit` workgroups (dK / dV
-    partials summed in split order by attn_kv_reduce_kernel; rq_attn_qsplit_set forces the count) vs
+    partials summed in split order by attn_kv_reduce_kernel; the RQ_ATTN_QSPLIT(n) flag forces the count) vs
     the fp64 oracle on ragged long sequences (ML-32M lengths, causal and not) incl. an empty one and
     zero-padded tail rows; bitwise deterministic run to run."""
-    from rqvae_hip import _lib, ops
-    lib = _lib.load()
-    prev = lib.rq_attn_qsplit_set(qsplit)
-    try:
+    from rqvae_hip import ops
+    with ops.attn_policy(ops.ATTN_QSPLIT(qsplit)):
         for causal in (False, True):
             g = gi.rng(77 + qsplit + 5 * causal)
             H, hd = 6, 64
@@ -393,5 +382,4 @@ def test_fused_backward_query_splits(device, qsplit):
             for got, ref, what in ((dq, rdq, "dq"), (dk, rdk, "dk"), (dv, rdv, "dv")):
                 a = got[:n].cpu().double().numpy().reshape(ref.shape)
                 assert np.all(np.abs(a - ref) <= 1e-4 + 1e-3 * np.abs(ref)), (what, causal)
-    finally:
-        lib.rq_attn_qsplit_set(prev)
+

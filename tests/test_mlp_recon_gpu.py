@@ -45,8 +45,7 @@ def _ref64(e, x, ws):
 @pytest.mark.parametrize("p", [0.0, 0.3])
 def test_mlp_l2norm_recon_equals_composition(device, p):
     ops = _ops()
-    prev = ops.gemm_x3w_enable(2)   # forced: the split gradient's path onto the wide kernel
-    try:
+    with ops.gemm_policy(ops.GEMM_FORCE_WIDE):   # forced: the split gradient's path onto the wide kernel
         B, dims = 16384, [64, 128, 256, 512, 768]   # no split-K on the last data grad for either kernel
         gen = torch.Generator(device=device).manual_seed(21)
         ws = _weights(dims, gen, device)
@@ -81,23 +80,22 @@ def test_mlp_l2norm_recon_equals_composition(device, p):
         if p == 0.0:
             ref = _ref64(e.detach(), x, [w.detach() for w in ws])
             assert torch.allclose(rf.double(), ref, rtol=2e-4, atol=1e-6)
-    finally:
-        ops.gemm_x3w_enable(prev)
 
 
 def test_mlp_presplit_input_equals_fp32_input(device):
     ops = _ops()
-    prev = ops.gemm_x3w_enable(2)
-    try:
-        B, dims = 8192, [768, 512, 256]
-        gen = torch.Generator(device=device).manual_seed(5)
-        ws = _weights(dims, gen, device)
-        x = torch.randn(B, dims[0], generator=gen, device=device).requires_grad_(True)
-        g = torch.randn(B, dims[-1], generator=gen, device=device)
+    B, dims = 8192, [768, 512, 256]
+    gen = torch.Generator(device=device).manual_seed(5)
+    ws = _weights(dims, gen, device)
+    x = torch.randn(B, dims[0], generator=gen, device=device).requires_grad_(True)
+    g = torch.randn(B, dims[-1], generator=gen, device=device)
+    with ops.gemm_policy(ops.GEMM_FORCE_WIDE):
         assert ops._presplit_input(B, ws, len(ws))
+    with ops.gemm_policy(ops.GEMM_NO_WIDE):
+        assert not ops._presplit_input(B, ws, len(ws))
 
-        def run(wide):
-            ops.gemm_x3w_enable(2 if wide else False)
+    def run(wide):
+        with ops.gemm_policy(ops.GEMM_FORCE_WIDE if wide else ops.GEMM_NO_WIDE):
             for w in ws:
                 w.grad = None
             x.grad = None
@@ -105,14 +103,12 @@ def test_mlp_presplit_input_equals_fp32_input(device):
             y.backward(g)
             return y.detach().clone(), x.grad.clone(), [w.grad.clone() for w in ws]
 
-        yw, xw, gw = run(True)
-        yo, xo, go = run(False)
-        # the plain-store launches (last forward layer, input grad, weight grads) may split K into a
-        # different slab count on the two kernels: fp32 reassociation only
-        for a, b in [(yw, yo), (xw, xo), *zip(gw, go)]:
-            assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
-    finally:
-        ops.gemm_x3w_enable(prev)
+    yw, xw, gw = run(True)
+    yo, xo, go = run(False)
+    # the plain-store launches (last forward layer, input grad, weight grads) may split K into a
+    # different slab count on the two kernels: fp32 reassociation only
+    for a, b in [(yw, yo), (xw, xo), *zip(gw, go)]:
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
 
 
 def test_l2norm_recon_bwd_split_planes(device):

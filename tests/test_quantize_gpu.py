@@ -233,8 +233,8 @@ def test_tiled_and_register_kernels_agree(device, B, D, K, L):
         o = dict(ids=torch.empty(B, L, dtype=torch.int64, device=device), emb=torch.empty(L, B, D, device=device),
                  res=torch.empty(L, B, D, device=device), ql=torch.empty(B, device=device),
                  es=torch.empty(B, D, device=device))
-        call("rq_quantize_fwd_impl", ptr(xt), B, D, ptr(ct), ptr(csq), K, L, 3, 0.25, ptr(o["ids"]), ptr(o["emb"]),
-             ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle(device))
+        call("rq_quantize_fwd", ptr(xt), B, D, ptr(ct), ptr(csq), K, L, 3, 0.25, ptr(o["ids"]), ptr(o["emb"]),
+             ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), None, impl, stream_handle(device))
         outs[impl] = {k: v.cpu().numpy() for k, v in o.items()}
     for impl in impls:
         o = outs[impl]
@@ -263,8 +263,8 @@ def test_split_path_vs_oracle(device, B, D, K, L, mode):
         o = dict(ids=torch.empty(B, L, dtype=torch.int64, device=device), emb=torch.empty(L, B, D, device=device),
                  res=torch.empty(L, B, D, device=device), ql=torch.empty(B, device=device),
                  es=torch.empty(B, D, device=device))
-        call("rq_quantize_fwd_impl", ptr(xt), B, D, ptr(ct), ptr(csq), K, L, mode, 0.25, ptr(o["ids"]), ptr(o["emb"]),
-             ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle(device))
+        call("rq_quantize_fwd", ptr(xt), B, D, ptr(ct), ptr(csq), K, L, mode, 0.25, ptr(o["ids"]), ptr(o["emb"]),
+             ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), None, impl, stream_handle(device))
         outs[impl] = {k: v.cpu().numpy() for k, v in o.items()}
     o = outs[3]
     ok = (o["ids"] == f["ids"]).all(1)

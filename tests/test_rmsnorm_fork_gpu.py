@@ -1,12 +1,12 @@
 """RMSNorm fan-out node (ops.rmsnorm_fork: x -> norm_1(x) [dropout], [norm_2(x) [dropout]], x) and the
-RMSNorm backward's fusions (rq_rmsnorm_dropout_bwd2: residual gradient added in-kernel, weight grad
+RMSNorm backward's fusions (rq_rmsnorm_dropout_bwd: residual gradient added in-kernel, weight grad
 accumulated into a flat gradient bucket). Reference: modules/normalize.py:22-32 and the pre-norm block
 of modules/transformer/model.py:75-82 (x feeds attn_norm, cross_attn_norm and the residual add).
 
 Checks: the fork equals the composition of two ops.rmsnorm calls and the identity under the same
 dropout keys — outputs bitwise, the input gradient within fp32 summation order of the three branch
 gradients, weight gradients bitwise; direct accumulation into dp.GradBuckets flat views equals
-plain autograd; rq_rmsnorm_dropout_bwd2 with gres == bwd + gres.
+plain autograd; rq_rmsnorm_dropout_bwd with gres == bwd + gres.
 """
 import copy
 
@@ -49,7 +49,7 @@ def test_rmsnorm_fork_equals_composition(device, two, p):
         assert torch.equal(g2f, g2c)
 
 
-def test_rmsnorm_bwd2_gres_and_accumulate(device):
+def test_rmsnorm_bwd_gres_and_accumulate(device):
     from rqvae_hip import ops
     from rqvae_hip._lib import ptr, stream_handle
     B, D = 1000, 384
@@ -62,13 +62,13 @@ def test_rmsnorm_bwd2_gres_and_accumulate(device):
     nb = ops._lib.load().rq_rmsnorm_bwd_workspace(B, D)
     ws = torch.empty(nb, device=device, dtype=torch.uint8)
     gx0, gw0 = torch.empty_like(x), torch.empty(D, device=device)
-    ops.call("rq_rmsnorm_dropout_bwd", ptr(x), ptr(w), ptr(rstd), ptr(gy), B, D, 0.0, 0, ptr(gx0), ptr(gw0), ptr(ws), nb,
-             stream_handle(device))
+    ops.call("rq_rmsnorm_dropout_bwd", ptr(x), ptr(w), ptr(rstd), ptr(gy), None, B, D, 0.0, 0, ptr(gx0), ptr(gw0), 0, 0,
+             None, ptr(ws), nb, stream_handle(device))
     gx1 = torch.empty_like(x)
     gw1 = torch.randn(D, generator=gen, device=device)
     base = gw1.clone()
-    ops.call("rq_rmsnorm_dropout_bwd2", ptr(x), ptr(w), ptr(rstd), ptr(gy), ptr(gres), B, D, 0.0, 0, ptr(gx1), ptr(gw1), 1,
-             ptr(ws), nb, stream_handle(device))
+    ops.call("rq_rmsnorm_dropout_bwd", ptr(x), ptr(w), ptr(rstd), ptr(gy), ptr(gres), B, D, 0.0, 0, ptr(gx1), ptr(gw1), 1,
+             0, None, ptr(ws), nb, stream_handle(device))
     assert torch.equal(gx1, gx0 + gres)
     assert torch.equal(gw1, base + gw0)
 

@@ -29,28 +29,28 @@ def test_l2norm_recon_vs_torch(device, B, C):
 
 
 @pytest.mark.parametrize("B,C", [(65537, 768), (5, 96), (3, 4), (1001, 1024), (9, 1000)])
-def test_l2norm_recon_rows_per_wave_bitwise(device, B, C):
-    """The 2- and 4-rows-per-wave forms (ragged last wave included) give the 1-row results bitwise."""
-    from rqvae_hip import _lib, ops
+def test_l2norm_recon_ragged_vs_fp64(device, B, C):
+    """Ragged row counts (a partly filled last workgroup) and widths (a partial float4 vector per lane) with a
+    zero row (the F.normalize eps path): reconstruction loss and input gradient vs the fp64 composition
+    (modules/rqvae.py:145-150 with modules/loss.py:5-10), and bitwise repeatable."""
+    from rqvae_hip import ops
     g = torch.Generator(device=device).manual_seed(B * 3 + C)
     pre = torch.randn(B, C, generator=g, device=device)
     pre[-1] = 0.0
     x = F.normalize(torch.randn(B, C, generator=g, device=device), dim=-1)
     gr = torch.rand(B, generator=g, device=device)
-    lib = _lib.load()
     outs = []
-    prev = lib.rq_l2norm_recon_rows_per_wave(1)
-    try:
-        for rpw in (1, 2, 4):
-            lib.rq_l2norm_recon_rows_per_wave(rpw)
-            a = pre.clone().requires_grad_(True)
-            r = ops.l2norm_recon_loss(a, x)
-            (r * gr).sum().backward()
-            outs.append((r.detach(), a.grad))
-    finally:
-        lib.rq_l2norm_recon_rows_per_wave(prev)
-    for r, ga in outs[1:]:
-        assert torch.equal(r, outs[0][0]) and torch.equal(ga, outs[0][1])
+    for _ in range(2):
+        a = pre.clone().requires_grad_(True)
+        r = ops.l2norm_recon_loss(a, x)
+        (r * gr).sum().backward()
+        outs.append((r.detach(), a.grad))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    p64 = pre.double().requires_grad_(True)
+    r64 = ((F.normalize(p64, dim=-1, eps=1e-12) - x.double()) ** 2).sum(-1)
+    (r64 * gr.double()).sum().backward()
+    assert torch.allclose(outs[0][0].double(), r64.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(outs[0][1].double(), p64.grad, rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.parametrize("shape", [(11000, 512), (7, 128), (3, 5, 4096), (1, 4), (0, 64)])

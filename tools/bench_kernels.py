@@ -3,7 +3,7 @@
 
   python tools/bench_kernels.py [--rounds 5]
 
-Times rq_quantize_fwd_impl (1 = LDS-tiled, 2 = register-resident) at the BASELINE quantize
+Times rq_quantize_fwd with an explicit impl (1 = LDS-tiled, 2 = register-resident) at the BASELINE quantize
 shapes, the backward (rows + codebook reduction), jagged gather/scatter and varlen attention.
 Prints one JSON object per measurement.
 """
@@ -46,8 +46,8 @@ def quantize_case(B, D, K, L, dev):
 def run_impl(x, cbs, csq, o, impl, mode=3):
     B, D = x.shape
     L, K, _ = cbs.shape
-    call("rq_quantize_fwd_impl", ptr(x), B, D, ptr(cbs), ptr(csq), K, L, mode, 0.25, ptr(o["ids"]), ptr(o["emb"]),
-         ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), impl, stream_handle())
+    call("rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L, mode, 0.25, ptr(o["ids"]), ptr(o["emb"]),
+         ptr(o["res"]), ptr(o["ql"]), ptr(o["es"]), None, impl, stream_handle())
 
 
 def wgrad_bench(dev, rounds):

@@ -7,9 +7,9 @@ O="$R/gpurun_out"
 mkdir -p "$O"
 K="${1:-}"
 if [ -n "$K" ]; then
-  timeout -k 10 700 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 120 --timeout-method thread -k "$K" > "$O/gpu_tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 300 --timeout-method thread -k "$K" > "$O/gpu_tests.log" 2>&1
 else
-  timeout -k 10 700 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 300 --timeout-method thread > "$O/gpu_tests.log" 2>&1
 fi
 rc=$?
 tail -5 "$O/gpu_tests.log"

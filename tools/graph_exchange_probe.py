@@ -7,10 +7,14 @@ inside the graph (in_graph_exchange). Prints one JSON line: whether the collecti
 and the max |grad| difference of each replayed step against an eager step of an identical model
 copy (a one-rank all-reduce is the identity, so the gradients must match bit for bit).
 
-`race` (argv[2]): the capture runs while another thread keeps making HIP calls — it polls
-is_completed() of an eager all-reduce Work kept alive across the capture (what the process group's
-watchdog does) and pins host memory (what a trainer's feed thread does). Under the global capture mode
-such calls fail the capture (the round-3 watchdog abort); every capture here is thread-local."""
+`race` (argv[2]): the capture starts while an eager all-reduce is in flight and another thread does
+what the process group's watchdog does — polls the Work's is_completed() until it reports completion —
+and pins host memory (what a trainer's feed thread does). GraphedSteps quiesces (device sync + more
+than two watchdog periods) before an in-graph capture, so the exchange must be captured.
+`race_forever`: the poller never stops querying the (completed) Work: on ROCm that fails the capture
+even in thread-local mode ("dependency created on uncaptured work in another stream"), and
+GraphedSteps must fall back to the post-replay exchange with the same gradients.
+`race_pin`: pinning only (no poll)."""
 import copy
 import json
 import os
@@ -27,7 +31,7 @@ def main():
     port = sys.argv[1] if len(sys.argv) > 1 else "29533"
     mode = sys.argv[2] if len(sys.argv) > 2 else ""
     race = mode.startswith("race")
-    do_poll = race and mode in ("race", "race_poll", "race_poll_waited")
+    do_poll = race and mode in ("race", "race_forever")
     do_pin = race and mode in ("race", "race_pin")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     dev = torch.device("cuda", 0)
@@ -56,14 +60,12 @@ def main():
         if race and step == 1:   # step 1 captures: an eager collective in flight + a thread polling it
             side = torch.ones(1 << 20, device=dev)
             work = dist.all_reduce(side, async_op=True) if do_poll else None
-            if mode == "race_poll_waited":
-                work.wait()
-                torch.cuda.synchronize()
+            done = [work is None]
 
             def poll():
                 while not stop.is_set():
-                    if work is not None:
-                        work.is_completed()
+                    if not done[0]:   # the watchdog stops querying a Work once it has completed
+                        done[0] = work.is_completed() and mode != "race_forever"
                     if do_pin:
                         torch.empty(4096).pin_memory()
                     polls[0] += 1
