@@ -10,7 +10,7 @@ Execution: the L2-distance path (every config) runs the fused HIP kernel
 STE / eval output + VQ loss in one launch, and the matching VJP with a deterministic codebook
 gradient. GUMBEL_SOFTMAX training with the L2 distance (the reference's default codebook mode, differentiable
 through the full distance matrix) and the COSINE distance run as GPU torch composites of the same math; the
-Gumbel row kernels rq_gumbel_softmax_fwd / _bwd are parity-tested and opt-in (RQ_GUMBEL_HIP=1: slower than
+Gumbel row kernels rq_gumbel_softmax_fwd / _bwd are parity-tested and opt-in (GUMBEL_HIP = True: slower than
 the composite's library GEMMs as measured).
 """
 from enum import Enum

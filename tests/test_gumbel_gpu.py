@@ -1,17 +1,35 @@
 """Training-mode GUMBEL_SOFTMAX + L2 quantize on rq_gumbel_softmax_fwd / _bwd (modules/quantize.py:107-129,
-distributions/gumbel.py:14-18) against the torch composite of the reference math (RQ_GUMBEL_HIP=0 path),
-with the same injected noise: ids exact on margin-safe rows, emb / loss / grads within fp32 tolerance. The
-reference fixtures (tests/test_reference_fixtures_gpu.py::test_quantize_variant_vs_reference[gumbel*])
-pin the same path against the reference itself."""
+distributions/gumbel.py:14-18) against the reference math restated in fp64 on the CPU (`_ref64`, autograd for
+the gradients) with the same injected noise, next to the GPU torch composite (GUMBEL_HIP =
+False): ids exact on margin-safe rows; emb, loss, grad_x and grad_codebook within 3e-4 * max|fp64| — about 5x
+the largest kernel-vs-composite difference measured on MI355X (6.5e-5 * max, profiles/r03/gumbel_gpu_tests.txt)
+— and no further from fp64 than 5x the composite's own error. The reference fixtures
+(tests/test_reference_fixtures_gpu.py::test_quantize_variant_vs_reference[gumbel*-hip]) pin the same path
+against the reference itself."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
+def _ref64(x0, cb0, proj, noise, T, g_emb, beta=0.25):
+    """Reference Quantize.forward (modules/quantize.py:105-129,146 with distributions/gumbel.py:14-18 and
+    modules/loss.py:34-42) in fp64: (ids, emb, loss, grad_x, grad_codebook, dist) of the same objective."""
+    x = x0.double().requires_grad_(True)
+    w = cb0.double().requires_grad_(True)
+    codebook = w @ proj.double().t() if proj is not None else w
+    dist = (x ** 2).sum(1, keepdim=True) + (codebook.t() ** 2).sum(0, keepdim=True) - 2 * x @ codebook.t()
+    ids = dist.detach().min(1).indices
+    weights = torch.softmax((-dist + noise.double()) / T, dim=-1)
+    emb = weights @ codebook
+    loss = ((x.detach() - emb) ** 2).sum(-1) + beta * ((x - emb.detach()) ** 2).sum(-1)
+    ((emb * g_emb.double()).sum() + loss.sum()).backward()
+    return ids, emb.detach(), loss.detach(), x.grad, w.grad, dist.detach()
+
+
 @pytest.mark.parametrize("B,D,K,T,sim", [(1000, 32, 256, 0.5, False), (777, 64, 256, 0.2, False),
                                          (300, 16, 1000, 1.0, True), (65, 100, 64, 0.7, False)])
-def test_gumbel_hip_vs_composite(device, monkeypatch, B, D, K, T, sim):
+def test_gumbel_hip_vs_fp64(device, monkeypatch, B, D, K, T, sim):
     import distributions.gumbel as gumbel
     import modules.quantize as mq
     from modules.quantize import Quantize, QuantizeForwardMode
@@ -19,11 +37,11 @@ def test_gumbel_hip_vs_composite(device, monkeypatch, B, D, K, T, sim):
     x0 = torch.randn(B, D, generator=gen)
     cb0 = torch.randn(K, D, generator=gen) * 0.7
     u = torch.rand(B, K, generator=gen)
-    noise = (-torch.log(-torch.log(u + 1e-20) + 1e-20)).to(device)
-    monkeypatch.setattr(gumbel, "sample_gumbel", lambda shape, device, eps=1e-20: noise.reshape(shape))
-    g_emb = torch.randn(B, D, generator=gen).to(device)
-    out = {}
-    for hip in (True, False):
+    noise = -torch.log(-torch.log(u + 1e-20) + 1e-20)
+    g_emb = torch.randn(B, D, generator=gen)
+
+    def run(hip):
+        monkeypatch.setattr(gumbel, "sample_gumbel", lambda shape, device, eps=1e-20: noise.to(device).reshape(shape))
         monkeypatch.setattr(mq, "GUMBEL_HIP", hip)
         q = Quantize(D, K, do_kmeans_init=False, sim_vq=sim, forward_mode=QuantizeForwardMode.GUMBEL_SOFTMAX).to(device)
         with torch.no_grad():
@@ -33,29 +51,22 @@ def test_gumbel_hip_vs_composite(device, monkeypatch, B, D, K, T, sim):
         q.train(True)
         x = x0.clone().to(device).requires_grad_(True)
         o = q(x, temperature=T)
-        ((o.embeddings * g_emb).sum() + o.loss.sum()).backward()
-        out[hip] = (o.ids.cpu(), o.embeddings.detach().cpu(), o.loss.detach().cpu(), x.grad.cpu(),
-                    q.embedding.weight.grad.cpu())
-    a, b = out[True], out[False]
-    # fp64 truth of the forward from the same inputs and noise
-    cb = (cb0 @ (torch.eye(D) * 0.9).t() if sim else cb0).double()
-    xd = x0.double()
-    dist = (xd ** 2).sum(1, keepdim=True) + (cb ** 2).sum(1)[None] - 2 * xd @ cb.t()
-    w = torch.softmax((noise.cpu().double() - dist) / T, dim=1)
-    emb64 = w @ cb
+        ((o.embeddings * g_emb.to(device)).sum() + o.loss.sum()).backward()
+        return (o.ids.cpu(), o.embeddings.detach().cpu().double(), o.loss.detach().cpu().double(),
+                x.grad.cpu().double(), q.embedding.weight.grad.cpu().double())
+
+    hip, comp = run(True), run(False)
+    ref = _ref64(x0, cb0, torch.eye(D) * 0.9 if sim else None, noise, T, g_emb)
     # ids: exact where the two smallest distances are apart (fp32 dot orders differ between the paths)
+    dist = ref[5]
     top2 = dist.topk(2, dim=1, largest=False).values
     safe = (top2[:, 1] - top2[:, 0]) > 1e-4 * top2[:, 0].abs().clamp_min(1.0)
     assert safe.float().mean() > 0.9
-    assert torch.equal(a[0][safe], b[0][safe])
-    assert torch.equal(a[0][safe], dist.argmin(1)[safe])
-    # the HIP path is no further from fp64 than the torch composite (plus fp32 slack), and both agree
-    e_hip = (a[1].double() - emb64).abs().max().item()
-    e_ref = (b[1].double() - emb64).abs().max().item()
-    print(f"emb max |err| vs fp64: hip {e_hip:.3e}, composite {e_ref:.3e}")
-    assert e_hip <= 2 * e_ref + 1e-5, (e_hip, e_ref)
-    for i, name in ((2, "loss"), (3, "grad_x"), (4, "grad_codebook")):
-        d = (a[i] - b[i]).abs().max().item()
-        m = b[i].abs().max().item()
-        print(f"{name}: max |hip - composite| {d:.3e} (max |composite| {m:.3e})")
-        assert d <= 1e-2 * m + 1e-6, (name, d, m)   # the reference fixtures pin these tighter
+    assert torch.equal(hip[0][safe], ref[0][safe]) and torch.equal(comp[0][safe], ref[0][safe])
+    for i, name in ((1, "emb"), (2, "loss"), (3, "grad_x"), (4, "grad_codebook")):
+        m = ref[i].abs().max().item()
+        e_hip = (hip[i] - ref[i]).abs().max().item()
+        e_comp = (comp[i] - ref[i]).abs().max().item()
+        print(f"{name}: max |err| vs fp64 hip {e_hip:.3e}, composite {e_comp:.3e} (max |fp64| {m:.3e})")
+        assert e_hip <= 3e-4 * m, (name, e_hip, m)
+        assert e_hip <= 5 * e_comp + 1e-6 * m, (name, e_hip, e_comp)

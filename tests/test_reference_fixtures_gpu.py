@@ -50,10 +50,17 @@ _SPEC = {   # name: (forward_mode, distance, sim_vq, codebook_normalize, trainin
 }
 
 
-@pytest.mark.parametrize("name", VARIANTS)
-def test_quantize_variant_vs_reference(golden, device, monkeypatch, name):
+# the Gumbel-softmax training variants run both on the GPU torch composite (the default) and on the HIP row
+# kernels (modules.quantize.GUMBEL_HIP = True)
+_CASES = [(n, False) for n in VARIANTS] + [(n, True) for n in VARIANTS if "gumbel" in n and _SPEC[n][4]]
+
+
+@pytest.mark.parametrize("name,hip", _CASES, ids=[n + ("-hip" if h else "") for n, h in _CASES])
+def test_quantize_variant_vs_reference(golden, device, monkeypatch, name, hip):
     import distributions.gumbel as gumbel
+    import modules.quantize as mq
     from modules.quantize import Quantize, QuantizeDistance, QuantizeForwardMode
+    monkeypatch.setattr(mq, "GUMBEL_HIP", hip)
     z = golden("quantize_variants")
     B, D, K, seed = (int(z[k]) for k in ("B", "D", "K", "seed"))
     noise = gi.gumbel_noise((B, K), seed + 2)
