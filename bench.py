@@ -517,6 +517,8 @@ def measure_extras(model, device, x):
         out["b64_hipgraph_error"] = repr(e)[:300]
     out["quantize_synthetic"] = measure_quantize_synthetic(device)
     out["jagged_c5"] = measure_jagged_c5(device)
+    out["quantize_c5_rank"] = measure_quantize_c5_rank(device)
+    out["jagged_c5_rank"] = measure_jagged_c5_rank(device)
     return out
 
 
@@ -559,6 +561,101 @@ def measure_jagged_c5(device, B=4096, max_items=256, L1=5, D=128, reps=10):
     del x, vals, back
     torch.cuda.empty_cache()
     return res
+
+
+def _events_ms(fn):
+    """fn() bracketed by HIP events on torch's current stream (the stream every op here launches on)."""
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b)
+
+
+def measure_quantize_c5_rank(device, items=1_250_000, chunk=65536, D=1024, K=2048, L=4):
+    """BASELINE configs[4] at its per-rank scale: 10 M items over 8 GPUs = 1.25 M items of D = 1,024 per GPU
+    (5.1 GB fp32, resident before timing), streamed through the L = 4, K = 2,048 residual quantization in
+    65,536-item chunks — forward alone, then forward + backward (the codebook gradient accumulating over the
+    chunks, grad of the residual input per chunk), HIP events around the whole stream. FLOPs: 2 K D L per
+    item, the forward's distance GEMMs."""
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(91)
+    x = torch.randn(items, D, generator=g, device=device)
+    x = x / x.norm(dim=1, keepdim=True)
+    cbs = torch.randn(L, K, D, generator=g, device=device)
+    cbs = cbs / cbs.norm(dim=2, keepdim=True) * torch.tensor([1.0, 0.5, 0.25, 0.125], device=device).view(L, 1, 1)
+    cbs.requires_grad_(True)
+    spans = [(a, min(items, a + chunk)) for a in range(0, items, chunk)]
+
+    def fwd():
+        with torch.no_grad():
+            for a, b in spans:
+                ops.rq_quantize(x[a:b], cbs, ops.MODE_ROTATION, 0.25)
+
+    def fwd_bwd():
+        for a, b in spans:
+            r = x[a:b].detach().requires_grad_(True)
+            emb, res, ids, ql, es = ops.rq_quantize(r, cbs, ops.MODE_ROTATION, 0.25)
+            (es.sum() + ql.sum()).backward()
+    ops.rq_quantize(x[:chunk], cbs.detach(), ops.MODE_ROTATION, 0.25)   # warm-up (library init, plans)
+    t_f = _events_ms(fwd)
+    cbs.grad = None
+    t_fb = _events_ms(fwd_bwd)
+    tf = 2.0 * K * D * L * items / (t_f * 1e-3) / 1e12
+    out = {"shape": {"items": items, "chunk": chunk, "D": D, "K": K, "L": L}, "fwd_ms": round(t_f, 2),
+           "fwd_items_per_s": round(items / (t_f * 1e-3), 1), "fwd_TFLOPs": round(tf, 2),
+           "fwd_frac_fp32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "fwd_bwd_ms": round(t_fb, 2),
+           "fwd_bwd_items_per_s": round(items / (t_fb * 1e-3), 1),
+           "note": "1.25 M items = 10 M / 8 GPUs (BASELINE configs[4]); inputs resident in HBM before timing"}
+    del x, cbs
+    torch.cuda.empty_cache()
+    return out
+
+
+def measure_jagged_c5_rank(device, sequences=1 << 20, chunk=4096, max_items=256, L1=5, D=128):
+    """BASELINE configs[4]'s jagged half at a per-rank scale: 1,048,576 user sequences (50 M over 8 GPUs is
+    6.25 M; 1 M already moves ~0.7 TB) of 5 U{2..256} + 1 context rows x D = 128 fp32, streamed in chunks of
+    4,096 sequences through padded -> jagged (+1-1 rounding) and back (zero-filled scatter). The length
+    stream is seeded; every chunk's offsets are built before timing; one padded buffer serves every chunk
+    (a byte mover: contents do not change its work). Algorithmic bytes as measure_jagged_c5."""
+    from rqvae_hip import ops
+    from rqvae_hip._lib import call, ptr, stream_handle
+    g = np.random.Generator(np.random.PCG64(6))
+    lens = L1 * g.integers(2, max_items + 1, size=sequences) + 1
+    N = L1 * max_items + 1
+    x = torch.randn(chunk, N, D, device=device)
+    chunks = []
+    for a in range(0, sequences, chunk):
+        ln = lens[a:a + chunk]
+        chunks.append((ops.jagged_offsets(torch.from_numpy(ln).to(device), N), int(ln.sum()), len(ln)))
+    T_max = max(c[1] for c in chunks)
+    vals = torch.empty((T_max, D), device=device)
+    back = torch.empty_like(x)
+    st = stream_handle(device)
+
+    def gather():
+        for off, T, B in chunks:
+            call("jagged_from_padded_rows", ptr(x), B, N, D, ptr(off), ptr(vals), T, 0, 1, st)
+
+    def scatter():
+        for off, T, B in chunks:
+            call("jagged_to_padded", ptr(vals), ptr(off), B, N, D, ptr(back), 0, st)
+    off0, T0, B0 = chunks[0]
+    call("jagged_from_padded_rows", ptr(x), B0, N, D, ptr(off0), ptr(vals), T0, 0, 1, st)   # warm-up
+    tg, ts = _events_ms(gather), _events_ms(scatter)
+    T_all = int(lens.sum())
+    gb_g, gb_s = 2.0 * 4 * D * T_all / 1e9, 4.0 * D * (sequences * N + T_all) / 1e9
+    out = {"shape": {"sequences": sequences, "chunk": chunk, "max_rows": N, "D": D, "valid_rows": T_all},
+           "gather_ms": round(tg, 2), "scatter_ms": round(ts, 2),
+           "gather_rows_per_s": round(T_all / (tg * 1e-3), 1), "sequences_per_s": round(sequences / (tg * 1e-3), 1),
+           "gather_GBps": round(gb_g / (tg * 1e-3), 1), "scatter_GBps": round(gb_s / (ts * 1e-3), 1),
+           "gather_hbm_frac": round(gb_g / (tg * 1e-3) / HBM_PEAK_GBS, 4),
+           "scatter_hbm_frac": round(gb_s / (ts * 1e-3) / HBM_PEAK_GBS, 4)}
+    del x, vals, back, chunks
+    torch.cuda.empty_cache()
+    return out
 
 
 def measure_quantize_synthetic(device, B=16384, D=1024, K=2048, L=4):
