@@ -119,19 +119,30 @@ def time_region(fn, steps, warmup, sync_all):
 
 def gemm_launch_stats(timer, steps=1):
     """Split-bf16 GEMM launches recorded in the kernel-statistics pass (ops.TIMER keys
-    'gemm_bf16x3:MxNxK:<a_kc><b_kc>'): the shape with the largest total device time, its mean
-    launch time, fp32-matmul TFLOP/s (2MNK / time) and algorithmic bytes (fp32 A, B in, C out),
-    plus the aggregate over every GEMM launch of the step."""
+    'gemm_bf16x3:MxNxK:<a_kc><b_kc>...' and 'gemm_pair:<key1>+<key2>'): the single launch shape with the
+    largest total device time, its mean launch time, fp32-matmul TFLOP/s (2MNK / time) and algorithmic
+    bytes (fp32 A, B in, C out), plus the aggregate over every GEMM launch of the step (paired ones too)."""
     keys = [k for k in timer.events if k.startswith("gemm_bf16x3:")]
+    pairs = [k for k in timer.events if k.startswith("gemm_pair:")]   # one launch, two problems
     if not keys:
         return None
-    tot_ms, tot_flops, best = 0.0, 0.0, None
+
+    def mnk(k):
+        return tuple(int(v) for v in k.split(":")[1].split("x"))
+    tot_ms, tot_flops, best, n_launch = 0.0, 0.0, None, 0
+    for k in pairs:
+        ms, n = timer.mean_ms(k)
+        k1, k2 = k[len("gemm_pair:"):].split("+")
+        tot_ms += ms * n
+        tot_flops += sum(2.0 * a * b * c for a, b, c in (mnk(k1), mnk(k2))) * n
+        n_launch += n
     for k in keys:
         ms, n = timer.mean_ms(k)
-        M, N, K = (int(v) for v in k.split(":")[1].split("x"))
+        M, N, K = mnk(k)
         lay = [int(c) for c in k.split(":")[2]] + [0, 0, 0]
         tot_ms += ms * n
         tot_flops += 2.0 * M * N * K * n
+        n_launch += n
         # the roofline kernel: the largest-time launch with the plain epilogue (a PMC driver can
         # replay exactly that variant: same shape, layouts and operand formats)
         if lay[4] == 0 and (best is None or ms * n > best[0]):
@@ -145,8 +156,12 @@ def gemm_launch_stats(timer, steps=1):
             "launch_ms": round(ms, 4), "launches": n,
             "flops_per_launch": 2 * M * N * K, "algorithmic_bytes": 4 * (M * K + N * K + M * N),
             "achieved_tflops": round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 2),
-            "all_gemm_launches": {"count": sum(timer.mean_ms(k)[1] for k in keys), "ms_per_step_total": round(tot_ms / steps, 4),
-                                  "tflops": round(tot_flops / (tot_ms * 1e-3) / 1e12, 2)}}
+            "all_gemm_launches": {"launches_per_step": round(n_launch / steps, 1),
+                                  "paired_launches_per_step": round(sum(timer.mean_ms(k)[1] for k in pairs) / steps, 1),
+                                  "ms_per_step_total": round(tot_ms / steps, 4),
+                                  "tflops": round(tot_flops / (tot_ms * 1e-3) / 1e12, 2),
+                                  "note": "every split-bf16 GEMM launch of the step (single and paired: one launch, "
+                                          "two problems' FLOPs), device time by HIP events over 5 steps"}}
 
 
 def quantize_algorithmic_bytes(B, D, K, L):

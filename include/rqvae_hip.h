@@ -282,6 +282,17 @@ int rq_l2norm_recon_bwd(const float* pre, const float* x, const float* norms, co
  * decoder MLP's last data-grad / weight-grad GEMMs at matmul precision 'high'. */
 int rq_l2norm_recon_bwd_split(const float* pre, const float* x, const float* norms, const float* g_recon, int64_t B,
                               int64_t C, uint16_t* g_hi, uint16_t* g_lo, void* stream);
+/* rq_l2norm_recon_fwd plus, in the same pass over pre and x, the split gradient rq_l2norm_recon_bwd_split
+ * would write if g_recon[b] = gs for every row (the batch-mean loss, loss_means: gs = 1 / B) — speculative:
+ * the backward then only checks g_recon (rq_l2norm_recon_bwd_fix) instead of reading pre and x again. */
+int rq_l2norm_recon_fwd_grad(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
+                             float gs, uint16_t* g_hi, uint16_t* g_lo, void* stream);
+/* The backward after rq_l2norm_recon_fwd_grad: rows whose g_recon[b * g_stride] (g_stride 0: one value for
+ * every row, 1: one per row) is bitwise gs keep the planes the forward wrote; every other row is recomputed
+ * with rq_l2norm_recon_bwd_split's arithmetic (same bits as that call). */
+int rq_l2norm_recon_bwd_fix(const float* pre, const float* x, const float* norms, const float* g_recon,
+                            int64_t g_stride, int64_t B, int64_t C, float gs, uint16_t* g_hi, uint16_t* g_lo,
+                            void* stream);
 
 /* RqVae.forward statistics (modules/rqvae.py:151-162):
  *   rq_row_norms   out[r] = |x_r|_2 for rows (rows, D), D % 4 == 0 — embs_norm = emb.norm(dim=-1)

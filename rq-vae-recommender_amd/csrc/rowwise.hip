@@ -15,115 +15,132 @@
 
 namespace rqhip {
 
-template <int VPL, int RPW>   // float4 vectors per lane (C = 256 * VPL); rows per wave, all loads issued first
-__global__ void __launch_bounds__(256) l2norm_recon_fwd_kernel(const float* __restrict__ pre, const float* __restrict__ x,
-                                                                int64_t B, int C, float* __restrict__ recon,
-                                                                float* __restrict__ nrm) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  if (r0 >= B) return;
-  float4 pv[RPW][VPL], xv[RPW][VPL];
+// The gradient of one row from its values in registers (pre: av, x: bv, zero past C), its norm
+// |pre_r| (raw) and g_recon[r] (gr): shared by the backward kernel and the forward's speculative
+// gradient, so the two write the same bits for the same gr.
+template <int VPL, bool SPLIT>
+__device__ __forceinline__ void l2r_grad_row(const float4 (&av)[VPL], const float4 (&bv)[VPL], float raw, float gr,
+                                             int64_t r, int C, int lane, float* __restrict__ g_pre,
+                                             uint16_t* __restrict__ g_hi, uint16_t* __restrict__ g_lo) {
+  const float n = fmaxf(raw, 1e-12f);
+  const float g2 = 2.f * gr;
+  float4 yv[VPL], gy[VPL];
+  float dot = 0.f;
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const bool row = r0 + i < B;
-    const float* p = pre + (r0 + i) * C;
-    const float* q = x + (r0 + i) * C;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int c = (v * 64 + lane) * 4;
-      const bool ok = row && c < C;
-      pv[i][v] = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      xv[i][v] = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  for (int v = 0; v < VPL; ++v) {
+    const float4 a = av[v], b = bv[v];
+    yv[v] = make_float4(a.x / n, a.y / n, a.z / n, a.w / n);
+    gy[v] = make_float4(g2 * (yv[v].x - b.x), g2 * (yv[v].y - b.y), g2 * (yv[v].z - b.z), g2 * (yv[v].w - b.w));
+    dot += gy[v].x * yv[v].x + gy[v].y * yv[v].y + gy[v].z * yv[v].z + gy[v].w * yv[v].w;
   }
+  dot = group_sum<64>(dot);
+  const bool clamped = !(raw > 1e-12f);
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    float s = 0.f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v)
-      s += pv[i][v].x * pv[i][v].x + pv[i][v].y * pv[i][v].y + pv[i][v].z * pv[i][v].z + pv[i][v].w * pv[i][v].w;
-    s = group_sum<64>(s);
-    const float n = fmaxf(sqrtf(s), 1e-12f);
-    float acc = 0.f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      if ((v * 64 + lane) * 4 >= C) continue;
-      const float d0 = pv[i][v].x / n - xv[i][v].x, d1 = pv[i][v].y / n - xv[i][v].y;
-      const float d2 = pv[i][v].z / n - xv[i][v].z, d3 = pv[i][v].w / n - xv[i][v].w;
-      acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    if (c >= C) continue;
+    float4 o;
+    if (clamped) {
+      o = make_float4(gy[v].x / n, gy[v].y / n, gy[v].z / n, gy[v].w / n);
+    } else {
+      o = make_float4((gy[v].x - yv[v].x * dot) / n, (gy[v].y - yv[v].y * dot) / n, (gy[v].z - yv[v].z * dot) / n,
+                      (gy[v].w - yv[v].w * dot) / n);
     }
-    acc = group_sum<64>(acc);
-    if (lane == 0 && r0 + i < B) {
-      recon[r0 + i] = acc;
-      nrm[r0 + i] = sqrtf(s);
-    }
+    if constexpr (SPLIT)
+      split_store4(o, g_hi + r * C + c, g_lo + r * C + c);
+    else
+      *reinterpret_cast<float4*>(g_pre + r * C + c) = o;
   }
 }
 
-template <int VPL, bool SPLIT, int RPW>
+template <int VPL>
+__device__ __forceinline__ void l2r_load_row(const float* __restrict__ pre, const float* __restrict__ x, int64_t r,
+                                             int C, int lane, float4 (&pv)[VPL], float4 (&xv)[VPL]) {
+  const float* p = pre + r * C;
+  const float* q = x + r * C;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    const bool ok = c < C;
+    pv[v] = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xv[v] = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// Forward, one row per wave (C = 256 VPL at most). GRAD: also the split gradient the backward would
+// write for g_recon[r] = gs (the batch-mean loss's uniform 1 / B): the backward then only checks g_recon
+// (l2norm_recon_fix_kernel) instead of reading pre and x again.
+template <int VPL, bool GRAD>
+__global__ void __launch_bounds__(256) l2norm_recon_fwd_kernel(const float* __restrict__ pre, const float* __restrict__ x,
+                                                                int64_t B, int C, float* __restrict__ recon,
+                                                                float* __restrict__ nrm, float gs,
+                                                                uint16_t* __restrict__ g_hi, uint16_t* __restrict__ g_lo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float4 pv[VPL], xv[VPL];
+  l2r_load_row<VPL>(pre, x, r, C, lane, pv, xv);
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) s += pv[v].x * pv[v].x + pv[v].y * pv[v].y + pv[v].z * pv[v].z + pv[v].w * pv[v].w;
+  s = group_sum<64>(s);
+  const float n = fmaxf(sqrtf(s), 1e-12f);
+  float acc = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    if ((v * 64 + lane) * 4 >= C) continue;
+    const float d0 = pv[v].x / n - xv[v].x, d1 = pv[v].y / n - xv[v].y;
+    const float d2 = pv[v].z / n - xv[v].z, d3 = pv[v].w / n - xv[v].w;
+    acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+  }
+  acc = group_sum<64>(acc);
+  if (lane == 0) {
+    recon[r] = acc;
+    nrm[r] = sqrtf(s);
+  }
+  if constexpr (GRAD) l2r_grad_row<VPL, true>(pv, xv, sqrtf(s), gs, r, C, lane, nullptr, g_hi, g_lo);
+}
+
+// Backward, one row per wave.
+template <int VPL, bool SPLIT>
 __global__ void __launch_bounds__(256) l2norm_recon_bwd_kernel(const float* __restrict__ pre, const float* __restrict__ x,
                                                                 const float* __restrict__ nrm,
                                                                 const float* __restrict__ g_recon, int64_t B, int C,
                                                                 float* __restrict__ g_pre, uint16_t* __restrict__ g_hi,
                                                                 uint16_t* __restrict__ g_lo) {
   const int lane = threadIdx.x & 63;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  if (r0 >= B) return;
-  float4 av[RPW][VPL], bv[RPW][VPL];
-  float raw[RPW], g2[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const bool row = r0 + i < B;
-    const float* p = pre + (r0 + i) * C;
-    const float* q = x + (r0 + i) * C;
-    raw[i] = row ? nrm[r0 + i] : 1.f;
-    g2[i] = row ? 2.f * g_recon[r0 + i] : 0.f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int c = (v * 64 + lane) * 4;
-      const bool ok = row && c < C;
-      av[i][v] = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      bv[i][v] = ok ? *reinterpret_cast<const float4*>(q + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float4 av[VPL], bv[VPL];
+  const float raw = nrm[r], gr = g_recon[r];
+  l2r_load_row<VPL>(pre, x, r, C, lane, av, bv);
+  l2r_grad_row<VPL, SPLIT>(av, bv, raw, gr, r, C, lane, g_pre, g_hi, g_lo);
+}
+
+// Backward after a GRAD forward: rows whose g_recon[r g_stride] is bitwise gs already hold their split
+// gradient; any other row (a weighted or scaled loss) is recomputed from pre and x. Waves stride over
+// the rows (at most 2,048 workgroups, not one per row: the common case reads one scalar per wave).
+template <int VPL>
+__global__ void __launch_bounds__(256) l2norm_recon_fix_kernel(const float* __restrict__ pre, const float* __restrict__ x,
+                                                                const float* __restrict__ nrm,
+                                                                const float* __restrict__ g_recon, int64_t g_stride,
+                                                                int64_t B, int C, uint32_t gs_bits,
+                                                                uint16_t* __restrict__ g_hi, uint16_t* __restrict__ g_lo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    const float gr = g_recon[r * g_stride];
+    if (__float_as_uint(gr) == gs_bits) {
+      if (g_stride == 0) return;   // one value for every row: all done
+      continue;
     }
-  }
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int64_t r = r0 + i;
-    const float n = fmaxf(raw[i], 1e-12f);
-    float4 yv[VPL], gy[VPL];
-    float dot = 0.f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const float4 a = av[i][v], b = bv[i][v];
-      yv[v] = make_float4(a.x / n, a.y / n, a.z / n, a.w / n);
-      gy[v] = make_float4(g2[i] * (yv[v].x - b.x), g2[i] * (yv[v].y - b.y), g2[i] * (yv[v].z - b.z),
-                          g2[i] * (yv[v].w - b.w));
-      dot += gy[v].x * yv[v].x + gy[v].y * yv[v].y + gy[v].z * yv[v].z + gy[v].w * yv[v].w;
-    }
-    dot = group_sum<64>(dot);
-    if (r >= B) continue;
-    const bool clamped = !(raw[i] > 1e-12f);
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int c = (v * 64 + lane) * 4;
-      if (c >= C) continue;
-      float4 o;
-      if (clamped) {
-        o = make_float4(gy[v].x / n, gy[v].y / n, gy[v].z / n, gy[v].w / n);
-      } else {
-        o = make_float4((gy[v].x - yv[v].x * dot) / n, (gy[v].y - yv[v].y * dot) / n, (gy[v].z - yv[v].z * dot) / n,
-                        (gy[v].w - yv[v].w * dot) / n);
-      }
-      if constexpr (SPLIT)
-        split_store4(o, g_hi + r * C + c, g_lo + r * C + c);
-      else
-        *reinterpret_cast<float4*>(g_pre + r * C + c) = o;
-    }
+    float4 av[VPL], bv[VPL];
+    l2r_load_row<VPL>(pre, x, r, C, lane, av, bv);
+    l2r_grad_row<VPL, true>(av, bv, nrm[r], gr, r, C, lane, nullptr, g_hi, g_lo);
   }
 }
 
-// The launches run one row per wave (the kernels' RPW = 1): 2 or 4 rows per wave were no faster at
-// 65,536 x 768 (profiles/r02/l2r_rpw_ab.txt).
+// One row per wave: 2 or 4 rows per wave were no faster at 65,536 x 768 (profiles/r02/l2r_rpw_ab.txt).
 
 // ---------------------------------------------------------------------------------------
 // RMSNorm (modules/normalize.py:22-32): t = x * rsqrt(mean(x^2) + eps), y = t * w.
@@ -640,23 +657,67 @@ int rq_col_sum(const float* P, int64_t S, int64_t n, float* out, int accumulate,
   return 0;
 }
 
-int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
-                        void* stream) {
-  RQ_CHECK_ARG(pre && x && recon && norms, "rq_l2norm_recon_fwd: null pointer");
+#define L2R_VPL_SWITCH(CASE)                                                                      \
+  switch (vpl) {                                                                                  \
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) \
+    CASE(13) CASE(14) CASE(15) CASE(16)                                                           \
+  }
+
+static int l2norm_recon_fwd_launch(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
+                                   float gs, uint16_t* g_hi, uint16_t* g_lo, void* stream) {
   RQ_CHECK_ARG(B >= 0 && C > 0 && C % 4 == 0 && C <= 4096, "rq_l2norm_recon_fwd: need C %% 4 == 0, C <= 4096");
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int vpl = (int)((C + 255) / 256);
   const dim3 g((unsigned)((B + 3) / 4));
-#define L2R_LAUNCH(V, R) hipLaunchKernelGGL((l2norm_recon_fwd_kernel<V, R>), g, dim3(256), 0, s, pre, x, B, (int)C, recon, norms)
-#define L2R_CASE1(V) case V: L2R_LAUNCH(V, 1); break;
-  switch (vpl) {
-    L2R_CASE1(1) L2R_CASE1(2) L2R_CASE1(3) L2R_CASE1(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
-    L2R_CASE1(9) L2R_CASE1(10) L2R_CASE1(11) L2R_CASE1(12) L2R_CASE1(13) L2R_CASE1(14) L2R_CASE1(15) L2R_CASE1(16)
-  }
-#undef L2R_CASE1
-#undef L2R_LAUNCH
+  const bool grad = g_hi != nullptr;
+#define L2R_CASE(V)                                                                                              \
+  case V:                                                                                                        \
+    if (grad)                                                                                                    \
+      hipLaunchKernelGGL((l2norm_recon_fwd_kernel<V, true>), g, dim3(256), 0, s, pre, x, B, (int)C, recon, norms, \
+                         gs, g_hi, g_lo);                                                                        \
+    else                                                                                                         \
+      hipLaunchKernelGGL((l2norm_recon_fwd_kernel<V, false>), g, dim3(256), 0, s, pre, x, B, (int)C, recon,      \
+                         norms, gs, g_hi, g_lo);                                                                 \
+    break;
+  L2R_VPL_SWITCH(L2R_CASE)
+#undef L2R_CASE
   RQ_LAUNCH_CHECK("rq_l2norm_recon_fwd");
+  return 0;
+}
+
+int rq_l2norm_recon_fwd(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
+                        void* stream) {
+  RQ_CHECK_ARG(pre && x && recon && norms, "rq_l2norm_recon_fwd: null pointer");
+  return l2norm_recon_fwd_launch(pre, x, B, C, recon, norms, 0.f, nullptr, nullptr, stream);
+}
+
+int rq_l2norm_recon_fwd_grad(const float* pre, const float* x, int64_t B, int64_t C, float* recon, float* norms,
+                             float gs, uint16_t* g_hi, uint16_t* g_lo, void* stream) {
+  RQ_CHECK_ARG(pre && x && recon && norms && g_hi && g_lo, "rq_l2norm_recon_fwd_grad: null pointer");
+  RQ_CHECK_ARG(((uintptr_t)g_hi | (uintptr_t)g_lo) % 8 == 0, "rq_l2norm_recon_fwd_grad: planes must be 8-byte aligned");
+  return l2norm_recon_fwd_launch(pre, x, B, C, recon, norms, gs, g_hi, g_lo, stream);
+}
+
+int rq_l2norm_recon_bwd_fix(const float* pre, const float* x, const float* norms, const float* g_recon,
+                            int64_t g_stride, int64_t B, int64_t C, float gs, uint16_t* g_hi, uint16_t* g_lo,
+                            void* stream) {
+  RQ_CHECK_ARG(pre && x && norms && g_recon && g_hi && g_lo && (g_stride == 0 || g_stride == 1),
+               "rq_l2norm_recon_bwd_fix: bad arguments");
+  RQ_CHECK_ARG(B >= 0 && C > 0 && C % 4 == 0 && C <= 4096, "rq_l2norm_recon_bwd_fix: need C %% 4 == 0, C <= 4096");
+  if (B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int vpl = (int)((C + 255) / 256);
+  const dim3 g((unsigned)std::min<int64_t>((B + 3) / 4, 2048));
+  const uint32_t bits = __builtin_bit_cast(uint32_t, gs);
+#define L2R_CASE(V)                                                                                                  \
+  case V:                                                                                                            \
+    hipLaunchKernelGGL((l2norm_recon_fix_kernel<V>), g, dim3(256), 0, s, pre, x, norms, g_recon, g_stride, B, (int)C, \
+                       bits, g_hi, g_lo);                                                                            \
+    break;
+  L2R_VPL_SWITCH(L2R_CASE)
+#undef L2R_CASE
+  RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd_fix");
   return 0;
 }
 
@@ -668,14 +729,11 @@ static int l2norm_recon_bwd_launch(const float* pre, const float* x, const float
   const int vpl = (int)((C + 255) / 256);
   const dim3 g((unsigned)((B + 3) / 4));
   const bool sp = g_hi != nullptr;
-#define L2R_LAUNCH(V, SP, R)                                                                                     \
-  hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, SP, R>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, \
+#define L2R_LAUNCH(V, SP)                                                                                     \
+  hipLaunchKernelGGL((l2norm_recon_bwd_kernel<V, SP>), g, dim3(256), 0, s, pre, x, norms, g_recon, B, (int)C, \
                      g_pre, g_hi, g_lo)
-#define L2R_CASE1(V) case V: if (sp) L2R_LAUNCH(V, true, 1); else L2R_LAUNCH(V, false, 1); break;
-  switch (vpl) {
-    L2R_CASE1(1) L2R_CASE1(2) L2R_CASE1(3) L2R_CASE1(4) L2R_CASE1(5) L2R_CASE1(6) L2R_CASE1(7) L2R_CASE1(8)
-    L2R_CASE1(9) L2R_CASE1(10) L2R_CASE1(11) L2R_CASE1(12) L2R_CASE1(13) L2R_CASE1(14) L2R_CASE1(15) L2R_CASE1(16)
-  }
+#define L2R_CASE1(V) case V: if (sp) L2R_LAUNCH(V, true); else L2R_LAUNCH(V, false); break;
+  L2R_VPL_SWITCH(L2R_CASE1)
 #undef L2R_CASE1
 #undef L2R_LAUNCH
   RQ_LAUNCH_CHECK("rq_l2norm_recon_bwd");

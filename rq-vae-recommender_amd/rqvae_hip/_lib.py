@@ -66,6 +66,8 @@ _SIGS = {
     "rq_gumbel_softmax_bwd": ([_P, _P, _P, _P, _I64, _I64, _I64, _F, _P, _P, _P], _I),
     "rq_l2norm_recon_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P], _I),
     "rq_l2norm_recon_bwd_split": ([_P, _P, _P, _P, _I64, _I64, _P, _P, _P], _I),
+    "rq_l2norm_recon_fwd_grad": ([_P, _P, _I64, _I64, _P, _P, _F, _P, _P, _P], _I),
+    "rq_l2norm_recon_bwd_fix": ([_P, _P, _P, _P, _I64, _I64, _I64, _F, _P, _P, _P], _I),
     "jagged_offsets": ([_P, _I64, _I64, _P, _P], _I),
     "jagged_from_padded": ([_P, _I64, _I64, _I64, _P, _P, _I, _I, _P], _I),
     "jagged_from_padded_rows": ([_P, _I64, _I64, _I64, _P, _P, _I64, _I, _I, _P], _I),

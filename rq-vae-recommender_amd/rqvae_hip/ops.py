@@ -797,19 +797,31 @@ class MLPL2ReconFunction(torch.autograd.Function):
     """The RqVae decoder (modules/rqvae.py:145-148: MLP chain ending in l2norm, modules/encoder.py:34)
     fused with ReconstructionLoss (modules/loss.py:5-10): recon_b = |l2norm(MLP(e)_b) - x_b|^2 at
     'high' matmul precision. Same as MLPFunction followed by L2NormReconFunction, except that the
-    row kernel's backward emits the output gradient already split (rq_l2norm_recon_bwd_split), so the
-    chain's last data-grad and weight-grad GEMMs take split operands (the wide kernel) without a
-    conversion pass. Gradients w.r.t. e and the weights (x is data)."""
+    output gradient comes already split, so the chain's last data-grad and weight-grad GEMMs take split
+    operands (the wide kernel) without a conversion pass — and it is written by the forward's row pass
+    for the batch-mean loss's g_recon = 1 / B (rq_l2norm_recon_fwd_grad; the backward's
+    rq_l2norm_recon_bwd_fix recomputes any row whose g_recon differs, bitwise the unspeculated result).
+    Gradients w.r.t. e and the weights (x is data)."""
 
     @staticmethod
-    def forward(ctx, e, x, p: float, *weights):
+    def forward(ctx, e, x, p: float, grad_mode: bool, *weights):
         x_in, rows, wsp, seeds = _mlp_prologue(e, p, weights)
         pre, zs, hs = _mlp_forward(x_in, wsp, rows, p, seeds)
         x2 = x.reshape(rows, -1).contiguous()
         C = pre.shape[1]
         recon = torch.empty((rows,), device=pre.device, dtype=torch.float32)
         norms = torch.empty((rows,), device=pre.device, dtype=torch.float32)
-        call("rq_l2norm_recon_fwd", ptr(pre), ptr(x2), rows, C, ptr(recon), ptr(norms), stream_handle(pre.device))
+        ctx.g, ctx.gs = None, 0.0
+        if grad_mode and any(ctx.needs_input_grad):
+            # the batch-mean loss (loss_means) hands every row g_recon = 1 / B: its split gradient is written
+            # in this pass over pre and x, and the backward only checks g_recon (rq_l2norm_recon_bwd_fix)
+            ctx.gs = float(torch.tensor(1.0, dtype=torch.float32) / rows)
+            ctx.g = Split(torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16),
+                          torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16))
+            call("rq_l2norm_recon_fwd_grad", ptr(pre), ptr(x2), rows, C, ptr(recon), ptr(norms), ctx.gs,
+                 ptr(ctx.g.hi), ptr(ctx.g.lo), stream_handle(pre.device))
+        else:
+            call("rq_l2norm_recon_fwd", ptr(pre), ptr(x2), rows, C, ptr(recon), ptr(norms), stream_handle(pre.device))
         ctx.n, ctx.p, ctx.seeds, ctx.eshape, ctx.weights = len(weights), float(p), seeds, e.shape, weights
         ctx.save_for_backward(*_mlp_save(ctx, x_in, wsp, zs, hs), pre, x2, norms)
         return recon.view(e.shape[:-1])
@@ -819,21 +831,29 @@ class MLPL2ReconFunction(torch.autograd.Function):
         x_in, wsp, zs, hs, k = _mlp_load(ctx, ctx.n, ctx.saved_tensors)
         pre, x2, norms = ctx.saved_tensors[k:k + 3]
         rows, C = pre.shape
-        g = Split(torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16),
-                  torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16))
-        call("rq_l2norm_recon_bwd_split", ptr(pre), ptr(x2), ptr(norms), ptr(g_recon.contiguous()), rows, C, ptr(g.hi),
-             ptr(g.lo), stream_handle(pre.device))
-        de, dws = _mlp_backward(g, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[3:],
+        g_recon = g_recon.reshape(rows)
+        if ctx.g is not None:   # the forward's planes, rows with another g_recon recomputed
+            g, ctx.g = ctx.g, None
+            uniform = g_recon.stride(0) == 0   # the mean's expand: one value for every row
+            gr = g_recon if uniform else g_recon.contiguous()
+            call("rq_l2norm_recon_bwd_fix", ptr(pre), ptr(x2), ptr(norms), ptr(gr), 0 if uniform else 1, rows, C,
+                 ctx.gs, ptr(g.hi), ptr(g.lo), stream_handle(pre.device))
+        else:   # a second backward through the same graph: the planes were handed out already
+            g = Split(torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16),
+                      torch.empty((rows, C), device=pre.device, dtype=torch.bfloat16))
+            call("rq_l2norm_recon_bwd_split", ptr(pre), ptr(x2), ptr(norms), ptr(g_recon.contiguous()), rows, C,
+                 ptr(g.hi), ptr(g.lo), stream_handle(pre.device))
+        de, dws = _mlp_backward(g, x_in, wsp, zs, hs, rows, ctx.p, ctx.seeds, ctx.needs_input_grad[4:],
                                 ctx.needs_input_grad[0], ctx.weights)
         ctx.weights = None
-        return (None if de is None else de.view(ctx.eshape), None, None, *dws)
+        return (None if de is None else de.view(ctx.eshape), None, None, None, *dws)
 
 
 def mlp_l2norm_recon(e: torch.Tensor, x: torch.Tensor, weights, p: float = 0.0) -> torch.Tensor:
     """recon_b = |l2norm(MLP(e)_b) - x_b|^2 (MLPL2ReconFunction); fp32 device tensors, split-operand
     widths (mlp_fusable), x of the chain's output width."""
     require_gpu(e, x, what="mlp_l2norm_recon")
-    return MLPL2ReconFunction.apply(e, x, float(p), *weights)
+    return MLPL2ReconFunction.apply(e, x, float(p), torch.is_grad_enabled(), *weights)
 
 
 class LinearFunction(torch.autograd.Function):

@@ -82,6 +82,49 @@ def test_mlp_l2norm_recon_equals_composition(device, p):
             assert torch.allclose(rf.double(), ref, rtol=2e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("mode", ["mean", "mixed", "sum", "no_grad"])
+def test_mlp_l2norm_recon_speculative_gradient(device, mode):
+    """The fused node writes the split output gradient in its forward for g_recon = 1 / B (the batch-mean
+    loss) and its backward only checks g_recon: mean (one expanded value: every row speculated), mixed
+    (a per-row gradient, half the rows 1 / B: the others recomputed), sum (g_recon = 1: all recomputed) —
+    each bitwise the composition's gradients; under no_grad the forward writes no planes (same loss)."""
+    ops = _ops()
+    with ops.gemm_policy(ops.GEMM_FORCE_WIDE):
+        B, dims = 16384, [64, 128, 256, 512, 768]   # as above: no split-K on the last data grad
+        gen = torch.Generator(device=device).manual_seed(23)
+        ws = _weights(dims, gen, device)
+        e = torch.randn(B, dims[0], generator=gen, device=device).requires_grad_(True)
+        x = torch.nn.functional.normalize(torch.randn(B, dims[-1], generator=gen, device=device), dim=-1)
+        mixed = torch.where(torch.arange(B, device=device) % 2 == 0, torch.full((B,), 1.0 / B, device=device),
+                            torch.rand(B, generator=gen, device=device))
+
+        def run(fused):
+            _reset_seeds(ops)
+            for w in ws:
+                w.grad = None
+            e.grad = None
+            if mode == "no_grad":
+                with torch.no_grad():
+                    r = ops.mlp_l2norm_recon(e, x, ws) if fused else ops.l2norm_recon_loss(ops.mlp_chain(e, ws), x)
+                return r.clone(), None, []
+            r = ops.mlp_l2norm_recon(e, x, ws) if fused else ops.l2norm_recon_loss(ops.mlp_chain(e, ws), x)
+            if mode == "mean":
+                r.mean().backward()
+            elif mode == "mixed":
+                r.backward(mixed)
+            else:
+                r.sum().backward()
+            return r.detach().clone(), e.grad.clone(), [w.grad.clone() for w in ws]
+
+        rf, ef, wf = run(True)
+        rc, ec, wc = run(False)
+        assert torch.equal(rf, rc)
+        if mode != "no_grad":
+            assert torch.equal(ef, ec)
+            for i, (a, b) in enumerate(zip(wf, wc)):
+                assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()), i
+
+
 def test_mlp_presplit_input_equals_fp32_input(device):
     ops = _ops()
     B, dims = 8192, [768, 512, 256]

@@ -6,3 +6,5 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o rqonly -- python3 "$R/bench.py" --no-cpu-baseline \
   --no-pmc --no-extras --no-decoder > "$O/prof_rqonly.json" 2> "$O/prof_rqonly.err" || { tail "$O/prof_rqonly.err"; exit 1; }
 cat "$O/prof_rqonly.json"
+T=$(find "$O/prof" -name "rqonly_kernel_trace.csv" | head -1)
+python3 "$R/tools/step_breakdown.py" "$T" 10 60 > "$O/rq_step_breakdown.txt" && head -60 "$O/rq_step_breakdown.txt"
