@@ -280,16 +280,188 @@ struct FwdChunk {
   }
 };
 
-template <int HD, int NW>
+// ------------------------------------------------------------- split-bf16 forward (matmul 'high')
+// At the reference's matmul precision 'high' (modules/model.py:27, the same setting that puts every Linear
+// on the split-bf16 GEMM) the long-range forwards (HD = 64, 4-wave workgroups, 64-key chunks) multiply
+// S = Q K^T and O = P V as a = hi + lo bf16 pairs: hi*lo + lo*hi + hi*hi on v_mfma_f32_16x16x32_bf16
+// (fp32 accumulate; per-product relative error <= ~2^-16), 5.3x less MFMA time than the 16x16x4 fp32
+// chain. The softmax (max, exp, running sums, lse) stays fp32. K is staged as row-major hi / lo planes;
+// V transposed, with each 32-key block's keys in the order the S^T accumulator hands P^T to the PV
+// product (lane group g holds keys 4g..4g+3 of the block's two 16-key tiles: position 8g + j <- key
+// 4g + j (j < 4) / 16 + 4g + j - 4), so every operand fragment is one 16-B LDS read per plane.
+typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kX3Ld = 72;   // bf16 per staged row: 64 + 8 (144-B rows: the 16-row fragment reads spread over the banks)
+
+__device__ __forceinline__ void split8(const float (&v)[8], abf16x8& h, abf16x8& l) {
+  uint4 hh, ll;
+  split_bf16x2(v[0], v[1], hh.x, ll.x);
+  split_bf16x2(v[2], v[3], hh.y, ll.y);
+  split_bf16x2(v[4], v[5], hh.z, ll.z);
+  split_bf16x2(v[6], v[7], hh.w, ll.w);
+  h = __builtin_bit_cast(abf16x8, hh);
+  l = __builtin_bit_cast(abf16x8, ll);
+}
+
+__device__ __forceinline__ f32x4 mfma_x3(const abf16x8& ah, const abf16x8& al, const abf16x8& bh,
+                                         const abf16x8& bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+// position of chunk key r in the transposed V image (see above)
+__device__ __forceinline__ int x3_vpos(int r) { return (r & ~31) + 8 * ((r & 15) >> 2) + 4 * ((r & 31) >> 4) + (r & 3); }
+
+// A RowStage's registers (64 rows x 64 fp32) written as split planes: K row-major [row][kX3Ld], V transposed
+// [d][kX3Ld] at x3_vpos(row)
+template <int NT>
+__device__ __forceinline__ void x3_store_k(const RowStage<64, NT, 64>& st, uint16_t* Kh, uint16_t* Kl, int tid) {
+  constexpr int F4 = 16;
+#pragma unroll
+  for (int i = 0; i < RowStage<64, NT, 64>::PER; ++i) {
+    const int f = tid + i * NT;
+    if (f < 64 * F4) {
+      const int row = f / F4, c = (f % F4) * 4;
+      uint2 h, l;
+      split_bf16x2(st.r[i].x, st.r[i].y, h.x, l.x);
+      split_bf16x2(st.r[i].z, st.r[i].w, h.y, l.y);
+      *reinterpret_cast<uint2*>(Kh + row * kX3Ld + c) = h;
+      *reinterpret_cast<uint2*>(Kl + row * kX3Ld + c) = l;
+    }
+  }
+}
+template <int NT>
+__device__ __forceinline__ void x3_store_vt(const RowStage<64, NT, 64>& st, uint16_t* Vh, uint16_t* Vl, int tid) {
+  constexpr int F4 = 16;
+#pragma unroll
+  for (int i = 0; i < RowStage<64, NT, 64>::PER; ++i) {
+    const int f = tid + i * NT;
+    if (f < 64 * F4) {
+      const int pos = x3_vpos(f / F4), c = (f % F4) * 4;
+      uint32_t h0, l0, h1, l1;
+      split_bf16x2(st.r[i].x, st.r[i].y, h0, l0);
+      split_bf16x2(st.r[i].z, st.r[i].w, h1, l1);
+      Vh[(c + 0) * kX3Ld + pos] = (uint16_t)h0;
+      Vh[(c + 1) * kX3Ld + pos] = (uint16_t)(h0 >> 16);
+      Vh[(c + 2) * kX3Ld + pos] = (uint16_t)h1;
+      Vh[(c + 3) * kX3Ld + pos] = (uint16_t)(h1 >> 16);
+      Vl[(c + 0) * kX3Ld + pos] = (uint16_t)l0;
+      Vl[(c + 1) * kX3Ld + pos] = (uint16_t)(l0 >> 16);
+      Vl[(c + 2) * kX3Ld + pos] = (uint16_t)l1;
+      Vl[(c + 3) * kX3Ld + pos] = (uint16_t)(l1 >> 16);
+    }
+  }
+}
+
+// this lane's query fragments (d = 32 b + 8 (lane >> 4) + 0..7, b = 0, 1) as split planes
+__device__ __forceinline__ void x3_load_q(const float* p, bool valid, int lane, abf16x8 (&qh)[2], abf16x8 (&ql)[2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    float v[8];
+    const float* src = p + 32 * b + 8 * (lane >> 4);
+    const float4 x = valid ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 y = valid ? *reinterpret_cast<const float4*>(src + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    split8(v, qh[b], ql[b]);
+  }
+}
+
+// FwdChunk's online-softmax step on the split planes (HD = 64, 64-key chunk of NTT <= 4 tiles)
+struct FwdChunkX3 {
+  const uint16_t* Kh;
+  const uint16_t* Kl;
+  const uint16_t* Vh;
+  const uint16_t* Vl;
+  const abf16x8* qh;
+  const abf16x8* ql;
+  int lane, kc, lk, qi, causal;
+  float sl2;
+  float* m;
+  float* l;
+  f32x4* o;
+  template <int NTT, bool MASK>
+  __device__ __forceinline__ void run() {
+    const int g = lane >> 4, r = lane & 15;
+    f32x4 s[NTT];
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {   // S^T = K Q^T: rows = keys, columns = queries
+#pragma unroll
+      for (int t = 0; t < NTT; ++t) {
+        const int off = (16 * t + r) * kX3Ld + 32 * b + 8 * g;
+        const abf16x8 kh = *reinterpret_cast<const abf16x8*>(Kh + off);
+        const abf16x8 kl = *reinterpret_cast<const abf16x8*>(Kl + off);
+        s[t] = mfma_x3(kh, kl, qh[b], ql[b], s[t]);
+      }
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NTT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (MASK) {
+          const int key = kc + t * 16 + 4 * g + i;
+          if (!(key < lk && (!causal || key <= qi))) s[t][i] = -INFINITY;
+        }
+        mt = fmaxf(mt, s[t][i]);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(*m, mt * sl2);
+    const bool none = MASK && mn == -INFINITY;
+    const float alpha = none ? 1.f : exp2_fast(*m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[t][i] = none ? 0.f : exp2_fast(__builtin_fmaf(s[t][i], sl2, -mn));
+        ls += s[t][i];
+      }
+    *l = *l * alpha + ls;
+    *m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    constexpr int NKB = (NTT + 1) / 2;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {   // O^T += V^T P^T over the block's 32 keys (permuted order)
+      float p8[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p8[i] = s[2 * kb][i];
+        p8[4 + i] = 2 * kb + 1 < NTT ? s[2 * kb + 1 < NTT ? 2 * kb + 1 : 0][i] : 0.f;
+      }
+      abf16x8 ph, pl;
+      split8(p8, ph, pl);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int off = (16 * dt + r) * kX3Ld + 32 * kb + 8 * g;
+        const abf16x8 vh = *reinterpret_cast<const abf16x8*>(Vh + off);
+        const abf16x8 vl = *reinterpret_cast<const abf16x8*>(Vl + off);
+        o[dt] = mfma_x3(vh, vl, ph, pl, o[dt]);
+      }
+    }
+  }
+};
+
+// X3: the split-bf16 products (matmul 'high'; HD = 64, NW = 4 only)
+template <int HD, int NW, bool X3 = false>
 __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restrict__ q, int64_t sq, const float* __restrict__ k,
                                                         int64_t sk, const float* __restrict__ v, int64_t sv,
                                                         const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
                                                         int causal, float scale, float* __restrict__ out, int64_t so,
                                                         float* __restrict__ lse, int64_t Tq, const int* __restrict__ order) {
   constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
-  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
+  static_assert(!X3 || (HD == 64 && CH == 64), "split-bf16 form: HD 64, 64-key chunks");
+  constexpr int kSmemF = X3 ? (4 * 64 * kX3Ld) / 2 : 2 * CH * LD;   // floats
+  __shared__ __attribute__((aligned(16))) float smem[kSmemF];
   float* K_s = smem;
   float* V_s = smem + CH * LD;
+  uint16_t* const Kh = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const Kl = Kh + 64 * kX3Ld;
+  uint16_t* const Vh = Kl + 64 * kX3Ld;
+  uint16_t* const Vl = Vh + 64 * kX3Ld;
   const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4;
   if (z == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
@@ -304,7 +476,12 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restri
   const int qb = qwg + wave * 16, qi = qb + (lane & 15);
   const bool wave_on = qb < lq, qv = qi < lq;
   float qf[HD / 4];
-  load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+  abf16x8 qh[2], ql[2];
+  const float* qrow = q + (q0 + (qv ? qi : 0)) * sq + hh * HD;
+  if constexpr (X3)
+    x3_load_q(qrow, qv, lane, qh, ql);
+  else
+    load_frag<HD>(qrow + g * (HD / 4), qv, qf);
   f32x4 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -315,16 +492,27 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restri
   const float* vb_ = v + k0 * sv + hh * HD;
   RowStage<HD, 64 * NW, CH> stk, stv;
   FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, lk, qi, causal, scale * kLog2e, &m, &l, o};
+  FwdChunkX3 fx{Kh, Kl, Vh, Vl, qh, ql, lane, 0, lk, qi, causal, scale * kLog2e, &m, &l, o};
   for (int kc = 0; kc < kend; kc += CH) {
     stk.load(kb_, sk, kc, lk, tid);
     stv.load(vb_, sv, kc, lk, tid);
     __syncthreads();                          // the previous chunk's LDS reads are done
-    stk.store(K_s, tid);
-    stv.store(V_s, tid);
+    if constexpr (X3) {
+      x3_store_k<64 * NW>(stk, Kh, Kl, tid);
+      x3_store_vt<64 * NW>(stv, Vh, Vl, tid);
+    } else {
+      stk.store(K_s, tid);
+      stv.store(V_s, tid);
+    }
     __syncthreads();
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend_w - kc + 15) >> 4) : 0);
-    fc.kc = kc;
-    dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fc);
+    if constexpr (X3) {
+      fx.kc = kc;
+      dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fx);
+    } else {
+      fc.kc = kc;
+      dispatch_tiles<NTL>(nt, !causal && kc + CH <= lk, fc);
+    }
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -652,16 +840,22 @@ __global__ void __launch_bounds__(64) attn_fwd_split_kernel(const float* __restr
 // non-causal), each workgroup runs the same staged online softmax over its key block and writes the
 // unnormalised (o, m, l) partial in attn_fwd_split_kernel's layout; attn_fwd_combine_kernel merges them
 // in key-block order (deterministic).
-template <int HD, int NW, int kSplitKB>
+template <int HD, int NW, int kSplitKB, bool X3 = false>
 __global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, float scale, int64_t Tq,
     float* __restrict__ part, int nsplit) {
   constexpr int LD = HD + 4, DT = HD / 16, CH = Chunk<NW>::CH, NTL = Chunk<NW>::T;
   static_assert(kSplitKB % CH == 0, "key block of whole chunks");
-  __shared__ __attribute__((aligned(16))) float smem[2 * CH * LD];
+  static_assert(!X3 || (HD == 64 && CH == 64), "split-bf16 form: HD 64, 64-key chunks");
+  constexpr int kSmemF = X3 ? (4 * 64 * kX3Ld) / 2 : 2 * CH * LD;   // floats
+  __shared__ __attribute__((aligned(16))) float smem[kSmemF];
   float* K_s = smem;
   float* V_s = smem + CH * LD;
+  uint16_t* const Kh = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* const Kl = Kh + 64 * kX3Ld;
+  uint16_t* const Vh = Kl + 64 * kX3Ld;
+  uint16_t* const Vl = Vh + 64 * kX3Ld;
   const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4;
   const int j = blockIdx.x % nsplit, qblk = blockIdx.x / nsplit;
@@ -673,7 +867,12 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
   const int qb = qwg + wave * 16, qi = qb + (lane & 15);
   const bool wave_on = qb < lq, qv = qi < lq;
   float qf[HD / 4];
-  load_frag<HD>(q + (q0 + (qv ? qi : 0)) * sq + hh * HD + g * (HD / 4), qv, qf);
+  abf16x8 qh[2], ql[2];
+  const float* qrow = q + (q0 + (qv ? qi : 0)) * sq + hh * HD;
+  if constexpr (X3)
+    x3_load_q(qrow, qv, lane, qh, ql);
+  else
+    load_frag<HD>(qrow + g * (HD / 4), qv, qf);
   f32x4 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -682,16 +881,27 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
   const float* vb_ = v + k0 * sv + hh * HD;
   RowStage<HD, 64 * NW, CH> stk, stv;
   FwdChunk<HD> fc{K_s, V_s, qf, lane, 0, kend, qi, 0, scale * kLog2e, &m, &l, o};
+  FwdChunkX3 fx{Kh, Kl, Vh, Vl, qh, ql, lane, 0, kend, qi, 0, scale * kLog2e, &m, &l, o};
   for (int kc = kbeg; kc < kend; kc += CH) {
     stk.load(kb_, sk, kc, kend, tid);
     stv.load(vb_, sv, kc, kend, tid);
     __syncthreads();                          // the previous chunk's LDS reads are done
-    stk.store(K_s, tid);
-    stv.store(V_s, tid);
+    if constexpr (X3) {
+      x3_store_k<64 * NW>(stk, Kh, Kl, tid);
+      x3_store_vt<64 * NW>(stv, Vh, Vl, tid);
+    } else {
+      stk.store(K_s, tid);
+      stv.store(V_s, tid);
+    }
     __syncthreads();
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? min(NTL, (kend - kc + 15) >> 4) : 0);
-    fc.kc = kc;
-    dispatch_tiles<NTL>(nt, kc + CH <= kend, fc);
+    if constexpr (X3) {
+      fx.kc = kc;
+      dispatch_tiles<NTL>(nt, kc + CH <= kend, fx);
+    } else {
+      fc.kc = kc;
+      dispatch_tiles<NTL>(nt, kc + CH <= kend, fc);
+    }
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -2269,10 +2479,11 @@ static bool lpt_plan(int64_t B, int64_t max_len) { return RQ_ATTN_LPT && B >= 2 
 struct AttnPolicy {
   bool dma, fused, split;
   int qsplit;
+  bool x3;   // RQ_ATTN_SPLIT_BF16: the long-range forwards multiply in split-bf16 (matmul precision 'high')
 };
 static AttnPolicy attn_policy(int flags) {
   return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
-                    (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15};
+                    (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15, (flags & RQ_ATTN_SPLIT_BF16) != 0};
 }
 
 static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal, const AttnPolicy& pol) {
@@ -2322,8 +2533,15 @@ static bool short_fused_plan(int64_t hd, int64_t max_q, int64_t max_k, const Att
 template <int HD, int NW>
 static void fwd_nw(int64_t B, int64_t H, int64_t max_q, hipStream_t st, const float* q, int64_t sq, const float* k,
                    int64_t sk, const float* v, int64_t sv, const int64_t* cq, const int64_t* ck, int causal, float scale,
-                   float* out, int64_t so, float* lse, int64_t Tq, const int* order) {
+                   float* out, int64_t so, float* lse, int64_t Tq, const int* order, bool x3) {
   dim3 g((unsigned)std::max<int64_t>(1, (max_q + 16 * NW - 1) / (16 * NW)), (unsigned)H, (unsigned)B + 1);   // + tail slice
+  if constexpr (HD == 64 && NW == 4) {
+    if (x3) {
+      hipLaunchKernelGGL((attn_fwd_kernel<HD, NW, true>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, cq, ck, causal,
+                         scale, out, so, lse, Tq, order);
+      return;
+    }
+  }
   hipLaunchKernelGGL((attn_fwd_kernel<HD, NW>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out,
                      so, lse, Tq, order);
 }
@@ -2340,8 +2558,12 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
       constexpr int RPB = 256 / (HD / 4);
       const dim3 gs((unsigned)(((max_q + 63) / 64) * nsplit), (unsigned)H, (unsigned)B);
       const dim3 gc((unsigned)std::max<int64_t>(1, (max_q + RPB - 1) / RPB), (unsigned)H, (unsigned)B + 1);
-      hipLaunchKernelGGL((attn_fwd_kvsplit_kernel<HD, 4, kKvSplitKB>), gs, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck,
-                         scale, Tq, split_ws, nsplit);
+      if (pol.x3)
+        hipLaunchKernelGGL((attn_fwd_kvsplit_kernel<HD, 4, kKvSplitKB, true>), gs, dim3(256), 0, st, q, sq, k, sk, v, sv,
+                           cq, ck, scale, Tq, split_ws, nsplit);
+      else
+        hipLaunchKernelGGL((attn_fwd_kvsplit_kernel<HD, 4, kKvSplitKB>), gs, dim3(256), 0, st, q, sq, k, sk, v, sv, cq,
+                           ck, scale, Tq, split_ws, nsplit);
       hipLaunchKernelGGL((attn_fwd_combine_kernel<HD, kKvSplitKB>), gc, dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq, out,
                          so, lse);
       return;
@@ -2400,9 +2622,9 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     ord = order;
   }
   switch (waves_for(max_q)) {
-    case 1: fwd_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord); break;
-    case 2: fwd_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord); break;
-    default: fwd_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord); break;
+    case 1: fwd_nw<HD, 1>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord, false); break;
+    case 2: fwd_nw<HD, 2>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord, false); break;
+    default: fwd_nw<HD, 4>(B, H, max_q, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, ord, pol.x3); break;
   }
 }
 

@@ -1573,7 +1573,7 @@ class JaggedToPaddedValues(torch.autograd.Function):
 # ------------------------------------------------------------------------------ attention
 # Kernel policy of the attention calls (the `flags` argument, RQ_ATTN_* in include/rqvae_hip.h; 0 = the
 # measured-best forms): set only by kernel-vs-kernel tests and A/B probes through attn_policy().
-ATTN_NO_DMA, ATTN_TWO_PASS, ATTN_NO_SPLIT = 1, 2, 4
+ATTN_NO_DMA, ATTN_TWO_PASS, ATTN_NO_SPLIT, ATTN_SPLIT_BF16 = 1, 2, 4, 8
 _ATTN_POLICY = {"flags": 0}
 
 
@@ -1587,11 +1587,17 @@ def attn_policy(flags: int) -> _Policy:
     return _Policy(_ATTN_POLICY, flags)
 
 
+# False: exact-fp32 attention products at 'high' too (A/B probes set the attribute)
+_ATTN_X3 = True
+
+
 def _attn_fwd(q, k, v, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, lse):
-    """Forward launch(es) (varlen_attn_fwd with scratch for the LPT order and split-key partials)."""
+    """Forward launch(es) (varlen_attn_fwd with scratch for the LPT order and split-key partials). At matmul
+    precision 'high' (the reference's setting, modules/model.py:27) the long-range forms multiply in split-bf16
+    like every Linear (RQ_ATTN_SPLIT_BF16); 'highest' keeps exact fp32 products."""
     import ctypes
     Tq = q.shape[0]
-    flags = _ATTN_POLICY["flags"]
+    flags = _ATTN_POLICY["flags"] | (ATTN_SPLIT_BF16 if _ATTN_X3 and matmul_high() else 0)
     n = ctypes.c_int64(0)
     call("varlen_attn_fwd_ws_elems", B, H, hd, int(max_q), int(max_k), Tq, int(causal), flags, ctypes.byref(n))
     ws = torch.empty((max(1, int(n.value)),), device=q.device, dtype=torch.float32)

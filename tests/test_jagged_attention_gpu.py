@@ -383,3 +383,31 @@ def test_fused_backward_query_splits(device, qsplit):
                 a = got[:n].cpu().double().numpy().reshape(ref.shape)
                 assert np.all(np.abs(a - ref) <= 1e-4 + 1e-3 * np.abs(ref)), (what, causal)
 
+
+
+@pytest.mark.parametrize("B,max_q,max_k,H,hd,causal,same", [
+    (3, 200, 200, 6, 64, True, True),     # chunked forward, causal
+    (4, 150, 260, 6, 64, False, False),   # ragged q x k (key-split forward at few workgroups)
+    (2, 801, 801, 6, 64, False, True),    # ML-32M context length
+])
+def test_varlen_attention_split_bf16_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
+    """At matmul precision 'high' the long-range forwards multiply Q K^T and P V in split-bf16
+    (RQ_ATTN_SPLIT_BF16; per-product relative error <= ~2^-16, fp32 softmax): the same oracle tolerances as
+    the exact-fp32 forms, and within 1e-4 of them."""
+    from rqvae_hip import ops
+    prev = torch.get_float32_matmul_precision()
+    try:
+        torch.set_float32_matmul_precision("high")
+        _attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same)
+        g = gi.rng(B * 7 + max_k)
+        q, k, v, do, cq, ck = _varlen_case(g, B, max_q, max_k, H, hd, same)
+        A_ = H * hd
+        args = [torch.from_numpy(a.reshape(-1, A_)).to(device) for a in (q, k, v)]
+        cqt, ckt = torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device)
+        mq, mk = int(np.diff(cq).max()), int(np.diff(ck).max())
+        hi = ops.varlen_attention(*args, cqt, ckt, H, causal, mq, mk)
+        torch.set_float32_matmul_precision("highest")
+        ex = ops.varlen_attention(*args, cqt, ckt, H, causal, mq, mk)
+        assert float((hi - ex).abs().max()) <= 1e-4 * float(ex.abs().max())
+    finally:
+        torch.set_float32_matmul_precision(prev)

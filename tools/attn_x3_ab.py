@@ -1,0 +1,31 @@
+"""Same-process A/B of the ML-32M decoder steps (8 and 64 sequences per GPU) with the long-range attention
+forwards in split-bf16 (ops._ATTN_X3, matmul 'high') vs exact fp32, interleaved rounds of
+bench.measure_decoder. One JSON line per (batch, round, mode)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rq-vae-recommender_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def main():
+    import bench
+    from rqvae_hip import gemm_tuning, ops
+    gemm_tuning.enable()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    for B in (8, 64):
+        for rnd in range(3):
+            for x3 in (True, False):
+                ops._ATTN_X3 = x3
+                r = bench.measure_decoder(dev, cfg=bench.DEC_DM, B=B, stats=False)
+                print(json.dumps({"B": B, "round": rnd, "attn_x3": x3, "ms_per_step": r["ms_per_step"]}), flush=True)
+    ops._ATTN_X3 = True
+
+
+if __name__ == "__main__":
+    main()
