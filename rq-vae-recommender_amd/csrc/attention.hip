@@ -312,45 +312,55 @@ __device__ __forceinline__ f32x4 mfma_x3(const abf16x8& ah, const abf16x8& al, c
 // position of chunk key r in the transposed V image (see above)
 __device__ __forceinline__ int x3_vpos(int r) { return (r & ~31) + 8 * ((r & 15) >> 2) + 4 * ((r & 31) >> 4) + (r & 3); }
 
-// A RowStage's registers (64 rows x 64 fp32) written as split planes: K row-major [row][kX3Ld], V transposed
-// [d][kX3Ld] at x3_vpos(row)
-template <int NT>
-__device__ __forceinline__ void x3_store_k(const RowStage<64, NT, 64>& st, uint16_t* Kh, uint16_t* Kl, int tid) {
+// A RowStage's registers (CH rows x 64 fp32) written as split planes: row-major [row][ld], or transposed
+// [d][ld] at column x3_vpos(row) (PERM: the accumulator's order) or row
+template <int NT, int CH>
+__device__ __forceinline__ void x3_store_rows(const RowStage<64, NT, CH>& st, uint16_t* Xh, uint16_t* Xl, int ld,
+                                              int tid) {
   constexpr int F4 = 16;
 #pragma unroll
-  for (int i = 0; i < RowStage<64, NT, 64>::PER; ++i) {
+  for (int i = 0; i < RowStage<64, NT, CH>::PER; ++i) {
     const int f = tid + i * NT;
-    if (f < 64 * F4) {
+    if (f < CH * F4) {
       const int row = f / F4, c = (f % F4) * 4;
       uint2 h, l;
       split_bf16x2(st.r[i].x, st.r[i].y, h.x, l.x);
       split_bf16x2(st.r[i].z, st.r[i].w, h.y, l.y);
-      *reinterpret_cast<uint2*>(Kh + row * kX3Ld + c) = h;
-      *reinterpret_cast<uint2*>(Kl + row * kX3Ld + c) = l;
+      *reinterpret_cast<uint2*>(Xh + row * ld + c) = h;
+      *reinterpret_cast<uint2*>(Xl + row * ld + c) = l;
+    }
+  }
+}
+template <int NT, int CH, bool PERM>
+__device__ __forceinline__ void x3_store_cols(const RowStage<64, NT, CH>& st, uint16_t* Xh, uint16_t* Xl, int ld,
+                                              int tid) {
+  constexpr int F4 = 16;
+#pragma unroll
+  for (int i = 0; i < RowStage<64, NT, CH>::PER; ++i) {
+    const int f = tid + i * NT;
+    if (f < CH * F4) {
+      const int pos = PERM ? x3_vpos(f / F4) : f / F4, c = (f % F4) * 4;
+      uint32_t h0, l0, h1, l1;
+      split_bf16x2(st.r[i].x, st.r[i].y, h0, l0);
+      split_bf16x2(st.r[i].z, st.r[i].w, h1, l1);
+      Xh[(c + 0) * ld + pos] = (uint16_t)h0;
+      Xh[(c + 1) * ld + pos] = (uint16_t)(h0 >> 16);
+      Xh[(c + 2) * ld + pos] = (uint16_t)h1;
+      Xh[(c + 3) * ld + pos] = (uint16_t)(h1 >> 16);
+      Xl[(c + 0) * ld + pos] = (uint16_t)l0;
+      Xl[(c + 1) * ld + pos] = (uint16_t)(l0 >> 16);
+      Xl[(c + 2) * ld + pos] = (uint16_t)l1;
+      Xl[(c + 3) * ld + pos] = (uint16_t)(l1 >> 16);
     }
   }
 }
 template <int NT>
+__device__ __forceinline__ void x3_store_k(const RowStage<64, NT, 64>& st, uint16_t* Kh, uint16_t* Kl, int tid) {
+  x3_store_rows<NT, 64>(st, Kh, Kl, kX3Ld, tid);
+}
+template <int NT>
 __device__ __forceinline__ void x3_store_vt(const RowStage<64, NT, 64>& st, uint16_t* Vh, uint16_t* Vl, int tid) {
-  constexpr int F4 = 16;
-#pragma unroll
-  for (int i = 0; i < RowStage<64, NT, 64>::PER; ++i) {
-    const int f = tid + i * NT;
-    if (f < 64 * F4) {
-      const int pos = x3_vpos(f / F4), c = (f % F4) * 4;
-      uint32_t h0, l0, h1, l1;
-      split_bf16x2(st.r[i].x, st.r[i].y, h0, l0);
-      split_bf16x2(st.r[i].z, st.r[i].w, h1, l1);
-      Vh[(c + 0) * kX3Ld + pos] = (uint16_t)h0;
-      Vh[(c + 1) * kX3Ld + pos] = (uint16_t)(h0 >> 16);
-      Vh[(c + 2) * kX3Ld + pos] = (uint16_t)h1;
-      Vh[(c + 3) * kX3Ld + pos] = (uint16_t)(h1 >> 16);
-      Vl[(c + 0) * kX3Ld + pos] = (uint16_t)l0;
-      Vl[(c + 1) * kX3Ld + pos] = (uint16_t)(l0 >> 16);
-      Vl[(c + 2) * kX3Ld + pos] = (uint16_t)l1;
-      Vl[(c + 3) * kX3Ld + pos] = (uint16_t)(l1 >> 16);
-    }
-  }
+  x3_store_cols<NT, 64, true>(st, Vh, Vl, kX3Ld, tid);
 }
 
 // this lane's query fragments (d = 32 b + 8 (lane >> 4) + 0..7, b = 0, 1) as split planes
@@ -1164,6 +1174,201 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
           for (int j = 0; j < DTW; ++j) acc[j] = mfma4(base[i * LD + j * 16], w[i], acc[j]);
       }
       const int qi = qc + qt * 16 + (lane & 15);
+      if (qi < lq) {
+        float* rowp = dst + (int64_t)qi * dstride + d0 * 16 + 4 * g;
+#pragma unroll
+        for (int j = 0; j < DTW; ++j)
+          *reinterpret_cast<float4*>(rowp + j * 16) =
+              make_float4(acc[j][0] * mul, acc[j][1] * mul, acc[j][2] * mul, acc[j][3] * mul);
+      }
+    }
+  }
+  if (!kv) return;
+  if (qsplit == 1) {
+    store_rowT<HD>(dk + (k0 + kj) * sdk + hh * HD, dka, scale, lane);
+    store_rowT<HD>(dv + (k0 + kj) * sdv + hh * HD, dva, 1.f, lane);
+  } else {   // partials [2][qsplit][Tk][H HD], unscaled
+    store_rowT<HD>(kvpart + (((int64_t)qs * Tk + k0 + kj) * HH + hh * HD), dka, 1.f, lane);
+    store_rowT<HD>(kvpart + (((int64_t)(qsplit + qs) * Tk + k0 + kj) * HH + hh * HD), dva, 1.f, lane);
+  }
+}
+
+// ------------------------------------------------- split-bf16 fused backward (matmul 'high')
+// attn_bwd_fused_kernel's schedule (64-key block per workgroup, 32-query chunks, 4 waves of 16 keys, dQ
+// from the chunk's dS in LDS) with every product on v_mfma_f32_16x16x32_bf16 over hi / lo pairs: S = Q K^T
+// and dP = dO V^T (Q, dO row-major planes x this wave's K / V fragments), dV^T += dO^T P and dK^T += Q^T dS
+// (dO^T, Q^T planes transposed with the chunk's 32 queries in the S accumulator's order x the P / dS values
+// split in registers), dQ^T += K^T dS^T (the block's K^T planes x the fp32 dS rows split at the read).
+// P, dS, the softmax statistics and all accumulation stay fp32.
+constexpr int kX3Tq = 40;   // transposed chunk rows: 32 queries + 8 bf16 (80-B rows)
+template <int NW, int CH>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ dout, int64_t sdo, const float* __restrict__ lse,
+    const float* __restrict__ delta, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ part, float* __restrict__ dk,
+    int64_t sdk, float* __restrict__ dv, int64_t sdv, int64_t Tk, const int* __restrict__ order, int qsplit,
+    float* __restrict__ kvpart) {
+  constexpr int HD = 64, DT = 4, KB = 16 * NW, NTL = CH / 16, LDS_ = KB + 4;
+  constexpr int DSPLIT = NW >= NTL ? NW / NTL : 1, DTW = DT / DSPLIT;
+  static_assert(CH == 32 && NW == 4 && DT % DSPLIT == 0, "split-bf16 fused backward: 32-query chunks, 4 waves");
+  constexpr int kRow = CH * kX3Ld, kCol = HD * kX3Tq, kKt = HD * kX3Ld;   // bf16 per plane
+  __shared__ __attribute__((aligned(16))) uint16_t planes[2 * (2 * kRow + 2 * kCol + kKt)];
+  __shared__ __attribute__((aligned(16))) float fsm[CH * LDS_ + 2 * CH];
+  uint16_t* const Qh = planes;
+  uint16_t* const Ql = Qh + kRow;
+  uint16_t* const Oh = Ql + kRow;   // dO
+  uint16_t* const Ol = Oh + kRow;
+  uint16_t* const QTh = Ol + kRow;
+  uint16_t* const QTl = QTh + kCol;
+  uint16_t* const OTh = QTl + kCol;
+  uint16_t* const OTl = OTh + kCol;
+  uint16_t* const KTh = OTl + kCol;
+  uint16_t* const KTl = KTh + kKt;
+  float* const dS_s = fsm;
+  float* const lse_s = dS_s + CH * LDS_;
+  float* const dl_s = lse_s + CH;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r = lane & 15;
+  if (z == (int)gridDim.z - 1) {              // tail slice: gradient rows past the last sequence
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[z], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[z], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[z], Tq, hh, tid);
+    return;
+  }
+  const int b = seq_of(order, z);
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  const int kbi = (int)blockIdx.x / qsplit, qs = (int)blockIdx.x - kbi * qsplit;
+  const int kwg = kbi * KB;
+  if (kwg >= lk) {
+    if (lk == 0) zero_rows<HD, 64 * NW>(dq, sdq, q0, q0 + lq, hh, tid);
+    return;
+  }
+  const int nkb = (lk + KB - 1) / KB;
+  const int kb = kwg + wave * 16, kj = kb + r;
+  const bool wave_on = kb < lk, kv = kj < lk;
+  const int64_t krow = k0 + (kv ? kj : 0);
+  abf16x8 kh[2], kl[2], vh[2], vl[2];   // this lane's key row (d = 32 b + 8 g + 0..7)
+  x3_load_q(k + krow * sk + hh * HD, kv, lane, kh, kl);
+  x3_load_q(v + krow * sv + hh * HD, kv, lane, vh, vl);
+  {
+    RowStage<HD, 64 * NW, KB> stk;
+    stk.load(k + k0 * sk + hh * HD, sk, kwg, lk, tid);
+    x3_store_cols<64 * NW, KB, false>(stk, KTh, KTl, kX3Ld, tid);   // published by the first chunk's barrier
+  }
+  f32x4 dka[DT], dva[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  const int qstart = causal ? (kwg / CH) * CH : 0;
+  const float* qb_ = q + q0 * sq + hh * HD;
+  const float* ob_ = dout + q0 * sdo + hh * HD;
+  const float* lse_h = lse + (int64_t)hh * Tq + q0;
+  const float* dl_h = delta + (int64_t)hh * Tq + q0;
+  const int64_t HH = (int64_t)gridDim.y * HD;
+  float* dst;
+  int64_t dstride;
+  float mul;
+  if (nkb == 1) { dst = dq + q0 * sdq + hh * HD; dstride = sdq; mul = scale; }
+  else { dst = part + ((int64_t)kbi * Tq + q0) * HH + hh * HD; dstride = HH; mul = 1.f; }
+  const int nch = lq > qstart ? (lq - qstart + CH - 1) / CH : 0;
+  const int c_lo = qstart + (qs * nch / qsplit) * CH;
+  const int c_hi = min(lq, qstart + ((qs + 1) * nch / qsplit) * CH);
+  RowStage<HD, 64 * NW, CH> stq, sto;
+  const float sl2 = scale * kLog2e;
+  const int col = wave * 16 + r;
+  float lse_r = 0.f, dl_r = 0.f;
+  for (int qc = c_lo; qc < c_hi; qc += CH) {
+    stq.load(qb_, sq, qc, lq, tid);
+    sto.load(ob_, sdo, qc, lq, tid);
+    {
+      const bool ok = tid < CH && qc + tid < lq;
+      lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
+      dl_r = ok ? dl_h[qc + tid] : 0.f;
+    }
+    __syncthreads();                          // previous chunk's plane / dS reads are done
+    x3_store_rows<64 * NW, CH>(stq, Qh, Ql, kX3Ld, tid);
+    x3_store_rows<64 * NW, CH>(sto, Oh, Ol, kX3Ld, tid);
+    x3_store_cols<64 * NW, CH, true>(stq, QTh, QTl, kX3Tq, tid);
+    x3_store_cols<64 * NW, CH, true>(sto, OTh, OTl, kX3Tq, tid);
+    if (tid < CH) {
+      lse_s[tid] = lse_r;
+      dl_s[tid] = dl_r;
+    }
+    __syncthreads();
+    const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);
+    const int nt = __builtin_amdgcn_readfirstlane(wave_on ? max(0, min(NTL, (lq - qc + 15) >> 4) - t0) : 0);
+    f32x4 s[NTL], dp[NTL];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool on = t >= t0 && t < t0 + nt;
+      if (on) {
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {   // S = Q K^T, dP = dO V^T: rows = queries, columns = keys
+          const int off = (16 * t + r) * kX3Ld + 32 * bb + 8 * g;
+          const abf16x8 ah = *reinterpret_cast<const abf16x8*>(Qh + off), al = *reinterpret_cast<const abf16x8*>(Ql + off);
+          const abf16x8 oh = *reinterpret_cast<const abf16x8*>(Oh + off), ol = *reinterpret_cast<const abf16x8*>(Ol + off);
+          s[t] = mfma_x3(ah, al, kh[bb], kl[bb], s[t]);
+          dp[t] = mfma_x3(oh, ol, vh[bb], vl[bb], dp[t]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = t * 16 + 4 * g + i;
+        const int qq = qc + qr;
+        float p = exp2_fast(__builtin_fmaf(s[t][i], sl2, -lse_s[qr]));
+        if (!(on && qq < lq && (!causal || kj <= qq))) p = 0.f;
+        s[t][i] = p;
+        dp[t][i] = p * (dp[t][i] - dl_s[qr]);   // dS
+        dS_s[qr * LDS_ + col] = kv ? dp[t][i] : 0.f;
+      }
+    }
+    {   // dV^T += dO^T P, dK^T += Q^T dS over the chunk's 32 queries (the accumulator's order)
+      float p8[8], d8[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p8[i] = s[0][i];
+        p8[4 + i] = s[1][i];
+        d8[i] = dp[0][i];
+        d8[4 + i] = dp[1][i];
+      }
+      abf16x8 ph, pl, dh, dl;
+      split8(p8, ph, pl);
+      split8(d8, dh, dl);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int off = (16 * dt + r) * kX3Tq + 8 * g;
+        const abf16x8 oth = *reinterpret_cast<const abf16x8*>(OTh + off), otl = *reinterpret_cast<const abf16x8*>(OTl + off);
+        const abf16x8 qth = *reinterpret_cast<const abf16x8*>(QTh + off), qtl = *reinterpret_cast<const abf16x8*>(QTl + off);
+        dva[dt] = mfma_x3(oth, otl, ph, pl, dva[dt]);
+        dka[dt] = mfma_x3(qth, qtl, dh, dl, dka[dt]);
+      }
+    }
+    __syncthreads();                          // dS of every wave in LDS
+    // dQ^T (16 queries x DTW*16 dims) += K^T dS^T over the block's keys (keys past lk: zero K^T, zero dS)
+    const int nkk = __builtin_amdgcn_readfirstlane((min(NW, (lk - kwg + 15) >> 4) + 1) >> 1);   // 32-key blocks
+    for (int u = wave; u < NTL * DSPLIT; u += NW) {
+      const int qt = u % NTL, d0 = (u / NTL) * DTW;
+      if (qc + qt * 16 >= lq) continue;
+      f32x4 acc[DTW];
+#pragma unroll
+      for (int j = 0; j < DTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk < nkk; ++kk) {
+        const float* dsrow = dS_s + (qt * 16 + r) * LDS_ + 32 * kk + 8 * g;
+        const float4 x = *reinterpret_cast<const float4*>(dsrow), y = *reinterpret_cast<const float4*>(dsrow + 4);
+        const float w8[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        abf16x8 wh, wl;
+        split8(w8, wh, wl);
+#pragma unroll
+        for (int j = 0; j < DTW; ++j) {
+          const int off = (16 * (d0 + j) + r) * kX3Ld + 32 * kk + 8 * g;
+          const abf16x8 th = *reinterpret_cast<const abf16x8*>(KTh + off), tl = *reinterpret_cast<const abf16x8*>(KTl + off);
+          acc[j] = mfma_x3(th, tl, wh, wl, acc[j]);
+        }
+      }
+      const int qi = qc + qt * 16 + r;
       if (qi < lq) {
         float* rowp = dst + (int64_t)qi * dstride + d0 * 16 + 4 * g;
 #pragma unroll
@@ -2862,8 +3067,12 @@ static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k,
     if (qs > 1 && ws_elems < fused_ws_elems(B, H, HD, max_q, max_k, Tq, pol, Tk)) qs = 1;
     float* kvpart = qs > 1 ? ws + fused_ws_elems(B, H, HD, max_q, max_k, Tq, pol) : nullptr;
     const dim3 g((unsigned)(std::max<int64_t>(1, (max_k + KB - 1) / KB) * qs), (unsigned)H, (unsigned)B + 1);   // + tail
-    hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, NW, CH>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse,
-                       delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord, qs, kvpart);
+    if (pol.x3 && NW == 4 && CH == 32)
+      hipLaunchKernelGGL((attn_bwd_fused_x3_kernel<NW, CH>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo, lse,
+                         delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord, qs, kvpart);
+    else
+      hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, NW, CH>), g, dim3(64 * NW), 0, st, q, sq, k, sk, v, sv, dout, sdo,
+                         lse, delta, Tq, cq, ck, causal, scale, dq, sdq, ws, dk, sdk, dv, sdv, Tk, ord, qs, kvpart);
     if (qs > 1 && Tk > 0) {
       const int64_t n = Tk * H * (HD / 4);
       hipLaunchKernelGGL((attn_kv_reduce_kernel<HD>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, kvpart, qs, Tk,

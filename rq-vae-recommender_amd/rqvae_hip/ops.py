@@ -1587,8 +1587,9 @@ def attn_policy(flags: int) -> _Policy:
     return _Policy(_ATTN_POLICY, flags)
 
 
-# False: exact-fp32 attention products at 'high' too (A/B probes set the attribute)
+# False: exact-fp32 attention products at 'high' too (A/B probes set the attributes; _ATTN_X3_BWD: the backward)
 _ATTN_X3 = True
+_ATTN_X3_BWD = True
 
 
 def _attn_fwd(q, k, v, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, lse):
@@ -1608,10 +1609,10 @@ def _attn_fwd(q, k, v, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, l
 
 def _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv):
     """Backward launch(es) of varlen attention into dq / dk / dv (row-strided views); scratch sized for
-    the fused form's query splits (Tk given)."""
+    the fused form's query splits (Tk given). At 'high' the fused long-range form multiplies in split-bf16."""
     import ctypes
     Tq, A = q.shape
-    flags = _ATTN_POLICY["flags"]
+    flags = _ATTN_POLICY["flags"] | (ATTN_SPLIT_BF16 if _ATTN_X3 and _ATTN_X3_BWD and matmul_high() else 0)
     delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
     n = ctypes.c_int64(0)
     call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0], flags, ctypes.byref(n))

@@ -388,12 +388,14 @@ def test_fused_backward_query_splits(device, qsplit):
 @pytest.mark.parametrize("B,max_q,max_k,H,hd,causal,same", [
     (3, 200, 200, 6, 64, True, True),     # chunked forward, causal
     (4, 150, 260, 6, 64, False, False),   # ragged q x k (key-split forward at few workgroups)
-    (2, 801, 801, 6, 64, False, True),    # ML-32M context length
+    (2, 801, 801, 6, 64, False, True),    # ML-32M context length (fused backward with query splits)
+    (2, 700, 700, 4, 64, True, True),     # causal, several key blocks (dQ partials)
 ])
 def test_varlen_attention_split_bf16_vs_oracle(device, B, max_q, max_k, H, hd, causal, same):
-    """At matmul precision 'high' the long-range forwards multiply Q K^T and P V in split-bf16
-    (RQ_ATTN_SPLIT_BF16; per-product relative error <= ~2^-16, fp32 softmax): the same oracle tolerances as
-    the exact-fp32 forms, and within 1e-4 of them."""
+    """At matmul precision 'high' the long-range forwards and the fused backward multiply in split-bf16
+    (RQ_ATTN_SPLIT_BF16; per-product relative error <= ~2^-16, fp32 softmax / P / dS): the same oracle
+    tolerances as the exact-fp32 forms, and within 1e-4 (forward) / 2e-4 (gradients) of them, relative to
+    the largest magnitude."""
     from rqvae_hip import ops
     prev = torch.get_float32_matmul_precision()
     try:
@@ -405,9 +407,16 @@ def test_varlen_attention_split_bf16_vs_oracle(device, B, max_q, max_k, H, hd, c
         args = [torch.from_numpy(a.reshape(-1, A_)).to(device) for a in (q, k, v)]
         cqt, ckt = torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device)
         mq, mk = int(np.diff(cq).max()), int(np.diff(ck).max())
-        hi = ops.varlen_attention(*args, cqt, ckt, H, causal, mq, mk)
-        torch.set_float32_matmul_precision("highest")
-        ex = ops.varlen_attention(*args, cqt, ckt, H, causal, mq, mk)
-        assert float((hi - ex).abs().max()) <= 1e-4 * float(ex.abs().max())
+        dot = torch.from_numpy(do.reshape(-1, A_)).to(device)
+        res = []
+        for prec in ("high", "highest"):
+            torch.set_float32_matmul_precision(prec)
+            xs = [a.clone().requires_grad_(True) for a in args]
+            o = ops.varlen_attention(*xs, cqt, ckt, H, causal, mq, mk)
+            o.backward(dot)
+            res.append([o.detach()] + [x.grad for x in xs])
+        for i, (a, b) in enumerate(zip(*res)):
+            tol = 1e-4 if i == 0 else 2e-4
+            assert float((a - b).abs().max()) <= tol * float(b.abs().max()), ("out", "dq", "dk", "dv")[i]
     finally:
         torch.set_float32_matmul_precision(prev)

@@ -1,6 +1,7 @@
 """Same-process A/B of the ML-32M decoder steps (8 and 64 sequences per GPU) with the long-range attention
-forwards in split-bf16 (ops._ATTN_X3, matmul 'high') vs exact fp32, interleaved rounds of
-bench.measure_decoder. One JSON line per (batch, round, mode)."""
+in split-bf16 (matmul 'high') vs exact fp32, interleaved rounds of bench.measure_decoder. `--bwd`: split-bf16
+forwards in both arms, the fused backward's split-bf16 form (ops._ATTN_X3_BWD) on vs off; default: the
+forwards (ops._ATTN_X3) on vs off. One JSON line per (batch, round, mode)."""
 import json
 import os
 import sys
@@ -18,13 +19,15 @@ def main():
     gemm_tuning.enable()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    attr = "_ATTN_X3_BWD" if "--bwd" in sys.argv else "_ATTN_X3"
     for B in (8, 64):
         for rnd in range(3):
             for x3 in (True, False):
-                ops._ATTN_X3 = x3
+                setattr(ops, attr, x3)
                 r = bench.measure_decoder(dev, cfg=bench.DEC_DM, B=B, stats=False)
-                print(json.dumps({"B": B, "round": rnd, "attn_x3": x3, "ms_per_step": r["ms_per_step"]}), flush=True)
-    ops._ATTN_X3 = True
+                print(json.dumps({"B": B, "round": rnd, attr.lower().lstrip("_"): x3, "ms_per_step": r["ms_per_step"]}),
+                      flush=True)
+    setattr(ops, attr, True)
 
 
 if __name__ == "__main__":
