@@ -285,12 +285,15 @@ struct FwdChunk {
 // on the split-bf16 GEMM) the long-range forwards (HD = 64, 4-wave workgroups, 64-key chunks) multiply
 // S = Q K^T and O = P V as a = hi + lo bf16 pairs: hi*lo + lo*hi + hi*hi on v_mfma_f32_16x16x32_bf16
 // (fp32 accumulate; per-product relative error <= ~2^-16), 5.3x less MFMA time than the 16x16x4 fp32
-// chain. The softmax (max, exp, running sums, lse) stays fp32. K is staged as row-major hi / lo planes;
-// V transposed, with each 32-key block's keys in the order the S^T accumulator hands P^T to the PV
+// chain. The softmax (max, exp, running sums, lse) stays fp32. K and V are staged as row-major hi / lo
+// planes: K fragments are one 16-B row read per plane, V^T fragments two ds_read_b64_tr_b16 transposed
+// reads (x3_tr_frag) whose 8 keys per lane follow the order the S^T accumulator hands P^T to the PV
 // product (lane group g holds keys 4g..4g+3 of the block's two 16-key tiles: position 8g + j <- key
-// 4g + j (j < 4) / 16 + 4g + j - 4), so every operand fragment is one 16-B LDS read per plane.
+// 4g + j (j < 4) / 16 + 4g + j - 4). (A transposed V image written by 16-bit scattered stores measured
+// 2-way+ bank conflicts on 72% of the LDS cycles: profiles/r04/attn_tr/.)
 typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
-constexpr int kX3Ld = 72;   // bf16 per staged row: 64 + 8 (144-B rows: the 16-row fragment reads spread over the banks)
+constexpr int kX3Ld = 80;   // bf16 per plane row (160 B): the 16-row fragment reads (ds_read_b128) and the transposed
+                            // reads of 4-row blocks 4 rows apart (ds_read_b64_tr_b16) are both bank-conflict-free
 
 __device__ __forceinline__ void split8(const float (&v)[8], abf16x8& h, abf16x8& l) {
   uint4 hh, ll;
@@ -309,11 +312,7 @@ __device__ __forceinline__ f32x4 mfma_x3(const abf16x8& ah, const abf16x8& al, c
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
 }
 
-// position of chunk key r in the transposed V image (see above)
-__device__ __forceinline__ int x3_vpos(int r) { return (r & ~31) + 8 * ((r & 15) >> 2) + 4 * ((r & 31) >> 4) + (r & 3); }
-
-// A RowStage's registers (CH rows x 64 fp32) written as split planes: row-major [row][ld], or transposed
-// [d][ld] at column x3_vpos(row) (PERM: the accumulator's order) or row
+// A RowStage's registers (CH rows x 64 fp32) written as row-major split planes [row][ld]
 template <int NT, int CH>
 __device__ __forceinline__ void x3_store_rows(const RowStage<64, NT, CH>& st, uint16_t* Xh, uint16_t* Xl, int ld,
                                               int tid) {
@@ -331,38 +330,19 @@ __device__ __forceinline__ void x3_store_rows(const RowStage<64, NT, CH>& st, ui
     }
   }
 }
-template <int NT, int CH, bool PERM>
-__device__ __forceinline__ void x3_store_cols(const RowStage<64, NT, CH>& st, uint16_t* Xh, uint16_t* Xl, int ld,
-                                              int tid) {
-  constexpr int F4 = 16;
-#pragma unroll
-  for (int i = 0; i < RowStage<64, NT, CH>::PER; ++i) {
-    const int f = tid + i * NT;
-    if (f < CH * F4) {
-      const int pos = PERM ? x3_vpos(f / F4) : f / F4, c = (f % F4) * 4;
-      uint32_t h0, l0, h1, l1;
-      split_bf16x2(st.r[i].x, st.r[i].y, h0, l0);
-      split_bf16x2(st.r[i].z, st.r[i].w, h1, l1);
-      Xh[(c + 0) * ld + pos] = (uint16_t)h0;
-      Xh[(c + 1) * ld + pos] = (uint16_t)(h0 >> 16);
-      Xh[(c + 2) * ld + pos] = (uint16_t)h1;
-      Xh[(c + 3) * ld + pos] = (uint16_t)(h1 >> 16);
-      Xl[(c + 0) * ld + pos] = (uint16_t)l0;
-      Xl[(c + 1) * ld + pos] = (uint16_t)(l0 >> 16);
-      Xl[(c + 2) * ld + pos] = (uint16_t)l1;
-      Xl[(c + 3) * ld + pos] = (uint16_t)(l1 >> 16);
-    }
-  }
+typedef short x3s4 __attribute__((ext_vector_type(4)));
+// Fragment (8 bf16, k = 8 g + e) of a product contracting over the ROWS of a row-major bf16 plane [.][ld]:
+// element e of lane (g, c) = plane[row0 + x3 order(8 g + e)][col0 + c] with x3 order 4 g + e (e < 4) /
+// 16 + 4 g + e - 4 — the S accumulator's query order (two ds_read_b64_tr_b16 of 4-row blocks). EXEC must be
+// all ones (wave-uniform control flow only).
+__device__ __forceinline__ abf16x8 x3_tr_frag(const uint16_t* plane, int ld, int row0, int col0, int lane) {
+  const uint16_t* a = plane + (row0 + 4 * (lane >> 4) + ((lane >> 2) & 3)) * ld + col0 + 4 * (lane & 3);
+  const x3s4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) x3s4*)a);
+  const x3s4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) x3s4*)(a + 16 * ld));
+  typedef short x3s8 __attribute__((ext_vector_type(8)));
+  const x3s8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  return __builtin_bit_cast(abf16x8, v);
 }
-template <int NT>
-__device__ __forceinline__ void x3_store_k(const RowStage<64, NT, 64>& st, uint16_t* Kh, uint16_t* Kl, int tid) {
-  x3_store_rows<NT, 64>(st, Kh, Kl, kX3Ld, tid);
-}
-template <int NT>
-__device__ __forceinline__ void x3_store_vt(const RowStage<64, NT, 64>& st, uint16_t* Vh, uint16_t* Vl, int tid) {
-  x3_store_cols<NT, 64, true>(st, Vh, Vl, kX3Ld, tid);
-}
-
 // this lane's query fragments (d = 32 b + 8 (lane >> 4) + 0..7, b = 0, 1) as split planes
 __device__ __forceinline__ void x3_load_q(const float* p, bool valid, int lane, abf16x8 (&qh)[2], abf16x8 (&ql)[2]) {
 #pragma unroll
@@ -446,9 +426,8 @@ struct FwdChunkX3 {
       split8(p8, ph, pl);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int off = (16 * dt + r) * kX3Ld + 32 * kb + 8 * g;
-        const abf16x8 vh = *reinterpret_cast<const abf16x8*>(Vh + off);
-        const abf16x8 vl = *reinterpret_cast<const abf16x8*>(Vl + off);
+        const abf16x8 vh = x3_tr_frag(Vh, kX3Ld, 32 * kb, 16 * dt, lane);
+        const abf16x8 vl = x3_tr_frag(Vl, kX3Ld, 32 * kb, 16 * dt, lane);
         o[dt] = mfma_x3(vh, vl, ph, pl, o[dt]);
       }
     }
@@ -508,8 +487,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const float* __restri
     stv.load(vb_, sv, kc, lk, tid);
     __syncthreads();                          // the previous chunk's LDS reads are done
     if constexpr (X3) {
-      x3_store_k<64 * NW>(stk, Kh, Kl, tid);
-      x3_store_vt<64 * NW>(stv, Vh, Vl, tid);
+      x3_store_rows<64 * NW, 64>(stk, Kh, Kl, kX3Ld, tid);
+      x3_store_rows<64 * NW, 64>(stv, Vh, Vl, kX3Ld, tid);
     } else {
       stk.store(K_s, tid);
       stv.store(V_s, tid);
@@ -897,8 +876,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kvsplit_kernel(
     stv.load(vb_, sv, kc, kend, tid);
     __syncthreads();                          // the previous chunk's LDS reads are done
     if constexpr (X3) {
-      x3_store_k<64 * NW>(stk, Kh, Kl, tid);
-      x3_store_vt<64 * NW>(stv, Vh, Vl, tid);
+      x3_store_rows<64 * NW, 64>(stk, Kh, Kl, kX3Ld, tid);
+      x3_store_rows<64 * NW, 64>(stv, Vh, Vl, kX3Ld, tid);
     } else {
       stk.store(K_s, tid);
       stv.store(V_s, tid);
@@ -1197,10 +1176,11 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_kernel(
 // attn_bwd_fused_kernel's schedule (64-key block per workgroup, 32-query chunks, 4 waves of 16 keys, dQ
 // from the chunk's dS in LDS) with every product on v_mfma_f32_16x16x32_bf16 over hi / lo pairs: S = Q K^T
 // and dP = dO V^T (Q, dO row-major planes x this wave's K / V fragments), dV^T += dO^T P and dK^T += Q^T dS
-// (dO^T, Q^T planes transposed with the chunk's 32 queries in the S accumulator's order x the P / dS values
-// split in registers), dQ^T += K^T dS^T (the block's K^T planes x the fp32 dS rows split at the read).
-// P, dS, the softmax statistics and all accumulation stay fp32.
-constexpr int kX3Tq = 40;   // transposed chunk rows: 32 queries + 8 bf16 (80-B rows)
+// (the same Q / dO planes read transposed by ds_read_b64_tr_b16, the chunk's 32 queries in the S
+// accumulator's order, x the P / dS values split in registers), dQ^T += K^T dS^T (the block's row-major K
+// planes read transposed, keys in that order, x the fp32 dS rows split at the read). One row-major image
+// per operand: no transposed copies, no 16-bit scattered stores. P, dS, the softmax statistics and all
+// accumulation stay fp32.
 template <int NW, int CH>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
@@ -1212,19 +1192,15 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
   constexpr int HD = 64, DT = 4, KB = 16 * NW, NTL = CH / 16, LDS_ = KB + 4;
   constexpr int DSPLIT = NW >= NTL ? NW / NTL : 1, DTW = DT / DSPLIT;
   static_assert(CH == 32 && NW == 4 && DT % DSPLIT == 0, "split-bf16 fused backward: 32-query chunks, 4 waves");
-  constexpr int kRow = CH * kX3Ld, kCol = HD * kX3Tq, kKt = HD * kX3Ld;   // bf16 per plane
-  __shared__ __attribute__((aligned(16))) uint16_t planes[2 * (2 * kRow + 2 * kCol + kKt)];
+  constexpr int kRow = CH * kX3Ld, kKr = KB * kX3Ld;   // bf16 per plane
+  __shared__ __attribute__((aligned(16))) uint16_t planes[2 * (2 * kRow + kKr)];
   __shared__ __attribute__((aligned(16))) float fsm[CH * LDS_ + 2 * CH];
   uint16_t* const Qh = planes;
   uint16_t* const Ql = Qh + kRow;
   uint16_t* const Oh = Ql + kRow;   // dO
   uint16_t* const Ol = Oh + kRow;
-  uint16_t* const QTh = Ol + kRow;
-  uint16_t* const QTl = QTh + kCol;
-  uint16_t* const OTh = QTl + kCol;
-  uint16_t* const OTl = OTh + kCol;
-  uint16_t* const KTh = OTl + kCol;
-  uint16_t* const KTl = KTh + kKt;
+  uint16_t* const Kh = Ol + kRow;
+  uint16_t* const Kl = Kh + kKr;
   float* const dS_s = fsm;
   float* const lse_s = dS_s + CH * LDS_;
   float* const dl_s = lse_s + CH;
@@ -1255,7 +1231,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
   {
     RowStage<HD, 64 * NW, KB> stk;
     stk.load(k + k0 * sk + hh * HD, sk, kwg, lk, tid);
-    x3_store_cols<64 * NW, KB, false>(stk, KTh, KTl, kX3Ld, tid);   // published by the first chunk's barrier
+    x3_store_rows<64 * NW, KB>(stk, Kh, Kl, kX3Ld, tid);   // published by the first chunk's barrier
   }
   f32x4 dka[DT], dva[DT];
 #pragma unroll
@@ -1289,8 +1265,6 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
     __syncthreads();                          // previous chunk's plane / dS reads are done
     x3_store_rows<64 * NW, CH>(stq, Qh, Ql, kX3Ld, tid);
     x3_store_rows<64 * NW, CH>(sto, Oh, Ol, kX3Ld, tid);
-    x3_store_cols<64 * NW, CH, true>(stq, QTh, QTl, kX3Tq, tid);
-    x3_store_cols<64 * NW, CH, true>(sto, OTh, OTl, kX3Tq, tid);
     if (tid < CH) {
       lse_s[tid] = lse_r;
       dl_s[tid] = dl_r;
@@ -1339,15 +1313,15 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
       split8(d8, dh, dl);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const int off = (16 * dt + r) * kX3Tq + 8 * g;
-        const abf16x8 oth = *reinterpret_cast<const abf16x8*>(OTh + off), otl = *reinterpret_cast<const abf16x8*>(OTl + off);
-        const abf16x8 qth = *reinterpret_cast<const abf16x8*>(QTh + off), qtl = *reinterpret_cast<const abf16x8*>(QTl + off);
+        const abf16x8 oth = x3_tr_frag(Oh, kX3Ld, 0, 16 * dt, lane), otl = x3_tr_frag(Ol, kX3Ld, 0, 16 * dt, lane);
+        const abf16x8 qth = x3_tr_frag(Qh, kX3Ld, 0, 16 * dt, lane), qtl = x3_tr_frag(Ql, kX3Ld, 0, 16 * dt, lane);
         dva[dt] = mfma_x3(oth, otl, ph, pl, dva[dt]);
         dka[dt] = mfma_x3(qth, qtl, dh, dl, dka[dt]);
       }
     }
     __syncthreads();                          // dS of every wave in LDS
-    // dQ^T (16 queries x DTW*16 dims) += K^T dS^T over the block's keys (keys past lk: zero K^T, zero dS)
+    // dQ^T (16 queries x DTW*16 dims) += K^T dS^T over the block's keys in the x3 order of each 32-key block
+    // (keys past lk: zero K rows, zero dS)
     const int nkk = __builtin_amdgcn_readfirstlane((min(NW, (lk - kwg + 15) >> 4) + 1) >> 1);   // 32-key blocks
     for (int u = wave; u < NTL * DSPLIT; u += NW) {
       const int qt = u % NTL, d0 = (u / NTL) * DTW;
@@ -1356,15 +1330,15 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
 #pragma unroll
       for (int j = 0; j < DTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int kk = 0; kk < nkk; ++kk) {
-        const float* dsrow = dS_s + (qt * 16 + r) * LDS_ + 32 * kk + 8 * g;
-        const float4 x = *reinterpret_cast<const float4*>(dsrow), y = *reinterpret_cast<const float4*>(dsrow + 4);
+        const float* dsrow = dS_s + (qt * 16 + r) * LDS_ + 32 * kk + 4 * g;
+        const float4 x = *reinterpret_cast<const float4*>(dsrow), y = *reinterpret_cast<const float4*>(dsrow + 16);
         const float w8[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
         abf16x8 wh, wl;
         split8(w8, wh, wl);
 #pragma unroll
         for (int j = 0; j < DTW; ++j) {
-          const int off = (16 * (d0 + j) + r) * kX3Ld + 32 * kk + 8 * g;
-          const abf16x8 th = *reinterpret_cast<const abf16x8*>(KTh + off), tl = *reinterpret_cast<const abf16x8*>(KTl + off);
+          const abf16x8 th = x3_tr_frag(Kh, kX3Ld, 32 * kk, 16 * (d0 + j), lane);
+          const abf16x8 tl = x3_tr_frag(Kl, kX3Ld, 32 * kk, 16 * (d0 + j), lane);
           acc[j] = mfma_x3(th, tl, wh, wl, acc[j]);
         }
       }
