@@ -355,10 +355,11 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
 #define RQ_ATTN_NO_DMA 1          /* register-staged short forms instead of the LDS-DMA ones */
 #define RQ_ATTN_TWO_PASS 2        /* two-pass backward everywhere (no one-pass / fused forms) */
 #define RQ_ATTN_NO_SPLIT 4        /* no split-key / key-split forward */
-#define RQ_ATTN_SPLIT_BF16 8      /* matmul precision 'high': the long-range forwards (hd 64, > 96 queries per
-                                     sequence, and the key-split form) multiply Q K^T and P V in split-bf16 (3 bf16
-                                     MFMA products, fp32 accumulate and softmax) instead of exact fp32; so does the
-                                     fused long-range backward (S, dP, dV, dK and dQ products; P, dS fp32) */
+#define RQ_ATTN_SPLIT_BF16 8      /* matmul precision 'high': the hd-64 forwards with more than 16 queries per
+                                     sequence over more than 32 keys (chunked, key-split and short forms) multiply
+                                     Q K^T and P V in split-bf16 (3 bf16 MFMA products, fp32 accumulate and
+                                     softmax) instead of exact fp32; so does the fused long-range backward (S, dP,
+                                     dV, dK and dQ products; P, dS fp32) */
 #define RQ_ATTN_QSPLIT_SHIFT 8
 #define RQ_ATTN_QSPLIT(n) ((n) << RQ_ATTN_QSPLIT_SHIFT)   /* fused backward query splits forced to n (1..8; 1 = off) */
 int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,

@@ -1253,15 +1253,19 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
   RowStage<HD, 64 * NW, CH> stq, sto;
   const float sl2 = scale * kLog2e;
   const int col = wave * 16 + r;
+  // Q / dO / lse / delta of a chunk: global -> registers, then LDS; the next chunk's loads are issued
+  // once the current one is in LDS, so they fly while it is multiplied (no occupancy cost here: the
+  // kernel holds 2 waves per SIMD either way)
   float lse_r = 0.f, dl_r = 0.f;
-  for (int qc = c_lo; qc < c_hi; qc += CH) {
+  auto load_chunk = [&](int qc) {
     stq.load(qb_, sq, qc, lq, tid);
     sto.load(ob_, sdo, qc, lq, tid);
-    {
-      const bool ok = tid < CH && qc + tid < lq;
-      lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
-      dl_r = ok ? dl_h[qc + tid] : 0.f;
-    }
+    const bool ok = tid < CH && qc + tid < lq;
+    lse_r = ok ? lse_h[qc + tid] * kLog2e : 0.f;
+    dl_r = ok ? dl_h[qc + tid] : 0.f;
+  };
+  if (c_lo < c_hi) load_chunk(c_lo);
+  for (int qc = c_lo; qc < c_hi; qc += CH) {
     __syncthreads();                          // previous chunk's plane / dS reads are done
     x3_store_rows<64 * NW, CH>(stq, Qh, Ql, kX3Ld, tid);
     x3_store_rows<64 * NW, CH>(sto, Oh, Ol, kX3Ld, tid);
@@ -1270,6 +1274,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fused_x3_kernel(
       dl_s[tid] = dl_r;
     }
     __syncthreads();
+    if (qc + CH < c_hi) load_chunk(qc + CH);
     const int t0 = __builtin_amdgcn_readfirstlane(causal ? max(0, (kb - qc) >> 4) : 0);
     const int nt = __builtin_amdgcn_readfirstlane(wave_on ? max(0, min(NTL, (lq - qc + 15) >> 4) - t0) : 0);
     f32x4 s[NTL], dp[NTL];
@@ -1746,6 +1751,74 @@ __global__ void __launch_bounds__(64 * NW, R <= 64 ? 4 : 3) attn_fwd_dma_kernel(
       for (int i = 0; i < 4; ++i)
         *reinterpret_cast<float4*>(orow + 4 * i) = make_float4(o[0][i] * inv, o[1][i] * inv, o[2][i] * inv, o[3][i] * inv);
       if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (mn + log2f(l)) * kLn2 : 0.f;
+    }
+  }
+}
+
+// Split-bf16 form of the short forward (matmul 'high'): the head's K and V rows (<= R) staged once as
+// row-major hi / lo planes, each wave's 16-query tiles (w, w + 4, ...) run FwdChunkX3 over ALL key tiles in
+// one pass (a single chunk from m = -inf: the max and sum are exact, as in attn_fwd_dma_kernel).
+template <int R>
+__global__ void __launch_bounds__(256) attn_fwd_short_x3_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
+  constexpr int HD = 64, NW = 4, NKT = R / 16;
+  static_assert(R % 32 == 0 && R <= 128, "staged rows");
+  __shared__ __attribute__((aligned(16))) uint16_t planes[4 * R * kX3Ld];
+  uint16_t* const Kh = planes;
+  uint16_t* const Kl = Kh + R * kX3Ld;
+  uint16_t* const Vh = Kl + R * kX3Ld;
+  uint16_t* const Vl = Vh + R * kX3Ld;
+  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  if (b == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
+    zero_rows<HD, 256>(out, so, cu_q[b], Tq, hh, tid);
+    return;
+  }
+  const int64_t q0 = cu_q[b], k0 = cu_k[b];
+  const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+  if (lq <= 0) return;
+  {
+    RowStage<HD, 256, R> stk, stv;   // rows past lk are zero
+    stk.load(k + k0 * sk + hh * HD, sk, 0, lk, tid);
+    stv.load(v + k0 * sv + hh * HD, sv, 0, lk, tid);
+    x3_store_rows<256, R>(stk, Kh, Kl, kX3Ld, tid);
+    x3_store_rows<256, R>(stv, Vh, Vl, kX3Ld, tid);
+  }
+  __syncthreads();
+  const float sl2 = scale * kLog2e;
+  const int nqt = (lq + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += NW) {
+    const int qi = qt * 16 + (lane & 15);
+    const bool qv = qi < lq;
+    abf16x8 qh[2], ql[2];
+    x3_load_q(q + (q0 + (qv ? qi : 0)) * sq + hh * HD, qv, lane, qh, ql);
+    const int kend = causal ? min(lk, qt * 16 + 16) : lk;
+    const int nkt = __builtin_amdgcn_readfirstlane(min((kend + 15) >> 4, NKT));
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    FwdChunkX3 fx{Kh, Kl, Vh, Vl, qh, ql, lane, 0, lk, qi, causal, sl2, &m, &l, o};
+    switch (nkt) {
+      case 1: fx.run<1, true>(); break;
+      case 2: fx.run<2, true>(); break;
+      case 3: if constexpr (NKT >= 3) fx.run<3, true>(); break;
+      case 4: if constexpr (NKT >= 4) fx.run<4, true>(); break;
+      case 5: if constexpr (NKT >= 5) fx.run<5, true>(); break;
+      case 6: if constexpr (NKT >= 6) fx.run<6, true>(); break;
+      case 7: if constexpr (NKT >= 7) fx.run<7, true>(); break;
+      case 8: if constexpr (NKT >= 8) fx.run<8, true>(); break;
+      default: break;                         // no key: zero output, lse 0
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qv) {
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      store_rowT<HD>(out + (q0 + qi) * so + hh * HD, o, inv, lane);
+      if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (m + log2f(l)) * kLn2 : 0.f;
     }
   }
 }
@@ -2772,6 +2845,18 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     }
     if (dma_fwd_plan(HD, max_q, max_k, pol)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
+      if (pol.x3 && max_k > 32) {   // split-bf16 form at matmul 'high'
+#define RQ_FX(R_)                                                                                                \
+  hipLaunchKernelGGL((attn_fwd_short_x3_kernel<R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, \
+                     out, so, lse, Tq)
+        switch (dma_rows_for(max_k)) {
+          case 64: RQ_FX(64); break;
+          case 96: RQ_FX(96); break;
+          default: RQ_FX(128); break;
+        }
+#undef RQ_FX
+        return;
+      }
 #define RQ_FD(R_)                                                                                              \
   hipLaunchKernelGGL((attn_fwd_dma_kernel<4, R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, \
                      out, so, lse, Tq)
