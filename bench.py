@@ -871,7 +871,10 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
                         "flops_per_step_per_gpu": round((dense + attn) / steps / ws),
                         "attention_flops_share": round(attn / (dense + attn), 4),
                         "note": "algorithmic FLOPs (SURVEY 8d, step = 3 x forward); peak = split-bf16 GEMM ceiling "
-                                "(2.5 PF / 3); frac_of_step_roofline = (dense / 833 TF + attention / 157.3 TF) / step time"}}
+                                "(2.5 PF / 3); frac_of_step_roofline = (dense / 833 TF + attention / 157.3 TF) / step time "
+                                "(attention priced at the fp32 MFMA peak: the short backward is exact fp32, while the "
+                                "forwards and the long-range backward run split-bf16 at 'high' against the 833 TF "
+                                "ceiling, so this t_min is an upper bound for those launches)"}}
     if gs is not None and gs.capture_error:
         out["graph_capture_error"] = gs.capture_error
     if stats and rk == 0:
