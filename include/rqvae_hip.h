@@ -355,8 +355,9 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
 #define RQ_ATTN_NO_DMA 1          /* register-staged short forms instead of the LDS-DMA ones */
 #define RQ_ATTN_TWO_PASS 2        /* two-pass backward everywhere (no one-pass / fused forms) */
 #define RQ_ATTN_NO_SPLIT 4        /* no split-key / key-split forward */
-#define RQ_ATTN_SPLIT_BF16 8      /* matmul precision 'high': the hd-64 forwards with more than 16 queries per
-                                     sequence over more than 32 keys (chunked, key-split and short forms) multiply
+#define RQ_ATTN_SPLIT_BF16 8      /* matmul precision 'high': the hd-64 forwards over more than 32 keys with more
+                                     than 16 queries per sequence (chunked, key-split and short forms) or with
+                                     few queries over long key ranges (cross-attention, key-split form) multiply
                                      Q K^T and P V in split-bf16 (3 bf16 MFMA products, fp32 accumulate and
                                      softmax) instead of exact fp32; so does the fused long-range backward (S, dP,
                                      dV, dK and dQ products; P, dS fp32) */

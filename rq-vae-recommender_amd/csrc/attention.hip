@@ -2826,6 +2826,13 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
       constexpr int RPB = 256 / (HD / 4);
       const dim3 gs((unsigned)nsplit, (unsigned)H, (unsigned)B);
       const dim3 gc((unsigned)std::max<int64_t>(1, (max_q + RPB - 1) / RPB), (unsigned)H, (unsigned)B + 1);
+      if (pol.x3 && kb == kKvSplitKB) {   // split-bf16: the key-split form (4 waves stage each 128-key block)
+        hipLaunchKernelGGL((attn_fwd_kvsplit_kernel<HD, 4, kKvSplitKB, true>), gs, dim3(256), 0, st, q, sq, k, sk, v,
+                           sv, cq, ck, scale, Tq, split_ws, nsplit);
+        hipLaunchKernelGGL((attn_fwd_combine_kernel<HD, kKvSplitKB>), gc, dim3(256), 0, st, split_ws, nsplit, cq, ck, Tq,
+                           out, so, lse);
+        return;
+      }
 #define RQ_SPL(KB_)                                                                                                \
   hipLaunchKernelGGL((attn_fwd_split_kernel<HD, KB_>), gs, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, scale, Tq, \
                      split_ws, nsplit);                                                                            \
