@@ -4,6 +4,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <mutex>
+
 #include "common.h"
 
 namespace rqhip {
@@ -23,13 +25,32 @@ const char* rq_last_error(void) { return rqhip::g_err; }
 
 int rq_abi_version(void) { return 3; }
 
-// Dropout epoch (common.h): the three translation units' device copies on the current device, resolved
-// per call (no process-wide cache: the addresses are per device).
+// Dropout epoch (common.h): the three translation units' device copies, resolved once per device
+// (the symbol addresses differ per device) and cached; resolving costs three runtime lookups, and the
+// epoch is advanced on every step, inside captured graphs too.
 static int epoch_addrs(void** p) {
+  constexpr int kMaxDev = 64;
+  static std::mutex mu;
+  static void* cache[kMaxDev][3];
+  static bool have[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) {
+    rqhip::set_error("rq_seed_epoch: hipGetDevice failed");
+    return rqhip::kBadArg;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  if (dev < kMaxDev && have[dev]) {
+    for (int i = 0; i < 3; ++i) p[i] = cache[dev][i];
+    return 0;
+  }
   if (rqhip::seed_epoch_addr_dropout(&p[0]) || rqhip::seed_epoch_addr_rowwise(&p[1]) ||
       rqhip::seed_epoch_addr_linear(&p[2])) {
     rqhip::set_error("rq_seed_epoch: hipGetSymbolAddress failed");
     return rqhip::kBadArg;
+  }
+  if (dev < kMaxDev) {
+    for (int i = 0; i < 3; ++i) cache[dev][i] = p[i];
+    have[dev] = true;
   }
   return 0;
 }

@@ -78,9 +78,12 @@ class SeqData(Dataset):
 
     Indexing with an int returns one sample (the reference's per-item form, collated by the
     DataLoader); indexing with a list / array of ints returns the collated SeqBatch of those samples
-    in one vectorised numpy pass — the same fields, shapes and sub-window draws as collating the
-    per-item samples (`__getitem__([i, j])` == default_collate([self[i], self[j]]) for the same rng
-    state). The reference fetches and collates per item (~12 ms per 256-sequence batch on this host,
+    in one vectorised numpy pass — the same fields, shapes and sub-window draws as collating THIS
+    class's per-item samples (`__getitem__([i, j])` == default_collate([self[i], self[j]]) for the same
+    rng state). The window bounds follow the reference's distribution, not its random stream; and since
+    round 4 (uniform floats per sample, one flat draw of the synthetic histories) a given seed yields a
+    different synthetic corpus and windows than earlier rounds, so their logged losses are not
+    comparable. The reference fetches and collates per item (~12 ms per 256-sequence batch on this host,
     slower than the decoder's GPU step); `batch_loader` drives the batched form with the reference
     DataLoader's sampling order."""
 

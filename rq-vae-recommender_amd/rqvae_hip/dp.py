@@ -48,6 +48,30 @@ def rank():
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
+_FR_ENV = ("TORCH_FR_BUFFER_SIZE", "TORCH_NCCL_TRACE_BUFFER_SIZE")
+
+
+def watchdog_record_enabled() -> bool:
+    """True when torch's flight recorder records RCCL collectives (read once by torch, when the first
+    process group is created): GraphedSteps then checks that the watchdog has retired every eager
+    collective before it captures the exchange (graph.watchdog_retired)."""
+    for k in _FR_ENV:
+        try:
+            if int(os.environ.get(k, "0") or 0) > 0:
+                return True
+        except ValueError:
+            pass
+    return False
+
+
+def enable_watchdog_record(entries: int = 256):
+    """Turn on torch's flight recorder (a ring of the last `entries` collectives and their state)
+    unless the environment already configures it. Must run before the first RCCL process group is
+    created; init_from_env does."""
+    if not watchdog_record_enabled():
+        os.environ["TORCH_FR_BUFFER_SIZE"] = str(int(entries))
+
+
 def init_from_env(backend: Optional[str] = None):
     """Initialise torch.distributed from RANK / WORLD_SIZE / MASTER_* (torchrun env). Returns
     (rank, world, local_rank). No-op for WORLD_SIZE=1.
@@ -65,6 +89,7 @@ def init_from_env(backend: Optional[str] = None):
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
+            enable_watchdog_record()
             torch.cuda.set_device(lr)
             dist.init_process_group(backend, device_id=torch.device("cuda", lr))
         else:

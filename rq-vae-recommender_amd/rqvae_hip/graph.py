@@ -47,6 +47,38 @@ def _in_graph_default(buckets) -> bool:
     return dist.get_backend() == "nccl"
 
 
+WATCHDOG_RETIRE_S = 5.0
+
+
+def watchdog_retired(timeout_s: float = None):
+    """Before an in-graph capture: wait until the RCCL process groups' watchdogs have RETIRED every
+    eager collective of this process. On ROCm a watchdog query of such a collective's event while the
+    exchange is being captured fails the capture even in thread-local mode ("dependency created on
+    uncaptured work in another stream", tools/graph_exchange_probe.py race_forever); the watchdog stops
+    querying a Work when it retires it. The flight recorder (dp.enable_watchdog_record, on by default in
+    dp.init_from_env) marks each recorded collective `retired` exactly then, and captured collectives
+    are never recorded (tools/fr_probe.py), so "every entry retired" is the watchdog's list being empty.
+    Returns True once it is (device work synchronised first: the watchdog retires completed work only),
+    False if it is not within the bound, None when the flight recorder is off (nothing to check)."""
+    import json
+    import threading
+    import time
+    from .dp import watchdog_record_enabled
+    if not watchdog_record_enabled():
+        return None
+    import torch._C._distributed_c10d as c10d
+    torch.cuda.synchronize()
+    deadline = time.monotonic() + (WATCHDOG_RETIRE_S if timeout_s is None else timeout_s)
+    poll = threading.Event()
+    while True:
+        d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=True, onlyActive=False))
+        if all(e.get("retired", False) for e in d.get("entries", [])):
+            return True
+        if time.monotonic() > deadline:
+            return False
+        poll.wait(0.002)   # poll interval: the watchdog wakes every ~100 ms (retired ~40 ms after completion)
+
+
 class GraphedSteps:
     """One captured forward + backward per input "key" for steps whose shapes depend on the data
     only through a small set of host-known keys — the decoder train step: its context rows are
@@ -170,59 +202,54 @@ class GraphedSteps:
             torch.cuda.synchronize()
 
     def _capture(self, key, batch):
+        """Warm up and capture a new key's step. The decision whether this key's graph holds the
+        exchange is LOCAL to the rank: a rank whose capture of the collectives fails (or cannot be
+        made safe, below) records a graph without them and exchanges after its replay. Every rank
+        still issues the same all-reduces in bucket order once per step, in the graph or after it,
+        so ranks that decide differently — or that capture different keys in the same step (the
+        decoder's keys come from each rank's own shard), or replay while another rank captures or
+        runs eagerly past `max_graphs` — stay matched. No collective depends on the key."""
         if self.prepare is not None:
             self.prepare(self.static, batch)
         self._warm()
-        if not self.capture:
-            self.graphs[key] = (None, None)
-            return self.graphs[key]
+        exchanged = self.in_graph
         # thread_local capture mode everywhere: other threads of the process keep making HIP calls while
         # the step is captured — the process group's watchdog polls the events of earlier (eager)
         # collectives, a trainer's feed thread pins host memory (the caching host allocator queries and
         # records events) — and under the default global mode any such call fails the capture ("operation
         # not permitted when stream is capturing", seen on MI355X with the watchdog)
-        if self.in_graph:
-            self._quiesce()
-        g, out, err = self._try_capture(self.in_graph)
-        if self.in_graph and self._world() > 1:
-            # one decision for all ranks: if any rank failed to capture its collectives, every rank
-            # exchanges after the replay (a mixed in-graph / post-replay world would still issue the same
-            # all-reduces, but nothing would test it)
-            ok = torch.tensor([0.0 if err is not None else 1.0], device=self._device())
-            import torch.distributed as dist
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if float(ok.item()) == 0.0:
-                err = err or "capture of the exchange failed on another rank"
+        if exchanged and self.capture:
+            idle = watchdog_retired()
+            if not idle:
+                exchanged = False
+                if idle is None:   # cannot be checked in this process: never capture the exchange
+                    self.in_graph = False
+                    self.capture_error = "flight recorder off: the watchdog's work list cannot be checked"
+                else:              # this key exchanges after its replay; later keys try again
+                    self.capture_error = f"watchdog kept an eager collective past {WATCHDOG_RETIRE_S} s"
+        g, out, err = self._try_capture(exchanged)
         if err is not None:
-            if not self.in_graph:
+            if not exchanged:
                 raise err if isinstance(err, BaseException) else RuntimeError(err)
             self.capture_error = repr(err)[:300]
-            self.in_graph = False
-            torch.cuda.synchronize()
+            self.in_graph = False   # this rank exchanges after the replay from now on
+            exchanged = False
+            if self.capture:
+                torch.cuda.synchronize()
             g, out, err2 = self._try_capture(False)
             if err2 is not None:
                 raise err2
-        if self.pool is None:
+        if g is not None and self.pool is None:
             self.pool = g.pool()
-        self.graphs[key] = (g, out)
+        self.graphs[key] = (g, out, exchanged)
         return self.graphs[key]
 
-    # ProcessGroupNCCL's watchdog thread wakes every 100 ms and queries the end events of the collectives
-    # it tracks until it sees them complete. On ROCm a query of such an event from another thread while
-    # the exchange is being captured fails the capture even in thread-local mode ("dependency created on
-    # uncaptured work in another stream", tools/graph_exchange_probe.py race_forever), so before an
-    # in-graph capture every earlier collective is completed on the device and the watchdog is given
-    # more than two of its polling periods to retire them.
-    QUIESCE_S = 0.3
-
-    def _quiesce(self):
-        import time
-        torch.cuda.synchronize()
-        time.sleep(self.QUIESCE_S)
-
     def _try_capture(self, in_graph: bool):
-        """Capture one step body: (graph, its output, None) or (None, None, the exception)."""
+        """Capture one step body: (graph, its output, None) or (None, None, the exception).
+        capture=False: (None, None, None) — the body runs eagerly at every call."""
         import contextlib
+        if not self.capture:
+            return None, None, None
         g = torch.cuda.CUDAGraph()
         susp = contextlib.nullcontext() if in_graph else self.buckets.suspended()
         try:
@@ -268,13 +295,16 @@ class GraphedSteps:
         self._copy_in(batch, sig)
         if entry is None:
             entry = self._capture(key, batch)
-        g, out = entry
+        g, out, exchanged = entry
         if g is None:   # capture=False: the body runs eagerly, with the captured form's exchange
+            import contextlib
             if self.prepare is not None:
                 self.prepare(self.static, batch)
-            out = self._body(exchange=self.in_graph)
+            susp = self.buckets.suspended() if (self.buckets is not None and not exchanged) else contextlib.nullcontext()
+            with susp:
+                out = self._body(exchange=exchanged)
         else:
             g.replay()
-        if self.in_graph and self.buckets is not None:
+        if exchanged and self.buckets is not None:
             self.buckets.mark_graph_exchanged()
         return out

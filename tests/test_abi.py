@@ -82,3 +82,45 @@ def test_library_exports_nothing_undeclared():
     c_names = {n for n in exported if not n.startswith("_")}   # C++ (mangled) symbols are not the ABI
     assert c_names == set(_declared()), sorted(c_names ^ set(_declared()))
 
+
+
+_LIB_NAMES = {"lib", "typed", "L", "_L"}   # names the repo binds the loaded CDLL to
+
+
+def _abi_call_sites():
+    """Every literal call into the C ABI in the repo's Python: `call("name", ...)`,
+    `TIMER.around(key, call, "name", ...)` and `<lib>.name(...)` with `name` a typed entry point."""
+    import ast
+    from rqvae_hip import _lib
+    files = [os.path.join(ROOT, "bench.py"), os.path.join(ROOT, "__graft_entry__.py")]
+    for d in ("tools", "tests", "rq-vae-recommender_amd"):
+        for dp, _, fns in os.walk(os.path.join(ROOT, d)):
+            files += [os.path.join(dp, f) for f in fns if f.endswith(".py")]
+    for path in files:
+        tree = ast.parse(open(path).read(), filename=path)
+        for node in ast.walk(tree):
+            if not isinstance(node, ast.Call):
+                continue
+            f = node.func
+            fname = f.id if isinstance(f, ast.Name) else f.attr if isinstance(f, ast.Attribute) else None
+            name, args = None, None
+            lit = [a.value if isinstance(a, ast.Constant) else None for a in node.args]
+            if fname == "call" and lit and lit[0] in _lib._SIGS:
+                name, args = lit[0], node.args[1:]
+            elif fname == "around" and len(lit) >= 3 and lit[2] in _lib._SIGS:
+                name, args = lit[2], node.args[3:]
+            elif isinstance(f, ast.Attribute) and f.attr in _lib._SIGS and (
+                    isinstance(f.value, ast.Call) or (isinstance(f.value, ast.Name) and f.value.id in _LIB_NAMES)):
+                name, args = f.attr, node.args   # `_lib.load().name(...)`, `lib.name(...)`
+            if name is None or any(isinstance(a, ast.Starred) for a in args) or node.keywords:
+                continue
+            yield os.path.relpath(path, ROOT), node.lineno, name, len(args), len(_lib._SIGS[name][0])
+
+
+def test_abi_call_sites_match_signatures():
+    """Guards tools / tests / bench against ABI drift: a call with the wrong argument count only
+    fails at run time on the GPU box (round 4: tools/pmc_quantize.py passed 15 of 17 arguments)."""
+    sites = list(_abi_call_sites())
+    assert len(sites) > 60
+    bad = [s for s in sites if s[3] != s[4]]
+    assert not bad, bad

@@ -115,7 +115,7 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
             buckets = dp.GradBuckets([ps[len(ps) // 2:][::-1], ps[:len(ps) // 2][::-1]], bucket_bytes=bucket_bytes)
         elif mode == "empty":   # buckets in forward order: the last bucket's grads are ready first
             buckets = dp.GradBuckets([list(model.parameters())], bucket_bytes=bucket_bytes)
-        elif mode in ("graphed", "tied"):
+        elif mode in ("graphed", "graphed_mixed", "tied"):
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes, flat_views=True)
         else:
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
@@ -129,10 +129,26 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
             from rqvae_hip.graph import GraphedSteps
             gs = GraphedSteps(lambda xb: _loss(model, xb) * dp.shard_weight(b - a, gb), lambda xb: 0, buckets,
                               capture=False, in_graph_exchange=True)
-        for _ in range(2):                     # two steps: zero_grad must reset the flat buffers
+        elif mode == "graphed_mixed":
+            # ranks disagree step by step: rank 0 keeps one key (probe, capture with the
+            # in-body exchange, replay); rank 1 sees a new key every step with max_graphs=1 and its
+            # capture of the exchange fails (probe, graph without the exchange + post-replay exchange,
+            # then an eager step past max_graphs). Every rank must still run the same collectives.
+            from rqvae_hip.graph import GraphedSteps
+            step = [0]
+            gs = GraphedSteps(lambda xb: _loss(model, xb) * dp.shard_weight(b - a, gb),
+                              lambda xb: step[0] if r == 1 else 0, buckets, capture=False, in_graph_exchange=True,
+                              max_graphs=1)
+            if r == 1:
+                orig = gs._try_capture
+                gs._try_capture = lambda in_graph: ((None, None, RuntimeError("simulated capture failure"))
+                                                    if in_graph else orig(in_graph))
+        for _ in range(_steps(mode)):          # >= two steps: zero_grad must reset the flat buffers
             if gs is not None:                 # step 1: eager probe; step 2: warm-ups + the in-body exchange
                 gs(x[a:b].clone())
                 assert gs.graphs or _ == 0
+                if mode == "graphed_mixed":
+                    step[0] += 1
                 buckets.synchronize()
                 grads = {n: (None if p.grad is None else p.grad.detach().numpy().copy())
                          for n, p in model.named_parameters()}
@@ -163,10 +179,16 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
         # numpy copies: tensors sent through a torch.multiprocessing queue are shared-memory handles
         # that die with this process (the parent may read after we exit)
         params = {n: p.detach().numpy().copy() for n, p in model.named_parameters()}
+        if mode == "graphed_mixed":
+            assert (gs.in_graph, gs.eager_steps, len(gs.graphs)) == ((True, 1, 1) if r == 0 else (False, 2, 1))
         q.put((r, (a, b), params, grads, len(buckets.buckets), mine))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def _steps(mode):
+    return 3 if mode == "graphed_mixed" else 2
 
 
 def _run(world, gb, bucket_bytes, mode):
@@ -190,7 +212,7 @@ def _single_process(state0, gb, mode, world):
     opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
     x, lengths, toks = _data(gb)
     grads = None
-    for _ in range(2):
+    for _ in range(_steps(mode)):
         opt.zero_grad(set_to_none=True)
         if mode == "accum":
             ((_loss(model, x) + _loss(model, x.flip(0))) / 2).backward()
@@ -211,6 +233,7 @@ def _single_process(state0, gb, mode, world):
     (3, 61, 4096, "tokens"),        # token-balanced variable-length shards (unequal sequence counts)
     (3, 2, 2048, "empty"),          # global batch < world: rank 2 has no sequences, several buckets
     (2, 64, 2048, "graphed"),       # GraphedSteps bodies with the in-graph exchange (run eagerly)
+    (2, 64, 2048, "graphed_mixed"),  # ranks with different keys / capture outcomes / eager fallbacks
     (2, 64, 1024, "tied"),          # one weight, two direct-gradient contributions per backward
 ])
 def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode):

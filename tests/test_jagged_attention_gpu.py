@@ -424,3 +424,40 @@ def test_varlen_attention_split_bf16_vs_oracle(device, B, max_q, max_k, H, hd, c
             assert float((a - b).abs().max()) <= tol * float(b.abs().max()), ("out", "dq", "dk", "dv")[i]
     finally:
         torch.set_float32_matmul_precision(prev)
+
+
+@pytest.mark.parametrize("fwd_prec,bwd_prec", [("highest", "high"), ("high", "highest")])
+@pytest.mark.parametrize("B,max_q,max_k,H,hd,causal,same", [
+    (2, 700, 700, 4, 64, True, True),     # chunked fwd / fused bwd (both split-bf16 at 'high')
+    (8, 81, 81, 8, 64, False, True),      # short split-bf16 fwd at 'high' / short fp32 bwd always
+    (6, 5, 81, 8, 64, False, False),      # few-query fp32 fwd always / few-query fp32 bwd
+    (5, 6, 801, 6, 64, False, False),     # key-split fwd (split at 'high') / fused bwd (split at 'high')
+    (5, 20, 20, 4, 64, True, True),       # max_k <= 32: fp32 fwd always / short bwd
+])
+def test_varlen_attention_precision_pairings_vs_oracle(device, fwd_prec, bwd_prec, B, max_q, max_k, H, hd, causal,
+                                                       same):
+    """lse (and O) may come from a forward at one product precision while the backward recomputes P from S at
+    the other: the kernel a launch picks decides whether its products are split-bf16 or exact fp32 at 'high'
+    (forwards: key-split, short_x3 (> 32 keys), chunked NW=4 split; fewq, NW 1/2 and <= 32 keys fp32;
+    backward: only the fused long-range kernel is split). Every pairing — including the matmul precision
+    changed between forward and backward — stays within the oracle tolerances of the exact forms."""
+    from rqvae_hip import ops
+    prev = torch.get_float32_matmul_precision()
+    try:
+        g = gi.rng(B * 977 + max_k)
+        q, k, v, do, cq, ck = _varlen_case(g, B, max_q, max_k, H, hd, same)
+        A_ = H * hd
+        xs = [torch.from_numpy(a.reshape(-1, A_)).to(device).requires_grad_(True) for a in (q, k, v)]
+        cqt, ckt = torch.from_numpy(cq).to(device), torch.from_numpy(ck).to(device)
+        torch.set_float32_matmul_precision(fwd_prec)
+        out = ops.varlen_attention(*xs, cqt, ckt, H, causal, int(np.diff(cq).max()), int(np.diff(ck).max()))
+        torch.set_float32_matmul_precision(bwd_prec)
+        out.backward(torch.from_numpy(do.reshape(-1, A_)).to(device))
+        ref, _ = A.attn_fwd(q, k, v, cq, ck, causal)
+        rg = A.attn_bwd(q, k, v, do, cq, ck, causal)
+        for got, want, atol, rtol, what in ((out, ref, 2e-5, 2e-4, "out"), (xs[0].grad, rg[0], 1e-4, 1e-3, "dq"),
+                                            (xs[1].grad, rg[1], 1e-4, 1e-3, "dk"), (xs[2].grad, rg[2], 1e-4, 1e-3, "dv")):
+            a = got.detach().cpu().double().numpy().reshape(want.shape)
+            assert np.all(np.abs(a - want) <= atol + rtol * np.abs(want)), (what, float(np.abs(a - want).max()))
+    finally:
+        torch.set_float32_matmul_precision(prev)

@@ -9,8 +9,8 @@ copy (a one-rank all-reduce is the identity, so the gradients must match bit for
 
 `race` (argv[2]): the capture starts while an eager all-reduce is in flight and another thread does
 what the process group's watchdog does — polls the Work's is_completed() until it reports completion —
-and pins host memory (what a trainer's feed thread does). GraphedSteps quiesces (device sync + more
-than two watchdog periods) before an in-graph capture, so the exchange must be captured.
+and pins host memory (what a trainer's feed thread does). GraphedSteps waits until the watchdog has
+retired every eager collective (flight recorder) before an in-graph capture, so the exchange must be captured.
 `race_forever`: the poller never stops querying the (completed) Work: on ROCm that fails the capture
 even in thread-local mode ("dependency created on uncaptured work in another stream"), and
 GraphedSteps must fall back to the post-replay exchange with the same gradients.
@@ -36,6 +36,8 @@ def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    from rqvae_hip import dp as _dp
+    _dp.enable_watchdog_record()   # what dp.init_from_env does: GraphedSteps checks the watchdog's list
     dist.init_process_group("nccl", device_id=dev)
     from data.processed import synthetic_tokenized_batch
     from modules.model import EncoderDecoderRetrievalModel

@@ -32,7 +32,7 @@ def main():
     ql, es = torch.empty(B, device=dev), torch.empty(B, D, device=dev)
     for _ in range(n):
         call("rq_quantize_fwd", ptr(x), B, D, ptr(cbs), ptr(csq), K, L, 3, 0.25, ptr(ids), ptr(emb), ptr(res), ptr(ql),
-             ptr(es), stream_handle())
+             ptr(es), None, 0, stream_handle())
     torch.cuda.synchronize()
     print(f"pmc_quantize: {n} launches of rq_quantize_fwd at B={B} D={D} K={K} L={L}")
 
