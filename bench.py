@@ -472,10 +472,23 @@ def measure_trainers(iters=30):
                               "wall_s": round(time.perf_counter() - t0, 1)}
         ckpt = sorted(glob.glob(tmp + "/vae/checkpoint_*.pt"))[-1]
         t0 = time.perf_counter()
-        train_decoder.train(iterations=2 * iters, batch_size=DEC["B"], learning_rate=DEC["lr"], weight_decay=DEC["wd"],
-                            dataset=RecDataset.AMAZON, pretrained_rqvae_path=ckpt, decoder_embed_dim=DEC["E"],
-                            dropout_p=DEC["dropout"], attn_heads=DEC["H"], attn_embed_dim=DEC["A"],
-                            attn_layers=DEC["layers"], save_dir_root=tmp + "/dec/", log_every=10 ** 9, **vae)
+        # the synthetic Amazon corpus at the bench step's length distribution (histories of U{3..21} items,
+        # whole windows: U{2..20} context items per sequence), so the trainer's tokens/s compares with
+        # decoder_amazon.ctx_tokens_per_s at matched batches
+        from data import processed
+        prev = processed.SYNTHETIC_HIST_LEN.get(RecDataset.AMAZON)
+        processed.SYNTHETIC_HIST_LEN[RecDataset.AMAZON] = (DEC.get("min_items", 2) + 1, DEC["max_items"] + 2)
+        try:
+            train_decoder.train(iterations=2 * iters, batch_size=DEC["B"], learning_rate=DEC["lr"],
+                                weight_decay=DEC["wd"], dataset=RecDataset.AMAZON, pretrained_rqvae_path=ckpt,
+                                decoder_embed_dim=DEC["E"], dropout_p=DEC["dropout"], attn_heads=DEC["H"],
+                                attn_embed_dim=DEC["A"], attn_layers=DEC["layers"], save_dir_root=tmp + "/dec/",
+                                log_every=10 ** 9, train_data_subsample=False, **vae)
+        finally:
+            if prev is None:
+                processed.SYNTHETIC_HIST_LEN.pop(RecDataset.AMAZON, None)
+            else:
+                processed.SYNTHETIC_HIST_LEN[RecDataset.AMAZON] = prev
         r = dict(train_decoder.LAST_RUN)
         out["decoder_amazon"] = {**{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()},
                                  "wall_s": round(time.perf_counter() - t0, 1)}
@@ -858,7 +871,8 @@ def measure_decoder(device, ws=1, rk=0, cfg=DEC, B=None, steps=20, warmup=5, gra
     out = {"config": f"decoder_{cfg['name']} (A={cfg['A']}, H={cfg['H']}, {cfg['layers']} layers, max "
                      f"{cfg['max_items']} items -> ctx <= {cfg['max_items'] * cfg['sem_id_dim'] + 1})",
            "ctx_tokens_per_s": round(toks / dt, 1), "ctx_plus_fut_tokens_per_s": round((toks + fut) / dt, 1),
-           "ms_per_step": round(ms, 3), "per_gpu_batch": B, "n_gpus": ws, "parallelism": f"dp{ws}",
+           "ms_per_step": round(ms, 3), "per_gpu_batch": B, "ctx_tokens_per_step_rank": round(toks / steps / ws, 1),
+           "n_gpus": ws, "parallelism": f"dp{ws}",
            "scaling": "weak", "step_mode": "hipgraph per row bucket" if graphs else "eager",
            "graphs_captured": len(gs.graphs) if gs is not None else 0,
            "grad_exchange": ("none (1 rank)" if ws == 1 else

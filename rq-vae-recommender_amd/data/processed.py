@@ -33,6 +33,10 @@ DATASET_NAME_TO_MAX_SEQ_LEN = {RecDataset.AMAZON: 20, RecDataset.ML_1M: 200, Rec
 # public corpus sizes used for the synthetic stand-ins
 SYNTHETIC_N_ITEMS = {RecDataset.AMAZON: 12101, RecDataset.ML_1M: 3706, RecDataset.ML_32M: 87585}
 SYNTHETIC_N_USERS = {RecDataset.AMAZON: 22363, RecDataset.ML_1M: 6040, RecDataset.ML_32M: 200948}
+# Synthetic history lengths per dataset: U{lo..hi-1} items (None: U{4..2 max_seq_len - 1}). bench.py sets
+# AMAZON to (3, 22) for its trainer line: with train_data_subsample=False every window is the whole
+# history, i.e. U{2..20} context items per sequence — the length distribution of its decoder step.
+SYNTHETIC_HIST_LEN = {}
 
 
 def synthetic_items(n: int, dim: int = 768, seed: int = 0) -> torch.Tensor:
@@ -105,7 +109,8 @@ class SeqData(Dataset):
         self.rng = np.random.Generator(np.random.PCG64(seed + 2))
         g = np.random.Generator(np.random.PCG64(seed + 3))
         # histories as one flat item array + per-user offsets (user u: flat[off[u]:off[u+1]])
-        self.hist_len = g.integers(4, 2 * self._max_seq_len, size=self.n_users)
+        lo, hi = SYNTHETIC_HIST_LEN.get(dataset) or (4, 2 * self._max_seq_len)
+        self.hist_len = g.integers(lo, hi, size=self.n_users)
         self.hist_off = np.concatenate([[0], np.cumsum(self.hist_len)])
         self.hist_flat = g.integers(0, self.n_items, size=int(self.hist_off[-1]))
         self.split = "train" if is_train else "test"

@@ -135,6 +135,11 @@ class SemanticIdTokenizer(nn.Module):
         rows = self.cached_ids[ids.flatten()]
         return rows.reshape(ids.shape[0], -1)
 
+    def cache_hit(self, ids_max: int) -> bool:
+        """True when every id up to `ids_max` (host int) maps through the precomputed corpus cache: forward
+        then launches only device lookups (no RQ-VAE pass, no host read), so it can be captured."""
+        return self.cached_ids is not None and int(ids_max) < self.cached_ids.shape[0]
+
     @torch.no_grad()
     @eval_mode
     def forward(self, batch: SeqBatch, ids_max: Optional[int] = None) -> TokenizedSeqBatch:

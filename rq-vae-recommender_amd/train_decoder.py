@@ -37,7 +37,7 @@ from modules.utils import parse_config
 from rqvae_hip import dp, gemm_tuning
 from rqvae_hip import optim as hip_optim
 from rqvae_hip.graph import GraphedSteps
-from ops.jagged import copy_row_counts, register_row_counts
+from ops.jagged import copy_row_counts, register_row_counts, row_counts
 
 
 def token_balanced_shard(seq_mask: torch.Tensor, rank: int, world: int) -> torch.Tensor:
@@ -177,12 +177,24 @@ def train(iterations=500000, batch_size=64, learning_rate=0.001, weight_decay=0.
     bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
 
     def graph_body(inp):
-        tok, w = inp
+        # the raw (device) SeqBatch goes into the graph and is tokenized there: the tokenizer's cache lookups,
+        # mask expansion and token types are ~10 small launches whose host cost (~2 ms per iteration) the
+        # replay removes. The caller checked on the host that every id hits the cache (ids_max); the raw
+        # mask carries the TOKENIZED row counts (register_row_counts in the loop), handed to the tokenized
+        # mask so the jagged conversions size their buffers without a device read.
+        data, w = inp
+        tok = tokenizer(data, ids_max=0)
+        copy_row_counts(tok.seq_mask, data.seq_mask)
         out = model(tok)
         (out.loss * w).backward()
         return out.loss.detach()
 
-    graphed = GraphedSteps(graph_body, lambda inp: model.context_rows(inp[0], bucket), buckets, run_backward=False,
+    def graph_key(inp):
+        c = row_counts(inp[0].seq_mask)   # (sum, min, max, rows) of the tokenized context counts
+        total = c[0] + c[3]               # + the user token per sequence (model.context_rows)
+        return total if not bucket else (total + bucket - 1) // bucket * bucket
+
+    graphed = GraphedSteps(graph_body, graph_key, buckets, run_backward=False,
                            prepare=lambda static, inp: copy_row_counts(static[0].seq_mask, inp[0].seq_mask)
                            ) if use_graphs else None
     feed = _Prefetch(loader, rank, world, tokenizer.sem_ids_dim)
@@ -239,18 +251,24 @@ def _train_loop(feed, model, tokenizer, graphed, buckets, opt, sched, device, ra
             if t_mark is not None:
                 toks += sum(counts) + len(counts)   # context tokens (+ the user token per sequence)
                 s_toks += sum(counts) + len(counts)
-            tok = tokenizer(batch_to(data, device), ids_max=ids_max)
-            register_row_counts(tok.seq_mask, counts)
             # this rank's shard mean -> share of the GLOBAL-batch mean (unequal, token-balanced shards)
             w = dp.shard_weight(len(counts), n_glob) / gradient_accumulate_every
-            c2 = clock()
-            phase["tokenize"] += c2 - c1
-            if graphed is not None:
+            data = batch_to(data, device)
+            if graphed is not None and tokenizer.cache_hit(ids_max):   # tokenized inside the replayed graph
+                register_row_counts(data.seq_mask, counts)
+                c2 = clock()
+                phase["tokenize"] += c2 - c1
                 wt = w_dev.get(w)
                 if wt is None:   # a few distinct weights over a run: one device scalar each, no per-step copy
                     wt = w_dev[w] = torch.tensor(w, device=device)
-                loss = graphed((tok, wt)).clone()   # the graph's output buffer is overwritten by the next replay
+                loss = graphed((data, wt)).clone()   # the graph's output buffer is overwritten by the next replay
             else:
+                if graphed is not None:   # an id past the cache (never with a precomputed corpus): eager step
+                    buckets.zero_grad()
+                tok = tokenizer(data, ids_max=ids_max)
+                register_row_counts(tok.seq_mask, counts)
+                c2 = clock()
+                phase["tokenize"] += c2 - c1
                 out = model(tok)
                 last = micro == gradient_accumulate_every - 1
                 with (contextlib.nullcontext() if last else buckets.no_sync()):
@@ -280,7 +298,7 @@ def _train_loop(feed, model, tokenizer, graphed, buckets, opt, sched, device, ra
                 ds = t_end - s_mark
                 n_s = iterations - s_from
                 steady = dict(steady_iter_ms=ds * 1e3 / n_s, steady_iters=n_s,
-                              steady_ctx_tokens_per_s_rank=s_toks / ds,
+                              steady_ctx_tokens_per_s_rank=s_toks / ds, ctx_tokens_per_iter_rank=s_toks / n_s,
                               host_ms_per_iter={k: round(v * 1e3 / n_s, 4) for k, v in phase.items()})
             LAST_RUN.update(iter_ms=dt * 1e3 / max(1, iterations - t_from), timed_iters=iterations - t_from,
                             ctx_tokens_per_s_rank=toks / dt, world=world, **steady,

@@ -461,3 +461,4 @@ def test_varlen_attention_precision_pairings_vs_oracle(device, fwd_prec, bwd_pre
             assert np.all(np.abs(a - want) <= atol + rtol * np.abs(want)), (what, float(np.abs(a - want).max()))
     finally:
         torch.set_float32_matmul_precision(prev)
+
