@@ -330,6 +330,24 @@ int jagged_from_padded_rows(const void* x, int64_t B, int64_t N, int64_t D, cons
 int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int64_t N, int64_t D, void* x, int dtype,
                      void* stream);
 
+/* Decoder input embeddings straight into the two jagged batches (reference modules/model.py:101-129
+ * `_predict` up to padded_to_jagged_tensor, with modules/embedding/id_embedder.py:28-53 SemIdEmbedder /
+ * UserIdEmbedder): context row 0 = user_w[user_ids[b] mod n_buckets]; context row 1 + j = wpe_w[j] +
+ * sem_w[seq_mask ? type_ids * K + sem_ids : pad] for j < sum(seq_mask[b]); future row 0 = bos, future row
+ * 1 + t = sem_w[type_ids_fut * K + sem_ids_fut] + tte_w[type_ids_fut]; every value through the jagged
+ * gather's (v + 1) - 1 (ops/triton/jagged.py:65): bitwise the reference composition.
+ *   ids (B, N) / (B, L) int64, seq_mask (B, N) bool, tables fp32 row-major with E columns (E % 4 == 0);
+ *   ctx_values (ctx_alloc_rows, E): rows past ctx_offsets[B] zero; ctx_offsets (B+1) = [0, cumsum(sum(mask)+1)];
+ *   fut_values (B * (L+1), E), fut_offsets (B+1) = b (L+1); keys (B, N+L) int64 = the context's sem-table rows
+ *   then the future's (the backward's segmented-sum keys), uid_mod (B) int64. Two launches; graph-capturable. */
+int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const int64_t* type_ids, const bool* seq_mask,
+                        const int64_t* sem_ids_fut, const int64_t* type_ids_fut, int64_t B, int64_t N, int64_t L,
+                        int64_t E, const float* user_w, int64_t n_buckets, const float* sem_w, int64_t n_sem_rows,
+                        int64_t K, int64_t pad, const float* wpe_w, int64_t n_wpe_rows, const float* tte_w,
+                        int64_t n_tte_rows, const float* bos, float* ctx_values, int64_t ctx_alloc_rows,
+                        int64_t* ctx_offsets, float* fut_values, int64_t* fut_offsets, int64_t* keys, int64_t* uid_mod,
+                        void* stream);
+
 /* Varlen multi-head attention on packed rows = F.scaled_dot_product_attention on NJT q/k/v
  * (modules/transformer/attention.py:113-124), dropout 0, is_causal top-left.
  *   q[t][h][d] at q + t*sq + h*hd + d (likewise k, v, out, dout, dq, dk, dv with their strides);

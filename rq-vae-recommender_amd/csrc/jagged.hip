@@ -98,6 +98,142 @@ __global__ void __launch_bounds__(256) jagged_gather_kernel(const T* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ decoder prologue (forward)
+// The generative-retrieval decoder's input embeddings straight into its two jagged batches
+// (reference modules/model.py:101-129 _predict with modules/embedding/id_embedder.py:28-53):
+//   context row 0      user_w[uid mod nb]
+//   context row 1 + j  sem_w[mask ? type * K + sem : pad] + wpe_w[j]            (j < sum(mask[b]))
+//   future  row 0      bos
+//   future  row 1 + t  sem_w[type_fut * K + sem_fut] + tte_w[type_fut]
+// every value through padded_to_jagged's (v + 1) - 1 (ops/triton/jagged.py:65), the context at
+// offsets [0, cumsum(sum(mask[b]) + 1)] with the allocation's tail rows zero, the future at b * nf:
+// bitwise the composition (gathers, one fp32 add, the +1-1), in two launches instead of ~24.
+// Also writes the table rows the backward's segmented sums key on: keys (B, N + L) = the context's
+// sem-table rows (pad where masked) then the future's, and uid mod nb (B).
+constexpr int kDecLensLds = 4096;   // sequences whose lengths the offsets kernel keeps in LDS
+__global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* __restrict__ mask, int64_t B, int64_t N,
+                                                                    int64_t nf, int64_t* __restrict__ off_ctx,
+                                                                    int64_t* __restrict__ off_fut) {
+  __shared__ int64_t part[1024];
+  __shared__ int64_t lens[kDecLensLds];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // lengths sum(mask[b]) + 1: one wave per sequence, coalesced byte loads, a wave reduction
+  const bool in_lds = B <= kDecLensLds;
+  if (in_lds) {
+    for (int64_t b = wave; b < B; b += 16) {
+      int c = 0;
+      for (int64_t j = lane; j < N; j += 64) c += mask[b * N + j] ? 1 : 0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (lane == 0) lens[b] = c + 1;
+    }
+    __syncthreads();
+  }
+  auto len_of = [&](int64_t i) -> int64_t {
+    if (in_lds) return lens[i];
+    int64_t c = 1;   // the user token
+    for (int64_t j = 0; j < N; ++j) c += mask[i * N + j] ? 1 : 0;
+    return c;
+  };
+  const int64_t per = (B + 1023) / 1024;
+  const int64_t a = t * per, e = a + per < B ? a + per : B;
+  int64_t s = 0;
+  for (int64_t i = a; i < e; ++i) s += len_of(i);
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int64_t v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;
+  if (t == 0) off_ctx[0] = 0;
+  for (int64_t i = a; i < e; ++i) {
+    run += len_of(i);
+    off_ctx[i + 1] = run;
+  }
+  for (int64_t i = t; i <= B; i += 1024) off_fut[i] = i * nf;
+}
+
+struct DecPrologueArgs {
+  const int64_t *uid, *sem, *typ, *sem_fut, *typ_fut;
+  const bool* mask;
+  const float *w_user, *w_sem, *w_wpe, *w_tte, *bos;
+  int64_t n_buckets, K, pad, n_sem_rows, n_wpe_rows, n_tte_rows;
+  int64_t B, N, L, E;
+  const int64_t* off_ctx;
+  float *ctx, *fut;
+  int64_t alloc_rows;
+  int64_t *keys, *uid_mod;
+};
+
+__device__ __forceinline__ int64_t clamp_row(int64_t r, int64_t n) { return r < 0 ? 0 : (r >= n ? n - 1 : r); }
+
+// Grid (ceil((1 + max(N, L)) * E / 4 / 256), 2 B + 1): y < B the context rows of sequence y, y == B the
+// context allocation's tail, y > B the future rows of sequence y - B - 1. Block x == 0 also writes the keys.
+__global__ void __launch_bounds__(256) dec_prologue_fwd_kernel(DecPrologueArgs a) {
+  const int64_t y = blockIdx.y, E = a.E;
+  if (y == a.B) {   // zero the context tail rows [off_ctx[B], alloc_rows)
+    const int64_t e0 = a.off_ctx[a.B] * E, e1 = a.alloc_rows * E;
+    for (int64_t e = e0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; e < e1; e += (int64_t)gridDim.x * 256 * 4)
+      *reinterpret_cast<float4*>(a.ctx + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const bool ctx = y < a.B;
+  const int64_t b = ctx ? y : y - a.B - 1;
+  if (blockIdx.x == 0) {   // keys of the backward's segmented sums (context then future), uid mod nb
+    if (ctx) {
+      for (int64_t j = threadIdx.x; j < a.N; j += 256) {
+        const int64_t o = b * a.N + j;
+        a.keys[b * (a.N + a.L) + j] = a.mask[o] ? a.typ[o] * a.K + a.sem[o] : a.pad;
+      }
+      if (threadIdx.x == 0) {
+        const int64_t u = a.uid[b] % a.n_buckets;
+        a.uid_mod[b] = u < 0 ? u + a.n_buckets : u;   // torch's remainder: the divisor's sign
+      }
+    } else {
+      for (int64_t t = threadIdx.x; t < a.L; t += 256) {
+        const int64_t o = b * a.L + t;
+        a.keys[b * (a.N + a.L) + a.N + t] = a.typ_fut[o] * a.K + a.sem_fut[o];
+      }
+    }
+  }
+  const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t r = idx / E, d = idx - r * E;   // E % 4 == 0: a float4 never crosses a row
+  float4 v;
+  float* dst;
+  if (ctx) {
+    const int64_t o0 = a.off_ctx[b], len = a.off_ctx[b + 1] - o0;
+    if (r >= len || o0 + r >= a.alloc_rows) return;   // (an allocation below the valid total drops rows, never faults)
+    if (r == 0) {
+      int64_t u = a.uid[b] % a.n_buckets;
+      u = u < 0 ? u + a.n_buckets : u;
+      v = *reinterpret_cast<const float4*>(a.w_user + u * E + d);
+    } else {
+      const int64_t j = r - 1, o = b * a.N + j;
+      const int64_t row = clamp_row(a.mask[o] ? a.typ[o] * a.K + a.sem[o] : a.pad, a.n_sem_rows);
+      const float4 se = *reinterpret_cast<const float4*>(a.w_sem + row * E + d);
+      const float4 pe = *reinterpret_cast<const float4*>(a.w_wpe + clamp_row(j, a.n_wpe_rows) * E + d);
+      v = make_float4(pe.x + se.x, pe.y + se.y, pe.z + se.z, pe.w + se.w);
+    }
+    dst = a.ctx + (o0 + r) * E + d;
+  } else {
+    if (r > a.L) return;
+    if (r == 0) {
+      v = *reinterpret_cast<const float4*>(a.bos + d);
+    } else {
+      const int64_t o = b * a.L + r - 1;
+      const int64_t row = clamp_row(a.typ_fut[o] * a.K + a.sem_fut[o], a.n_sem_rows);
+      const float4 se = *reinterpret_cast<const float4*>(a.w_sem + row * E + d);
+      const float4 te = *reinterpret_cast<const float4*>(a.w_tte + clamp_row(a.typ_fut[o], a.n_tte_rows) * E + d);
+      v = make_float4(se.x + te.x, se.y + te.y, se.z + te.z, se.w + te.w);
+    }
+    dst = a.fut + (b * (a.L + 1) + r) * E + d;
+  }
+  *reinterpret_cast<float4*>(dst) = make_float4(p1m1(v.x), p1m1(v.y), p1m1(v.z), p1m1(v.w));
+}
+
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) jagged_scatter_kernel(const T* __restrict__ values, const int64_t* __restrict__ off,
                                                               int64_t N, int64_t D, T* __restrict__ x) {
@@ -179,6 +315,33 @@ int jagged_from_padded(const void* x, int64_t B, int64_t N, int64_t D, const int
                        int add_one_sub_one, void* stream) {
   if (N == 0) return (x && offsets && values) ? 0 : jagged_from_padded_rows(x, B, N, D, offsets, values, -1, dtype, 0, stream);
   return jagged_from_padded_rows(x, B, N, D, offsets, values, -1, dtype, add_one_sub_one, stream);
+}
+
+int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const int64_t* type_ids, const bool* seq_mask,
+                        const int64_t* sem_ids_fut, const int64_t* type_ids_fut, int64_t B, int64_t N, int64_t L,
+                        int64_t E, const float* user_w, int64_t n_buckets, const float* sem_w, int64_t n_sem_rows,
+                        int64_t K, int64_t pad, const float* wpe_w, int64_t n_wpe_rows, const float* tte_w,
+                        int64_t n_tte_rows, const float* bos, float* ctx_values, int64_t ctx_alloc_rows,
+                        int64_t* ctx_offsets, float* fut_values, int64_t* fut_offsets, int64_t* keys, int64_t* uid_mod,
+                        void* stream) {
+  RQ_CHECK_ARG(user_ids && sem_ids && type_ids && seq_mask && sem_ids_fut && type_ids_fut && user_w && sem_w && wpe_w &&
+                   tte_w && bos && ctx_values && ctx_offsets && fut_values && fut_offsets && keys && uid_mod,
+               "rq_dec_prologue_fwd: null pointer");
+  RQ_CHECK_ARG(B >= 0 && 2 * B + 1 < 65535 && N >= 0 && L >= 0 && E > 0 && E % 4 == 0 && n_buckets > 0 && K > 0 &&
+                   n_sem_rows > 0 && n_wpe_rows >= N && n_tte_rows > 0 && ctx_alloc_rows >= B,
+               "rq_dec_prologue_fwd: bad shape (E %% 4 == 0, wpe rows >= N, 2 B + 1 < 65535)");
+  if (B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(dec_prologue_offsets_kernel, dim3(1), dim3(1024), 0, s, seq_mask, B, N, L + 1, ctx_offsets,
+                     fut_offsets);
+  DecPrologueArgs a{user_ids, sem_ids, type_ids, sem_ids_fut, type_ids_fut, seq_mask, user_w, sem_w, wpe_w, tte_w, bos,
+                    n_buckets, K, pad, n_sem_rows, n_wpe_rows, n_tte_rows, B, N, L, E, ctx_offsets, ctx_values,
+                    fut_values, ctx_alloc_rows, keys, uid_mod};
+  const int64_t rows = 1 + (N > L ? N : L);
+  const dim3 g((unsigned)((rows * E / 4 + 255) / 256), (unsigned)(2 * B + 1));
+  hipLaunchKernelGGL(dec_prologue_fwd_kernel, g, dim3(256), 0, s, a);
+  RQ_LAUNCH_CHECK("rq_dec_prologue_fwd");
+  return 0;
 }
 
 int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int64_t N, int64_t D, void* x, int dtype,

@@ -23,7 +23,7 @@ from modules.embedding.id_embedder import Embedding, SemIdEmbedder, UserIdEmbedd
 from modules.normalize import RMSNorm
 from modules.transformer.model import TransformerEncoderDecoder
 from modules.utils import eval_mode, maybe_repeat_interleave, reset_encoder_cache
-from ops.jagged import jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged, row_counts
+from ops.jagged import Jagged, jagged_to_flattened_tensor, jagged_to_padded_tensor, padded_to_jagged, row_counts
 from rqvae_hip import gemm_tuning
 from rqvae_hip import ops as hip_ops
 
@@ -31,6 +31,7 @@ from rqvae_hip import ops as hip_ops
 # op (tests / A-B probes set these module attributes; nothing reads the environment):
 _BATCH_SUM = True   # False: torch's broadcast add / repeat (and their reduction backward) in the prologue
 _FUSED_CE = True    # False: the loss head as torch's slice + cross_entropy + means
+_FUSED_PROLOGUE = True   # False: the input embeddings as gathers / adds / cats + padded -> jagged (the composition)
 
 # As the reference (modules/model.py:27): fp32 matmuls at 'high' precision (split-bf16 GEMM on
 # gfx950, rqvae_hip.ops.gemm_bf16x3); 'highest' restores the exact-fp32 library path.
@@ -88,7 +89,32 @@ class EncoderDecoderRetrievalModel(nn.Module):
         total = host[0] + B if host is not None and host[3] == B else int(batch.seq_mask.sum()) + B
         return total if not bucket else (total + bucket - 1) // bucket * bucket
 
+    def _prologue_fused(self, batch: TokenizedSeqBatch, alloc: int):
+        """Context / future jagged inputs in one HIP op (hip_ops.decoder_prologue), or None where it does not
+        apply (generation: no future tokens)."""
+        se, ue = self.sem_id_embedder, self.user_id_embedder
+        args = (ue.emb.weight, se.emb.weight, self.wpe.weight, self.tte.weight, self.bos_emb, batch.user_ids,
+                batch.sem_ids, batch.token_type_ids, batch.seq_mask, batch.sem_ids_fut, batch.token_type_ids_fut)
+        if not (_FUSED_PROLOGUE and hip_ops.decoder_prologue_supported(*args) and
+                all(e.max_norm is None for e in (se.emb, ue.emb, self.wpe, self.tte)) and
+                all(e.padding_idx is None for e in (ue.emb, self.wpe, self.tte))):
+            return None
+        B, N = batch.sem_ids.shape
+        nf = batch.sem_ids_fut.shape[1] + 1
+        ctx_v, ctx_off, fut_v, fut_off = hip_ops.decoder_prologue(*args, ue.num_buckets, se.num_embeddings,
+                                                                   se.padding_idx, alloc)
+        return Jagged(ctx_v, ctx_off, N + 1, 0, None), Jagged(fut_v, fut_off, nf, nf, B * nf)
+
     def _predict(self, batch: TokenizedSeqBatch):
+        bucket = gemm_tuning.ROW_BUCKET if gemm_tuning.is_enabled() else None
+        fused = self._prologue_fused(batch, self.context_rows(batch, bucket))
+        if fused is not None:
+            ctx_j, fut_j = fused
+            transformer_context = ctx_j.with_values(self.in_proj_context(self.norm.forward_dropout(ctx_j.values(),
+                                                                                                   self.do)))
+            transformer_input = fut_j.with_values(self.in_proj(self.norm_cxt.forward_dropout(fut_j.values(), self.do)))
+            return self.transformer(x=transformer_input, context=transformer_context, padding_mask=batch.seq_mask,
+                                    jagged=True)
         user_emb = self.user_id_embedder(batch.user_ids)                  # (B, 1, E)
         sem = self.sem_id_embedder(batch)
         seq_emb, fut_emb = sem.seq, sem.fut                               # (B, N, E), (B, L+1, E)

@@ -1308,6 +1308,101 @@ def batch_repeat(p: torch.Tensor, B: int) -> torch.Tensor:
     return p.unsqueeze(0).repeat((B,) + (1,) * p.dim())
 
 
+class DecoderPrologueFunction(torch.autograd.Function):
+    """The decoder's input embeddings (user / sem-ID / position / token-type tables, bos) written straight
+    into the context and future jagged batches (rq_dec_prologue_fwd: reference modules/model.py:101-129,
+    modules/embedding/id_embedder.py:28-53): two launches instead of the ~24 of the composition (gathers,
+    masks, adds, cats, offsets, padded -> jagged), bitwise the same values. The backward is the
+    composition's: the context's padded gradient by the jagged scatter, the position table's batch sum
+    (rq_col_sum) and the four tables' deterministic segmented sums (deferred into their flat buckets when
+    GradBuckets batches them), bos's batch sum — the same reductions in the same order, so the same bits."""
+
+    @staticmethod
+    def forward(ctx, user_w, sem_w, wpe_w, tte_w, bos, user_ids, sem_ids, type_ids, seq_mask, sem_fut, type_fut,
+                n_buckets: int, K: int, pad: int, alloc: int):
+        require_gpu(user_w, sem_w, wpe_w, tte_w, bos, user_ids, sem_ids, type_ids, seq_mask, sem_fut, type_fut,
+                    what="decoder_prologue")
+        B, N = sem_ids.shape
+        L = sem_fut.shape[1]
+        E = sem_w.shape[1]
+        dev = sem_w.device
+        i64 = torch.int64
+        ctx_vals = torch.empty((int(alloc), E), device=dev, dtype=torch.float32)
+        fut_vals = torch.empty((B * (L + 1), E), device=dev, dtype=torch.float32)
+        ctx_off = torch.empty((B + 1,), device=dev, dtype=i64)
+        fut_off = torch.empty((B + 1,), device=dev, dtype=i64)
+        keys = torch.empty((B, N + L), device=dev, dtype=i64)
+        uid_mod = torch.empty((B,), device=dev, dtype=i64)
+        c = [t.contiguous() for t in (user_ids, sem_ids, type_ids, seq_mask, sem_fut, type_fut)]
+        TIMER.around("dec_prologue", call, "rq_dec_prologue_fwd", *[ptr(t) for t in c], B, N, L, E, ptr(user_w),
+                     int(n_buckets), ptr(sem_w), sem_w.shape[0], int(K), int(pad), ptr(wpe_w), wpe_w.shape[0],
+                     ptr(tte_w), tte_w.shape[0], ptr(bos), ptr(ctx_vals), int(alloc), ptr(ctx_off), ptr(fut_vals),
+                     ptr(fut_off), ptr(keys), ptr(uid_mod), stream_handle(dev))
+        ctx.save_for_backward(ctx_off, keys, uid_mod, c[5])
+        ctx.meta = (B, N, L, E, int(pad))
+        ctx.tables = tuple(w if isinstance(w, torch.nn.Parameter) else None for w in (user_w, sem_w, wpe_w, tte_w))
+        ctx.rows = (user_w.shape[0], sem_w.shape[0], wpe_w.shape[0], tte_w.shape[0])
+        ctx.mark_non_differentiable(ctx_off, fut_off)
+        return ctx_vals, ctx_off, fut_vals, fut_off
+
+    @staticmethod
+    def backward(ctx, g_ctx, _g_off, g_fut, _g_foff):
+        ctx_off, keys, uid_mod, type_fut = ctx.saved_tensors
+        B, N, L, E, pad = ctx.meta
+        w_user, w_sem, w_wpe, w_tte = ctx.tables
+        k_user, k_sem, k_wpe, k_tte = ctx.rows
+        dev = ctx_off.device
+        need = ctx.needs_input_grad
+        if g_ctx is None:
+            g_ctx = torch.zeros((1, E), device=dev)   # rows past the offsets are never read
+        g_ctx = g_ctx.contiguous()
+        g_pad = torch.empty((B, N + 1, E), device=dev, dtype=torch.float32)
+        call("jagged_to_padded", ptr(g_ctx), ptr(ctx_off), B, N + 1, E, ptr(g_pad), _DTYPES[torch.float32],
+             stream_handle(dev))
+        g_futp = (torch.zeros((B, L + 1, E), device=dev) if g_fut is None else g_fut.contiguous().view(B, L + 1, E))
+        g_seq = g_pad[:, 1:]
+        gu = _emb_grad(w_user, g_pad[:, :1].reshape(-1, E), uid_mod, k_user, None) if need[0] else None
+        gw = None
+        if need[2]:   # the position table: batch sum, then its gather's backward over rows 0..N-1
+            gp = col_sum(g_seq).unsqueeze(0)
+            gw = _emb_grad(w_wpe, gp.reshape(-1, E), torch.arange(N, device=dev), k_wpe, None)
+        gs = None
+        if need[1]:   # one segmented sum over the context and future rows (EmbeddingPairFunction's order)
+            g = torch.cat([g_seq, g_futp[:, 1:]], dim=1).reshape(-1, E)
+            gs = _emb_grad(w_sem, g, keys.reshape(-1), k_sem, pad)
+        gt = _emb_grad(w_tte, g_futp[:, 1:].reshape(-1, E), type_fut.reshape(-1), k_tte, None) if need[3] else None
+        gb = col_sum(g_futp[:, :1]).view(E) if need[4] else None
+        return (gu, gs, gw, gt, gb) + (None,) * 10
+
+
+def decoder_prologue_supported(user_w, sem_w, wpe_w, tte_w, bos, user_ids, sem_ids, type_ids, seq_mask, sem_fut,
+                               type_fut) -> bool:
+    """Shapes / dtypes rq_dec_prologue_fwd serves (the training batch, future tokens present); the model keeps
+    its composition otherwise."""
+    if sem_fut is None or type_fut is None:
+        return False
+    ts = (user_w, sem_w, wpe_w, tte_w, bos)
+    if not all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in ts):
+        return False
+    E = sem_w.shape[1]
+    if not (E % 4 == 0 and all(embedding_supported(w) for w in ts[:4]) and all(w.shape[1] == E for w in ts[:4]) and
+            bos.shape == (E,)):
+        return False
+    ids = (user_ids, sem_ids, type_ids, sem_fut, type_fut)
+    if not all(t.is_cuda and t.dtype == torch.int64 for t in ids) or not (seq_mask.is_cuda and seq_mask.dtype == torch.bool):
+        return False
+    B, N = sem_ids.shape
+    return (user_ids.numel() == B and type_ids.shape == (B, N) and seq_mask.shape == (B, N) and sem_fut.dim() == 2 and
+            sem_fut.shape[0] == B and type_fut.shape == sem_fut.shape and wpe_w.shape[0] >= N and 2 * B + 1 < 65535)
+
+
+def decoder_prologue(user_w, sem_w, wpe_w, tte_w, bos, user_ids, sem_ids, type_ids, seq_mask, sem_fut, type_fut,
+                     n_buckets: int, K: int, pad: int, alloc: int):
+    """(ctx values (alloc, E), ctx offsets (B+1), fut values (B (L+1), E), fut offsets) — DecoderPrologueFunction."""
+    return DecoderPrologueFunction.apply(user_w, sem_w, wpe_w, tte_w, bos, user_ids, sem_ids, type_ids, seq_mask,
+                                         sem_fut, type_fut, n_buckets, K, pad, alloc)
+
+
 def embedding_supported(weight: torch.Tensor) -> bool:
     """Shapes the HIP gather + segmented-sum backward (rq_segment_sum: float4 rows) serve; other tables
     take torch's embedding op."""

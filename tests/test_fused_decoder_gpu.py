@@ -262,3 +262,57 @@ def test_mlp_residual_dropout_equals_composition(device, rows):
         res.append((out.detach(), x.grad, h.grad, *[w.grad for w in ws]))
     for a, b, what in zip(res[0], res[1], ("out", "dx", "dh", "dw0", "dw1")):
         assert torch.equal(a, b), f"{what}: max abs diff {(a - b).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("buckets", [False, True])
+@pytest.mark.parametrize("B,max_items,sem_id_dim", [(16, 20, 4), (3, 7, 3), (40, 200, 4)])
+def test_decoder_prologue_equals_composition(device, monkeypatch, buckets, B, max_items, sem_id_dim):
+    """The fused input embeddings (rq_dec_prologue_fwd: user / sem-ID / position / token-type gathers, the
+    adds, bos, the +1-1 jagged gather, both offsets) vs the model's composition of the same ops: loss and
+    every parameter gradient bitwise equal, with plain .grad accumulation and with the flat-bucket
+    (deferred segmented sum) path; the context's allocation tail zero."""
+    from data.processed import synthetic_tokenized_batch
+    from modules import model as model_mod
+    from ops.jagged import row_counts
+    from rqvae_hip import dp, ops
+    torch.manual_seed(0)
+    m = model_mod.EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.0, num_heads=4, n_layers=2,
+                                               num_embeddings=64, sem_id_dim=sem_id_dim, inference_verifier_fn=None,
+                                               max_pos=max_items * sem_id_dim).to(device)
+    m.do.p = 0.0
+    batch = synthetic_tokenized_batch(B, max_items, sem_id_dim, 64, 7, device)
+    batch = batch._replace(user_ids=batch.user_ids - 500_000)   # negative ids: remainder's sign convention
+    from ops.jagged import register_row_counts
+    register_row_counts(batch.seq_mask, batch.seq_mask.sum(1).tolist())
+    gb = dp.GradBuckets(m.parameters(), flat_views=True) if buckets else None
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(model_mod, "_FUSED_PROLOGUE", fused)
+        if gb is not None:
+            gb.zero_grad()
+        else:
+            m.zero_grad(set_to_none=True)
+        loss = m(batch).loss
+        loss.backward()
+        if gb is not None:
+            ops.flush_reductions()
+        res[fused] = (loss.detach().clone(), {n: (None if p.grad is None else p.grad.detach().clone())
+                                              for n, p in m.named_parameters()})
+    assert torch.equal(res[True][0], res[False][0])
+    for n in res[False][1]:
+        a, b = res[True][1][n], res[False][1][n]
+        assert (a is None) == (b is None), n
+        if a is not None:
+            assert torch.equal(a, b), (n, float((a - b).abs().max()))
+    # the op alone: values of the allocation tail are zero, offsets as the composition's
+    se, ue = m.sem_id_embedder, m.user_id_embedder
+    alloc = m.context_rows(batch, 64)
+    cv, co, fv, fo = ops.decoder_prologue(ue.emb.weight, se.emb.weight, m.wpe.weight, m.tte.weight, m.bos_emb,
+                                          batch.user_ids, batch.sem_ids, batch.token_type_ids, batch.seq_mask,
+                                          batch.sem_ids_fut, batch.token_type_ids_fut, ue.num_buckets,
+                                          se.num_embeddings, se.padding_idx, alloc)
+    lens = batch.seq_mask.sum(1) + 1
+    assert torch.equal(co, torch.cat([lens.new_zeros(1), lens.cumsum(0)]))
+    assert torch.equal(fo, torch.arange(B + 1, device=device) * (batch.sem_ids_fut.shape[1] + 1))
+    assert torch.count_nonzero(cv[int(co[-1]):]) == 0
+    assert row_counts(batch.seq_mask)[0] + B == int(co[-1])
