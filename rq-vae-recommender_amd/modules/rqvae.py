@@ -120,7 +120,10 @@ class RqVae(nn.Module):
         [, |emb| (L,B) without grad when with_norms])."""
         mode = self._fused_kernel_mode()
         if mode is not None:
-            codebooks = torch.stack([layer.codebook() for layer in self.layers])
+            if all(isinstance(m, nn.Identity) for layer in self.layers for m in layer.out_proj):   # codebook() == weight
+                codebooks = hip_ops.stack_params([layer.embedding.weight for layer in self.layers])
+            else:
+                codebooks = torch.stack([layer.codebook() for layer in self.layers])
             return hip_ops.rq_quantize(res0, codebooks, mode, self.commitment_weight, with_norms)
         # generic per-level path (k-means init pending, gumbel / cosine layers)
         res, qloss = res0, 0

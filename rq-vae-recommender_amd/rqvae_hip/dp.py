@@ -324,8 +324,13 @@ class GradBuckets:
             from . import ops
             ops.flush_reductions()
         unused = self._unused or ()
+        flats = [b["flat"] for b in self.buckets]
+        if len(flats) > 1 and all(f.is_cuda for f in flats):
+            torch._foreach_zero_(flats)   # every bucket in one multi-tensor launch
+        else:
+            for f in flats:
+                f.zero_()
         for b in self.buckets:
-            b["flat"].zero_()
             b["used"].clear()
             b["fired"].clear()
             b["ready"] = False

@@ -126,6 +126,43 @@ def rq_quantize(x, codebooks, mode=MODE_ROTATION, beta=0.25, with_norms=False):
     return RqQuantizeFunction.apply(x, codebooks, mode, beta, with_norms)
 
 
+class StackParamsFunction(torch.autograd.Function):
+    """torch.stack(params) whose backward adds each slice of the gradient straight into the parameter's
+    flat-bucket view through the step's batched reduction (rq_reduce_partials, like the split-K weight
+    gradients) when its GradBuckets defers reductions — instead of autograd's stack backward plus one
+    AccumulateGrad add kernel per parameter (the RQ-VAE's per-level codebooks: 3 launches a step). Same
+    values: the view receives view + g[i] either way."""
+
+    @staticmethod
+    def forward(ctx, *ps):
+        ctx.ps = ps
+        return torch.stack(ps)
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import dp
+        ps, ctx.ps = ctx.ps, None
+        out = []
+        for i, p in enumerate(ps):
+            gi = g[i]
+            sink = dp.direct_grad(p) if isinstance(p, torch.nn.Parameter) and dp.defer_ok(p) else None
+            if (sink is not None and sink.is_contiguous() and gi.is_contiguous() and gi.numel() % 4 == 0 and
+                    (sink.data_ptr() | gi.data_ptr()) % 16 == 0 and sink.data_ptr() not in _DEFER["outs"]):
+                _defer_push(gi, sink, gi.numel(), 1, 0)
+                dp.direct_grad_done(p)
+                out.append(None)
+            else:
+                out.append(gi)
+        return tuple(out)
+
+
+def stack_params(ps) -> torch.Tensor:
+    """torch.stack of parameters with the deferred-gradient backward (StackParamsFunction) on the device."""
+    if all(p.is_cuda and p.dtype == torch.float32 for p in ps):
+        return StackParamsFunction.apply(*ps)
+    return torch.stack(list(ps))
+
+
 def segment_sum(rows: torch.Tensor, keys: torch.Tensor, K: int, with_counts: bool = True, out: torch.Tensor = None):
     """(sums (K, D), counts (K,) or None) of `rows` grouped by `keys` — deterministic (no float
     atomics). Rows whose key is outside [0, K) are skipped. `out`: a contiguous fp32 (K, D) destination."""
@@ -1911,7 +1948,12 @@ def _wgrad_multi_into(weights, g, x, O_all: int, I: int, rows: int, dw=None):
     dw = dw_in if dw_in is not None else gemm_x3(g, False, x, False, O_all, I, rows)
     for i, sk in enumerate(sinks):
         if sk is not None:
-            sk.add_(dw[i * O:(i + 1) * O])
+            blk = dw[i * O:(i + 1) * O]
+            if (dp.defer_ok(weights[i]) and sk.is_contiguous() and (sk.data_ptr() | blk.data_ptr()) % 16 == 0 and blk.numel() % 4 == 0
+                    and sk.data_ptr() not in _DEFER["outs"]):
+                _defer_push(blk, sk, blk.numel(), 1, 0)   # into the step's one batched reduction (sk + blk)
+            else:
+                sk.add_(blk)
             dp.direct_grad_done(weights[i])
     return [None if sk is not None else dw[i * O:(i + 1) * O] for i, sk in enumerate(sinks)]
 
