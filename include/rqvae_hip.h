@@ -339,14 +339,16 @@ int jagged_to_padded(const void* values, const int64_t* offsets, int64_t B, int6
  *   ids (B, N) / (B, L) int64, seq_mask (B, N) bool, tables fp32 row-major with E columns (E % 4 == 0);
  *   ctx_values (ctx_alloc_rows, E): rows past ctx_offsets[B] zero; ctx_offsets (B+1) = [0, cumsum(sum(mask)+1)];
  *   fut_values (B * (L+1), E), fut_offsets (B+1) = b (L+1); keys (B, N+L) int64 = the context's sem-table rows
- *   then the future's (the backward's segmented-sum keys), uid_mod (B) int64. Two launches; graph-capturable. */
+ *   then the future's (the backward's segmented-sum keys), uid_mod (B) int64; lpt_order (NULL or B int32, B <= 4096):
+ *   the contexts longest-first (the ranking of the attention LPT order, for RQ_ATTN_ORDER_GIVEN). Two launches;
+ *   graph-capturable. */
 int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const int64_t* type_ids, const bool* seq_mask,
                         const int64_t* sem_ids_fut, const int64_t* type_ids_fut, int64_t B, int64_t N, int64_t L,
                         int64_t E, const float* user_w, int64_t n_buckets, const float* sem_w, int64_t n_sem_rows,
                         int64_t K, int64_t pad, const float* wpe_w, int64_t n_wpe_rows, const float* tte_w,
                         int64_t n_tte_rows, const float* bos, float* ctx_values, int64_t ctx_alloc_rows,
                         int64_t* ctx_offsets, float* fut_values, int64_t* fut_offsets, int64_t* keys, int64_t* uid_mod,
-                        void* stream);
+                        int* lpt_order, void* stream);
 
 /* Varlen multi-head attention on packed rows = F.scaled_dot_product_attention on NJT q/k/v
  * (modules/transformer/attention.py:113-124), dropout 0, is_causal top-left.
@@ -379,6 +381,11 @@ int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const i
                                      Q K^T and P V in split-bf16 (3 bf16 MFMA products, fp32 accumulate and
                                      softmax) instead of exact fp32; so does the fused long-range backward (S, dP,
                                      dV, dK and dQ products; P, dS fp32) */
+#define RQ_ATTN_LPT_SHORT 32      /* the short / few-query forms (<= 128 keys) also dispatch their sequences longest-first
+                                     (an order launch; the backward's scratch then holds B ints) */
+#define RQ_ATTN_ORDER_GIVEN 64    /* ws[0, B) (as int32) already holds the longest-first order of cu_k's segments (e.g. from
+                                     rq_dec_prologue_fwd): the forwards and the short backwards use it without an order
+                                     launch (the fused long-range backward keeps its own) */
 #define RQ_ATTN_QSPLIT_SHIFT 8
 #define RQ_ATTN_QSPLIT(n) ((n) << RQ_ATTN_QSPLIT_SHIFT)   /* fused backward query splits forced to n (1..8; 1 = off) */
 int varlen_attn_fwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, int64_t max_k, int64_t Tq, int causal,

@@ -1762,7 +1762,7 @@ template <int R>
 __global__ void __launch_bounds__(256) attn_fwd_short_x3_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
-    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq, const int* __restrict__ order) {
   constexpr int HD = 64, NW = 4, NKT = R / 16;
   static_assert(R % 32 == 0 && R <= 128, "staged rows");
   __shared__ __attribute__((aligned(16))) uint16_t planes[4 * R * kX3Ld];
@@ -1770,13 +1770,14 @@ __global__ void __launch_bounds__(256) attn_fwd_short_x3_kernel(
   uint16_t* const Kl = Kh + R * kX3Ld;
   uint16_t* const Vh = Kl + R * kX3Ld;
   uint16_t* const Vl = Vh + R * kX3Ld;
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  if (b == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
-    zero_rows<HD, 256>(out, so, cu_q[b], Tq, hh, tid);
+  if (z == (int)gridDim.z - 1) {              // tail slice: output rows past the last sequence
+    zero_rows<HD, 256>(out, so, cu_q[z], Tq, hh, tid);
     return;
   }
+  const int b = seq_of(order, z);   // longest-first when an LPT order is given
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   if (lq <= 0) return;
@@ -2101,17 +2102,18 @@ template <int NW>
 __global__ void __launch_bounds__(64 * NW) attn_fwd_fewq_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
-    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq) {
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq, const int* __restrict__ order) {
   constexpr int HD = 64, TPW = 2;   // key tiles per wave (<= 128 keys over 4 waves)
   __shared__ __attribute__((aligned(16))) float part_o[NW][16][HD + kPartPad];
   __shared__ float part_m[NW][16], part_l[NW][16];
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  if (b == (int)gridDim.z - 1) {
-    zero_rows<HD, 64 * NW>(out, so, cu_q[b], Tq, hh, tid);
+  if (z == (int)gridDim.z - 1) {
+    zero_rows<HD, 64 * NW>(out, so, cu_q[z], Tq, hh, tid);
     return;
   }
+  const int b = seq_of(order, z);   // longest-first when an LPT order is given
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   if (lq <= 0) return;
@@ -2337,18 +2339,20 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_fewq_fused_kernel(
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
-    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out) {
+    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out,
+    const int* __restrict__ order) {
   constexpr int HD = 64, TPW = 2;   // key tiles per wave (<= 128 keys over 4 waves)
   __shared__ __attribute__((aligned(16))) float part[NW][16][HD + kPartPad];
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
-  if (b == (int)gridDim.z - 1) {   // tail slice: rows past the last sequence
-    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
-    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[b], Tk, hh, tid);
-    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[b], Tk, hh, tid);
+  if (z == (int)gridDim.z - 1) {   // tail slice: rows past the last sequence
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[z], Tq, hh, tid);
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[z], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[z], Tk, hh, tid);
     return;
   }
+  const int b = seq_of(order, z);   // longest-first when an LPT order is given
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   const int nkt = (lk + 15) >> 4;   // every key tile gets its dK / dV rows written (zeros past the queries)
@@ -2502,7 +2506,8 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_bwd_short_fused_kernel(
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
     int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
-    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out) {
+    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out,
+    const int* __restrict__ order) {
   constexpr int HD = 64, NT = R / 16, TPW = (NT + NW - 1) / NW;
   static_assert(R % 16 == 0 && R <= 128 && TPW <= 2, "staged rows");
   __shared__ __attribute__((aligned(16))) char lds[2 * R * 256];
@@ -2510,15 +2515,16 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_bwd_short_fused_kernel(
   __shared__ float lse_s[R], dl_s[R];
   char* Q_s = lds;
   char* O_s = lds + R * 256;
-  const int b = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int z = blockIdx.z, hh = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
-  if (b == (int)gridDim.z - 1) {   // tail slice: rows past the last sequence
-    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[b], Tq, hh, tid);
-    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[b], Tk, hh, tid);
-    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[b], Tk, hh, tid);
+  if (z == (int)gridDim.z - 1) {   // tail slice: rows past the last sequence
+    zero_rows<HD, 64 * NW>(dq, sdq, cu_q[z], Tq, hh, tid);
+    zero_rows<HD, 64 * NW>(dk, sdk, cu_k[z], Tk, hh, tid);
+    zero_rows<HD, 64 * NW>(dv, sdv, cu_k[z], Tk, hh, tid);
     return;
   }
+  const int b = seq_of(order, z);   // longest-first when an LPT order is given
   const int64_t q0 = cu_q[b], k0 = cu_k[b];
   const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
   const int nqt = min((lq + 15) >> 4, NT), nkt = min((lk + 15) >> 4, NT);
@@ -2732,11 +2738,16 @@ struct AttnPolicy {
   bool dma, fused, split;
   int qsplit;
   bool x3;   // RQ_ATTN_SPLIT_BF16: the long-range forwards multiply in split-bf16 (matmul precision 'high')
+  bool lpt_short;   // RQ_ATTN_LPT_SHORT: longest-first sequence order for the short / few-query forms too
+  bool order_given;   // RQ_ATTN_ORDER_GIVEN: ws[0, B) already holds the LPT order of cu_k (no order launch)
 };
 static AttnPolicy attn_policy(int flags) {
   return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
-                    (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15, (flags & RQ_ATTN_SPLIT_BF16) != 0};
+                    (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15, (flags & RQ_ATTN_SPLIT_BF16) != 0,
+                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0};
 }
+// LPT order of the short / few-query forms (by key length: their work per workgroup grows with it)
+static bool short_lpt_plan(int64_t B, const AttnPolicy& pol) { return RQ_ATTN_LPT && pol.lpt_short && B >= 2 && B <= kOrderMax; }
 
 static bool split_plan(int64_t hd, int64_t max_q, int64_t max_k, int causal, const AttnPolicy& pol) {
   return RQ_ATTN_SPLIT && pol.split && hd == 64 && !causal && max_q <= 16 && max_k >= RQ_ATTN_SPLIT_MIN_K;
@@ -2841,12 +2852,17 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
 #undef RQ_SPL
       return;
     }
+    const int* sord = nullptr;   // LPT order of the short / few-query forms
+    if (order && short_lpt_plan(B, pol) && (fewq_plan(HD, max_q, max_k, pol) || dma_fwd_plan(HD, max_q, max_k, pol))) {
+      if (!pol.order_given) hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, ck, (int)B, order);
+      sord = order;
+    }
     if (fewq_plan(HD, max_q, max_k, pol)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
       switch (fewq_waves(max_k)) {
-        case 1: hipLaunchKernelGGL((attn_fwd_fewq_kernel<1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
-        case 2: hipLaunchKernelGGL((attn_fwd_fewq_kernel<2>), g, dim3(128), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
-        default: hipLaunchKernelGGL((attn_fwd_fewq_kernel<4>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq); break;
+        case 1: hipLaunchKernelGGL((attn_fwd_fewq_kernel<1>), g, dim3(64), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, sord); break;
+        case 2: hipLaunchKernelGGL((attn_fwd_fewq_kernel<2>), g, dim3(128), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, sord); break;
+        default: hipLaunchKernelGGL((attn_fwd_fewq_kernel<4>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, out, so, lse, Tq, sord); break;
       }
       return;
     }
@@ -2855,7 +2871,7 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
       if (pol.x3 && max_k > 32) {   // split-bf16 form at matmul 'high'
 #define RQ_FX(R_)                                                                                                \
   hipLaunchKernelGGL((attn_fwd_short_x3_kernel<R_>), g, dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck, causal, scale, \
-                     out, so, lse, Tq)
+                     out, so, lse, Tq, sord)
         switch (dma_rows_for(max_k)) {
           case 64: RQ_FX(64); break;
           case 96: RQ_FX(96); break;
@@ -2889,7 +2905,7 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
   }
   const int* ord = nullptr;
   if (order && lpt_plan(B, max_k)) {
-    hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, ck, (int)B, order);
+    if (!pol.order_given) hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, ck, (int)B, order);
     ord = order;
   }
   switch (waves_for(max_q)) {
@@ -2936,7 +2952,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
                        const float* k, int64_t sk, const float* v, int64_t sv, const float* out, int64_t so,
                        const float* dout, int64_t sdo, const float* lse, int64_t Tq, const int64_t* cq, const int64_t* ck,
                        int causal, float scale, float* dq, int64_t sdq, float* dk, int64_t sdk, float* dv, int64_t sdv,
-                       int64_t Tk, float* delta, const AttnPolicy& pol) {
+                       int64_t Tk, float* delta, const AttnPolicy& pol, const int* order = nullptr) {
   // dQ pass first: it also writes delta_q = dO.O, which the dK/dV pass reads per query chunk
   bool dq_done = false, kv_done = false;
   if constexpr (HD == 64) {
@@ -2945,7 +2961,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     if (short_fused_plan(HD, max_q, max_k, pol)) {
 #define RQ_SHF(NW_, R_)                                                                                              \
   hipLaunchKernelGGL((attn_bwd_short_fused_kernel<NW_, R_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, \
-                     dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
+                     dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, order)
       // 4 waves with up to two key tiles each (one key tile per wave, R / 16 waves, measured slower on the
       // Amazon step: 6.20-6.22 vs 6.10-6.15 ms, profiles/r03/short_tpw_ab.txt — more waves idle on short
       // sequences)
@@ -2961,7 +2977,7 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     if (fewq_plan(HD, max_q, max_k, pol) && pol.fused) {
 #define RQ_FQF(NW_)                                                                                                   \
   hipLaunchKernelGGL((attn_bwd_fewq_fused_kernel<NW_>), g, dim3(64 * NW_), 0, st, q, sq, k, sk, v, sv, out, so, dout, \
-                     sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta)
+                     sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, order)
       switch (fewq_waves(max_k)) {
         case 1: RQ_FQF(1); break;
         case 2: RQ_FQF(2); break;
@@ -3108,6 +3124,12 @@ static int64_t fused_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, i
   return base + (qs > 1 ? 2 * qs * Tk * H * hd : 0);
 }
 
+// the one-pass short / few-query backwards in LPT order (scratch: B ints)
+static bool short_lpt_bwd(int64_t B, int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {
+  return short_lpt_plan(B, pol) && !fused_plan(hd, max_q, max_k, pol) &&
+         (short_fused_plan(hd, max_q, max_k, pol) || (fewq_plan(hd, max_q, max_k, pol) && pol.fused));
+}
+
 template <int HD>
 static void launch_bwd_fused(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipStream_t st, const float* q,
                              int64_t sq, const float* k, int64_t sk, const float* v, int64_t sv, const float* out,
@@ -3206,7 +3228,9 @@ int varlen_attn_bwd_ws_elems(int64_t B, int64_t H, int64_t hd, int64_t max_q, in
                              int flags, int64_t* elems) {
   RQ_CHECK_ARG(elems, "varlen_attn_bwd_ws_elems: null pointer");
   RQ_CHECK_ARG(attn_args_ok(B, H, hd, max_q, max_k) && Tq >= 0, "varlen_attn_bwd_ws_elems: bad shape");
-  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq, attn_policy(flags), Tk);
+  const AttnPolicy pol = attn_policy(flags);
+  *elems = fused_ws_elems(B, H, hd, max_q, max_k, Tq, pol, Tk);
+  if (*elems == 0 && short_lpt_bwd(B, hd, max_q, max_k, pol)) *elems = (B + 3) & ~(int64_t)3;   // the LPT order
   return 0;
 }
 
@@ -3231,6 +3255,11 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   }
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  int* sord = nullptr;
+  if (!fused && ws != nullptr && ws_elems >= B && short_lpt_bwd(B, hd, max_q, max_k, pol)) {
+    sord = reinterpret_cast<int*>(ws);
+    if (!pol.order_given) hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, cu_k, (int)B, sord);
+  }
   if (fused) {
     launch_bwd_fused<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal,
                          scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, ws, ws_elems, pol);
@@ -3240,7 +3269,7 @@ int varlen_attn_bwd(const float* q, int64_t sq, const float* k, int64_t sk, cons
   switch (hd) {
     case 16: launch_bwd<16>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
     case 32: launch_bwd<32>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
-    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
+    case 64: launch_bwd<64>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol, sord); break;
     case 128: launch_bwd<128>(B, H, max_q, max_k, st, q, sq, k, sk, v, sv, out, so, dout, sdo, lse, Tq, cu_q, cu_k, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, pol); break;
   }
   RQ_LAUNCH_CHECK("varlen_attn_bwd");

@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(256) jagged_gather_kernel(const T* __restrict_
 constexpr int kDecLensLds = 4096;   // sequences whose lengths the offsets kernel keeps in LDS
 __global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* __restrict__ mask, int64_t B, int64_t N,
                                                                     int64_t nf, int64_t* __restrict__ off_ctx,
-                                                                    int64_t* __restrict__ off_fut) {
+                                                                    int64_t* __restrict__ off_fut, int* __restrict__ order) {
   __shared__ int64_t part[1024];
   __shared__ int64_t lens[kDecLensLds];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -154,6 +154,16 @@ __global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* 
     off_ctx[i + 1] = run;
   }
   for (int64_t i = t; i <= B; i += 1024) off_fut[i] = i * nf;
+  // longest-first order of the contexts (attention.hip attn_order_kernel's ranking: length descending,
+  // ties by index), for the attention launches over these offsets (RQ_ATTN_ORDER_GIVEN)
+  if (order != nullptr && in_lds) {
+    for (int64_t b = t; b < B; b += 1024) {
+      const int64_t lb = lens[b];
+      int64_t rank = 0;
+      for (int64_t j = 0; j < B; ++j) rank += (lens[j] > lb) || (lens[j] == lb && j < b);
+      order[rank] = (int)b;
+    }
+  }
 }
 
 struct DecPrologueArgs {
@@ -323,7 +333,8 @@ int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const i
                         int64_t K, int64_t pad, const float* wpe_w, int64_t n_wpe_rows, const float* tte_w,
                         int64_t n_tte_rows, const float* bos, float* ctx_values, int64_t ctx_alloc_rows,
                         int64_t* ctx_offsets, float* fut_values, int64_t* fut_offsets, int64_t* keys, int64_t* uid_mod,
-                        void* stream) {
+                        int* lpt_order, void* stream) {
+  RQ_CHECK_ARG(lpt_order == nullptr || B <= kDecLensLds, "rq_dec_prologue_fwd: lpt_order needs B <= %d", kDecLensLds);
   RQ_CHECK_ARG(user_ids && sem_ids && type_ids && seq_mask && sem_ids_fut && type_ids_fut && user_w && sem_w && wpe_w &&
                    tte_w && bos && ctx_values && ctx_offsets && fut_values && fut_offsets && keys && uid_mod,
                "rq_dec_prologue_fwd: null pointer");
@@ -333,7 +344,7 @@ int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const i
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(dec_prologue_offsets_kernel, dim3(1), dim3(1024), 0, s, seq_mask, B, N, L + 1, ctx_offsets,
-                     fut_offsets);
+                     fut_offsets, lpt_order);
   DecPrologueArgs a{user_ids, sem_ids, type_ids, sem_ids_fut, type_ids_fut, seq_mask, user_w, sem_w, wpe_w, tte_w, bos,
                     n_buckets, K, pad, n_sem_rows, n_wpe_rows, n_tte_rows, B, N, L, E, ctx_offsets, ctx_values,
                     fut_values, ctx_alloc_rows, keys, uid_mod};

@@ -73,7 +73,7 @@ _SIGS = {
     "jagged_from_padded_rows": ([_P, _I64, _I64, _I64, _P, _P, _I64, _I, _I, _P], _I),
     "jagged_to_padded": ([_P, _P, _I64, _I64, _I64, _P, _I, _P], _I),
     "rq_dec_prologue_fwd": ([_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P,
-                             _I64, _P, _P, _I64, _P, _P, _P, _P, _P, _P], _I),
+                             _I64, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P], _I),
     "varlen_attn_fwd_ws_elems": ([_I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _P], _I),
     "varlen_attn_fwd": ([_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _F, _P, _I64, _P,
                          _I64, _P, _I64, _I, _P], _I),

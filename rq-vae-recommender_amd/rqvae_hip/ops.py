@@ -1370,16 +1370,20 @@ class DecoderPrologueFunction(torch.autograd.Function):
         fut_off = torch.empty((B + 1,), device=dev, dtype=i64)
         keys = torch.empty((B, N + L), device=dev, dtype=i64)
         uid_mod = torch.empty((B,), device=dev, dtype=i64)
+        # the contexts' LPT order (int32, padded like the attention scratch's order slot) when B allows
+        order = torch.empty(((B + 3) & ~3,), device=dev, dtype=torch.int32) if 2 <= B <= 4096 else None
         c = [t.contiguous() for t in (user_ids, sem_ids, type_ids, seq_mask, sem_fut, type_fut)]
         TIMER.around("dec_prologue", call, "rq_dec_prologue_fwd", *[ptr(t) for t in c], B, N, L, E, ptr(user_w),
                      int(n_buckets), ptr(sem_w), sem_w.shape[0], int(K), int(pad), ptr(wpe_w), wpe_w.shape[0],
                      ptr(tte_w), tte_w.shape[0], ptr(bos), ptr(ctx_vals), int(alloc), ptr(ctx_off), ptr(fut_vals),
-                     ptr(fut_off), ptr(keys), ptr(uid_mod), stream_handle(dev))
+                     ptr(fut_off), ptr(keys), ptr(uid_mod), ptr(order), stream_handle(dev))
         ctx.save_for_backward(ctx_off, keys, uid_mod, c[5])
         ctx.meta = (B, N, L, E, int(pad))
         ctx.tables = tuple(w if isinstance(w, torch.nn.Parameter) else None for w in (user_w, sem_w, wpe_w, tte_w))
         ctx.rows = (user_w.shape[0], sem_w.shape[0], wpe_w.shape[0], tte_w.shape[0])
         ctx.mark_non_differentiable(ctx_off, fut_off)
+        if order is not None:
+            ctx_off._rq_lpt_order = order   # self-attention launches over these offsets reuse it (RQ_ATTN_ORDER_GIVEN)
         return ctx_vals, ctx_off, fut_vals, fut_off
 
     @staticmethod
@@ -1705,7 +1709,7 @@ class JaggedToPaddedValues(torch.autograd.Function):
 # ------------------------------------------------------------------------------ attention
 # Kernel policy of the attention calls (the `flags` argument, RQ_ATTN_* in include/rqvae_hip.h; 0 = the
 # measured-best forms): set only by kernel-vs-kernel tests and A/B probes through attn_policy().
-ATTN_NO_DMA, ATTN_TWO_PASS, ATTN_NO_SPLIT, ATTN_SPLIT_BF16 = 1, 2, 4, 8
+ATTN_NO_DMA, ATTN_TWO_PASS, ATTN_NO_SPLIT, ATTN_SPLIT_BF16, ATTN_LPT_SHORT, ATTN_ORDER_GIVEN = 1, 2, 4, 8, 32, 64
 _ATTN_POLICY = {"flags": 0}
 
 
@@ -1724,31 +1728,58 @@ _ATTN_X3 = True
 _ATTN_X3_BWD = True
 
 
+_GIVEN_ORDER = True   # False: ignore the prologue's LPT order (A/B probes set the attribute)
+
+
+def _given_order(cu_q, cu_k, n_needed: int):
+    """The LPT order the decoder prologue attached to a context's offsets (`_rq_lpt_order`, int32), usable as
+    the whole scratch of a self-attention launch over those offsets (RQ_ATTN_ORDER_GIVEN) when the launch
+    needs nothing else; else None."""
+    order = getattr(cu_k, "_rq_lpt_order", None) if _GIVEN_ORDER else None
+    if order is None or cu_q is not cu_k or n_needed != order.numel():
+        return None
+    return order
+
+
 def _attn_fwd(q, k, v, cu_q, cu_k, B, H, hd, max_q, max_k, causal, scale, out, lse):
     """Forward launch(es) (varlen_attn_fwd with scratch for the LPT order and split-key partials). At matmul
     precision 'high' (the reference's setting, modules/model.py:27) the long-range forms multiply in split-bf16
-    like every Linear (RQ_ATTN_SPLIT_BF16); 'highest' keeps exact fp32 products."""
+    like every Linear (RQ_ATTN_SPLIT_BF16); 'highest' keeps exact fp32 products. A self-attention over offsets
+    that carry the prologue's LPT order dispatches its sequences longest-first without an order launch."""
     import ctypes
     Tq = q.shape[0]
     flags = _ATTN_POLICY["flags"] | (ATTN_SPLIT_BF16 if _ATTN_X3 and matmul_high() else 0)
     n = ctypes.c_int64(0)
     call("varlen_attn_fwd_ws_elems", B, H, hd, int(max_q), int(max_k), Tq, int(causal), flags, ctypes.byref(n))
-    ws = torch.empty((max(1, int(n.value)),), device=q.device, dtype=torch.float32)
+    ws = _given_order(cu_q, cu_k, int(n.value))
+    if ws is not None:
+        flags |= ATTN_LPT_SHORT | ATTN_ORDER_GIVEN
+    else:
+        ws = torch.empty((max(1, int(n.value)),), device=q.device, dtype=torch.float32)
     TIMER.around("varlen_attn_fwd", call, "varlen_attn_fwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
                  v.stride(0), ptr(cu_q), ptr(cu_k), B, H, hd, int(max_q), int(max_k), int(causal), float(scale),
                  ptr(out), out.stride(0), ptr(lse), Tq, ptr(ws), ws.numel(), flags, stream_handle(q.device))
+    return ws if flags & ATTN_ORDER_GIVEN else None
 
 
-def _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv):
+def _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv, order=None):
     """Backward launch(es) of varlen attention into dq / dk / dv (row-strided views); scratch sized for
-    the fused form's query splits (Tk given). At 'high' the fused long-range form multiplies in split-bf16."""
+    the fused form's query splits (Tk given). At 'high' the fused long-range form multiplies in split-bf16.
+    `order`: the forward's given LPT order (the short one-pass forms then dispatch longest-first too)."""
     import ctypes
     Tq, A = q.shape
     flags = _ATTN_POLICY["flags"] | (ATTN_SPLIT_BF16 if _ATTN_X3 and _ATTN_X3_BWD and matmul_high() else 0)
     delta = torch.empty((H, Tq), device=q.device, dtype=torch.float32)   # scratch: rowsum(dO * O)
     n = ctypes.c_int64(0)
-    call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0], flags, ctypes.byref(n))
-    ws = torch.empty((int(n.value),), device=q.device, dtype=torch.float32) if n.value else None
+    ws = None
+    if order is not None:
+        call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0],
+             flags | ATTN_LPT_SHORT, ctypes.byref(n))
+        if n.value == order.numel():
+            ws, flags = order, flags | ATTN_LPT_SHORT | ATTN_ORDER_GIVEN
+    if ws is None:
+        call("varlen_attn_bwd_ws_elems", B, H, A // H, int(max_q), int(max_k), Tq, k.shape[0], flags, ctypes.byref(n))
+        ws = torch.empty((int(n.value),), device=q.device, dtype=torch.float32) if n.value else None
     TIMER.around("varlen_attn_bwd", call, "varlen_attn_bwd", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
                  v.stride(0), ptr(out), out.stride(0), ptr(dout), dout.stride(0), ptr(lse), Tq, ptr(cu_q), ptr(cu_k), B,
                  H, A // H, int(max_q), int(max_k), int(causal), float(scale), ptr(dq), dq.stride(0), ptr(dk),
@@ -1769,7 +1800,7 @@ class VarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        _attn_fwd(q, k, v, cu_q, cu_k, B, num_heads, hd, max_q, max_k, causal, scale, out, lse)
+        ctx.order = _attn_fwd(q, k, v, cu_q, cu_k, B, num_heads, hd, max_q, max_k, causal, scale, out, lse)
         ctx.save_for_backward(q, k, v, out, lse, cu_q, cu_k)
         ctx.cfg = (num_heads, bool(causal), int(max_q), int(max_k), float(scale))
         return out
@@ -1784,7 +1815,8 @@ class VarlenAttentionFunction(torch.autograd.Function):
         dq = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         dk = torch.empty((k.shape[0], A), device=q.device, dtype=torch.float32)
         dv = torch.empty((v.shape[0], A), device=q.device, dtype=torch.float32)
-        _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv)
+        _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv, ctx.order)
+        ctx.order = None
         return dq, dk, dv, None, None, None, None, None, None, None
 
 
@@ -1813,7 +1845,7 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         B = cu_q.shape[0] - 1
         out = torch.empty((Tq, A), device=q.device, dtype=torch.float32)
         lse = torch.empty((num_heads, Tq), device=q.device, dtype=torch.float32)
-        _attn_fwd(q, k, v, cu_q, cu_k, B, num_heads, hd, max_q, max_k, causal, scale, out, lse)
+        ctx.order = _attn_fwd(q, k, v, cu_q, cu_k, B, num_heads, hd, max_q, max_k, causal, scale, out, lse)
         if self_attn:
             ctx.save_for_backward(qsrc, out, lse, cu_q, cu_k)
         else:
@@ -1844,7 +1876,8 @@ class PackedVarlenAttentionFunction(torch.autograd.Function):
         q, k, v = qsrc[:, :A], src_kv[:, koff:koff + A], src_kv[:, koff + A:koff + 2 * A]
         dq, dk, dv = gq_src[:, :A], gkv_src[:, koff:koff + A], gkv_src[:, koff + A:koff + 2 * A]
         B = cu_q.shape[0] - 1
-        _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv)
+        _attn_bwd(q, k, v, out, dout, lse, cu_q, cu_k, B, H, max_q, max_k, causal, scale, dq, dk, dv, ctx.order)
+        ctx.order = None
         return gq_src, (None if self_attn else gkv_src), None, None, None, None, None, None, None
 
 

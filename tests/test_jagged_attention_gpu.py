@@ -462,3 +462,38 @@ def test_varlen_attention_precision_pairings_vs_oracle(device, fwd_prec, bwd_pre
     finally:
         torch.set_float32_matmul_precision(prev)
 
+
+
+@pytest.mark.parametrize("lq,lk,causal", [
+    ([81, 9, 45, 0, 17, 64, 33, 81], None, False),    # Amazon encoder self-attention (short one-pass forms)
+    ([5, 1, 16, 7, 3], None, True),                    # few-query causal self-attention
+    ([300, 12, 801, 45], None, False),                 # long ranges (LPT forward; fused backward)
+])
+def test_varlen_attention_lpt_order_bitwise(device, lq, lk, causal):
+    """Longest-first dispatch of the short / few-query forms (RQ_ATTN_LPT_SHORT, computed by an order launch or
+    taken from the offsets' attached order: RQ_ATTN_ORDER_GIVEN, as the decoder prologue provides it) only
+    reorders independent (sequence, head) workgroups: out and gradients bitwise the default order's."""
+    from rqvae_hip import ops
+    g = gi.rng(sum(lq) * 5 + 3)
+    H, hd = 8, 64
+    A_ = H * hd
+    lens = np.array(lq, dtype=np.int64)
+    cu_np = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    Tq = int(cu_np[-1]) + 2
+    q0, k0, v0, do = (torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device) for _ in range(4))
+    order_np = sorted(range(len(lq)), key=lambda b: (-lq[b], b))
+    res = {}
+    for mode in ("default", "lpt", "given"):
+        cu = torch.from_numpy(cu_np).to(device)
+        if mode == "given":
+            o = np.zeros(((len(lq) + 3) & ~3,), dtype=np.int32)
+            o[:len(lq)] = order_np
+            cu._rq_lpt_order = torch.from_numpy(o).to(device)
+        with ops.attn_policy(ops.ATTN_LPT_SHORT if mode == "lpt" else 0):
+            qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
+            out = ops.varlen_attention(qt, kt, vt, cu, cu, H, causal, max(lq), max(lq))
+            out.backward(do)
+        res[mode] = (out.detach(), qt.grad, kt.grad, vt.grad)
+    for mode in ("lpt", "given"):
+        for a, b, what in zip(res[mode], res["default"], ("out", "dq", "dk", "dv")):
+            assert torch.equal(a, b), (mode, what)

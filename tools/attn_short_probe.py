@@ -40,14 +40,28 @@ def main():
     cu = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(dev)
     T, mx = int(lens.sum()), int(lens.max())
     q, k, v, do = (torch.randn(T, A, device=dev) for _ in range(4))
-    for mode in ("x3", "fp32"):
-        ops._ATTN_X3 = ops._ATTN_X3_BWD = mode == "x3"
-        qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
-        fwd = timed(lambda: ops.varlen_attention(qs, ks, vs, cu, cu, H, causal, mx, mx))
-        o = ops.varlen_attention(qs, ks, vs, cu, cu, H, causal, mx, mx)
-        bwd = timed(lambda: torch.autograd.grad(o, (qs, ks, vs), do, retain_graph=True))
-        print(json.dumps({"B": B, "H": H, "causal": causal, "tokens": T, "mode": mode, "fwd_us": round(fwd, 1),
-                          "bwd_us": round(bwd, 1)}), flush=True)
+    flags = [int(f) for f in os.environ.get("PROBE_FLAGS", "0").split(",")]
+    modes = os.environ.get("PROBE_MODES", "x3,fp32").split(",")
+    # the decoder's cross-attention at the same contexts: L+2 = 5 future queries per sequence
+    nf = 5
+    cuq = torch.arange(B + 1, device=dev, dtype=torch.int64) * nf
+    qc, doc = torch.randn(B * nf, A, device=dev), torch.randn(B * nf, A, device=dev)
+    for rnd in range(int(os.environ.get("PROBE_ROUNDS", "1"))):
+        for fl in flags:
+            for mode in modes:
+                ops._ATTN_X3 = ops._ATTN_X3_BWD = mode == "x3"
+                with ops.attn_policy(fl):
+                    qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
+                    fwd = timed(lambda: ops.varlen_attention(qs, ks, vs, cu, cu, H, causal, mx, mx))
+                    o = ops.varlen_attention(qs, ks, vs, cu, cu, H, causal, mx, mx)
+                    bwd = timed(lambda: torch.autograd.grad(o, (qs, ks, vs), do, retain_graph=True))
+                    xq, xk, xv = (t.clone().requires_grad_(True) for t in (qc, k, v))
+                    cf = timed(lambda: ops.varlen_attention(xq, xk, xv, cuq, cu, H, False, nf, mx))
+                    oc = ops.varlen_attention(xq, xk, xv, cuq, cu, H, False, nf, mx)
+                    cb = timed(lambda: torch.autograd.grad(oc, (xq, xk, xv), doc, retain_graph=True))
+                print(json.dumps({"B": B, "H": H, "causal": causal, "tokens": T, "mode": mode, "flags": fl, "round": rnd,
+                                  "fwd_us": round(fwd, 1), "bwd_us": round(bwd, 1), "cross_fwd_us": round(cf, 1),
+                                  "cross_bwd_us": round(cb, 1)}), flush=True)
     ops._ATTN_X3 = ops._ATTN_X3_BWD = True
 
 
