@@ -108,6 +108,18 @@ int rq_rmsnorm_dropout_fwd(const float* x, const float* w, int64_t B, int64_t D,
 int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, const float* gy, const float* gres,
                            int64_t B, int64_t D, float p, uint64_t seed, float* gx, float* gw, int accumulate_gw,
                            int defer, int* parts, void* workspace, size_t ws_bytes, void* stream);
+/* Two RMSNorms of the same rows (the decoder block's attn_norm and cross_attn_norm of x,
+ * modules/transformer/model.py:75-82), each with its own weight, dropout p and seed: one rstd, y1 and y2 —
+ * bitwise two rq_rmsnorm_dropout_fwd calls, in one launch. The backward returns gx = norm2'(gy2) +
+ * (norm1'(gy1) + gres) (the chained single-norm calls' roundings) and both weight gradients (accumulate /
+ * defer as rq_rmsnorm_dropout_bwd; deferred: w1's partials at workspace, w2's at workspace +
+ * rq_rmsnorm_bwd_workspace(B, D), *parts rows each). workspace >= 2 rq_rmsnorm_bwd_workspace(B, D) bytes. */
+int rq_rmsnorm2_dropout_fwd(const float* x, const float* w1, const float* w2, int64_t B, int64_t D, float eps, float p1,
+                            uint64_t seed1, float p2, uint64_t seed2, float* y1, float* y2, float* rstd, void* stream);
+int rq_rmsnorm2_dropout_bwd(const float* x, const float* w1, const float* w2, const float* rstd, const float* gy1,
+                            const float* gy2, const float* gres, int64_t B, int64_t D, float p1, uint64_t seed1, float p2,
+                            uint64_t seed2, float* gx, float* gw1, float* gw2, int accumulate_gw, int defer, int* parts,
+                            void* workspace, size_t ws_bytes, void* stream);
 /* Elementwise dropout fusions over n fp32 elements (n % 4 == 0, 16-byte aligned), same mask
  * generator as above (element index = position in the buffer):
  *   rq_silu_dropout_fwd  h = Dropout(SiLU(z))         the MLP hidden layer (modules/encoder.py:20-28)
@@ -251,7 +263,7 @@ int rq_ce_loss_bwd(const float* X, int64_t ldx, int64_t K, const int64_t* tgt, c
                    void* stream);
 /* x (n fp32) -> hi = RN_bf16(x), lo = RN_bf16(x - hi) (bf16 bit patterns). */
 int rq_split_bf16x3(const float* x, int64_t n, uint16_t* hi, uint16_t* lo, void* stream);
-/* The same for count <= 16 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device
+/* The same for count <= 48 tensors in one launch (x[t], n[t], hi[t], lo[t]: host arrays of device
  * pointers / element counts). */
 int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, uint16_t* const* hi,
                           uint16_t* const* lo, void* stream);

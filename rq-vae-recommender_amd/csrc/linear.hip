@@ -1239,7 +1239,7 @@ __global__ void __launch_bounds__(256) split_bf16x3_kernel(const float* __restri
 }
 
 // Several tensors at once (all weights of an MLP chain: one launch instead of one per weight).
-constexpr int kSplitMax = 16;
+constexpr int kSplitMax = 48;   // a decoder's every GEMM weight in one launch (kernel arguments ~1.6 KB)
 struct SplitMulti {
   const float* x[kSplitMax];
   uint16_t* hi[kSplitMax];
@@ -1254,8 +1254,12 @@ template <bool VEC>
 __global__ void __launch_bounds__(256) split_bf16x3_multi_kernel(SplitMulti sm) {
   const int64_t total = sm.start[sm.count];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    int t = 0;
-    while (t + 1 < sm.count && i >= sm.start[t + 1]) ++t;
+    int lo_t = 0, hi_t = sm.count - 1;   // the tensor holding i: start[t] <= i < start[t + 1]
+    while (lo_t < hi_t) {
+      const int mid = (lo_t + hi_t + 1) >> 1;
+      if (i >= sm.start[mid]) lo_t = mid; else hi_t = mid - 1;
+    }
+    const int t = lo_t;
     const int64_t j = i - sm.start[t];
     if constexpr (VEC)
       split_store4(reinterpret_cast<const float4*>(sm.x[t])[j], sm.hi[t] + 4 * j, sm.lo[t] + 4 * j);

@@ -267,6 +267,153 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(const float* __restric
   }
 }
 
+// Two RMSNorms of the same rows (the decoder block's attn_norm and cross_attn_norm of x,
+// modules/transformer/model.py:75-82): rstd once, y1 = Dropout_1(t w1), y2 = Dropout_2(t w2) — bitwise the two
+// single-norm launches, in one. The backward gives gx = norm2'(g2) + (norm1'(g1) + gres) in that order (the
+// chained single-norm launches' roundings) and both weight-gradient partials.
+template <int VPL>
+__global__ void __launch_bounds__(256) rmsnorm2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                           const float* __restrict__ w2, int64_t B, int D, float eps,
+                                                           uint32_t thr1, float ds1, uint64_t seed1, uint32_t thr2,
+                                                           float ds2, uint64_t seed2, float* __restrict__ y1,
+                                                           float* __restrict__ y2, float* __restrict__ rstd) {
+  seed1 = epoch_seed(seed1);
+  seed2 = epoch_seed(seed2);
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const float* p = x + r * D;
+  float4 xv[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    xv[v] = c < D ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s = __builtin_fmaf(xv[v].x, xv[v].x, s);
+    s = __builtin_fmaf(xv[v].y, xv[v].y, s);
+    s = __builtin_fmaf(xv[v].z, xv[v].z, s);
+    s = __builtin_fmaf(xv[v].w, xv[v].w, s);
+  }
+  s = group_sum<64>(s);
+  const float rs = rsqrtf(s / (float)D + eps);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    if (c >= D) continue;
+    const float4 t = make_float4(xv[v].x * rs, xv[v].y * rs, xv[v].z * rs, xv[v].w * rs);
+    const float4 a = *reinterpret_cast<const float4*>(w1 + c);
+    const float4 b = *reinterpret_cast<const float4*>(w2 + c);
+    const uint64_t e = (uint64_t)(r * D + c) / 4;
+    *reinterpret_cast<float4*>(y1 + r * D + c) =
+        drop4(make_float4(t.x * a.x, t.y * a.y, t.z * a.z, t.w * a.w), seed1, e, thr1, ds1);
+    *reinterpret_cast<float4*>(y2 + r * D + c) =
+        drop4(make_float4(t.x * b.x, t.y * b.y, t.z * b.z, t.w * b.w), seed2, e, thr2, ds2);
+  }
+  if (lane == 0) rstd[r] = rs;
+}
+
+template <int VPL>
+__device__ __forceinline__ void rms_part_store(float4 (&part)[4][VPL * 64], const float4 (&gwa)[VPL], int wave, int lane,
+                                               int D, float* __restrict__ gw_part) {
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) part[wave][v * 64 + lane] = gwa[v];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      if (c >= D) continue;
+      float4 a = part[0][v * 64 + lane];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const float4 b = part[q][v * 64 + lane];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      *reinterpret_cast<float4*>(gw_part + (int64_t)blockIdx.x * D + c) = a;
+    }
+  }
+  __syncthreads();   // part is reused by the next call
+}
+
+template <int VPL>
+__global__ void __launch_bounds__(256) rmsnorm2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                           const float* __restrict__ w2, const float* __restrict__ rstd,
+                                                           const float* __restrict__ gy1, const float* __restrict__ gy2,
+                                                           int64_t B, int D, uint32_t thr1, float ds1, uint64_t seed1,
+                                                           uint32_t thr2, float ds2, uint64_t seed2,
+                                                           const float* __restrict__ gres, float* __restrict__ gx,
+                                                           float* __restrict__ gw1_part, float* __restrict__ gw2_part,
+                                                           int rows) {
+  seed1 = epoch_seed(seed1);
+  seed2 = epoch_seed(seed2);
+  __shared__ float4 part[4][VPL * 64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float4 wa[VPL], wb[VPL], ga[VPL], gb[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c = (v * 64 + lane) * 4;
+    wa[v] = c < D ? *reinterpret_cast<const float4*>(w1 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    wb[v] = c < D ? *reinterpret_cast<const float4*>(w2 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    ga[v] = gb[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float invD = 1.f / (float)D;
+  for (int i = wave; i < rows; i += 4) {
+    const int64_t r = (int64_t)blockIdx.x * rows + i;
+    if (r >= B) break;
+    const float rs = rstd[r];
+    float4 xv[VPL], t1[VPL], t2[VPL];
+    float d1 = 0.f, d2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      const bool ok = c < D;
+      const uint64_t e = (uint64_t)(r * D + c) / 4;
+      xv[v] = ok ? *reinterpret_cast<const float4*>(x + r * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g1 = ok ? drop4(*reinterpret_cast<const float4*>(gy1 + r * D + c), seed1, e, thr1, ds1)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g2 = ok ? drop4(*reinterpret_cast<const float4*>(gy2 + r * D + c), seed2, e, thr2, ds2)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      t1[v] = make_float4(wa[v].x * g1.x, wa[v].y * g1.y, wa[v].z * g1.z, wa[v].w * g1.w);
+      t2[v] = make_float4(wb[v].x * g2.x, wb[v].y * g2.y, wb[v].z * g2.z, wb[v].w * g2.w);
+      d1 = __builtin_fmaf(t1[v].x, xv[v].x, d1);
+      d1 = __builtin_fmaf(t1[v].y, xv[v].y, d1);
+      d1 = __builtin_fmaf(t1[v].z, xv[v].z, d1);
+      d1 = __builtin_fmaf(t1[v].w, xv[v].w, d1);
+      d2 = __builtin_fmaf(t2[v].x, xv[v].x, d2);
+      d2 = __builtin_fmaf(t2[v].y, xv[v].y, d2);
+      d2 = __builtin_fmaf(t2[v].z, xv[v].z, d2);
+      d2 = __builtin_fmaf(t2[v].w, xv[v].w, d2);
+      ga[v].x = __builtin_fmaf(g1.x, xv[v].x * rs, ga[v].x);
+      ga[v].y = __builtin_fmaf(g1.y, xv[v].y * rs, ga[v].y);
+      ga[v].z = __builtin_fmaf(g1.z, xv[v].z * rs, ga[v].z);
+      ga[v].w = __builtin_fmaf(g1.w, xv[v].w * rs, ga[v].w);
+      gb[v].x = __builtin_fmaf(g2.x, xv[v].x * rs, gb[v].x);
+      gb[v].y = __builtin_fmaf(g2.y, xv[v].y * rs, gb[v].y);
+      gb[v].z = __builtin_fmaf(g2.z, xv[v].z * rs, gb[v].z);
+      gb[v].w = __builtin_fmaf(g2.w, xv[v].w * rs, gb[v].w);
+    }
+    d1 = group_sum<64>(d1);
+    d2 = group_sum<64>(d2);
+    const float k1 = rs * rs * rs * invD * d1, k2 = rs * rs * rs * invD * d2;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      if (c >= D) continue;
+      float4 o = make_float4(rs * t1[v].x - xv[v].x * k1, rs * t1[v].y - xv[v].y * k1, rs * t1[v].z - xv[v].z * k1,
+                             rs * t1[v].w - xv[v].w * k1);
+      if (gres) {
+        const float4 e = *reinterpret_cast<const float4*>(gres + r * D + c);
+        o = make_float4(o.x + e.x, o.y + e.y, o.z + e.z, o.w + e.w);
+      }
+      const float4 q = make_float4(rs * t2[v].x - xv[v].x * k2, rs * t2[v].y - xv[v].y * k2,
+                                   rs * t2[v].z - xv[v].z * k2, rs * t2[v].w - xv[v].w * k2);
+      *reinterpret_cast<float4*>(gx + r * D + c) = make_float4(q.x + o.x, q.y + o.y, q.z + o.z, q.w + o.w);
+    }
+  }
+  rms_part_store<VPL>(part, ga, wave, lane, D, gw1_part);
+  rms_part_store<VPL>(part, gb, wave, lane, D, gw2_part);
+}
+
 // out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): a workgroup owns kRedCols float4
 // columns; its 256 / kRedCols row lanes q sum s = q, q + 64, ... (8 loads in flight), then the 64
 // partials are combined by a fixed-shape tree through LDS. Deterministic, no atomics. Few columns per
@@ -844,6 +991,64 @@ int rq_rmsnorm_dropout_bwd(const float* x, const float* w, const float* rstd, co
   hipLaunchKernelGGL(rms_reduce_kernel, dim3((unsigned)((D / 4 + kRedCols - 1) / kRedCols)), dim3(256), 0, s, part, nblk, D, gw,
                      accumulate_gw);
   RQ_LAUNCH_CHECK("rq_rmsnorm_bwd(reduce)");
+  return 0;
+}
+
+int rq_rmsnorm2_dropout_fwd(const float* x, const float* w1, const float* w2, int64_t B, int64_t D, float eps, float p1,
+                            uint64_t seed1, float p2, uint64_t seed2, float* y1, float* y2, float* rstd, void* stream) {
+  RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm2_fwd: need D %% 4 == 0, D <= 4096");
+  if (B == 0) return 0;
+  RQ_CHECK_ARG(x && w1 && w2 && y1 && y2 && rstd, "rq_rmsnorm2_fwd: null pointer");
+  uint32_t thr1, thr2;
+  float ds1, ds2;
+  dropout_params(p1, &thr1, &ds1);
+  dropout_params(p2, &thr2, &ds2);
+  dim3 g((unsigned)((B + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+#define RMS_F2(V) hipLaunchKernelGGL((rmsnorm2_fwd_kernel<V>), g, dim3(256), 0, s, x, w1, w2, B, (int)D, eps, thr1, ds1, seed1, thr2, ds2, seed2, y1, y2, rstd);
+  RMS_SWITCH((int)((D + 255) / 256), RMS_F2)
+#undef RMS_F2
+  RQ_LAUNCH_CHECK("rq_rmsnorm2_fwd");
+  return 0;
+}
+
+int rq_rmsnorm2_dropout_bwd(const float* x, const float* w1, const float* w2, const float* rstd, const float* gy1,
+                            const float* gy2, const float* gres, int64_t B, int64_t D, float p1, uint64_t seed1, float p2,
+                            uint64_t seed2, float* gx, float* gw1, float* gw2, int accumulate_gw, int defer, int* parts,
+                            void* workspace, size_t ws_bytes, void* stream) {
+  if (parts) *parts = 0;
+  RQ_CHECK_ARG(B >= 0 && D > 0 && D % 4 == 0 && D <= 4096, "rq_rmsnorm2_bwd: need D %% 4 == 0, D <= 4096");
+  RQ_CHECK_ARG(gw1 && gw2 && (B == 0 || (x && w1 && w2 && rstd && gy1 && gy2 && gx)), "rq_rmsnorm2_bwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (B == 0) {
+    if (!accumulate_gw) {
+      RQ_HIP(zero_async(gw1, (size_t)D * sizeof(float), s));
+      RQ_HIP(zero_async(gw2, (size_t)D * sizeof(float), s));
+    }
+    return 0;
+  }
+  const size_t half = rq_rmsnorm_bwd_workspace(B, D);
+  RQ_CHECK_ARG(workspace && ws_bytes >= 2 * half, "rq_rmsnorm2_bwd: workspace too small (2 x rq_rmsnorm_bwd_workspace)");
+  uint32_t thr1, thr2;
+  float ds1, ds2;
+  dropout_params(p1, &thr1, &ds1);
+  dropout_params(p2, &thr2, &ds2);
+  float* part1 = static_cast<float*>(workspace);
+  float* part2 = part1 + half / sizeof(float);
+  const int rows = rms_rows_per_blk(B);
+  const int nblk = (int)((B + rows - 1) / rows);
+#define RMS_B2(V) hipLaunchKernelGGL((rmsnorm2_bwd_kernel<V>), dim3((unsigned)nblk), dim3(256), 0, s, x, w1, w2, rstd, gy1, gy2, B, (int)D, thr1, ds1, seed1, thr2, ds2, seed2, gres, gx, part1, part2, rows);
+  RMS_SWITCH((int)((D + 255) / 256), RMS_B2)
+#undef RMS_B2
+  RQ_LAUNCH_CHECK("rq_rmsnorm2_bwd");
+  if (defer && parts) {   // both weights' partials [nblk][D] at workspace and workspace + half: rq_reduce_partials
+    *parts = nblk;
+    return 0;
+  }
+  const dim3 rg((unsigned)((D / 4 + kRedCols - 1) / kRedCols));
+  hipLaunchKernelGGL(rms_reduce_kernel, rg, dim3(256), 0, s, part1, nblk, D, gw1, accumulate_gw);
+  hipLaunchKernelGGL(rms_reduce_kernel, rg, dim3(256), 0, s, part2, nblk, D, gw2, accumulate_gw);
+  RQ_LAUNCH_CHECK("rq_rmsnorm2_bwd(reduce)");
   return 0;
 }
 

@@ -36,6 +36,9 @@ _SIGS = {
     "rq_rmsnorm_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_rmsnorm_dropout_fwd": ([_P, _P, _I64, _I64, _F, _F, _U64, _P, _P, _P], _I),
     "rq_rmsnorm_dropout_bwd": ([_P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _P, _P, _I, _I, _P, _P, _SZ, _P], _I),
+    "rq_rmsnorm2_dropout_fwd": ([_P, _P, _P, _I64, _I64, _F, _F, _U64, _F, _U64, _P, _P, _P, _P], _I),
+    "rq_rmsnorm2_dropout_bwd": ([_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _F, _U64, _F, _U64, _P, _P, _P, _I, _I, _P, _P, _SZ,
+                                 _P], _I),
     "rq_dropout_params": ([_F, _P, _P], _I),
     "rq_silu_dropout_fwd": ([_P, _I64, _F, _U64, _P, _P], _I),
     "rq_silu_dropout_bwd": ([_P, _P, _I64, _F, _U64, _P, _P], _I),

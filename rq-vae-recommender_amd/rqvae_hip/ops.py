@@ -284,14 +284,17 @@ def split_bf16x3(x: torch.Tensor) -> Split:
     return Split(hi, lo)
 
 
+_SPLIT_MULTI_MAX = 48   # rq_split_bf16x3_multi's tensor table
+
+
 def split_bf16x3_many(xs) -> list:
-    """split_bf16x3 of up to 16 tensors in one launch (rq_split_bf16x3_multi)."""
+    """split_bf16x3 of up to 48 tensors in one launch (rq_split_bf16x3_multi)."""
     import ctypes
     xs = [x.contiguous() for x in xs]
     if not xs:
         return []
     require_gpu(*xs, what="split_bf16x3_many")
-    assert len(xs) <= 16
+    assert len(xs) <= _SPLIT_MULTI_MAX
     out = [Split(torch.empty(x.shape, device=x.device, dtype=torch.bfloat16),
                  torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)) for x in xs]
     n = len(xs)
@@ -307,15 +310,16 @@ _WSPLIT = {}   # id(weight) -> (Split, weight): the current forward's pre-split 
 @contextlib.contextmanager
 def weight_split_scope(params):
     """Split every GEMM weight among `params` (2-D fp32 device tensors, both dims % 8) once, in a few
-    multi-tensor launches (rq_split_bf16x3_multi, 16 per launch), for the forward run inside the
+    multi-tensor launches (rq_split_bf16x3_multi, 48 per launch), for the forward run inside the
     scope: the Linear / MLP ops take their split operand from here instead of one split launch per
     weight per call (the decoder: ~32 -> 3 launches per step). Only at matmul precision 'high'."""
     ws = [p for p in params if p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 and p.shape[0] % 8 == 0
           and p.shape[1] % 8 == 0] if matmul_high() else []
     prev = dict(_WSPLIT)
     with torch.no_grad():
-        for i in range(0, len(ws), 16):
-            for w, sp in zip(ws[i:i + 16], split_bf16x3_many([w.detach() for w in ws[i:i + 16]])):
+        for i in range(0, len(ws), _SPLIT_MULTI_MAX):
+            chunk = ws[i:i + _SPLIT_MULTI_MAX]
+            for w, sp in zip(chunk, split_bf16x3_many([w.detach() for w in chunk])):
                 _WSPLIT[id(w)] = (sp, w)
     try:
         yield
@@ -335,8 +339,8 @@ def split_weights(weights) -> list:
     out = [(_WSPLIT.get(id(w)) or (None, None)) for w in weights]
     miss = [i for i, (sp, w) in enumerate(out) if sp is None or w is not weights[i]]
     res = [sp for sp, _ in out]
-    for j in range(0, len(miss), 16):
-        idx = miss[j:j + 16]
+    for j in range(0, len(miss), _SPLIT_MULTI_MAX):
+        idx = miss[j:j + _SPLIT_MULTI_MAX]
         for i, sp in zip(idx, split_bf16x3_many([weights[i] for i in idx])):
             res[i] = sp
     return res
@@ -1076,6 +1080,47 @@ def _rmsnorm_bwd(x2, weight, rstd, gy, gres, p: float, seed: int, need_w: bool):
     return gx, (gw if need_w else None)
 
 
+_RMS_DUAL = True   # False: the fork's two norms as two launches each way (A/B probes set the attribute)
+
+
+def _rmsnorm2_bwd(x2, ws_, rstd, g1, g2, gres, ps, seeds, need):
+    """(gx, gw1, gw2) of the fork's two norms in one rq_rmsnorm2_dropout_bwd launch — gx = norm2'(g2) +
+    (norm1'(g1) + gres), the chained calls' order; weight gradients into their flat-bucket views (deferred
+    like _rmsnorm_bwd's) or returned. None when the two weights' gradient destinations differ in kind
+    (one bucket view, one returned tensor): the caller chains two single-norm backwards then."""
+    from . import dp
+    w1, w2 = ws_
+    B, D = x2.shape
+    s1 = dp.direct_grad(w1) if need[0] else None
+    s2 = dp.direct_grad(w2) if need[1] else None
+    if (s1 is None) != (s2 is None) or not (need[0] and need[1]):
+        return None
+    sinks = s1 is not None
+    defer = sinks and dp.defer_ok(w1) and dp.defer_ok(w2)
+    if defer and (s1.data_ptr() in _DEFER["outs"] or s2.data_ptr() in _DEFER["outs"]):
+        flush_reductions()
+    half = _lib.load().rq_rmsnorm_bwd_workspace(B, D)
+    ws = torch.empty((2 * half,), device=x2.device, dtype=torch.uint8)
+    gw1 = s1 if sinks else torch.empty((D,), device=x2.device, dtype=torch.float32)
+    gw2 = s2 if sinks else torch.empty((D,), device=x2.device, dtype=torch.float32)
+    gx = torch.empty_like(x2)
+    import ctypes
+    parts = ctypes.c_int(0)
+    g1c, g2c = g1.contiguous().view(B, D), g2.contiguous().view(B, D)
+    call("rq_rmsnorm2_dropout_bwd", ptr(x2), ptr(w1), ptr(w2), ptr(rstd), ptr(g1c), ptr(g2c),
+         ptr(None if gres is None else gres.contiguous().view(B, D)), B, D, float(ps[0]), int(seeds[0]), float(ps[1]),
+         int(seeds[1]), ptr(gx), ptr(gw1), ptr(gw2), int(sinks), int(defer), ctypes.byref(parts), ptr(ws), 2 * half,
+         stream_handle(x2.device))
+    if defer and parts.value > 0:
+        _defer_push(ws[:half], s1, D, parts.value, 1)
+        _defer_push(ws[half:], s2, D, parts.value, 1)
+    if sinks:
+        dp.direct_grad_done(w1)
+        dp.direct_grad_done(w2)
+        return gx, None, None
+    return gx, gw1, gw2
+
+
 class RMSNormForkFunction(torch.autograd.Function):
     """x -> (RMSNorm_1(x) [dropout], [RMSNorm_2(x) [dropout]], x): the pre-norm block's fan-out of x to
     its norm branches and to the residual stream (modules/transformer/model.py:75-82: h = x +
@@ -1091,7 +1136,14 @@ class RMSNormForkFunction(torch.autograd.Function):
         x2 = x.contiguous().view(-1, D)
         B = x2.shape[0]
         outs, saved = [], [x2]
-        for w, p, sd in ((w1, p1, seed1), (w2, p2, seed2)):
+        if w2 is not None and _RMS_DUAL:   # both norms in one launch (one rstd, shared by both backward halves)
+            y1, y2 = torch.empty_like(x2), torch.empty_like(x2)
+            rstd = torch.empty((B,), device=x.device, dtype=torch.float32)
+            call("rq_rmsnorm2_dropout_fwd", ptr(x2), ptr(w1), ptr(w2), B, D, float(eps), float(p1), int(seed1),
+                 float(p2), int(seed2), ptr(y1), ptr(y2), ptr(rstd), stream_handle(x.device))
+            outs = [y1.view(x.shape), y2.view(x.shape)]
+            saved += [w1, rstd, w2, rstd]
+        for w, p, sd in (((w1, p1, seed1), (w2, p2, seed2)) if not outs else ()):
             if w is None:
                 continue
             y = torch.empty_like(x2)
@@ -1111,6 +1163,13 @@ class RMSNormForkFunction(torch.autograd.Function):
         n = (len(saved) - 1) // 2
         g_pass = grads[n]
         gres, gws = g_pass, [None, None]
+        if n == 2 and _RMS_DUAL:
+            r = _rmsnorm2_bwd(x2, ctx.ws, saved[2], grads[0], grads[1], g_pass, ctx.ps, ctx.seeds,
+                              (ctx.needs_input_grad[6], ctx.needs_input_grad[7]))
+            if r is not None:
+                gx, gw1, gw2 = r
+                ctx.ws = None
+                return gx.view(ctx.shape), None, None, None, None, None, gw1, gw2
         for i in range(n):   # gx = norm_1' g_1 + norm_2' g_2 + g_pass, each norm backward adding the previous sum
             w, rstd = saved[1 + 2 * i], saved[2 + 2 * i]
             gres, gws[i] = _rmsnorm_bwd(x2, ctx.ws[i], rstd, grads[i], gres, ctx.ps[i], ctx.seeds[i],
@@ -1490,6 +1549,7 @@ class CrossEntropyLossFunction(torch.autograd.Function):
              ptr(loss_d), stream_handle(dev))
         ctx.save_for_backward(X, t, lse)
         ctx.dims = (B, npos, npos_x)
+        ctx.set_materialize_grads(False)   # unused outputs (loss_d, logits in training) arrive as NULL: no zero fills
         return loss, loss_d, logits
 
     @staticmethod

@@ -110,3 +110,34 @@ def test_fork_direct_grad_equals_autograd(device):
                 assert torch.equal(pa.grad, pb.grad), n
     finally:
         torch.set_float32_matmul_precision("highest")
+
+
+@pytest.mark.parametrize("p1,p2,B,D", [(0.0, 0.0, 3001, 512), (0.3, 0.3, 2049, 384), (0.1, 0.5, 40, 384)])
+@pytest.mark.parametrize("buckets", [False, True])
+def test_rmsnorm_fork_dual_kernel_bitwise(device, monkeypatch, p1, p2, B, D, buckets):
+    """The fork's two norms in one launch each way (rq_rmsnorm2_dropout_fwd / _bwd) vs the chained single-norm
+    launches: outputs, the input gradient (norm2'(g2) + (norm1'(g1) + g_pass)) and both weight gradients
+    bitwise — returned to autograd, or added into flat gradient-bucket views through the deferred reduction."""
+    from rqvae_hip import dp, ops
+    gen = torch.Generator(device=device).manual_seed(11)
+    x = torch.randn(B, D, generator=gen, device=device)
+    w1 = torch.nn.Parameter(torch.randn(D, generator=gen, device=device))
+    w2 = torch.nn.Parameter(torch.randn(D, generator=gen, device=device))
+    gs = [torch.randn(B, D, generator=gen, device=device) for _ in range(3)]
+    gb = dp.GradBuckets([w1, w2], flat_views=True) if buckets else None
+    res = {}
+    for dual in (True, False):
+        monkeypatch.setattr(ops, "_RMS_DUAL", dual)
+        if gb is not None:
+            gb.zero_grad()
+        else:
+            w1.grad = w2.grad = None
+        xx = x.clone().requires_grad_(True)
+        ops._SEED["n"] = 0
+        outs = ops.rmsnorm_fork(xx, 1e-6, w1, p1, w2, p2)
+        sum((o * g).sum() for o, g in zip(outs, gs)).backward()
+        if gb is not None:
+            ops.flush_reductions()
+        res[dual] = [o.detach().clone() for o in outs] + [xx.grad.clone(), w1.grad.clone(), w2.grad.clone()]
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
