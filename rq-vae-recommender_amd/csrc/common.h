@@ -106,6 +106,25 @@ __device__ __forceinline__ void split_store4(const float4 o, uint16_t* hi, uint1
   *reinterpret_cast<uint2*>(lo) = l;
 }
 
+// 0 + P[s0] + P[s0 + stride] + P[s0 + 2 stride] + ... (s ascending) over the (n)-float partials P[s][..] at
+// float4 column j: the order every split-K / partial reduction here is defined by. Eight partial loads are in
+// flight per round whatever S is — indices past the end re-read partial S - 1 (a cache hit) and are not
+// added — so a lane with 5..8 partials waits for one round trip instead of up to five dependent ones.
+__device__ __forceinline__ float4 strided_slab_sum(const float* __restrict__ P, int S, int64_t n, int64_t j, int s0,
+                                                   int stride) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = s0; s < S; s += 8 * stride) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = *reinterpret_cast<const float4*>(P + (int64_t)min(s + stride * u, S - 1) * n + j);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (s + stride * u < S) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+  }
+  return a;
+}
+
 // Correctly rounded a / b (bitwise the IEEE quotient) for a divisor shared by many numerators:
 // y = 1.0f / b is computed once with the IEEE division, then q0 = RN(a*y) is within an ulp of
 // a/b and one fma correction returns RN(a/b) (Markstein's theorem) whenever the residual

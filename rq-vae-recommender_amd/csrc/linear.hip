@@ -148,7 +148,7 @@ wgrad_partial_kernel(const float* __restrict__ g, int64_t ldg, const float* __re
 }
 
 // out[j] = sum_{s=0}^{S-1} P[s*n + j] in a fixed order (n % 4 == 0): workgroup = 64 float4
-// columns x 4 waves; wave w sums s = w, w+4, ... (4 independent loads in flight per step), then
+// columns x 4 waves; wave w sums s = w, w+4, ... (strided_slab_sum), then
 // the four wave partials are added in wave order through LDS. Deterministic, no atomics.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ P, int S, int64_t n,
                                                            float* __restrict__ out) {
@@ -157,27 +157,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   const int64_t j = ((int64_t)blockIdx.x * 64 + lane) * 4;
   const bool ok = j < n;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (ok) {
-    int s = wave;
-    for (; s + 28 < S; s += 32) {   // 8 slab loads in flight; adds in s order (same bits)
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-    }
-    for (; s + 12 < S; s += 16) {
-      float4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-    }
-    for (; s < S; s += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-  }
+  if (ok) a = strided_slab_sum(P, S, n, j, wave, 4);
   part[wave][lane] = a;
   __syncthreads();
   if (wave == 0 && ok) {
@@ -1178,27 +1158,7 @@ __global__ void __launch_bounds__(256) x3_reduce_kernel(const float* __restrict_
   const int64_t j = ((int64_t)blockIdx.x * 64 + lane) * 4;
   const bool ok = j < n;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (ok) {
-    int s = wave;
-    for (; s + 28 < S; s += 32) {   // 8 slab loads in flight; adds in s order (same bits)
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-    }
-    for (; s + 12 < S; s += 16) {
-      float4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-    }
-    for (; s < S; s += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-  }
+  if (ok) a = strided_slab_sum(P, S, n, j, wave, 4);
   part[wave][lane] = a;
   __syncthreads();
   if (wave == 0 && ok) {
@@ -1305,7 +1265,11 @@ static unsigned x3s_pad_lds(const P& pl) {
 //    CU with its two workgroups, ~0.4 for a lone workgroup; wide kernel 1.3x) — the wide kernel's
 //    256 x 256 tiles quantise into 4x coarser rounds (decoder context rows: a 1,536-wide projection is
 //    270 wide tiles, two rounds, the second nearly empty);
-//  * split-K: the slabs written and re-read, (S + 1) M N fp32 at ~5 TB/s, plus a ~4 us reduce launch.
+//  * split-K: the slabs written by the GEMM and read back by the reduction, 2 S M N fp32 at ~3 TB/s (the
+//    rate the batched deferred reductions reach), plus a ~4 us reduce launch. Round 4 priced (S + 1) M N at
+//    5 TB/s, which chose 256 x 256-tile plans with S = 21..30 for the decoder's 11k-row weight gradients:
+//    ~64 MB of slabs per weight, 444 MB (C4) / 800 MB (Amazon) a step. Same-process A/B on MI355X: C4
+//    2.766 -> 2.678 ms, Amazon 5.415 -> 5.355, RQ-VAE 1.957 -> 1.924 (half the rate, 1.5 TB/s, loses).
 // Checked against tools/gemm_ab.py on MI355X (RQ-VAE and decoder shapes, both kernels forced).
 #ifndef RQ_X3W_SPEED
 #define RQ_X3W_SPEED 1.3
@@ -1320,6 +1284,9 @@ static unsigned x3s_pad_lds(const P& pl) {
 // gap it adds between launches in a replayed step (4 us measured best of 4 / 8 / 16 at both decoder
 // configs, profiles/r03/reduce_us_ab.txt).
 constexpr double kX3ReduceUs = 4.0;
+#ifndef RQ_X3_SLAB_BPUS
+#define RQ_X3_SLAB_BPUS 3.0e6   // slab bytes per us (written + read back)
+#endif
 static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   const int64_t cus = resident_slots() / 2;
   const int64_t wgs = (int64_t)p.tiles * p.S;
@@ -1335,7 +1302,7 @@ static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
     const int64_t rounds = (wgs + slots - 1) / slots;
     t = (double)rounds * per_cu * tile * (double)p.chunk / (rate * 1e6);
   }
-  if (p.S > 1) t += (double)(p.S + 1) * (double)(M * N) * 4.0 / 5e6 + kX3ReduceUs;
+  if (p.S > 1) t += (double)(2 * p.S) * (double)(M * N) * 4.0 / RQ_X3_SLAB_BPUS + kX3ReduceUs;
   return t;
 }
 
@@ -1860,29 +1827,7 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(RedSegTable t) {
     const int64_t j = ((int64_t)lb * 64 + lane) * 4;
     const bool ok = j < n;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok) {
-      // 8 slab loads in flight per lane (a deferred batch has S ~ 10..42: one load at a time left the
-      // launch latency-bound at ~2.6 TB/s); the adds stay in s order, so the sum is the same bits.
-      int s = wave;
-      for (; s + 28 < S; s += 32) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-      }
-      for (; s + 12 < S; s += 16) {
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + 4 * u) * n + j);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-      }
-      for (; s < S; s += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
-        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-      }
-    }
+    if (ok) a = strided_slab_sum(P, S, n, j, wave, 4);
     red[wave * 64 + lane] = a;
     __syncthreads();
     if (wave == 0 && ok) {
@@ -1904,11 +1849,7 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(RedSegTable t) {
     const int64_t j = ((int64_t)lb * kC + c) * 4;
     const bool ok = j < n;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok)
-      for (int s = q; s < S; s += kQ) {
-        const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
-        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-      }
+    if (ok) a = strided_slab_sum(P, S, n, j, q, kQ);
     red[q * kC + c] = a;
     __syncthreads();
 #pragma unroll

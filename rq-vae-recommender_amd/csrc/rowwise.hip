@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256) rmsnorm2_bwd_kernel(const float* __restri
 }
 
 // out[j] = sum_{s < S} P[s*n + j] in a fixed order (n % 4 == 0): a workgroup owns kRedCols float4
-// columns; its 256 / kRedCols row lanes q sum s = q, q + 64, ... (8 loads in flight), then the 64
+// columns; its 256 / kRedCols row lanes q sum s = q, q + 64, ... (strided_slab_sum), then the 64
 // partials are combined by a fixed-shape tree through LDS. Deterministic, no atomics. Few columns per
 // workgroup: at D = 512 and ~700 partials the sum is latency-bound, so more workgroups with shorter
 // chains (32 x 11 loads per lane, not 8 x 44).
@@ -428,20 +428,7 @@ __global__ void __launch_bounds__(256) rms_reduce_kernel(const float* __restrict
   const int64_t j = ((int64_t)blockIdx.x * kRedCols + c) * 4;
   const bool ok = j < n;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (ok) {
-    int s = q;
-    for (; s + 7 * kQ < S; s += 8 * kQ) {
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)(s + kQ * u) * n + j);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
-    }
-    for (; s < S; s += kQ) {
-      const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)s * n + j);
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-  }
+  if (ok) a = strided_slab_sum(P, S, n, j, q, kQ);
   red[q][c] = a;
   __syncthreads();
 #pragma unroll
