@@ -174,6 +174,12 @@ int rq_gemm_bf16x3(const float* A, int64_t lda, int a_kcontig, const float* B, i
 #define RQ_GEMM_NO_WIDE 8     /* never the wide kernel (128- / 64-tile chosen by the model) */
 #define RQ_GEMM_MASKED 16     /* masked k staging even for whole 32-deep stages (bitwise the unmasked path) */
 #define RQ_GEMM_NO_PAIR 32    /* rq_gemm_bf16x3_pair: two launches */
+/* flags | RQ_GEMM_SPLIT(S): split K into S chunks (1..4095; 0 = the planner's count) on the kernel the other
+ * flags / the planner pick — a tuned plan for a known shape. S > 1 needs S x M x N fp32 of workspace (which
+ * rq_gemm_bf16x3_workspace does not size for a forced S). Bits of a result depend on the chunking. */
+#define RQ_GEMM_SPLIT_SHIFT 16
+#define RQ_GEMM_SPLIT_MASK 0xFFF
+#define RQ_GEMM_SPLIT(S) ((int)(S) << RQ_GEMM_SPLIT_SHIFT)
 
 /* One general split-bf16 GEMM call (the fused MLP chain, modules/encoder.py:7-36 — Linear, SiLU,
  * [Dropout], ..., Linear — and every decoder Linear). An operand is fp32 (X_lo == NULL) or pre-split:

@@ -1260,7 +1260,9 @@ static unsigned x3s_pad_lds(const P& pl) {
 }
 
 // Modelled time (us) of a plan, to choose the split-K factor and between the two kernels:
-//  * MMA: whole rounds of resident workgroups (a partly filled last round costs a full one) x the
+//  * MMA: rounds of resident workgroups (fractional: a partly filled last round costs its share — fitted
+//    on measured plan sweeps, tools/plan_model_fit.py over profiles/r05/plan_sweep/; the whole-round count
+//    it replaced mispriced the 64-tile form at 4 per CU, e.g. C4's 4,608 x 1,024 x 384 SiLU launches) x the
 //    MACs a CU does per round, at the measured per-CU rates (128-tile kernel ~0.53 M fp32-MAC/us per
 //    CU with its two workgroups, ~0.4 for a lone workgroup; wide kernel 1.3x) — the wide kernel's
 //    256 x 256 tiles quantise into 4x coarser rounds (decoder context rows: a 1,536-wide projection is
@@ -1282,8 +1284,12 @@ static unsigned x3s_pad_lds(const P& pl) {
 #endif
 // Modelled cost (us) of the separate slab-reduction launch of a split-K call: the reduction kernel plus the
 // gap it adds between launches in a replayed step (4 us measured best of 4 / 8 / 16 at both decoder
-// configs, profiles/r03/reduce_us_ab.txt).
-constexpr double kX3ReduceUs = 4.0;
+// configs in round 3, profiles/r03/reduce_us_ab.txt; 3 with the fractional rounds, fitted on the round-5
+// plan sweeps: a back-to-back tiny launch costs ~2.7 us in a replayed graph).
+#ifndef RQ_X3_FRAC_ROUNDS
+#define RQ_X3_FRAC_ROUNDS 1   // 0: whole rounds and a 4 us reduction (the model before the round-5 sweeps; A/B)
+#endif
+constexpr double kX3ReduceUs = RQ_X3_FRAC_ROUNDS ? 3.0 : 4.0;
 #ifndef RQ_X3_SLAB_BPUS
 #define RQ_X3_SLAB_BPUS 3.0e6   // slab bytes per us (written + read back)
 #endif
@@ -1299,8 +1305,10 @@ static double x3_plan_time(const X3Plan& p, int64_t M, int64_t N, bool wide) {
   } else {
     const int per_cu = wide ? 1 : (small ? x3s_resident(wgs) : kXWG);
     const int64_t slots = cus * per_cu;
-    const int64_t rounds = (wgs + slots - 1) / slots;
-    t = (double)rounds * per_cu * tile * (double)p.chunk / (rate * 1e6);
+    // a partly filled last round costs its share; one round at least
+    const double rounds = !RQ_X3_FRAC_ROUNDS ? (double)((wgs + slots - 1) / slots)
+                                             : (wgs > slots ? (double)wgs / (double)slots : 1.0);
+    t = rounds * per_cu * tile * (double)p.chunk / (rate * 1e6);
   }
   if (p.S > 1) t += (double)(2 * p.S) * (double)(M * N) * 4.0 / RQ_X3_SLAB_BPUS + kX3ReduceUs;
   return t;
@@ -1515,6 +1523,9 @@ static int x3_prepare(const rq_gemm_desc& d, hipStream_t s, X3Call* c, bool dry 
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, flags, &pw);
   if (wide) pl = pw;
+  // a tuned plan: RQ_GEMM_SPLIT(S) forces the split-K count on the kernel the policy picked
+  const int forced_s = (flags >> RQ_GEMM_SPLIT_SHIFT) & RQ_GEMM_SPLIT_MASK;
+  if (forced_s > 0) pl = x3_plan_s(M, N, K, forced_s, wide, wide ? kWT2 : pl.ts);
   // slab path: split-K partials go to the workspace with the plain store, and x3_reduce_kernel applies
   // the real epilogue (and the accumulation); an unsplit accumulating call adds in the GEMM's epilogue
   const bool slab = pl.S > 1;

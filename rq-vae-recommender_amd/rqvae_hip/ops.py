@@ -391,6 +391,12 @@ def _wgrad_result(weight, spec, result):
 # time model's choice): set only by kernel-vs-kernel tests and A/B probes through gemm_policy(); the library
 # itself keeps no state — the flags travel in every descriptor.
 GEMM_ONLY_128, GEMM_ONLY_64, GEMM_FORCE_WIDE, GEMM_NO_WIDE, GEMM_MASKED, GEMM_NO_PAIR = 1, 2, 4, 8, 16, 32
+GEMM_SPLIT_SHIFT, GEMM_SPLIT_MASK = 16, 0xFFF
+
+
+def gemm_split(S: int) -> int:
+    """RQ_GEMM_SPLIT(S): policy bits forcing S split-K chunks on the kernel the other bits / the planner pick."""
+    return (int(S) & GEMM_SPLIT_MASK) << GEMM_SPLIT_SHIFT
 _GEMM_POLICY = {"flags": 0}
 
 
@@ -468,14 +474,18 @@ def _x3_setup(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, ep
     if epilogue in (EPI_SILU_FWD, EPI_SILU_BWD):
         H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
+    flags = _GEMM_POLICY["flags"]
     nbytes = _x3_workspace(M, N, K)
+    forced = (flags >> GEMM_SPLIT_SHIFT) & GEMM_SPLIT_MASK
+    if forced > 1:   # a forced split count: its slabs (the library sizes only the planner's)
+        nbytes = max(nbytes, forced * M * N * 4)
     ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8) if nbytes else None
     defer = bool(defer and accumulate and nbytes)
     if defer and C.data_ptr() in _DEFER["outs"]:
         flush_reductions()   # a pending reduction into the same output must land first
     fields = (ptr(ah), ptr(al), lda, int(a_kcontig), ptr(bh), ptr(bl), ldb, int(b_kcontig), M, N, K, ptr(C), N,
               int(epilogue), ptr(Z), ptr(H.hi if H else None), ptr(H.lo if H else None), N, float(p), int(seed),
-              int(accumulate), int(defer), ptr(ws), nbytes, _GEMM_POLICY["flags"], 0)
+              int(accumulate), int(defer), ptr(ws), nbytes, flags, 0)
     key = f"gemm_bf16x3:{M}x{N}x{K}:{int(a_kcontig)}{int(b_kcontig)}{asp}{bsp}{epilogue}{int(accumulate)}"
     return _X3Call(fields, C, H, ws, defer, key, epilogue, M, N, dev)
 
