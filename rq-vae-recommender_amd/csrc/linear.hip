@@ -1707,6 +1707,18 @@ static bool x3_pair_ts(int k1, const X3Call& c1, const X3Call& c2, dim3 grid, un
   }
 }
 
+template <int TS>
+static bool x3_pair_fwd_ts(const X3Call& c1, const X3Call& c2, dim3 grid, unsigned pad, hipStream_t s, int n1) {
+  using F32 = X3Body<true, false, true, true, kEpiStore, false, TS>;   // fp32 A
+  using SPL = X3Body<true, true, true, true, kEpiStore, false, TS>;    // split A
+  const bool a1 = c1.asp, a2 = c2.asp;
+  if (!a1 && !a2) x3_pair_go<F32, F32>(c1, c2, grid, pad, s, n1);
+  else if (!a1) x3_pair_go<F32, SPL>(c1, c2, grid, pad, s, n1);
+  else if (!a2) x3_pair_go<SPL, F32>(c1, c2, grid, pad, s, n1);
+  else x3_pair_go<SPL, SPL>(c1, c2, grid, pad, s, n1);
+  return true;
+}
+
 // The paired launch of a data-gradient problem c1 and a weight-gradient problem c2 (both on the 128- or
 // 64-tile kernel with the same tile size), for the operand forms of the decoder's backward: c1 = g W
 // (A fp32 or split k-contiguous, B split n-contiguous; plain or SiLU'-with-dropout epilogue), c2 = g^T x
@@ -1720,11 +1732,20 @@ static int x3_pair_k1(const X3Call& c1) {
 // form pair, and at least one of them leaving resident slots idle alone (the decoder's 40..11,332-row
 // launches; two launches that each fill the chip already — the RQ-VAE's 65,536-row 64-tile layers — gain
 // nothing and measured 4 us slower paired).
+// Two forward projections of different inputs (the decoder block's self-attention qkv of attn_norm(x) and
+// cross-attention q of cross_attn_norm(x)): k-contiguous A (fp32 / split) x k-contiguous split B, plain store.
+static bool x3_fwd_form(const X3Call& c) {
+  return c.epi_k == kEpiStore && (c.code == (16 | 4 | 2) || c.code == (16 | 8 | 4 | 2));
+}
+
 static bool x3_pairable(const X3Call& c1, const X3Call& c2) {
   if (c1.wide || c2.wide || c1.pl.ts != c2.pl.ts) return false;
-  if (c2.epi_k != kEpiStore || c2.code != (c2.code & (8 | 2))) return false;   // c2: m-contig A, n-contig B
-  const int k1 = x3_pair_k1(c1);
-  if (k1 != (16 | 2) && k1 != (16 | 8 | 2) && k1 != (16 | 2 | 32) && k1 != (16 | 2 | 64)) return false;
+  const bool fwd = x3_fwd_form(c1) && x3_fwd_form(c2);
+  if (!fwd) {
+    if (c2.epi_k != kEpiStore || c2.code != (c2.code & (8 | 2))) return false;   // c2: m-contig A, n-contig B
+    const int k1 = x3_pair_k1(c1);
+    if (k1 != (16 | 2) && k1 != (16 | 8 | 2) && k1 != (16 | 2 | 32) && k1 != (16 | 2 | 64)) return false;
+  }
   const int64_t w1 = (int64_t)c1.pl.tiles * c1.pl.S, w2 = (int64_t)c2.pl.tiles * c2.pl.S;
   const int64_t slots = c1.pl.ts == 64 ? (int64_t)x3s_resident(w1 + w2) * (resident_slots() / 2) : x3_slots();
   return !(w1 >= slots && w2 >= slots);
@@ -1738,6 +1759,8 @@ static bool x3_pair_launch(const X3Call& c1, const X3Call& c2, hipStream_t s) {
   const bool t64 = c1.pl.ts == 64;
   unsigned pad = 0;
   if (t64 && RQ_X3S_COMPACT && x3s_resident(w1 + w2) == kXWG) pad = 32768u;   // few workgroups: 2 per CU (x3s_pad_lds)
+  if (x3_fwd_form(c1) && x3_fwd_form(c2))
+    return t64 ? x3_pair_fwd_ts<64>(c1, c2, grid, pad, s, n1) : x3_pair_fwd_ts<128>(c1, c2, grid, 0u, s, n1);
   const int k1 = x3_pair_k1(c1);
   return t64 ? x3_pair_ts<64>(k1, c1, c2, grid, pad, s, n1) : x3_pair_ts<128>(k1, c1, c2, grid, 0u, s, n1);
 }
@@ -1778,6 +1801,16 @@ int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream) {
     }
   } else {
     RQ_LAUNCH_CHECK("gemm_x3_pair_kernel");
+  }
+  // two plain-store slab outputs: one batched reduction (rq_reduce_partials layout 0 = x3_reduce_kernel's
+  // order, bitwise) instead of two launches
+  auto plain_slab = [](const X3Call& x) { return !x.trivial && x.slab && x.epilogue == kEpiStore && !x.accumulate; };
+  if (plain_slab(c[0]) && plain_slab(c[1])) {
+    const float* P[2] = {c[0].out, c[1].out};
+    float* out[2] = {c[0].C, c[1].C};
+    const int64_t n[2] = {c[0].M * c[0].N, c[1].M * c[1].N};
+    const int S[2] = {c[0].pl.S, c[1].pl.S}, layout[2] = {0, 0}, acc[2] = {0, 0};
+    return rq_reduce_partials(2, P, out, n, S, layout, acc, stream);
   }
   for (int i = 0; i < 2; ++i) {
     if (c[i].trivial) continue;

@@ -82,11 +82,14 @@ class MultiHeadAttention(nn.Module):
 
     def forward(self, x: AttentionInput, x_kv: Optional[AttentionInput] = None, padding_mask: Optional[Tensor] = None,
                 is_causal: Optional[bool] = True, jagged: bool = False, use_cache: bool = False,
-                residual: Optional[Tensor] = None, kv_values: Optional[Tensor] = None) -> AttentionInput:
+                residual: Optional[Tensor] = None, kv_values: Optional[Tensor] = None,
+                proj_values: Optional[Tensor] = None) -> AttentionInput:
         """`residual` (this build's extension, default None = the reference's contract): values
         (T, d_out) added to the output projection inside its GEMM (out = proj(ctx) + residual).
         `kv_values` (extension, cross-attention): this layer's `self.kv(x_kv)` already computed by the
-        decoder's hoisted projection of the shared context (TransformerDecoder.forward)."""
+        decoder's hoisted projection of the shared context (TransformerDecoder.forward).
+        `proj_values` (extension): `self.qkv(x)` (self-attention) or `self.q(x)` (cross-attention) already
+        computed — by the block's paired projection launch (TransformerBlock._forward_fork)."""
         assert not self.cross_attn or x_kv is not None, "Found null x_kv in cross attn. layer"
         if not jagged:
             raise Exception("Unjagged attention currently not supported.")
@@ -96,11 +99,13 @@ class MultiHeadAttention(nn.Module):
         if self.cross_attn:
             jkv = as_jagged(x_kv)
             kv = self.kv(jkv.values()) if kv_values is None else kv_values
-            ctx = hip_ops.varlen_attention_packed(self.q(jx.values()), kv, jx.offsets(),
+            q = self.q(jx.values()) if proj_values is None else proj_values
+            ctx = hip_ops.varlen_attention_packed(q, kv, jx.offsets(),
                                                   jkv.offsets(), self.num_heads, bool(is_causal), jx.max_len,
                                                   jkv.max_len)
         else:
-            ctx = hip_ops.varlen_attention_packed(self.qkv(jx.values()), None, jx.offsets(), jx.offsets(),
+            qkv = self.qkv(jx.values()) if proj_values is None else proj_values
+            ctx = hip_ops.varlen_attention_packed(qkv, None, jx.offsets(), jx.offsets(),
                                                   self.num_heads, bool(is_causal), jx.max_len, jx.max_len)
         out = self.proj(ctx) if residual is None else hip_ops.linear_add(ctx, self.proj.weight, residual)
         return jx.with_values(out) if isinstance(x, Jagged) else _wrap_like(out, x)

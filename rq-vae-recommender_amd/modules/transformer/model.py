@@ -28,6 +28,7 @@ from rqvae_hip import ops as hip_ops
 # False selects the unfused form (tests / A-B probes set these module attributes):
 _FF_RESIDUAL = True   # False: the feed-forward output as MLP + dropout_add
 _HOIST_KV = True      # False: per-layer cross-attention K/V projections
+_PAIR_PROJ = True     # False: the self-attention qkv and cross-attention q projections as two launches
 
 
 class KVCacheOpsMixin:
@@ -122,11 +123,15 @@ class TransformerBlock(nn.Module):
                                               self.cross_attn_norm.weight, p)
         else:
             n1, xr = hip_ops.rmsnorm_fork(xv, self.attn_norm.eps, self.attn_norm.weight, p)
+        qkv = q2 = None
+        if self.do_cross_attn and _PAIR_PROJ and self._pair_ok(n1, n2):
+            # the two projections of x's two norms are independent: one paired launch
+            qkv, q2 = hip_ops.linear_pair(n1, self.attention.qkv.weight, n2, self.cross_attention.q.weight)
         h = self.attention(jx.with_values(n1), is_causal=is_causal, jagged=True, use_cache=use_cache,
-                           residual=xr).values()
+                           residual=xr, proj_values=qkv).values()
         if self.do_cross_attn:
             h = self.cross_attention(x=jx.with_values(n2), x_kv=jkv, is_causal=False, jagged=True,
-                                     use_cache=use_cache, residual=h, kv_values=kv).values()
+                                     use_cache=use_cache, residual=h, kv_values=kv, proj_values=q2).values()
         n3, hr = hip_ops.rmsnorm_fork(h, norm.eps, norm.weight)
         fused = self._ff_residual(mlp, drop, n3, hr)
         if fused is not None:
@@ -135,6 +140,11 @@ class TransformerBlock(nn.Module):
         if drop.training and drop.p > 0 and hip_ops.dropout_fusable(hr) and hip_ops.dropout_fusable(y):
             return jx.with_values(hip_ops.dropout_add(hr, y, drop.p))
         return jx.with_values(hr + drop(y))
+
+    def _pair_ok(self, n1, n2) -> bool:
+        a, c = self.attention, self.cross_attention
+        return (a.qkv.bias is None and c.q.bias is None and
+                hip_ops.linear_pair_supported(n1, a.qkv.weight, n2, c.q.weight))
 
     def reset_kv_cache(self):
         raise NotImplementedError("KV Cache currently not supported")

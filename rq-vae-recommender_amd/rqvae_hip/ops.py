@@ -971,6 +971,67 @@ class LinearFunction(torch.autograd.Function):
         return gx, dW, db if ctx.has_bias else None
 
 
+def _linear_bwd_high(x, g, weight, wsp, need_x: bool, need_w: bool):
+    """(gx, dW) of y = x W^T at 'high' with W's split planes wsp: data and weight gradient in one paired launch
+    where both are needed (the weight gradient straight into its bucket: dW None), else one each."""
+    O, I = weight.shape
+    g2 = g.reshape(-1, O)
+    x2 = x.reshape(-1, I)
+    if g2.shape[0] == 0:
+        return (torch.zeros_like(x) if need_x else None), (torch.zeros_like(weight) if need_w else None)
+    if need_x and need_w:
+        wspec = _wgrad_spec(weight, g2.contiguous(), False, x2.contiguous(), False, O, I, g2.shape[0])
+        if wspec is not None:
+            gx, wres = gemm_x3_pair(dict(a=g2, a_kcontig=True, b=wsp, b_kcontig=False, M=g2.shape[0], N=I, K=O), wspec)
+            return gx.view(x.shape), _wgrad_result(weight, wspec, wres)
+    gx = gemm_x3(g2, True, wsp, False, g2.shape[0], I, O).view(x.shape) if need_x else None
+    dW = _wgrad_into(weight, g2.contiguous(), False, x2.contiguous(), False, O, I, g2.shape[0]) if need_w else None
+    return gx, dW
+
+
+class LinearPairFunction(torch.autograd.Function):
+    """(x1 W1^T, x2 W2^T): two bias-free projections of different inputs in ONE launch (rq_gemm_bf16x3_pair's
+    forward pairing; split-K slabs of both reduced in one batched launch) — the decoder block's self-attention
+    qkv of attn_norm(x) and cross-attention q of cross_attn_norm(x) (modules/transformer/model.py:68-82,
+    modules/transformer/attention.py:96-104). Backward: each projection's paired data + weight gradient, as
+    LinearFunction's. Results bitwise two LinearFunction calls (same plans per problem)."""
+
+    @staticmethod
+    def forward(ctx, x1, w1, x2, w2):
+        (O1, I1), (O2, I2) = w1.shape, w2.shape
+        a1, a2 = x1.reshape(-1, I1), x2.reshape(-1, I2)
+        s1, s2 = split_weight(w1), split_weight(w2)
+        y1, y2 = gemm_x3_pair(dict(a=a1, a_kcontig=True, b=s1, b_kcontig=True, M=a1.shape[0], N=O1, K=I1),
+                              dict(a=a2, a_kcontig=True, b=s2, b_kcontig=True, M=a2.shape[0], N=O2, K=I2))
+        ctx.save_for_backward(x1, x2)
+        ctx.w, ctx.wsp = (w1, w2), (s1, s2)
+        return y1.view(*x1.shape[:-1], O1), y2.view(*x2.shape[:-1], O2)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        x1, x2 = ctx.saved_tensors
+        (w1, w2), (s1, s2) = ctx.w, ctx.wsp
+        ni = ctx.needs_input_grad
+        gx1 = dW1 = gx2 = dW2 = None
+        if g1 is not None:
+            gx1, dW1 = _linear_bwd_high(x1, g1, w1, s1, ni[0], ni[1])
+        if g2 is not None:
+            gx2, dW2 = _linear_bwd_high(x2, g2, w2, s2, ni[2], ni[3])
+        ctx.w = ctx.wsp = None
+        return gx1, dW1, gx2, dW2
+
+
+def linear_pair_supported(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor, w2: torch.Tensor) -> bool:
+    """LinearPairFunction applies: 'high' precision, fp32 device tensors, split-operand widths, rows."""
+    return (matmul_high() and all(t.is_cuda and t.dtype == torch.float32 for t in (x1, w1, x2, w2)) and
+            w1.shape[1] % 8 == 0 and w2.shape[1] % 8 == 0 and x1.shape[-1] == w1.shape[1] and
+            x2.shape[-1] == w2.shape[1] and x1.numel() > 0 and x2.numel() > 0)
+
+
+def linear_pair(x1, w1, x2, w2):
+    return LinearPairFunction.apply(x1, w1, x2, w2)
+
+
 class LinearAddFunction(torch.autograd.Function):
     """y = x W^T + r (bias-free Linear followed by a residual add, e.g. the attention output
     projection plus the block input, modules/transformer/model.py:75-78) as ONE split-bf16 GEMM

@@ -316,3 +316,79 @@ def test_decoder_prologue_equals_composition(device, monkeypatch, buckets, B, ma
     assert torch.equal(fo, torch.arange(B + 1, device=device) * (batch.sem_ids_fut.shape[1] + 1))
     assert torch.count_nonzero(cv[int(co[-1]):]) == 0
     assert row_counts(batch.seq_mask)[0] + B == int(co[-1])
+
+
+@pytest.mark.parametrize("M,I,O1,O2", [(40, 384, 1152, 384), (1280, 512, 1536, 512), (300, 64, 192, 64)])
+def test_linear_pair_equals_two_linears(device, M, I, O1, O2):
+    """linear_pair (the block's self-attention qkv + cross-attention q projections of two inputs in one
+    rq_gemm_bf16x3_pair launch, slab reductions batched) vs two LinearFunction calls: outputs and all four
+    gradients bitwise, at split-K row counts (40: the C4 future tokens) and unsplit ones."""
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(M + I)
+    x1, x2 = (torch.randn(M, I, device=device, generator=g) for _ in range(2))
+    w1 = torch.randn(O1, I, device=device, generator=g) * 0.05
+    w2 = torch.randn(O2, I, device=device, generator=g) * 0.05
+    gy1 = torch.randn(M, O1, device=device, generator=g)
+    gy2 = torch.randn(M, O2, device=device, generator=g)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("high")
+    try:
+        res = []
+        for paired in (True, False):
+            ts = [t.clone().requires_grad_(True) for t in (x1, w1, x2, w2)]
+            if paired:
+                assert ops.linear_pair_supported(*ts)
+                y1, y2 = ops.linear_pair(*ts)
+            else:
+                y1 = ops.LinearFunction.apply(ts[0], ts[1], None)
+                y2 = ops.LinearFunction.apply(ts[2], ts[3], None)
+            torch.autograd.backward([y1, y2], [gy1, gy2])
+            res.append((y1.detach(), y2.detach(), *[t.grad for t in ts]))
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    for a, b, what in zip(res[0], res[1], ("y1", "y2", "dx1", "dw1", "dx2", "dw2")):
+        assert torch.equal(a, b), f"{what}: max abs diff {(a - b).abs().max().item():.3e}"
+    ref = x1 @ w1.t()
+    torch.testing.assert_close(res[0][0], ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("buckets", [False, True])
+def test_decoder_pair_proj_equals_separate(device, monkeypatch, buckets):
+    """The decoder with the block's qkv / cross-q projections paired (_PAIR_PROJ) vs two launches: loss and
+    every parameter gradient bitwise, with and without flat gradient buckets."""
+    from data.processed import synthetic_tokenized_batch
+    from modules import model as model_mod
+    from modules.transformer import model as tmodel
+    from rqvae_hip import dp, ops
+    torch.manual_seed(0)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("high")
+    try:
+        m = model_mod.EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.1, num_heads=4,
+                                                   n_layers=2, num_embeddings=64, sem_id_dim=4,
+                                                   inference_verifier_fn=None, max_pos=80).to(device)
+        batch = synthetic_tokenized_batch(24, 20, 4, 64, 7, device)
+        gb = dp.GradBuckets(m.parameters(), flat_views=True) if buckets else None
+        res = {}
+        for paired in (True, False):
+            monkeypatch.setattr(tmodel, "_PAIR_PROJ", paired)
+            if gb is not None:
+                gb.zero_grad()
+            else:
+                m.zero_grad(set_to_none=True)
+            torch.manual_seed(5)
+            ops._SEED["base"] = None   # restart the dropout-key counter: both passes draw the same masks
+            loss = m(batch).loss
+            loss.backward()
+            if gb is not None:
+                ops.flush_reductions()
+            res[paired] = (loss.detach().clone(), {n: (None if p.grad is None else p.grad.detach().clone())
+                                                   for n, p in m.named_parameters()})
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    assert torch.equal(res[True][0], res[False][0])
+    for n in res[False][1]:
+        a, b = res[True][1][n], res[False][1][n]
+        assert (a is None) == (b is None), n
+        if a is not None:
+            assert torch.equal(a, b), (n, float((a - b).abs().max()))
