@@ -492,7 +492,13 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 #endif
 
 #ifndef RQ_X3_INTERLEAVE
-#define RQ_X3_INTERLEAVE 0   // 1: next-stage LDS writes between the MFMAs (measured 20 % slower)
+#define RQ_X3_INTERLEAVE 0   // 1: next-stage LDS writes between the MFMAs (measured 20 % slower); 2: the
+                             // 128-tile stage as 8 groups of (6 MFMA, 1 LDS write, 7 VALU) after its reads
+#endif
+
+#ifndef RQ_X3_PEEL
+#define RQ_X3_PEEL 1   // 0: the second stage slot of each loop iteration multiplies under a runtime test (the
+                       // round-4 loop; the MFMAs then sit in their own basic block, apart from the staging)
 #endif
 
 #ifndef RQ_X3_MFMA16
@@ -735,7 +741,7 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
   // reads, and a conditional store would leave the set's loads possibly pending, so the compiler
   // would wait vmcnt(0) before reloading it). RQ_X3_INTERLEAVE issues the write (its VALU and
   // ds_writes) between the MFMAs instead of after them.
-#if RQ_X3_INTERLEAVE
+#if RQ_X3_INTERLEAVE == 1
 #define RQ_X3_BODY(SA, SB)                                                                                    \
   SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
   SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                  \
@@ -744,6 +750,24 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
     __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                                                        \
     __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                                                        \
     __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);                                                        \
+  }
+#elif RQ_X3_INTERLEAVE == 2
+#define RQ_X3_BODY(SA, SB)                                                                                    \
+  if constexpr (TS == 128) {                                                                                  \
+    SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                \
+    SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                \
+    if (on_) RQ_X3_MMA                                                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);                                                       \
+    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                        \
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);                                                      \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                                                      \
+      __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);                                                      \
+    }                                                                                                         \
+  } else {                                                                                                    \
+    if (on_) RQ_X3_MMA                                                                                        \
+    SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                \
+    SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                \
   }
 #else
 #define RQ_X3_BODY(SA, SB)                                                                                    \
@@ -766,16 +790,36 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
       RQ_X3_STAGE(st + 3, sa3, sb3, sa0, sb0, st + 3 < nst)
     }
   } else if constexpr (kDepth == 3) {
+#if RQ_X3_PEEL
+    int st = 0;
+    for (; st + 2 < nst; st += 3) {
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+      RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2, true)
+      RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0, true)
+    }
+    if (st < nst) RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+    if (st + 1 < nst) RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2, true)
+#else
     for (int st = 0; st < nst; st += 3) {
       RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
       RQ_X3_STAGE(st + 1, sa1, sb1, sa2, sb2, st + 1 < nst)
       RQ_X3_STAGE(st + 2, sa2, sb2, sa0, sb0, st + 2 < nst)
     }
+#endif
   } else {
+#if RQ_X3_PEEL
+    int st = 0;
+    for (; st + 1 < nst; st += 2) {
+      RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+      RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0, true)
+    }
+    if (st < nst) RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
+#else
     for (int st = 0; st < nst; st += 2) {
       RQ_X3_STAGE(st, sa0, sb0, sa1, sb1, true)
       RQ_X3_STAGE(st + 1, sa1, sb1, sa0, sb0, st + 1 < nst)
     }
+#endif
   }
 #undef RQ_X3_STAGE
 #undef RQ_X3_BODY
