@@ -231,7 +231,11 @@ int rq_gemm_bf16x3_run(const rq_gemm_desc* d, int* splits, void* stream);
  * instantiation exists — a Linear's backward: d[0] the data gradient g W (SiLU'-with-dropout epilogue
  * allowed), d[1] the weight gradient g^T x (modules/encoder.py:7-36, modules/transformer: autograd's
  * grad_input / grad_weight of nn.Linear) — both problems' workgroups run in ONE launch (one launch instead
- * of two; together they fill the chip where each alone cannot). RQ_GEMM_NO_PAIR in either: two launches. */
+ * of two; together they fill the chip where each alone cannot). Also two forward projections of different
+ * inputs (k-contiguous A, k-contiguous split B, plain store: the decoder block's self-attention qkv and
+ * cross-attention q, modules/transformer/model.py:75-80); when both then use split-K, their slabs are
+ * reduced in one launch (rq_reduce_partials' layout 0, bitwise the two reductions). RQ_GEMM_NO_PAIR in
+ * either: two launches. */
 int rq_gemm_bf16x3_pair(const rq_gemm_desc* d, int* splits, void* stream);
 /* Host-only planning of a descriptor (pointers may be NULL): the kernel rq_gemm_bf16x3_run would launch —
  * 1 = the wide 256 x 256-tile kernel (both operands split, LDS-DMA staged, 8 waves), 0 = the 128 x 128-tile

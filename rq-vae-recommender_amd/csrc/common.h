@@ -125,6 +125,28 @@ __device__ __forceinline__ float4 strided_slab_sum(const float* __restrict__ P, 
   return a;
 }
 
+// The four-way slab sum of the split-K reductions by ONE thread: p_w = 0 + P[w] + P[w + 4] + ... (ascending s,
+// w = s mod 4), returned as ((p0 + p1) + p2) + p3 — bitwise strided_slab_sum(.., w, 4) per wave combined in
+// wave order (the layout-0 order), without the LDS exchange and its barrier, 16 partial loads in flight per
+// round (past-the-end indices re-read partial S - 1 and are not added).
+__device__ __forceinline__ float4 slab_sum_w4(const float* __restrict__ P, int S, int64_t n, int64_t j) {
+  float4 p[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) p[w] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < S; s += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(P + (int64_t)min(s + u, S - 1) * n + j);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (s + u < S) { p[u & 3].x += v[u].x; p[u & 3].y += v[u].y; p[u & 3].z += v[u].z; p[u & 3].w += v[u].w; }
+  }
+  float4 r = p[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) { r.x += p[w].x; r.y += p[w].y; r.z += p[w].z; r.w += p[w].w; }
+  return r;
+}
+
 // Correctly rounded a / b (bitwise the IEEE quotient) for a divisor shared by many numerators:
 // y = 1.0f / b is computed once with the IEEE division, then q0 = RN(a*y) is within an ulp of
 // a/b and one fma correction returns RN(a/b) (Markstein's theorem) whenever the residual

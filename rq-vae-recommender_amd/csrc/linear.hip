@@ -610,6 +610,28 @@ __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo
       acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);              \
     }                                                                                                         \
   }
+// The same products in two halves (A fragment rows [0, kP/2) then [kP/2, kP)) with MID between them.
+#define RQ_X3_MMA2(MID)                                                                                       \
+  {                                                                                                           \
+    bf16x8_t fa_h[kP], fa_l[kP], fb_h[kP], fb_l[kP];                                                          \
+    _Pragma("unroll") for (int p = 0; p < kP; ++p) {                                                          \
+      fb_h[p] = xfrag16<BKC, TS>(bh, wn * kWTile + 16 * p, lane);                                             \
+      fb_l[p] = xfrag16<BKC, TS>(bl, wn * kWTile + 16 * p, lane);                                             \
+    }                                                                                                         \
+    _Pragma("unroll") for (int h_ = 0; h_ < 2; ++h_) {                                                        \
+      _Pragma("unroll") for (int p = h_ * kP / 2; p < (h_ + 1) * kP / 2; ++p) {                               \
+        fa_h[p] = xfrag16<AKC, TS>(ah, wm * kWTile + 16 * p, lane);                                           \
+        fa_l[p] = xfrag16<AKC, TS>(al, wm * kWTile + 16 * p, lane);                                           \
+      }                                                                                                       \
+      _Pragma("unroll") for (int p = h_ * kP / 2; p < (h_ + 1) * kP / 2; ++p)                                 \
+      _Pragma("unroll") for (int q = 0; q < kP; ++q) {                                                        \
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_l[p], acc[p][q], 0, 0, 0);            \
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_l[q], fa_h[p], acc[p][q], 0, 0, 0);            \
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb_h[q], fa_h[p], acc[p][q], 0, 0, 0);            \
+      }                                                                                                       \
+      if (h_ == 0) { MID }                                                                                    \
+    }                                                                                                         \
+  }
 #else
 #define RQ_X3_MMA                                                                                             \
   _Pragma("unroll") for (int ks = 0; ks < kXK / 16; ++ks) {                                                   \
@@ -769,6 +791,16 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
     SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                \
     SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);                                                \
   }
+#elif RQ_X3_INTERLEAVE == 3   // A's staging store before the MFMAs, B's after
+#define RQ_X3_BODY(SA, SB)                                                                                    \
+  SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);                                                  \
+  if (on_) RQ_X3_MMA                                                                                          \
+  SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
+#elif RQ_X3_INTERLEAVE == 4   // the MFMAs in two halves, A's staging store between them, B's after
+#define RQ_X3_BODY(SA, SB)                                                                                    \
+  static_assert(RQ_X3_PEEL, "every slot multiplies");                                                         \
+  RQ_X3_MMA2(SA.store(plane(buf ^ 1, 0, 0), plane(buf ^ 1, 0, 1), tid);)                                      \
+  SB.store(plane(buf ^ 1, 1, 0), plane(buf ^ 1, 1, 1), tid);
 #else
 #define RQ_X3_BODY(SA, SB)                                                                                    \
   if (on_) {                                                                                                  \
@@ -824,6 +856,7 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
 #undef RQ_X3_STAGE
 #undef RQ_X3_BODY
 #undef RQ_X3_MMA
+#undef RQ_X3_MMA2
 
   // Each lane stores C[m][n .. n + 3] quads: 16-B fp32 / 8-B bf16 stores (N % 4 == 0).
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
@@ -1193,10 +1226,28 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 // x3_epi4 at (m, n) = (j / N, j % N). Lets every epilogue — SiLU fwd / bwd with dropout, residual
 // add, accumulation into an existing gradient — use split-K when the output tiles cannot fill the
 // chip (the decoder's 1,280 future-token rows: 40 tiles of 128 x 128).
+#ifndef RQ_SLAB_THREAD
+#define RQ_SLAB_THREAD 1   // 0: four waves over s per float4 column combined through LDS (the round-4 form)
+#endif
+constexpr int kRedColsPerWg = RQ_SLAB_THREAD ? 256 : 64;   // float4 columns per workgroup (layout 0)
+
 template <int EPI, bool DROP, bool ACC>
 __global__ void __launch_bounds__(256) x3_reduce_kernel(const float* __restrict__ P, int S, int64_t n, int N,
                                                         float* __restrict__ C, X3Epilogue ep) {
   ep.seed = epoch_seed(ep.seed);
+#if RQ_SLAB_THREAD   // one thread per float4 column, the same order (slab_sum_w4)
+  {
+    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (j >= n) return;
+    float4 r = slab_sum_w4(P, S, n, j);
+    if constexpr (ACC) {
+      const float4 c = *reinterpret_cast<const float4*>(C + j);
+      r = make_float4(c.x + r.x, c.y + r.y, c.z + r.z, c.w + r.w);
+    }
+    x3_epi4<EPI, DROP>(r, (int)(j / N), (int)(j % N), N, C, C, N, ep);
+    return;
+  }
+#endif
   __shared__ float4 part[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t j = ((int64_t)blockIdx.x * 64 + lane) * 4;
@@ -1709,7 +1760,7 @@ static int x3_post(const X3Call& c, int* splits, hipStream_t s) {
   }
   const int64_t n = c.M * c.N;
   const int N = (int)c.N;
-  const dim3 rg((unsigned)((n / 4 + 63) / 64)), rb(256);
+  const dim3 rg((unsigned)((n / 4 + kRedColsPerWg - 1) / kRedColsPerWg)), rb(256);
   const X3Epilogue& ep = c.xa.ep;
   const bool drop = ep.thr != 0 && c.epilogue != kEpiStore;
   float* out = c.out;
@@ -1910,7 +1961,16 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(RedSegTable t) {
   const int64_t n = t.n[e];
   const int S = t.S[e];
   const int tid = threadIdx.x;
-  if (t.layout[e] == 0) {
+  if (t.layout[e] == 0 && RQ_SLAB_THREAD) {   // one thread per float4 column (slab_sum_w4: the same order)
+    const int64_t j = ((int64_t)lb * 256 + tid) * 4;
+    if (j >= n) return;
+    float4 r = slab_sum_w4(P, S, n, j);
+    if (t.acc[e]) {
+      const float4 c = *reinterpret_cast<const float4*>(out + j);
+      r = make_float4(c.x + r.x, c.y + r.y, c.z + r.z, c.w + r.w);
+    }
+    *reinterpret_cast<float4*>(out + j) = r;
+  } else if (t.layout[e] == 0) {
     const int wave = tid >> 6, lane = tid & 63;
     const int64_t j = ((int64_t)lb * 64 + lane) * 4;
     const bool ok = j < n;
@@ -1980,7 +2040,7 @@ int rq_reduce_partials(int count, const float* const* P, float* const* out, cons
       t.layout[i] = layout[k];
       t.acc[i] = accumulate[k] != 0;
       t.blk0[i] = blk;
-      blk += (int)((n[k] / 4 + (layout[k] == 0 ? 63 : 3)) / (layout[k] == 0 ? 64 : 4));
+      blk += (int)((n[k] / 4 + (layout[k] == 0 ? kRedColsPerWg - 1 : 3)) / (layout[k] == 0 ? kRedColsPerWg : 4));
     }
     t.blk0[t.count] = blk;
     if (blk == 0) continue;

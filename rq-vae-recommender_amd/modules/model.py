@@ -150,10 +150,14 @@ class EncoderDecoderRetrievalModel(nn.Module):
     def _gemm_weights(self):
         return [m.weight for m in self.modules() if isinstance(m, nn.Linear)]
 
+    def _gemm_weight_stacks(self):
+        """Weights the forward multiplies as one concatenated matrix (the decoder's hoisted K/V)."""
+        return [st for st in (getattr(m, "hoisted_kv_weights", lambda: None)() for m in self.modules()) if st]
+
     def forward(self, batch: TokenizedSeqBatch) -> ModelOutput:
         B = batch.seq_mask.shape[0]
         # every Linear weight split once per forward in a few launches (no-op at 'highest')
-        with hip_ops.weight_split_scope(self._gemm_weights()):
+        with hip_ops.weight_split_scope(self._gemm_weights(), self._gemm_weight_stacks()):
             return self._forward(batch, B)
 
     def _forward(self, batch: TokenizedSeqBatch, B: int) -> ModelOutput:

@@ -175,6 +175,13 @@ class TransformerDecoder(nn.Module, KVCacheOpsMixin):
             h = layer._forward_jagged(h, ctx, is_causal, kvs[i] if kvs is not None else None)
         return h if isinstance(x, Jagged) else _wrap_like(h.values(), x)
 
+    def hoisted_kv_weights(self):
+        """The cross-attention K/V weights _hoisted_kv concatenates (for the forward's weight split), or None."""
+        if not (_HOIST_KV and self.do_cross_attn and len(self.layers) > 1):
+            return None
+        kvs = [layer.cross_attention.kv for layer in self.layers]
+        return None if any(m.bias is not None for m in kvs) else [m.weight for m in kvs]
+
     def _hoisted_kv(self, ctx: Optional[Jagged]):
         """Every layer's cross-attention `kv(context)` as one GEMM over the concatenated K/V weights
         (they all project the same encoder output): hip_ops.hoisted_projection — one launch instead of

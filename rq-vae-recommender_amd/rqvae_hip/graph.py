@@ -156,12 +156,26 @@ class GraphedSteps:
         return type(batch)(*items) if hasattr(batch, "_fields") else type(batch)(items)
 
     @staticmethod
-    def _copy(dst, src):
+    def _pairs(dst, src, out):
         if isinstance(dst, torch.Tensor):
-            dst.copy_(src, non_blocking=True)
+            out.append((dst, src))
         elif dst is not None:
             for d, s_ in zip(dst, src):
-                GraphedSteps._copy(d, s_)
+                GraphedSteps._pairs(d, s_, out)
+        return out
+
+    @staticmethod
+    def _copy(dst, src):
+        """The batch into the static inputs: one multi-tensor copy launch per dtype (torch's foreach copy
+        takes its single-launch route only for lists of one dtype) instead of one copy per field."""
+        groups = {}
+        for d, s_ in GraphedSteps._pairs(dst, src, []):
+            groups.setdefault((d.dtype, s_.dtype, d.device), []).append((d, s_))
+        for pairs in groups.values():
+            if len(pairs) == 1:
+                pairs[0][0].copy_(pairs[0][1], non_blocking=True)
+            else:
+                torch._foreach_copy_([d for d, _ in pairs], [s_ for _, s_ in pairs], non_blocking=True)
 
     def _copy_in(self, batch, sig):
         st = self.statics.get(sig)
@@ -178,7 +192,7 @@ class GraphedSteps:
             b.zero_grad()
         out = self.loss_fn(self.static)
         if self.run_backward:
-            out.backward()
+            out.backward(self._seed_grad(out))
             out = out.detach()
         ops.flush_reductions()    # deferred weight-grad reductions (their list lives only at capture)
         if exchange and b is not None:
@@ -279,9 +293,19 @@ class GraphedSteps:
             b.zero_grad()
         out = self.loss_fn(batch)
         if self.run_backward:
-            out.backward()
+            out.backward(self._seed_grad(out))
             out = out.detach()
         return out
+
+    def _seed_grad(self, out):
+        """d out / d out = 1 for a scalar loss, kept across steps (backward() would fill a fresh one: a
+        launch per step); None (autograd's own seed) for anything else."""
+        if out.dim() != 0:
+            return None
+        one = getattr(self, "_one", None)
+        if one is None or one.device != out.device or one.dtype != out.dtype:
+            one = self._one = torch.ones((), device=out.device, dtype=out.dtype)
+        return one
 
     def __call__(self, batch):
         sig = self._signature(batch)

@@ -287,16 +287,20 @@ def split_bf16x3(x: torch.Tensor) -> Split:
 _SPLIT_MULTI_MAX = 48   # rq_split_bf16x3_multi's tensor table
 
 
-def split_bf16x3_many(xs) -> list:
-    """split_bf16x3 of up to 48 tensors in one launch (rq_split_bf16x3_multi)."""
+def split_bf16x3_many(xs, outs=None) -> list:
+    """split_bf16x3 of up to 48 tensors in one launch (rq_split_bf16x3_multi); `outs`: per tensor a
+    contiguous Split of its shape to write (e.g. row blocks of one stacked pair of planes), or None."""
     import ctypes
     xs = [x.contiguous() for x in xs]
     if not xs:
         return []
     require_gpu(*xs, what="split_bf16x3_many")
     assert len(xs) <= _SPLIT_MULTI_MAX
-    out = [Split(torch.empty(x.shape, device=x.device, dtype=torch.bfloat16),
-                 torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)) for x in xs]
+    outs = outs or [None] * len(xs)
+    out = [o if o is not None else Split(torch.empty(x.shape, device=x.device, dtype=torch.bfloat16),
+                                         torch.empty(x.shape, device=x.device, dtype=torch.bfloat16))
+           for x, o in zip(xs, outs)]
+    assert all(o.hi.shape == x.shape and o.hi.is_contiguous() and o.lo.is_contiguous() for x, o in zip(xs, out))
     n = len(xs)
     P = ctypes.c_void_p * n
     call("rq_split_bf16x3_multi", n, P(*[x.data_ptr() for x in xs]), (ctypes.c_int64 * n)(*[x.numel() for x in xs]),
@@ -305,27 +309,58 @@ def split_bf16x3_many(xs) -> list:
 
 
 _WSPLIT = {}   # id(weight) -> (Split, weight): the current forward's pre-split weights (weight_split_scope)
+_WSTACK = {}   # ids of a weight stack -> (stacked Split, weights): their planes as row blocks of one pair
+
+
+def _splittable(p) -> bool:
+    return p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 and p.shape[0] % 8 == 0 and p.shape[1] % 8 == 0
 
 
 @contextlib.contextmanager
-def weight_split_scope(params):
+def weight_split_scope(params, stacks=()):
     """Split every GEMM weight among `params` (2-D fp32 device tensors, both dims % 8) once, in a few
     multi-tensor launches (rq_split_bf16x3_multi, 48 per launch), for the forward run inside the
     scope: the Linear / MLP ops take their split operand from here instead of one split launch per
-    weight per call (the decoder: ~32 -> 3 launches per step). Only at matmul precision 'high'."""
-    ws = [p for p in params if p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 and p.shape[0] % 8 == 0
-          and p.shape[1] % 8 == 0] if matmul_high() else []
-    prev = dict(_WSPLIT)
+    weight per call (the decoder: ~32 -> 3 launches per step). `stacks`: lists of equal-shape weights
+    whose planes are written as row blocks of one stacked pair (stacked_split: the hoisted cross-attention
+    K/V projection's concatenated weight, without a cat and a split launch of its own). Only at matmul
+    precision 'high'."""
+    ws = [p for p in params if _splittable(p)] if matmul_high() else []
+    prev, prev_st = dict(_WSPLIT), dict(_WSTACK)
+    dst = {}
     with torch.no_grad():
+        for st in (stacks if ws else ()):
+            st = list(st)
+            if not st or not all(_splittable(w) and w.shape == st[0].shape for w in st):
+                continue
+            O, I = st[0].shape
+            big = Split(torch.empty((len(st) * O, I), device=st[0].device, dtype=torch.bfloat16),
+                        torch.empty((len(st) * O, I), device=st[0].device, dtype=torch.bfloat16))
+            for j, w in enumerate(st):
+                dst[id(w)] = Split(big.hi[j * O:(j + 1) * O], big.lo[j * O:(j + 1) * O])
+            _WSTACK[tuple(id(w) for w in st)] = (big, st)
+        ids = {id(w) for w in ws}
+        ws = ws + [w for w in (w for st in stacks for w in st) if id(w) in dst and id(w) not in ids]
         for i in range(0, len(ws), _SPLIT_MULTI_MAX):
             chunk = ws[i:i + _SPLIT_MULTI_MAX]
-            for w, sp in zip(chunk, split_bf16x3_many([w.detach() for w in chunk])):
+            for w, sp in zip(chunk, split_bf16x3_many([w.detach() for w in chunk], [dst.get(id(w)) for w in chunk])):
                 _WSPLIT[id(w)] = (sp, w)
     try:
         yield
     finally:
         _WSPLIT.clear()
         _WSPLIT.update(prev)
+        _WSTACK.clear()
+        _WSTACK.update(prev_st)
+
+
+def stacked_split(weights) -> Split:
+    """The split planes of cat(weights, 0): the weight_split_scope's stacked pair when it registered this
+    stack, else a cat and one split launch."""
+    e = _WSTACK.get(tuple(id(w) for w in weights))
+    if e is not None and all(a is b for a, b in zip(e[1], weights)):
+        return e[0]
+    return split_bf16x3(torch.cat([w.detach() for w in weights], 0))
 
 
 def split_weight(w: torch.Tensor) -> Split:
@@ -453,7 +488,7 @@ class _X3Call(NamedTuple):
 
 def _x3_setup(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, epilogue: int = EPI_STORE,
               Z: torch.Tensor = None, p: float = 0.0, seed: int = 0, out: torch.Tensor = None,
-              accumulate: bool = False, defer: bool = False) -> _X3Call:
+              accumulate: bool = False, defer: bool = False, flags: int = None) -> _X3Call:
     def desc(t):
         if isinstance(t, Split):
             return t.hi, t.lo, t.hi.shape[-1], 1
@@ -474,7 +509,7 @@ def _x3_setup(a, a_kcontig: bool, b, b_kcontig: bool, M: int, N: int, K: int, ep
     if epilogue in (EPI_SILU_FWD, EPI_SILU_BWD):
         H = Split(torch.empty((M, N), device=dev, dtype=torch.bfloat16),
                   torch.empty((M, N), device=dev, dtype=torch.bfloat16))
-    flags = _GEMM_POLICY["flags"]
+    flags = _GEMM_POLICY["flags"] if flags is None else int(flags)   # per-call override (probes)
     nbytes = _x3_workspace(M, N, K)
     forced = (flags >> GEMM_SPLIT_SHIFT) & GEMM_SPLIT_MASK
     if forced > 1:   # a forced split count: its slabs (the library sizes only the planner's)
@@ -555,6 +590,45 @@ def gemm_x3_pair(spec1: dict, spec2: dict):
     return _x3_result(c1, splits[0]), _x3_result(c2, splits[1])
 
 
+_PAIR_RESPLIT = False  # False: a paired weight gradient keeps the split count it is planned with alone (A/B)
+_RESPLIT_CACHE = {}
+
+
+def _spec_key(sp: dict):
+    a, b = sp["a"], sp["b"]
+    return (int(sp["M"]), int(sp["N"]), int(sp["K"]), bool(sp["a_kcontig"]), bool(sp["b_kcontig"]),
+            isinstance(a, Split), isinstance(b, Split), int(sp.get("epilogue", EPI_STORE)))
+
+
+def _bwd_pair(dspec: dict, wspec: dict):
+    """gemm_x3_pair of a Linear's data gradient (dspec) and weight gradient (wspec) with the weight gradient's
+    split count chosen for the PAIR: where the data gradient alone leaves resident slots idle (128-tile
+    kernel, unsplit), the weight gradient's k chunks are sized like the data gradient's K (S = ceil(rows / K_d))
+    when that is fewer slabs than its own plan and the pair still spans more than one round of workgroups —
+    equal-length workgroups instead of a tail of short ones, and fewer slabs (measured on the paired launches of
+    the decoder's 11k-row qkv / MLP-up layers: 152 -> 127 and 93 -> 85 us, tools/pair_split_probe.py)."""
+    if _PAIR_RESPLIT and _GEMM_POLICY["flags"] == 0 and wspec.get("flags") is None and \
+            int(wspec.get("epilogue", EPI_STORE)) == EPI_STORE:
+        key = (_spec_key(dspec), _spec_key(wspec))
+        S = _RESPLIT_CACHE.get(key)
+        if S is None:
+            S = 0
+            kd, sd = gemm_x3_choice(*key[0][:3], key[0][5], key[0][6], key[0][3], key[0][4], key[0][7])
+            kw, sw = gemm_x3_choice(*key[1][:3], key[1][5], key[1][6], key[1][3], key[1][4], EPI_STORE)
+            if kd == "x3" and kw == "x3" and sd == 1 and sw > 1:
+                slots = 2 * torch.cuda.get_device_properties(dspec["a"].hi.device if isinstance(dspec["a"], Split)
+                                                             else dspec["a"].device).multi_processor_count
+                w1 = -(-int(dspec["M"]) // 128) * -(-int(dspec["N"]) // 128)
+                t2 = -(-int(wspec["M"]) // 128) * -(-int(wspec["N"]) // 128)
+                s_bal = -(-int(wspec["K"]) // int(dspec["K"]))
+                if w1 < slots and 1 < s_bal < sw and w1 + t2 * s_bal > slots:
+                    S = s_bal
+            _RESPLIT_CACHE[key] = S
+        if S:
+            wspec = dict(wspec, flags=gemm_split(S))
+    return gemm_x3_pair(dspec, wspec)
+
+
 # Deferred partial reductions (rq_reduce_partials): split-K weight-gradient slabs and RMSNorm weight-
 # gradient partials that accumulate into flat gradient buckets wait here and run as ONE launch (per 48)
 # at the next flush — before a bucket's exchange, in GradBuckets.finish / synchronize / zero_grad, and at
@@ -600,6 +674,25 @@ def _emb_grad(weight, g: torch.Tensor, keys: torch.Tensor, K: int, padding_idx):
             dp.direct_grad_done(weight)
             return None
     return _table_grad(g, keys, K, padding_idx)
+
+
+def _rows_grad(weight, rows: torch.Tensor, K: int):
+    """The gradient of a table whose first rows.shape[0] rows were each gathered once (keys 0..n-1): `rows`
+    itself — deferred as an add into the table's flat bucket prefix when its owner batches reductions
+    (returns None), else the (K, E) tensor. The segmented sum of such keys is each row alone, so this is
+    _emb_grad's result without the sort and sum."""
+    from . import dp
+    n, E = rows.shape
+    if weight is not None and dp.defer_ok(weight):
+        sink = dp.direct_grad(weight)
+        if sink is not None and sink.is_contiguous() and sink.data_ptr() % 16 == 0 and rows.is_contiguous() \
+                and rows.data_ptr() % 16 == 0 and (n * E) % 4 == 0 and sink.data_ptr() not in _DEFER["outs"]:
+            _defer_push(rows, sink, n * E, 1, 0)
+            dp.direct_grad_done(weight)
+            return None
+    out = rows.new_zeros((K, E))
+    out[:n] = rows
+    return out
 
 
 def _flush_embeddings() -> None:
@@ -735,7 +828,7 @@ def _mlp_backward(gcur, x_in, wsp, zs, hs, rows: int, p: float, seeds, need_w, n
             dspec = None
         wspec = _wgrad_spec(weights[i], gcur, False, inp, False, O, I, rows) if need_w[i] else None
         if dspec is not None and wspec is not None:   # dW = g^T h_{i-1} and the data grad in one launch
-            gnext, wres = gemm_x3_pair(dspec, wspec)
+            gnext, wres = _bwd_pair(dspec, wspec)
             dws[i] = _wgrad_result(weights[i], wspec, wres)
         else:
             if need_w[i]:
@@ -945,7 +1038,7 @@ class LinearFunction(torch.autograd.Function):
             wspec = _wgrad_spec(ctx.weight, g2.contiguous(), False, x.reshape(-1, I).contiguous(), False, O, I,
                                 g2.shape[0])
             if wspec is not None:   # data and weight gradient in one launch
-                gx, wres = gemm_x3_pair(dict(a=g2, a_kcontig=True, b=ctx.wsp, b_kcontig=False, M=g2.shape[0], N=I,
+                gx, wres = _bwd_pair(dict(a=g2, a_kcontig=True, b=ctx.wsp, b_kcontig=False, M=g2.shape[0], N=I,
                                              K=O), wspec)
                 dW = _wgrad_result(ctx.weight, wspec, wres)
                 ctx.wsp = ctx.weight = None
@@ -982,7 +1075,7 @@ def _linear_bwd_high(x, g, weight, wsp, need_x: bool, need_w: bool):
     if need_x and need_w:
         wspec = _wgrad_spec(weight, g2.contiguous(), False, x2.contiguous(), False, O, I, g2.shape[0])
         if wspec is not None:
-            gx, wres = gemm_x3_pair(dict(a=g2, a_kcontig=True, b=wsp, b_kcontig=False, M=g2.shape[0], N=I, K=O), wspec)
+            gx, wres = _bwd_pair(dict(a=g2, a_kcontig=True, b=wsp, b_kcontig=False, M=g2.shape[0], N=I, K=O), wspec)
             return gx.view(x.shape), _wgrad_result(weight, wspec, wres)
     gx = gemm_x3(g2, True, wsp, False, g2.shape[0], I, O).view(x.shape) if need_x else None
     dW = _wgrad_into(weight, g2.contiguous(), False, x2.contiguous(), False, O, I, g2.shape[0]) if need_w else None
@@ -1059,7 +1152,7 @@ class LinearAddFunction(torch.autograd.Function):
             wspec = _wgrad_spec(ctx.weight, g2.contiguous(), False, x.reshape(-1, I).contiguous(), False, O, I,
                                 g2.shape[0])
         if wspec is not None:   # data and weight gradient in one launch
-            gx, wres = gemm_x3_pair(dict(a=g2, a_kcontig=True, b=ctx.wsp, b_kcontig=False, M=g2.shape[0], N=I, K=O),
+            gx, wres = _bwd_pair(dict(a=g2, a_kcontig=True, b=ctx.wsp, b_kcontig=False, M=g2.shape[0], N=I, K=O),
                                     wspec)
             gx = gx.view(x.shape)
             dW = _wgrad_result(ctx.weight, wspec, wres)
@@ -1512,6 +1605,7 @@ class DecoderPrologueFunction(torch.autograd.Function):
         ctx.tables = tuple(w if isinstance(w, torch.nn.Parameter) else None for w in (user_w, sem_w, wpe_w, tte_w))
         ctx.rows = (user_w.shape[0], sem_w.shape[0], wpe_w.shape[0], tte_w.shape[0])
         ctx.mark_non_differentiable(ctx_off, fut_off)
+        ctx.set_materialize_grads(False)   # no zero-filled int64 "gradients" for the offsets (two launches)
         if order is not None:
             ctx_off._rq_lpt_order = order   # self-attention launches over these offsets reuse it (RQ_ATTN_ORDER_GIVEN)
         return ctx_vals, ctx_off, fut_vals, fut_off
@@ -1534,15 +1628,16 @@ class DecoderPrologueFunction(torch.autograd.Function):
         g_seq = g_pad[:, 1:]
         gu = _emb_grad(w_user, g_pad[:, :1].reshape(-1, E), uid_mod, k_user, None) if need[0] else None
         gw = None
-        if need[2]:   # the position table: batch sum, then its gather's backward over rows 0..N-1
-            gp = col_sum(g_seq).unsqueeze(0)
-            gw = _emb_grad(w_wpe, gp.reshape(-1, E), torch.arange(N, device=dev), k_wpe, None)
+        if need[2]:   # the position table: the batch sum of the sequence rows IS its gradient on rows 0..N-1
+            # (the gather over arange(N) hits each row once); the column sums of whole padded rows, user
+            # slot included, take the sequence rows' sums without a contiguous copy (same order per column)
+            gw = _rows_grad(w_wpe, col_sum(g_pad.view(B, (N + 1) * E)).view(N + 1, E)[1:], k_wpe)
         gs = None
         if need[1]:   # one segmented sum over the context and future rows (EmbeddingPairFunction's order)
             g = torch.cat([g_seq, g_futp[:, 1:]], dim=1).reshape(-1, E)
             gs = _emb_grad(w_sem, g, keys.reshape(-1), k_sem, pad)
         gt = _emb_grad(w_tte, g_futp[:, 1:].reshape(-1, E), type_fut.reshape(-1), k_tte, None) if need[3] else None
-        gb = col_sum(g_futp[:, :1]).view(E) if need[4] else None
+        gb = col_sum(g_futp.view(B, (L + 1) * E)).view(L + 1, E)[0] if need[4] else None
         return (gu, gs, gw, gt, gb) + (None,) * 10
 
 
@@ -2058,7 +2153,7 @@ class HoistedProjectionFunction(torch.autograd.Function):
     def forward(ctx, x, *weights):
         O, I = weights[0].shape
         T = x.shape[0]
-        wsp = split_bf16x3(torch.cat([w.detach() for w in weights], 0))
+        wsp = stacked_split(weights)
         # the shared input split once (4 B read + 4 B written per element): both uses — this forward
         # (T x n O x I) and the weight-gradient GEMM (its n-contiguous B) — then run on the wide LDS-DMA
         # kernel instead of splitting x while staging it
@@ -2090,7 +2185,7 @@ class HoistedProjectionFunction(torch.autograd.Function):
         dws = [None] * n
         if ctx.needs_input_grad[0] and any(ctx.needs_input_grad[1:]) and _pairing():
             # data gradient and the concatenated weight gradient in one launch
-            gx, dw = gemm_x3_pair(dict(a=g, a_kcontig=True, b=wsp, b_kcontig=False, M=T, N=I, K=n * O),
+            gx, dw = _bwd_pair(dict(a=g, a_kcontig=True, b=wsp, b_kcontig=False, M=T, N=I, K=n * O),
                                   dict(a=g, a_kcontig=False, b=xs, b_kcontig=False, M=n * O, N=I, K=T))
             dws = _wgrad_multi_into(weights, g, xs, n * O, I, T, dw=dw)
             return (gx, *dws)

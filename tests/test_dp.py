@@ -324,3 +324,24 @@ def test_all_gather_rows(world, n):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+def test_graphed_steps_copy_in_mixed_dtypes():
+    """GraphedSteps copies a nested batch into its static inputs with one foreach copy per dtype: every
+    field (int64, bool, fp32, a lone tensor of its dtype, None) lands exactly, shapes / storage unchanged."""
+    from collections import namedtuple
+    from rqvae_hip.graph import GraphedSteps
+    Batch = namedtuple("Batch", "a b mask x none nested")
+    g = torch.Generator().manual_seed(0)
+
+    def make():
+        return Batch(torch.randint(0, 100, (4, 5), generator=g), torch.randint(0, 9, (3,), generator=g),
+                     torch.rand(4, 5, generator=g) > 0.5, torch.randn(2, 3, generator=g), None,
+                     (torch.randint(0, 7, (6,), generator=g), torch.randn(5, generator=g)))
+    static, src = make(), make()
+    ptrs = [t.data_ptr() for t in (static.a, static.b, static.mask, static.x, *static.nested)]
+    GraphedSteps._copy(static, src)
+    for d, s_ in ((static.a, src.a), (static.b, src.b), (static.mask, src.mask), (static.x, src.x),
+                  (static.nested[0], src.nested[0]), (static.nested[1], src.nested[1])):
+        assert torch.equal(d, s_) and d.dtype == s_.dtype
+    assert ptrs == [t.data_ptr() for t in (static.a, static.b, static.mask, static.x, *static.nested)]

@@ -102,3 +102,59 @@ def test_accumulate_into_existing(device, M, N, K):
     ref = c0.double() + A @ B.t()
     bound = 3e-5 * (A.abs() @ B.abs().t()) + 1e-5
     assert ((c.double() - ref).abs() <= bound).all()
+
+
+def _emulated_slab_sum(P, S):
+    """The split-K reductions' defined order on torch fp32 adds: p_w = 0 + P[w] + P[w + 4] + ..., then
+    ((p0 + p1) + p2) + p3."""
+    p = [torch.zeros_like(P[0]) for _ in range(4)]
+    for s in range(S):
+        p[s % 4] = p[s % 4] + P[s]
+    return ((p[0] + p[1]) + p[2]) + p[3]
+
+
+@pytest.mark.parametrize("S,n", [(1, 64), (3, 4096), (4, 1000), (7, 4100), (16, 2048), (21, 6000), (40, 512)])
+def test_reduce_partials_order(device, S, n):
+    """rq_reduce_partials layout 0 (and with accumulate) is bitwise the defined four-way order, for S below,
+    at and past one 16-load round and n not a multiple of a workgroup's columns."""
+    import ctypes
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(S * 131 + n)
+    P = torch.randn(S, n, generator=g, device=device) * torch.logspace(-3, 3, n, device=device)
+    for acc in (0, 1):
+        out = torch.randn(n, generator=g, device=device)
+        ref = _emulated_slab_sum(P, S)
+        ref = out + ref if acc else ref
+        Pp = (ctypes.c_void_p * 1)(P.data_ptr())
+        Op = (ctypes.c_void_p * 1)(out.data_ptr())
+        ops.call("rq_reduce_partials", 1, Pp, Op, (ctypes.c_int64 * 1)(n), (ctypes.c_int * 1)(S), (ctypes.c_int * 1)(0),
+                 (ctypes.c_int * 1)(acc), ops.stream_handle(device))
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (S, n, acc)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(40, 512, 512, 8), (40, 1536, 384, 12), (1280, 512, 1024, 4), (96, 256, 2048, 21)])
+def test_splitk_reduction_order(device, M, N, K, S):
+    """A forced-split GEMM's immediate slab reduction (x3_reduce_kernel, accumulate) equals its deferred slabs
+    summed in the defined order, and the deferred batched reduction gives the same bits."""
+    from rqvae_hip import ops
+    g = torch.Generator(device=device).manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g, device=device)
+    b = ops.split_bf16x3(torch.randn(N, K, generator=g, device=device) * 0.05)
+    base = torch.randn(M, N, generator=g, device=device)
+    f = ops.gemm_split(S)
+    out_imm = base.clone()
+    with ops.gemm_policy(f):
+        ops.gemm_x3(a, True, b, True, M, N, K, out=out_imm, accumulate=True)
+        out_def = base.clone()
+        ops.flush_reductions()
+        ops.gemm_x3(a, True, b, True, M, N, K, out=out_def, accumulate=True, defer=True)
+        pend = list(ops._DEFER["pending"])
+        assert len(pend) == 1 and pend[0][3] > 1   # the forced count, rounded to whole 32-deep chunks
+        ws, _, n, S_, _, _ = pend[0]
+        slabs = ws.view(torch.float32)[:S_ * n].view(S_, n).clone()
+        ops.flush_reductions()
+    torch.cuda.synchronize()
+    ref = base.reshape(-1) + _emulated_slab_sum(slabs, S_)
+    assert torch.equal(out_imm.reshape(-1), ref)
+    assert torch.equal(out_def, out_imm)
