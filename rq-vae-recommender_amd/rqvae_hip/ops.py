@@ -590,7 +590,7 @@ def gemm_x3_pair(spec1: dict, spec2: dict):
     return _x3_result(c1, splits[0]), _x3_result(c2, splits[1])
 
 
-_PAIR_RESPLIT = False  # False: a paired weight gradient keeps the split count it is planned with alone (A/B)
+_PAIR_RESPLIT = True   # False: a paired weight gradient keeps the split count it is planned with alone (A/B)
 _RESPLIT_CACHE = {}
 
 
