@@ -572,14 +572,26 @@ __global__ void __launch_bounds__(256) ce_rows_kernel(const float* __restrict__ 
 
 // loss = (sum_b sum_j u[b][j]) / B, loss_d[j] = (sum_b u[b][j]) / B: one 256-thread workgroup; per-b row
 // sums in order, then a fixed LDS tree; per-position sums sequential over b (deterministic).
+constexpr int kCeStage = 8192;   // u values (B x npos) staged in LDS by the means kernel
 __global__ void __launch_bounds__(256) ce_means_kernel(const float* __restrict__ u, int B, int npos,
                                                        float* __restrict__ loss, float* __restrict__ loss_d) {
   __shared__ float red[256];
+  __shared__ float us[kCeStage];
   const int t = threadIdx.x;
+  // the per-position means walk b serially (fixed order); with u in LDS (one coalesced pass by the whole
+  // workgroup) those walks read LDS instead of issuing B dependent-order global loads per position (Amazon's
+  // 256 x 4 values: 16.5 -> a few us). Same order, same bits.
+  const int64_t nu = (int64_t)B * npos;
+  const bool staged = nu <= kCeStage;
+  if (staged) {
+    for (int64_t i = t; i < nu; i += 256) us[i] = u[i];
+    __syncthreads();
+  }
+  const float* __restrict__ src = staged ? us : u;
   float a = 0.f;
   for (int b = t; b < B; b += 256) {
     float sb = 0.f;
-    for (int j = 0; j < npos; ++j) sb += u[(int64_t)b * npos + j];
+    for (int j = 0; j < npos; ++j) sb += src[(int64_t)b * npos + j];
     a += sb;
   }
   red[t] = a;
@@ -591,7 +603,7 @@ __global__ void __launch_bounds__(256) ce_means_kernel(const float* __restrict__
   if (t == 0) loss[0] = red[0] / (float)B;
   for (int j = t; j < npos; j += 256) {
     float c = 0.f;
-    for (int b = 0; b < B; ++b) c += u[(int64_t)b * npos + j];
+    for (int b = 0; b < B; ++b) c += src[(int64_t)b * npos + j];
     loss_d[j] = c / (float)B;
   }
 }

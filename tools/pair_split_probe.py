@@ -3,7 +3,7 @@ weight gradient's split-K count forced (RQ_GEMM_SPLIT per descriptor), its defer
 inside the timed graph: does a pair want fewer weight-gradient slabs than the call planned alone? One JSON
 line per (shape, S).
 
-  python tools/pair_split_probe.py [future]
+  python tools/pair_split_probe.py [future | hoisted]
 """
 import json
 import os
@@ -44,6 +44,8 @@ def main():
     # (rows, O, I, data-grad A split?): Amazon qkv / MLP up / MLP down / proj; C4 context qkv / up
     shapes = [(11332, 1536, 512, False), (11332, 1024, 512, True), (11332, 512, 1024, False), (11332, 512, 512, False),
               (3200, 1152, 384, False), (3200, 1024, 384, True)]
+    if len(sys.argv) > 1 and sys.argv[1] == "hoisted":   # the decoder's hoisted cross-attention K/V backward
+        shapes = [(11332, 4096, 512, False), (3200, 3072, 384, False)]
     if len(sys.argv) > 1 and sys.argv[1] == "future":   # the future-token rows: Amazon 1,280, C4 40
         shapes = [(1280, 1536, 512, False), (1280, 512, 512, False), (1280, 1024, 512, True), (1280, 512, 1024, False),
                   (40, 1152, 384, False), (40, 384, 384, False), (40, 1024, 384, True), (40, 384, 1024, False)]
@@ -54,7 +56,8 @@ def main():
         W = ops.split_bf16x3(torch.randn(O, I, generator=gen, device=dev) * 0.05)
         dW = torch.zeros(O, I, device=dev)
         _, s_auto = ops.gemm_x3_choice(O, I, R, gsplit, False, False, False)
-        for S in [0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32]:
+        for S in ([0, 1, 2, 3, 4, 5, 6, 8] if len(sys.argv) > 1 and sys.argv[1] == "hoisted" else
+                  [0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32]):
             f = ops.gemm_split(S) if S else None
 
             def fn():
