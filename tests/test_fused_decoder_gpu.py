@@ -316,6 +316,10 @@ def test_decoder_prologue_equals_composition(device, monkeypatch, buckets, B, ma
     assert torch.equal(fo, torch.arange(B + 1, device=device) * (batch.sem_ids_fut.shape[1] + 1))
     assert torch.count_nonzero(cv[int(co[-1]):]) == 0
     assert row_counts(batch.seq_mask)[0] + B == int(co[-1])
+    # the longest-first order handed to the attention launches: length descending, ties by index
+    ln = lens.tolist()
+    want = sorted(range(B), key=lambda b: (-ln[b], b))
+    assert co._rq_lpt_order[:B].tolist() == want
 
 
 @pytest.mark.parametrize("M,I,O1,O2", [(40, 384, 1152, 384), (1280, 512, 1536, 512), (300, 64, 192, 64)])
