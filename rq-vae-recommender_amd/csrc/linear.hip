@@ -1295,31 +1295,49 @@ __global__ void __launch_bounds__(256) split_bf16x3_kernel(const float* __restri
 
 // Several tensors at once (all weights of an MLP chain: one launch instead of one per weight).
 constexpr int kSplitMax = 48;   // a decoder's every GEMM weight in one launch (kernel arguments ~1.6 KB)
+constexpr int kSplitPer = 4;    // units (float4 / scalars) per thread: one workgroup = 1,024 units of ONE tensor
 struct SplitMulti {
   const float* x[kSplitMax];
   uint16_t* hi[kSplitMax];
   uint16_t* lo[kSplitMax];
-  int64_t start[kSplitMax + 1];   // prefix sums of the element counts
+  int64_t n[kSplitMax];           // units per tensor
+  int blk0[kSplitMax + 1];        // prefix sums of the workgroups per tensor
   int count;
 };
 
-// VEC: every tensor's element count % 4 == 0 and its pointers aligned (16 B x, 8 B planes): one float4
-// and two 8-B plane stores per thread per iteration (start[] then counts float4 units); else scalar.
+// VEC: every tensor's element count % 4 == 0 and its pointers aligned (16 B x, 8 B planes): float4 units
+// with two 8-B plane stores each; else scalar units. Each workgroup owns 1,024 consecutive units of one
+// tensor, found by a uniform scan of blk0 (scalar kernel-argument loads: the per-thread binary search it
+// replaces indexed the argument block per lane, one dependent search per float4 — 2.6 TB/s on the
+// decoder's weights), and keeps its thread's 4 loads in flight.
 template <bool VEC>
 __global__ void __launch_bounds__(256) split_bf16x3_multi_kernel(SplitMulti sm) {
-  const int64_t total = sm.start[sm.count];
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    int lo_t = 0, hi_t = sm.count - 1;   // the tensor holding i: start[t] <= i < start[t + 1]
-    while (lo_t < hi_t) {
-      const int mid = (lo_t + hi_t + 1) >> 1;
-      if (i >= sm.start[mid]) lo_t = mid; else hi_t = mid - 1;
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < sm.count && b >= sm.blk0[t + 1]) ++t;
+  const int64_t n = sm.n[t];
+  const int64_t j0 = (int64_t)(b - sm.blk0[t]) * (256 * kSplitPer) + threadIdx.x;
+  const float* __restrict__ x = sm.x[t];
+  uint16_t* __restrict__ hi = sm.hi[t];
+  uint16_t* __restrict__ lo = sm.lo[t];
+  if constexpr (VEC) {
+    float4 v[kSplitPer];
+#pragma unroll
+    for (int u = 0; u < kSplitPer; ++u) {
+      const int64_t j = j0 + 256 * u;
+      if (j < n) v[u] = reinterpret_cast<const float4*>(x)[j];
     }
-    const int t = lo_t;
-    const int64_t j = i - sm.start[t];
-    if constexpr (VEC)
-      split_store4(reinterpret_cast<const float4*>(sm.x[t])[j], sm.hi[t] + 4 * j, sm.lo[t] + 4 * j);
-    else
-      split_store1(sm.x[t][j], sm.hi[t] + j, sm.lo[t] + j);
+#pragma unroll
+    for (int u = 0; u < kSplitPer; ++u) {
+      const int64_t j = j0 + 256 * u;
+      if (j < n) split_store4(v[u], hi + 4 * j, lo + 4 * j);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kSplitPer; ++u) {
+      const int64_t j = j0 + 256 * u;
+      if (j < n) split_store1(x[j], hi + j, lo + j);
+    }
   }
 }
 
@@ -2076,21 +2094,24 @@ int rq_split_bf16x3_multi(int count, const float* const* x, const int64_t* n, ui
                "rq_split_bf16x3_multi: 0 <= count <= %d tensors", kSplitMax);
   SplitMulti sm;
   sm.count = count;
-  sm.start[0] = 0;
+  sm.blk0[0] = 0;
   bool vec = true;
   for (int t = 0; t < count; ++t) {
     RQ_CHECK_ARG(n[t] >= 0 && (n[t] == 0 || (x[t] && hi[t] && lo[t])), "rq_split_bf16x3_multi: bad tensor %d", t);
     vec = vec && n[t] % 4 == 0 && (uintptr_t)x[t] % 16 == 0 && ((uintptr_t)hi[t] | (uintptr_t)lo[t]) % 8 == 0;
   }
+  int64_t blocks = 0;
   for (int t = 0; t < count; ++t) {
     sm.x[t] = x[t];
     sm.hi[t] = hi[t];
     sm.lo[t] = lo[t];
-    sm.start[t + 1] = sm.start[t] + (vec ? n[t] / 4 : n[t]);
+    sm.n[t] = vec ? n[t] / 4 : n[t];
+    blocks += (sm.n[t] + 256 * kSplitPer - 1) / (256 * kSplitPer);
+    RQ_CHECK_ARG(blocks < (1ll << 31), "rq_split_bf16x3_multi: too many elements");
+    sm.blk0[t + 1] = (int)blocks;
   }
-  if (count == 0 || sm.start[count] == 0) return 0;
-  const int64_t blocks = (sm.start[count] + 255) / 256;
-  const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
+  if (count == 0 || blocks == 0) return 0;
+  const dim3 grid((unsigned)blocks);
   if (vec)
     hipLaunchKernelGGL((split_bf16x3_multi_kernel<true>), grid, dim3(256), 0, (hipStream_t)stream, sm);
   else

@@ -317,7 +317,7 @@ def test_linear_add_epilogue_matches_fp64(device):
     assert close(y, yd) and close(x.grad, xd.grad) and close(W.grad, Wd.grad) and close(r.grad, rd.grad)
 
 
-@pytest.mark.parametrize("shapes", [((512, 768), (3,), (256, 512), (1, 7)),             # scalar path
+@pytest.mark.parametrize("shapes", [((512, 768), (3,), (0, 16), (256, 512), (1, 7)),   # scalar path, an empty one
                                     ((512, 768), (1024, 512), (8, 8), (64,), (1536, 512)),   # float4 path
                                     tuple((8 * (i % 7 + 1), 16 * (i % 5 + 1)) for i in range(48))])  # full table
 def test_split_many_matches_single(device, shapes):
