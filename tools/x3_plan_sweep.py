@@ -25,12 +25,12 @@ def record(step, ops):
     orig = ops._x3_setup
 
     def rec(a, a_kcontig, b, b_kcontig, M, N, K, epilogue=0, Z=None, p=0.0, seed=0, out=None, accumulate=False,
-            defer=False):
+            defer=False, flags=None):
         key = (int(M), int(N), int(K), bool(a_kcontig), bool(b_kcontig), isinstance(a, ops.Split),
                isinstance(b, ops.Split), int(epilogue), bool(accumulate))
         r = recs.setdefault(key, {"calls": 0, "p": float(p), "defer": bool(defer)})
         r["calls"] += 1
-        return orig(a, a_kcontig, b, b_kcontig, M, N, K, epilogue, Z, p, seed, out, accumulate, defer)
+        return orig(a, a_kcontig, b, b_kcontig, M, N, K, epilogue, Z, p, seed, out, accumulate, defer, flags)
 
     ops._x3_setup = rec
     try:
