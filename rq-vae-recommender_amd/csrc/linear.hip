@@ -1469,11 +1469,30 @@ static X3Plan x3_plan_t(int64_t M, int64_t N, int64_t K, bool allow_split, int t
 // 128-tile kernel, or its 64-tile form where the time model prefers it (the 128-tiles of a
 // 1,280-row operand are 40 workgroups: split-K slabs and their reduction cost more than the GEMM).
 // flags (the call's rq_gemm_desc.flags): RQ_GEMM_ONLY_128 / RQ_GEMM_ONLY_64 pin one tile size.
-static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, int flags, bool allow_split = true) {
+#ifndef RQ_X3_SHORTK_64
+#define RQ_X3_SHORTK_64 1   // 0: the time model picks the tile size for K <= 128 too
+#endif
+#ifndef RQ_X3_SKINNY_UNSPLIT
+#define RQ_X3_SKINNY_UNSPLIT 1   // 0: the time model decides split-K for one-row-of-tiles, short-K calls too
+#endif
+
+static X3Plan x3_plan(int64_t M, int64_t N, int64_t K, int flags, bool allow_split = true, int epilogue = 0) {
+  // One row of 64-tiles (the C4 decoder's 40 future-token rows) over K <= 384 with a plain or residual
+  // epilogue: unsplit. Measured per call (profiles/r05/plan_sweep2/sweep_c4.jsonl, hipGraph of 10 calls with
+  // their reductions): 6.7-7.2 us unsplit vs 7.1-7.3 at the model's S = 6 plus a reduction launch per call
+  // — the model underprices the short-K workgroups' fixed latency; the SiLU epilogues keep the model's split.
+  if (RQ_X3_SKINNY_UNSPLIT && !(flags & (RQ_GEMM_ONLY_128 | RQ_GEMM_ONLY_64)) && M <= 64 && K <= 384 &&
+      (epilogue == kEpiStore || epilogue == kEpiAdd))
+    allow_split = false;
   const X3Plan p = x3_plan_t(M, N, K, allow_split, kXT);
   if (flags & RQ_GEMM_ONLY_128) return p;
   const X3Plan q = x3_plan_t(M, N, K, allow_split, 64);
   if (flags & RQ_GEMM_ONLY_64) return q;
+  // K <= 128 (at most four 32-deep stages): the 64-tile form, whose 4 resident workgroups per CU hide the
+  // per-workgroup prologue / epilogue latency that such short k loops cannot — measured faster than the
+  // 128-tile kernel for every short-K call of the three bench steps (plan_sweep2: RQ-VAE 65,536 x 128 x 64
+  // SiLU' epilogue 27.6 -> 20.6 us, SiLU 23.4 -> 22.0; Amazon 11,520 x 512 x 128 14.6 -> 13.8)
+  if (RQ_X3_SHORTK_64 && K <= 128) return q;
   return x3_plan_time(q, M, N, false) < x3_plan_time(p, M, N, false) ? q : p;
 }
 
@@ -1632,7 +1651,7 @@ static int x3_prepare(const rq_gemm_desc& d, hipStream_t s, X3Call* c, bool dry 
     return 0;
   }
   const int flags = d.flags;
-  X3Plan pl = x3_plan(M, N, K, flags);
+  X3Plan pl = x3_plan(M, N, K, flags, true, epilogue);
   X3Plan pw;
   const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, flags, &pw);
   if (wide) pl = pw;
