@@ -2334,7 +2334,10 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_fewq_kernel(
 // + the transpose per tile pair; keys are read once. delta = rowsum(dO * O) per query comes in by lane
 // shuffles from the lanes that computed it (lane & 15 = query).
 template <int NW>
-__global__ void __launch_bounds__(64 * NW) attn_bwd_fewq_fused_kernel(
+#ifndef RQ_FEWQ_BWD_MINWG
+#define RQ_FEWQ_BWD_MINWG 1   // workgroups per CU the 4-wave few-query backward is compiled for (register budget)
+#endif
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? RQ_FEWQ_BWD_MINWG : 1) attn_bwd_fewq_fused_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
     int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
     const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
