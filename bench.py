@@ -67,7 +67,9 @@ def make_adamw(params, lr, wd):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Without torchrun env and N > 1, bench.py starts torch.distributed.run "
+                         "with N processes itself and exits with its status; under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="items per GPU per step")
@@ -240,13 +242,64 @@ def cpu_baseline(budget_s, B=2048):
                        f"ML-32M dims, {dt:.1f} s on {threads} host threads")
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(n, argv, port):
+    """The torch.distributed.run command that starts `n` ranks of this script on one node (the driver's
+    own form: --nnodes=1, 127.0.0.1 rendezvous), forwarding `argv` unchanged (it carries --gpus n)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` outside torchrun: start N fresh rank processes (one per GPU) as CHILDREN
+    of this process, which never touches the GPU itself (no exec: the box forbids replacing a process that
+    initialised the GPU). Rank 0's JSON line reaches stdout directly; torchrun's exit status — nonzero when
+    any rank dies — is returned."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC: RCCL / tensor sharing across ranks
+    return subprocess.run(launcher_cmd(n, argv, _free_port()), env=env).returncode
+
+
+def rank_census(device, ws):
+    """What the process group really spans: its size and backend, the number of ranks one all-reduce of
+    ones over it counts (RCCL's own count with the nccl backend), and each rank's device (index, PCI bus
+    id), gathered on every rank. Runs once, outside the timed region."""
+    props = torch.cuda.get_device_properties(device)
+    mine = {"device": device.index, "pci_bus_id": getattr(props, "pci_bus_id", None),
+            "name": props.name, "share_device": os.environ.get("RQVAE_SHARE_DEVICE", "0") == "1"}
+    if ws == 1:
+        return {"process_group_size": 1, "backend": None, "allreduce_rank_count": 1, "devices": [mine]}
+    one = torch.ones(1, device=device)
+    dist.all_reduce(one)
+    devs = [None] * ws
+    dist.all_gather_object(devs, mine)
+    return {"process_group_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "allreduce_rank_count": int(one.item()), "devices": devs,
+            "distinct_devices": len({(d["device"], d["pci_bus_id"]) for d in devs})}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     from rqvae_hip import dp, ops
     from data.schemas import SeqBatch
     rk, ws, lr = dp.init_from_env()
+    if args.gpus is not None and args.gpus != ws:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {ws} rank(s) (WORLD_SIZE)")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs an MI355X (no GPU visible)")
+    if os.environ.get("RQVAE_BENCH_FAIL_RANK") == str(rk):   # test hook: a rank that dies after init
+        raise RuntimeError(f"RQVAE_BENCH_FAIL_RANK: rank {rk} exits on purpose")
     if not args.no_tunable:
         # library GEMMs (fwd / data-grad) dispatched to the fastest measured hipBLASLt/rocBLAS
         # solution per shape; shapes missing from the shipped table are tuned in the warmup
@@ -260,6 +313,7 @@ def main():
         return
     device = torch.device("cuda", lr)
     torch.cuda.set_device(device)
+    census = rank_census(device, ws)
     B = args.batch
 
     model = build_model(device)
@@ -424,6 +478,7 @@ def main():
         "config": {"workload": "RQ-VAE MovieLens-32M train step (configs[1]): 768->[512,256,128]->D64, K256, L3, "
                                "ROTATION_TRICK, AdamW", "global_batch": ws * B, "per_gpu_batch": B,
                    "parallelism": f"dp{ws}"},
+        "rccl_ranks": census,
         "roofline": roof,
         "step_roofline": step_roof,
         "loss_last": round(loss, 5),
@@ -917,7 +972,7 @@ def decoder_kernel_stats(m, buckets, batch, ctx_lens, cfg, reps=3):
         m(batch).loss.backward()
     torch.cuda.synchronize()
     ops.TIMER.reset()
-    ops.TIMER.only = {"jagged_", "varlen_attn"}
+    ops.TIMER.only = {"jagged_", "varlen_attn", "dec_prologue"}
     ops.TIMER.enabled = True
     for _ in range(reps):
         buckets.zero_grad()
@@ -941,10 +996,41 @@ def decoder_kernel_stats(m, buckets, batch, ctx_lens, cfg, reps=3):
                                  "calls; bwd = 2 x fwd) / device time of the varlen_attn launches; GBps / "
                                  "frac_hbm_peak: algorithmic bytes (fwd q, k, v read + o written; bwd q, k, v, o, "
                                  "dO read + dq, dk, dv written, fp32, once each) over the same device time"},
-           "jagged_gather_GBps": round(ops.TIMER.gbps("jagged_from_padded"), 1),
-           "jagged_scatter_GBps": round(ops.TIMER.gbps("jagged_to_padded"), 1),
-           "jagged_hbm_frac": round(ops.TIMER.gbps("jagged_from_padded") / HBM_PEAK_GBS, 4)}
+           "jagged": jagged_stats(ops.TIMER, n, cfg, reps)}
     return res
+
+
+def jagged_stats(timer, n, cfg, reps):
+    """The decoder step's padded <-> jagged conversions. The step no longer runs the standalone
+    gather: the fused prologue (rq_dec_prologue_fwd, offsets + values launches) writes the jagged context
+    itself, and its backward scatters the context gradient with jagged_to_padded. Algorithmic bytes as C3 —
+    gather 2 * 4 E sum(n) (valid rows read + written), scatter 4 E (B (N + 1) + sum(n)) — plus the prologue's
+    own traffic (per context / future row: a sem-table row and a position / type row read, the row written,
+    12 E bytes) beside it, over the HIP-event device time of those launches."""
+    E, B = cfg["E"], len(n)
+    T, N1 = float(n.sum()), cfg["max_items"] * cfg["sem_id_dim"] + 1
+    nf = cfg["sem_id_dim"] + 1
+    p_ms, p_n = timer.mean_ms("dec_prologue")
+    s_ms, s_n = timer.mean_ms("jagged_to_padded")
+    out = {}
+    if p_n:
+        g_bytes, own = 2.0 * 4 * E * T, 12.0 * E * (T + B * nf)
+        out["prologue_fwd"] = {"launch_ms": round(p_ms, 4), "per_step": p_n // reps,
+                               "gather_equiv_bytes": round(g_bytes), "own_bytes": round(own),
+                               "gather_equiv_GBps": round(g_bytes / (p_ms * 1e-3) / 1e9, 1),
+                               "own_GBps": round(own / (p_ms * 1e-3) / 1e9, 1),
+                               "hbm_frac": round(own / (p_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if s_n:
+        s_bytes = 4.0 * E * (B * N1 + T)
+        out["scatter_bwd"] = {"launch_ms": round(s_ms, 4), "per_step": s_n // reps, "bytes": round(s_bytes),
+                              "GBps": round(s_bytes / (s_ms * 1e-3) / 1e9, 1),
+                              "hbm_frac": round(s_bytes / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    for k, name in (("gather_standalone", "jagged_from_padded"),):
+        if timer.events.get(name):   # composition path only (prologue off): the standalone gather
+            out[k] = {"GBps": round(timer.gbps(name), 1), "hbm_frac": round(timer.gbps(name) / HBM_PEAK_GBS, 4)}
+    out["note"] = ("the decoder's per-step context is ~11 k rows x 128 fp32 (~6 MB): these launches are latency-bound; "
+                   "the same kernels at HBM scale are bench jagged_c5 / jagged_c5_rank")
+    return out
 
 
 if __name__ == "__main__":

@@ -110,10 +110,18 @@ __global__ void __launch_bounds__(256) jagged_gather_kernel(const T* __restrict_
 // bitwise the composition (gathers, one fp32 add, the +1-1), in two launches instead of ~24.
 // Also writes the table rows the backward's segmented sums key on: keys (B, N + L) = the context's
 // sem-table rows (pad where masked) then the future's, and uid mod nb (B).
+// 1 in each byte of w that is nonzero, 0 elsewhere (bit 0 of byte k = OR of its bits 0..7)
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t w) {
+  w |= w >> 4;
+  w |= w >> 2;
+  w |= w >> 1;
+  return w & 0x01010101u;
+}
 constexpr int kDecLensLds = 4096;   // sequences whose lengths the offsets kernel keeps in LDS
 constexpr int kDecMaskLds = 24576;  // mask bytes (B x N) the offsets kernel stages in LDS
-__global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* __restrict__ mask, int64_t B, int64_t N,
-                                                                    int64_t nf, int64_t* __restrict__ off_ctx,
+__global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const unsigned char* __restrict__ mask, int64_t B, int64_t N,
+                                                                    int64_t nf, int64_t alloc_rows,
+                                                                    int64_t* __restrict__ off_ctx,
                                                                     int64_t* __restrict__ off_fut, int* __restrict__ order) {
   __shared__ int64_t part[1024];
   __shared__ int64_t lens[kDecLensLds];
@@ -128,8 +136,11 @@ __global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* 
   const bool staged = in_lds && nbytes <= kDecMaskLds && ((uintptr_t)mask & 15) == 0;
   if (staged) {
     const int64_t n16 = nbytes >> 4;
-    for (int64_t i = t; i < n16; i += 1024)
-      *reinterpret_cast<uint4*>(mask_s + 16 * i) = reinterpret_cast<const uint4*>(mask)[i];
+    for (int64_t i = t; i < n16; i += 1024) {   // bytes normalised to 0 / 1 (a bool tensor viewed from uint8 may
+      uint4 v = reinterpret_cast<const uint4*>(mask)[i];   // hold any nonzero byte; the byte sums below need 0 / 1)
+      v.x = nz_bytes(v.x), v.y = nz_bytes(v.y), v.z = nz_bytes(v.z), v.w = nz_bytes(v.w);
+      *reinterpret_cast<uint4*>(mask_s + 16 * i) = v;
+    }
     for (int64_t i = 16 * n16 + t; i < nbytes; i += 1024) mask_s[i] = mask[i] ? 1 : 0;
     __syncthreads();
   }
@@ -180,9 +191,9 @@ __global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* 
   }
   int64_t run = part[t] - s;
   if (t == 0) off_ctx[0] = 0;
-  for (int64_t i = a; i < e; ++i) {
-    run += len_of(i);
-    off_ctx[i + 1] = run;
+  for (int64_t i = a; i < e; ++i) {   // clamped to the allocation: host row counts that undercount the mask
+    run += len_of(i);                   // (stale registration) shorten the last sequences instead of sending
+    off_ctx[i + 1] = run < alloc_rows ? run : alloc_rows;   // every consumer past the values
   }
   for (int64_t i = t; i <= B; i += 1024) off_fut[i] = i * nf;
   // longest-first order of the contexts (attention.hip attn_order_kernel's ranking: length descending,
@@ -231,7 +242,7 @@ __global__ void __launch_bounds__(1024) dec_prologue_offsets_kernel(const bool* 
 
 struct DecPrologueArgs {
   const int64_t *uid, *sem, *typ, *sem_fut, *typ_fut;
-  const bool* mask;
+  const unsigned char* mask;   // the bool mask's bytes: any nonzero byte is true
   const float *w_user, *w_sem, *w_wpe, *w_tte, *bos;
   int64_t n_buckets, K, pad, n_sem_rows, n_wpe_rows, n_tte_rows;
   int64_t B, N, L, E;
@@ -406,9 +417,11 @@ int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const i
                "rq_dec_prologue_fwd: bad shape (E %% 4 == 0, wpe rows >= N, 2 B + 1 < 65535)");
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(dec_prologue_offsets_kernel, dim3(1), dim3(1024), 0, s, seq_mask, B, N, L + 1, ctx_offsets,
+  hipLaunchKernelGGL(dec_prologue_offsets_kernel, dim3(1), dim3(1024), 0, s,
+                     reinterpret_cast<const unsigned char*>(seq_mask), B, N, L + 1, ctx_alloc_rows, ctx_offsets,
                      fut_offsets, lpt_order);
-  DecPrologueArgs a{user_ids, sem_ids, type_ids, sem_ids_fut, type_ids_fut, seq_mask, user_w, sem_w, wpe_w, tte_w, bos,
+  DecPrologueArgs a{user_ids, sem_ids, type_ids, sem_ids_fut, type_ids_fut,
+                    reinterpret_cast<const unsigned char*>(seq_mask), user_w, sem_w, wpe_w, tte_w, bos,
                     n_buckets, K, pad, n_sem_rows, n_wpe_rows, n_tte_rows, B, N, L, E, ctx_offsets, ctx_values,
                     fut_values, ctx_alloc_rows, keys, uid_mod};
   const int64_t rows = 1 + (N > L ? N : L);

@@ -1532,7 +1532,10 @@ static bool x3w_choose(int64_t M, int64_t N, int64_t K, bool asp, bool bsp, bool
   const bool combo = epilogue == kEpiStore || (epilogue == kEpiSiluFwd && a_kc && b_kc) ||
                      (epilogue == kEpiSiluBwd && a_kc && !b_kc) || (epilogue == kEpiAdd && a_kc && b_kc);
   if (!(asp && bsp && combo && x3w_plan(M, N, K, true, p))) return false;
-  return (flags & RQ_GEMM_FORCE_WIDE) || x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K, flags), M, N, false);
+  // priced against the 128-/64-tile plan this call would really get (same epilogue: the skinny-unsplit rule
+  // applies to the store / add epilogues only)
+  return (flags & RQ_GEMM_FORCE_WIDE) ||
+         x3_plan_time(*p, M, N, true) < x3_plan_time(x3_plan(M, N, K, flags, true, epilogue), M, N, false);
 }
 
 }  // namespace rqhip

@@ -8,9 +8,11 @@ num_heads, cross_attn=False, dropout=0.0, qkv_bias=False, enable_kv_cache=False)
 and exceptions (KV cache unsupported :161; dense attention raises :228-229).
 
 MI355X path: NJT q/k/v values (row-strided views of the fused projection output, consumed in
-place) go to the HIP varlen attention kernels (rqvae_hip.ops.varlen_attention: fp32 MFMA,
-online softmax, deterministic two-pass backward). Attention dropout is always 0, as in the
-reference (Attend is built with dropout=False).
+place) go to the HIP varlen attention kernels (rqvae_hip.ops.varlen_attention: fp32 / split-bf16
+MFMA, online softmax, a one-pass fused backward per shape class — long key ranges, short
+self-attention, few-query cross-attention — with deterministic, fixed-order dQ sums; the two-pass
+form stays as an A/B policy). Attention dropout is always 0, as in the reference (Attend is built
+with dropout=False).
 """
 from typing import Optional, Union
 

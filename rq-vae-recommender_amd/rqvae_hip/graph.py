@@ -48,6 +48,15 @@ def _in_graph_default(buckets) -> bool:
 
 
 WATCHDOG_RETIRE_S = 5.0
+WATCHDOG_RETIRE_AGREED_S = 60.0   # world > 1 without the local fallback: wait longer, then fail loudly
+
+
+def _local_fallback_default() -> bool:
+    """RQVAE_LOCAL_EXCHANGE_FALLBACK=1 lets one rank of a world > 1 job move its exchange out of the graph
+    on its own (the round-5 behaviour). Off by default: RCCL with captured collectives on some ranks and
+    eager ones on others has never run on hardware, so a rank that cannot capture fails loudly instead."""
+    import os
+    return os.environ.get("RQVAE_LOCAL_EXCHANGE_FALLBACK", "0") == "1"
 
 
 def watchdog_retired(timeout_s: float = None):
@@ -101,8 +110,10 @@ class GraphedSteps:
     * Gradient exchange (N > 1): with an RCCL process group the buckets' all-reduces are captured
       where their hooks fire (in bucket order, overlapping the rest of the backward) together with
       the final wait / average (`in_graph_exchange`, the default there); `buckets.synchronize()` after
-      the replay then only finalises. With gloo (rehearsals, CPU tests) or when capturing the
-      collectives fails, the hooks are suspended in the graph and the exchange runs after the replay.
+      the replay then only finalises. With gloo (rehearsals, CPU tests) the hooks are suspended in the
+      graph and the exchange runs after the replay. When capturing the collectives fails on a rank, that
+      rank falls back to the post-replay exchange at world 1 (or with `local_fallback`); at world > 1
+      it raises by default, so the placement stays one decision shared by every rank (`_deviate`).
       Every rank runs exactly one exchange per step: the very first step is an eager probe (it also
       settles which parameters are unused on every rank), and a new key's warm-up passes do not
       communicate.
@@ -122,10 +133,11 @@ class GraphedSteps:
       break the capture. Drop such references (or `.detach()` them) before a new key's first call."""
 
     def __init__(self, loss_fn, key_fn, buckets, prepare=None, warmup: int = 2, run_backward: bool = True,
-                 in_graph_exchange=None, capture: bool = True, max_graphs: int = 16):
+                 in_graph_exchange=None, capture: bool = True, max_graphs: int = 16, local_fallback=None):
         self.loss_fn, self.key_fn, self.buckets, self.prepare, self.warmup = loss_fn, key_fn, buckets, prepare, warmup
         self.run_backward = run_backward
         self.in_graph = _in_graph_default(buckets) if in_graph_exchange is None else bool(in_graph_exchange)
+        self.local_fallback = _local_fallback_default() if local_fallback is None else bool(local_fallback)
         self.capture = capture
         self.capture_error = None
         self.max_graphs = max_graphs
@@ -215,14 +227,34 @@ class GraphedSteps:
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
 
+    def _agreed(self) -> bool:
+        """True when every rank must keep the same exchange placement: world > 1 without the opt-in
+        local fallback (RQVAE_LOCAL_EXCHANGE_FALLBACK=1 / local_fallback=True)."""
+        return self._world() > 1 and not self.local_fallback
+
+    def _deviate(self, why: str):
+        """This rank cannot capture the exchange. World 1 (or the opt-in local fallback): record why and
+        exchange after the replay. World > 1 by default: raise — a rank replaying RCCL collectives from a
+        graph while a peer issues the same all-reduces eagerly has never been run on hardware, and a
+        mismatch would hang the whole job; an error on one rank ends it (torchrun tears the others down)."""
+        self.capture_error = why[:300]
+        if self._agreed():
+            raise RuntimeError(
+                "GraphedSteps: rank %d cannot capture the gradient exchange (%s); its peers capture it, and "
+                "mixing captured and eager RCCL collectives across ranks is unverified. Set "
+                "RQVAE_LOCAL_EXCHANGE_FALLBACK=1 to let this rank exchange after its replay, or build the "
+                "GraphedSteps with in_graph_exchange=False on every rank." % (self._rank(), why))
+
     def _capture(self, key, batch):
-        """Warm up and capture a new key's step. The decision whether this key's graph holds the
-        exchange is LOCAL to the rank: a rank whose capture of the collectives fails (or cannot be
-        made safe, below) records a graph without them and exchanges after its replay. Every rank
-        still issues the same all-reduces in bucket order once per step, in the graph or after it,
-        so ranks that decide differently — or that capture different keys in the same step (the
-        decoder's keys come from each rank's own shard), or replay while another rank captures or
-        runs eagerly past `max_graphs` — stay matched. No collective depends on the key."""
+        """Warm up and capture a new key's step. Whether a graph holds the exchange is decided ONCE for
+        the job (`in_graph`, the same on every rank: the backend's, or the caller's argument). At world 1
+        a capture of the collectives that fails (or cannot be made safe, below) falls back to a graph
+        without them and an exchange after the replay. At world > 1 that deviation raises unless the
+        local fallback is enabled (`_deviate`); with it, every rank still issues the same all-reduces in
+        bucket order once per step, in the graph or after it, so ranks that decide differently — or that
+        capture different keys in the same step (the decoder's keys come from each rank's own shard), or
+        replay while another rank captures or runs eagerly past `max_graphs` — issue matching sequences.
+        No collective depends on the key."""
         if self.prepare is not None:
             self.prepare(self.static, batch)
         self._warm()
@@ -233,23 +265,24 @@ class GraphedSteps:
         # records events) — and under the default global mode any such call fails the capture ("operation
         # not permitted when stream is capturing", seen on MI355X with the watchdog)
         if exchanged and self.capture:
-            idle = watchdog_retired()
+            bound = WATCHDOG_RETIRE_AGREED_S if self._agreed() else WATCHDOG_RETIRE_S
+            idle = watchdog_retired(bound)
             if not idle:
                 exchanged = False
                 if idle is None:   # cannot be checked in this process: never capture the exchange
+                    self._deviate("flight recorder off: the watchdog's work list cannot be checked")
                     self.in_graph = False
-                    self.capture_error = "flight recorder off: the watchdog's work list cannot be checked"
                 else:              # this key exchanges after its replay; later keys try again
-                    self.capture_error = f"watchdog kept an eager collective past {WATCHDOG_RETIRE_S} s"
+                    self._deviate(f"watchdog kept an eager collective past {bound} s")
         g, out, err = self._try_capture(exchanged)
         if err is not None:
             if not exchanged:
                 raise err if isinstance(err, BaseException) else RuntimeError(err)
-            self.capture_error = repr(err)[:300]
-            self.in_graph = False   # this rank exchanges after the replay from now on
-            exchanged = False
             if self.capture:
                 torch.cuda.synchronize()
+            self._deviate(repr(err))
+            self.in_graph = False   # this rank exchanges after the replay from now on
+            exchanged = False
             g, out, err2 = self._try_capture(False)
             if err2 is not None:
                 raise err2
@@ -277,6 +310,11 @@ class GraphedSteps:
     def _world() -> int:
         import torch.distributed as dist
         return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+    @staticmethod
+    def _rank() -> int:
+        import torch.distributed as dist
+        return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
     def _device(self):
         b = self.buckets

@@ -1618,12 +1618,13 @@ class DecoderPrologueFunction(torch.autograd.Function):
         k_user, k_sem, k_wpe, k_tte = ctx.rows
         dev = ctx_off.device
         need = ctx.needs_input_grad
-        if g_ctx is None:
-            g_ctx = torch.zeros((1, E), device=dev)   # rows past the offsets are never read
-        g_ctx = g_ctx.contiguous()
-        g_pad = torch.empty((B, N + 1, E), device=dev, dtype=torch.float32)
-        call("jagged_to_padded", ptr(g_ctx), ptr(ctx_off), B, N + 1, E, ptr(g_pad), _DTYPES[torch.float32],
-             stream_handle(dev))
+        if g_ctx is None:   # no gradient reached the context rows: the padded gradient is all zeros
+            g_pad = torch.zeros((B, N + 1, E), device=dev, dtype=torch.float32)
+        else:
+            g_ctx = g_ctx.contiguous()
+            g_pad = torch.empty((B, N + 1, E), device=dev, dtype=torch.float32)
+            TIMER.around("jagged_to_padded", call, "jagged_to_padded", ptr(g_ctx), ptr(ctx_off), B, N + 1, E, ptr(g_pad),
+                         _DTYPES[torch.float32], stream_handle(dev))
         g_futp = (torch.zeros((B, L + 1, E), device=dev) if g_fut is None else g_fut.contiguous().view(B, L + 1, E))
         g_seq = g_pad[:, 1:]
         gu = _emb_grad(w_user, g_pad[:, :1].reshape(-1, E), uid_mod, k_user, None) if need[0] else None

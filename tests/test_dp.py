@@ -138,7 +138,7 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
             step = [0]
             gs = GraphedSteps(lambda xb: _loss(model, xb) * dp.shard_weight(b - a, gb),
                               lambda xb: step[0] if r == 1 else 0, buckets, capture=False, in_graph_exchange=True,
-                              max_graphs=1)
+                              max_graphs=1, local_fallback=True)
             if r == 1:
                 orig = gs._try_capture
                 gs._try_capture = lambda in_graph: ((None, None, RuntimeError("simulated capture failure"))
@@ -345,3 +345,33 @@ def test_graphed_steps_copy_in_mixed_dtypes():
                   (static.nested[0], src.nested[0]), (static.nested[1], src.nested[1])):
         assert torch.equal(d, s_) and d.dtype == s_.dtype
     assert ptrs == [t.data_ptr() for t in (static.a, static.b, static.mask, static.x, *static.nested)]
+
+
+@pytest.mark.parametrize("world,fallback", [(1, None), (2, None), (2, True)])
+def test_graphed_steps_capture_failure_policy(world, fallback, monkeypatch):
+    """A rank whose capture of the in-graph exchange fails: at world 1, or with the opt-in
+    local fallback, it records the graph without the collectives and exchanges after the replay; at
+    world > 1 by default it raises instead of silently replaying a different collective placement than
+    its peers (one agreed decision per job). Single process; the world size is what GraphedSteps sees."""
+    from rqvae_hip.graph import GraphedSteps
+    monkeypatch.delenv("RQVAE_LOCAL_EXCHANGE_FALLBACK", raising=False)
+    torch.manual_seed(0)
+    model = _Net()
+    buckets = dp.GradBuckets(model.parameters(), flat_views=True)
+    gs = GraphedSteps(lambda xb: _loss(model, xb), lambda xb: 0, buckets, capture=False, in_graph_exchange=True,
+                      local_fallback=fallback)
+    monkeypatch.setattr(GraphedSteps, "_world", staticmethod(lambda: world))
+    orig = gs._try_capture
+    gs._try_capture = lambda in_graph: ((None, None, RuntimeError("simulated capture failure"))
+                                        if in_graph else orig(in_graph))
+    x = _data(16)[0]
+    gs(x)                      # eager probe step
+    buckets.synchronize()
+    if world > 1 and not fallback:
+        with pytest.raises(RuntimeError, match="cannot capture the gradient exchange"):
+            gs(x)
+        assert "simulated capture failure" in gs.capture_error
+        return
+    gs(x)
+    buckets.synchronize()
+    assert not gs.in_graph and "simulated capture failure" in gs.capture_error and len(gs.graphs) == 1

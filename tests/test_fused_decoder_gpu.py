@@ -396,3 +396,37 @@ def test_decoder_pair_proj_equals_separate(device, monkeypatch, buckets):
         assert (a is None) == (b is None), n
         if a is not None:
             assert torch.equal(a, b), (n, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("B,max_items", [(256, 20), (16, 20), (5, 7)])
+def test_decoder_prologue_noncanonical_mask_and_short_alloc(device, B, max_items):
+    """a bool mask whose bytes are any nonzero value (a uint8 tensor viewed as bool) counts as the
+    canonical 0 / 1 mask (the staged many-sequence path sums bytes); an allocation below the valid total
+    clamps the context offsets to it, so no consumer reads past the values."""
+    from data.processed import synthetic_tokenized_batch
+    from modules import model as model_mod
+    from rqvae_hip import ops
+    torch.manual_seed(0)
+    m = model_mod.EncoderDecoderRetrievalModel(embedding_dim=64, attn_dim=128, dropout=0.0, num_heads=4, n_layers=2,
+                                               num_embeddings=64, sem_id_dim=4, inference_verifier_fn=None,
+                                               max_pos=max_items * 4).to(device)
+    batch = synthetic_tokenized_batch(B, max_items, 4, 64, 11, device)
+    se, ue = m.sem_id_embedder, m.user_id_embedder
+
+    def run(mask, alloc):
+        return ops.decoder_prologue(ue.emb.weight, se.emb.weight, m.wpe.weight, m.tte.weight, m.bos_emb,
+                                    batch.user_ids, batch.sem_ids, batch.token_type_ids, mask, batch.sem_ids_fut,
+                                    batch.token_type_ids_fut, ue.num_buckets, se.num_embeddings, se.padding_idx, alloc)
+    total = int(batch.seq_mask.sum()) + B
+    ref = run(batch.seq_mask, total)
+    raw = batch.seq_mask.to(torch.uint8) * torch.tensor([2, 255, 17, 128], dtype=torch.uint8, device=device).repeat(
+        batch.seq_mask.shape[1] // 4 + 1)[:batch.seq_mask.shape[1]]
+    odd = raw.view(torch.bool)
+    got = run(odd, total)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    short = total - max(1, total // 3)
+    cv, co, _, _ = run(batch.seq_mask, short)
+    assert int(co.max()) <= short and bool((co[1:] >= co[:-1]).all())
+    assert torch.equal(co, ref[1].clamp(max=short))
+    assert torch.equal(cv[:short], ref[0][:short])
