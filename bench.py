@@ -242,6 +242,12 @@ def cpu_baseline(budget_s, B=2048):
                        f"ML-32M dims, {dt:.1f} s on {threads} host threads")
 
 
+def _log(msg):
+    """Progress to stderr (stdout carries only rank 0's JSON line)."""
+    rk = os.environ.get("RANK", "0")
+    print(f"[bench rank {rk} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -314,6 +320,7 @@ def main():
     device = torch.device("cuda", lr)
     torch.cuda.set_device(device)
     census = rank_census(device, ws)
+    _log(f"world {ws}: {census['allreduce_rank_count']} ranks answered the census all-reduce")
     B = args.batch
 
     model = build_model(device)
@@ -353,6 +360,7 @@ def main():
         last = step()
     sync_all()
     elapsed = time.perf_counter() - t0
+    _log(f"rq-vae timed: {elapsed / args.steps * 1e3:.3f} ms/step")
     if ws > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -382,6 +390,7 @@ def main():
     # decoder-train tokens/s (BASELINE metric, second half): data parallel over the same ranks
     dec = dec_dm = None
     if not args.no_decoder:
+        _log("decoder amazon")
         dec = measure_decoder(device, ws, rk, DEC, graphs=not args.no_graph,
                               cpu_seconds=0.0 if args.no_cpu_baseline else 8.0)
         if ws == 1 and not args.no_extras and not args.no_graph:
@@ -390,11 +399,13 @@ def main():
         if not args.no_dm:
             dec_dm = {}
             for b in (8, 64):   # the config's global 64 split over 8 ranks, and 64 per rank (throughput)
+                _log(f"decoder ml32m, {b} sequences per rank")
                 # warmup >= the 4 cycled batches, so every row bucket's graph is captured before timing
                 dec_dm[f"per_gpu_batch_{b}"] = measure_decoder(device, ws, rk, DEC_DM, B=b, steps=10, warmup=5,
                                                                graphs=not args.no_graph, stats=(b == 64))
     extras = {}
     if not args.no_extras and rk == 0 and ws == 1:
+        _log("extras")
         extras = measure_extras(model, device, pool[0])
         extras["trainers"] = measure_trainers()
 
@@ -967,19 +978,22 @@ def decoder_kernel_stats(m, buckets, batch, ctx_lens, cfg, reps=3):
     T, Tf = n.sum(), nf * Bn
     attn_fwd_bytes = 4 * A * (Le * 4 * T + Ld * 4 * Tf + Ld * (2 * Tf + 2 * T))
     attn_bwd_bytes = 4 * A * (Le * 8 * T + Ld * 8 * Tf + Ld * (4 * Tf + 4 * T))
-    for _ in range(2):
+    # rank 0 alone runs these passes: the gradient hooks must not start an exchange its peers never join
+    with buckets.suspended():
+        for _ in range(2):
+            buckets.zero_grad()
+            m(batch).loss.backward()
+        torch.cuda.synchronize()
+        ops.TIMER.reset()
+        ops.TIMER.only = {"jagged_", "varlen_attn", "dec_prologue"}
+        ops.TIMER.enabled = True
+        for _ in range(reps):
+            buckets.zero_grad()
+            m(batch).loss.backward()
+        torch.cuda.synchronize()
+        ops.TIMER.enabled = False
+        ops.TIMER.only = None
         buckets.zero_grad()
-        m(batch).loss.backward()
-    torch.cuda.synchronize()
-    ops.TIMER.reset()
-    ops.TIMER.only = {"jagged_", "varlen_attn", "dec_prologue"}
-    ops.TIMER.enabled = True
-    for _ in range(reps):
-        buckets.zero_grad()
-        m(batch).loss.backward()
-    torch.cuda.synchronize()
-    ops.TIMER.enabled = False
-    ops.TIMER.only = None
     fwd_ms, nf_ = ops.TIMER.mean_ms("varlen_attn_fwd")
     bwd_ms, nb_ = ops.TIMER.mean_ms("varlen_attn_bwd")
     f_step, b_step = fwd_ms * nf_ / reps, bwd_ms * nb_ / reps

@@ -2493,6 +2493,168 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? RQ_FEWQ_BWD_MINWG : 1) attn
   }
 }
 
+// ------------------------------------- few-query fused backward, one wave per (sequence, head) unit
+// The round-6 form of attn_bwd_fewq_fused_kernel (the decoder's cross-attention: <= 16 future queries over
+// <= 128 context keys; its causal self-attention over <= 16 tokens). The workgroup form spread ONE unit's
+// <= 6 key tiles over 4 waves and merged their dQ partials through LDS: 2,048 workgroups in ~4 dependent
+// rounds of load -> compute -> LDS reduce -> store, bound by neither HBM nor MFMA (Amazon: 44 us a launch,
+// ~2.3 TB/s of its algorithmic K / V / dK / dV bytes). Here every wave owns whole units (unit u = rank
+// u / H of the LPT order, head u % H; waves stride over the units) and walks the unit's key tiles in order
+// with the NEXT tile's K / V fragments in flight while the current tile multiplies; dK / dV rows of a tile
+// are stored as soon as formed, dQ^T accumulates in registers over all the unit's tiles (ascending tile
+// order: deterministic, no LDS, no barrier) and is stored once. Per tile the products are the workgroup
+// form's (S and dP once in the dK / dV orientation, dV^T += dO^T P, dK^T += Q^T dS, the exact permutation
+// transpose of dS, dQ^T += K^T dS^T), so dK / dV are bitwise the workgroup form's; dQ sums the same terms
+// in tile order instead of (wave, tile) order.
+__global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
+    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
+    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out, const int* __restrict__ order,
+    int B, int H) {
+  constexpr int HD = 64, NWG = 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  {   // rows past the last sequence (a row-bucketed tail): zero dq / dk / dv over every head
+    const int64_t f4 = (int64_t)H * (HD / 4), nth = (int64_t)gridDim.x * 256, me = (int64_t)blockIdx.x * 256 + tid;
+    const int64_t rq = cu_q[B], rk = cu_k[B];
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t f = me; f < (Tq - rq) * f4; f += nth)
+      *reinterpret_cast<float4*>(dq + (rq + f / f4) * sdq + (f % f4) * 4) = z4;
+    for (int64_t f = me; f < (Tk - rk) * f4; f += nth) {
+      *reinterpret_cast<float4*>(dk + (rk + f / f4) * sdk + (f % f4) * 4) = z4;
+      *reinterpret_cast<float4*>(dv + (rk + f / f4) * sdv + (f % f4) * 4) = z4;
+    }
+  }
+  // 0/1 permutation operand of the transpose: step s, lane (g, c) = [c == 4 g + s]
+  float pe[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) pe[s] = c == 4 * g + s ? 1.f : 0.f;
+  const float sl2 = scale * kLog2e;
+  const int nunits = B * H;
+  for (int u = blockIdx.x * NWG + wave; u < nunits; u += gridDim.x * NWG) {
+    const int b = seq_of(order, u / H), hh = u % H;
+    const int64_t q0 = cu_q[b], k0 = cu_k[b];
+    const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+    const int nkt = (lk + 15) >> 4;   // every key tile gets its dK / dV rows written (zeros past the queries)
+    const float* kb_ = k + k0 * sk + hh * HD;
+    const float* vb_ = v + k0 * sv + hh * HD;
+    // the first key tile's K / V fragments go out before the query tile's loads (independent of them)
+    float4 kp[4], vk[4];
+    if (nkt > 0) {
+      frag_kpat(kb_, sk, 0, lk, lane, kp);
+      frag_kpat(vb_, sv, 0, lk, lane, vk);
+    }
+    // the query tile: Q, dO in the A pattern (row c, d = 16 g + 0..15) and the V pattern (rows 4 g + i,
+    // d = 4 c + 0..3); O (A pattern) only for delta
+    const bool qv = c < lq;
+    const int64_t qrow = q0 + (qv ? c : 0);
+    float qf[HD / 4], dof[HD / 4];
+    load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv, qf);
+    load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv, dof);
+    float4 qvp[4], dvp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qvp[i] = dvp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lq > 0) {
+      frag_vpat(q + q0 * sq + hh * HD, sq, 0, lq, lane, qvp);
+      frag_vpat(dout + q0 * sdo + hh * HD, sdo, 0, lq, lane, dvp);
+    }
+    float delta = 0.f, lse2 = 0.f;
+    if (lq > 0) {
+      float of[HD / 4];
+      load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+#pragma unroll
+      for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+      delta += __shfl_xor(delta, 16, 64);
+      delta += __shfl_xor(delta, 32, 64);
+      if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
+      lse2 = qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f;
+    }
+    float dl[4], ls[4];   // per-lane values of the queries 4 g + i (held by lane 4 g + i)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dl[i] = __shfl(delta, 4 * g + i, 64);
+      ls[i] = __shfl(lse2, 4 * g + i, 64);
+    }
+    f32x4 acc[4];   // dQ^T (d permuted) over the unit's key tiles, in tile order
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nkt; ++t) {
+      // next tile's K / V in flight (the last tile re-reads itself: cache hits, no branch)
+      const int tn = t + 1 < nkt ? t + 1 : t;
+      float4 kpn[4], vkn[4], kv[4];
+      frag_kpat(kb_, sk, tn, lk, lane, kpn);
+      frag_kpat(vb_, sv, tn, lk, lane, vkn);
+      frag_vpat(kb_, sk, t, lk, lane, kv);   // this tile's K in the V pattern (the kp lines: cache hits)
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        st = mfma4(qf[4 * s4], kp[s4].x, st);
+        dp = mfma4(dof[4 * s4], vk[s4].x, dp);
+        st = mfma4(qf[4 * s4 + 1], kp[s4].y, st);
+        dp = mfma4(dof[4 * s4 + 1], vk[s4].y, dp);
+        st = mfma4(qf[4 * s4 + 2], kp[s4].z, st);
+        dp = mfma4(dof[4 * s4 + 2], vk[s4].z, dp);
+        st = mfma4(qf[4 * s4 + 3], kp[s4].w, st);
+        dp = mfma4(dof[4 * s4 + 3], vk[s4].w, dp);
+      }
+      const int key = t * 16 + c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = 4 * g + i;
+        float p = exp2_fast(__builtin_fmaf(st[i], sl2, -ls[i]));
+        if (!(qr < lq && key < lk && (!causal || key <= qr))) p = 0.f;
+        st[i] = p;
+        dp[i] = p * (dp[i] - dl[i]);   // dS
+      }
+      f32x4 dka[4], dva[4], dst = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {   // dV^T += dO^T P, dK^T += Q^T dS (k = the query index 4 g + i)
+        dva[0] = mfma4(dvp[i].x, st[i], dva[0]);
+        dva[1] = mfma4(dvp[i].y, st[i], dva[1]);
+        dva[2] = mfma4(dvp[i].z, st[i], dva[2]);
+        dva[3] = mfma4(dvp[i].w, st[i], dva[3]);
+        dka[0] = mfma4(qvp[i].x, dp[i], dka[0]);
+        dka[1] = mfma4(qvp[i].y, dp[i], dka[1]);
+        dka[2] = mfma4(qvp[i].z, dp[i], dka[2]);
+        dka[3] = mfma4(qvp[i].w, dp[i], dka[3]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dst = mfma4(dp[s], pe[s], dst);   // dS^T: rows = keys 4 g + i, lanes = queries
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {   // dQ^T += K^T dS^T (k = the key index 4 g + i of the tile)
+        acc[0] = mfma4(kv[i].x, dst[i], acc[0]);
+        acc[1] = mfma4(kv[i].y, dst[i], acc[1]);
+        acc[2] = mfma4(kv[i].z, dst[i], acc[2]);
+        acc[3] = mfma4(kv[i].w, dst[i], acc[3]);
+      }
+      if (key < lk) {
+        float* rk = dk + (k0 + key) * sdk + hh * HD + 16 * g;
+        float* rv = dv + (k0 + key) * sdv + hh * HD + 16 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          *reinterpret_cast<float4*>(rk + 4 * i) =
+              make_float4(dka[0][i] * scale, dka[1][i] * scale, dka[2][i] * scale, dka[3][i] * scale);
+          *reinterpret_cast<float4*>(rv + 4 * i) = make_float4(dva[0][i], dva[1][i], dva[2][i], dva[3][i]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vk[j] = vkn[j]; }
+    }
+    if (qv) {   // lane (g, c): query c, d = 16 g + 4 i + 0..3 <- acc[0..3][i]
+      float* rq = dq + (q0 + c) * sdq + hh * HD + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(rq + 4 * i) =
+            make_float4(acc[0][i] * scale, acc[1][i] * scale, acc[2][i] * scale, acc[3][i] * scale);
+    }
+  }
+}
+
 // ----------------------------------------------- fused backward over short query and key ranges
 // The one-pass form of the few-query kernel above for self-attention over <= R rows (the Amazon encoder's
 // contexts, n <= 81: R = 96): one workgroup per (sequence, head), Q and dO staged by LDS-DMA (swizzled
@@ -2743,11 +2905,13 @@ struct AttnPolicy {
   bool x3;   // RQ_ATTN_SPLIT_BF16: the long-range forwards multiply in split-bf16 (matmul precision 'high')
   bool lpt_short;   // RQ_ATTN_LPT_SHORT: longest-first sequence order for the short / few-query forms too
   bool order_given;   // RQ_ATTN_ORDER_GIVEN: ws[0, B) already holds the LPT order of cu_k (no order launch)
+  bool wg_units;      // RQ_ATTN_WG_UNITS: the round-5 one-pass short / few-query backwards (a workgroup per unit)
 };
 static AttnPolicy attn_policy(int flags) {
   return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
                     (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15, (flags & RQ_ATTN_SPLIT_BF16) != 0,
-                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0};
+                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0,
+                    (flags & RQ_ATTN_WG_UNITS) != 0};
 }
 // LPT order of the short / few-query forms (by key length: their work per workgroup grows with it)
 static bool short_lpt_plan(int64_t B, const AttnPolicy& pol) { return RQ_ATTN_LPT && pol.lpt_short && B >= 2 && B <= kOrderMax; }
@@ -2975,6 +3139,13 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
         default: RQ_SHF(4, 128); break;
       }
 #undef RQ_SHF
+      return;
+    }
+    if (fewq_plan(HD, max_q, max_k, pol) && pol.fused && !pol.wg_units) {   // one wave per (sequence, head)
+      const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>((B * H + 3) / 4, 8192));
+      hipLaunchKernelGGL(attn_bwd_fewq_unit_kernel, dim3((unsigned)wgs), dim3(256), 0, st, q, sq, k, sk, v, sv, out, so,
+                         dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, order, (int)B,
+                         (int)H);
       return;
     }
     if (fewq_plan(HD, max_q, max_k, pol) && pol.fused) {

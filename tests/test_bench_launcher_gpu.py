@@ -15,6 +15,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--gpus", "2", "--no-extras", "--no-pmc", "--no-cpu-baseline", "--no-dm", "--steps", "3", "--warmup", "2"]
 
 
+def _run(env):
+    """bench.py as a child; its stderr (progress lines) streams into gpurun_out/ while it runs."""
+    log_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(log_dir, exist_ok=True)
+    with open(os.path.join(log_dir, "test_bench_launcher.log"), "a") as log:
+        p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), *ARGS], stdout=subprocess.PIPE,
+                           stderr=log, text=True, timeout=240, env=env, cwd=ROOT)
+    return p
+
+
 def _env(**kw):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(RQVAE_DIST_BACKEND="gloo", RQVAE_SHARE_DEVICE="1", PYTHONUNBUFFERED="1", **kw)
@@ -22,9 +32,8 @@ def _env(**kw):
 
 
 def test_bench_gpus_2_runs_two_ranks():
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), *ARGS], capture_output=True,
-                       text=True, timeout=240, env=_env(), cwd=ROOT)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    r = _run(_env())
+    assert r.returncode == 0, r.stdout[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{\"metric\"")]
     assert len(lines) == 1, r.stdout[-2000:]   # one line: rank 0 only
     line = json.loads(lines[0])
@@ -38,8 +47,8 @@ def test_bench_gpus_2_runs_two_ranks():
 
 
 def test_bench_gpus_2_rank_failure_is_nonzero_exit():
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), *ARGS], capture_output=True,
-                       text=True, timeout=240, env=_env(RQVAE_BENCH_FAIL_RANK="1"), cwd=ROOT)
+    r = _run(_env(RQVAE_BENCH_FAIL_RANK="1"))
     assert r.returncode != 0
-    assert "RQVAE_BENCH_FAIL_RANK: rank 1" in r.stdout + r.stderr
+    with open(os.path.join(ROOT, "gpurun_out", "test_bench_launcher.log")) as f:
+        assert "RQVAE_BENCH_FAIL_RANK: rank 1" in f.read()
     assert not [l for l in r.stdout.splitlines() if l.startswith("{\"metric\"")]
