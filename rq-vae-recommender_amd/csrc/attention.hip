@@ -2218,6 +2218,113 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_fewq_kernel(
   }
 }
 
+// Few-query forward, one wave per (sequence, head) unit (the round-6 form of attn_fwd_fewq_kernel, as
+// attn_bwd_fewq_unit_kernel for the backward): the wave walks the unit's key tiles in order with the next
+// tile's K / V fragments in flight, an online softmax over the tiles (running max and sum per query, the
+// partial O^T rescaled when the max grows), no LDS and no barrier; units in LPT order, waves striding over
+// them. S^T = K Q^T per tile (keys on the accumulator rows, query = lane & 15), O^T += V^T P^T (d permuted).
+__global__ void __launch_bounds__(256, 2) attn_fwd_fewq_unit_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
+    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq, const int* __restrict__ order, int B,
+    int H) {
+  constexpr int HD = 64, NWG = 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, qi = lane & 15;
+  {   // rows past the last sequence: zero out over every head
+    const int64_t f4 = (int64_t)H * (HD / 4), nth = (int64_t)gridDim.x * 256, me = (int64_t)blockIdx.x * 256 + tid;
+    const int64_t rq = cu_q[B];
+    for (int64_t f = me; f < (Tq - rq) * f4; f += nth)
+      *reinterpret_cast<float4*>(out + (rq + f / f4) * so + (f % f4) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float sl2 = scale * kLog2e;
+  const int nunits = B * H;
+  for (int u = blockIdx.x * NWG + wave; u < nunits; u += gridDim.x * NWG) {
+    const int b = seq_of(order, u / H), hh = u % H;
+    const int64_t q0 = cu_q[b], k0 = cu_k[b];
+    const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+    if (lq <= 0) continue;
+    const bool qv = qi < lq;
+    const int kend = causal ? min(lk, 16) : lk;
+    const int nkt = (kend + 15) >> 4;
+    const float* kb_ = k + k0 * sk + hh * HD;
+    const float* vb_ = v + k0 * sv + hh * HD;
+    float4 kp[4], vp[4];
+    if (nkt > 0) {
+      frag_kpat(kb_, sk, 0, lk, lane, kp);
+      frag_vpat(vb_, sv, 0, lk, lane, vp);
+    }
+    float qf[HD / 4];
+    load_frag<HD>(q + (q0 + min(qi, lq - 1)) * sq + hh * HD + g * (HD / 4), true, qf);
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) qf[d] = qv ? qf[d] : 0.f;
+    float mrun = -INFINITY, l = 0.f;   // running max (log2 units, scaled) and this lane's partial sum
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nkt; ++t) {
+      const int tn = t + 1 < nkt ? t + 1 : t;
+      float4 kpn[4], vpn[4];
+      frag_kpat(kb_, sk, tn, lk, lane, kpn);
+      frag_vpat(vb_, sv, tn, lk, lane, vpn);
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the tile's MFMAs
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        st = mfma4(kp[s4].x, qf[4 * s4], st);
+        st = mfma4(kp[s4].y, qf[4 * s4 + 1], st);
+        st = mfma4(kp[s4].z, qf[4 * s4 + 2], st);
+        st = mfma4(kp[s4].w, qf[4 * s4 + 3], st);
+      }
+      float mt = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {   // masks as selects
+        const int key = t * 16 + 4 * g + i;
+        const bool ok = (key < lk) & ((causal == 0) | (key <= qi));
+        st[i] = ok ? st[i] : -INFINITY;
+        mt = fmaxf(mt, st[i]);
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      // branch-free (a divergent branch here would make hipcc drain the prefetch at the loop head): every
+      // tile holds a valid key of every query (non-causal: keys < lk; causal: one tile, key 0), so mnew is
+      // finite; the selects only guard the all-masked case
+      const float mnew = fmaxf(mrun, mt * sl2);
+      const float msub = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = mrun == -INFINITY ? 0.f : exp2_fast(mrun - msub);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = o[dt] * alpha;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        st[i] = exp2_fast(__builtin_fmaf(st[i], sl2, -msub));
+        l += st[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[0] = mfma4(vp[i].x, st[i], o[0]);
+        o[1] = mfma4(vp[i].y, st[i], o[1]);
+        o[2] = mfma4(vp[i].z, st[i], o[2]);
+        o[3] = mfma4(vp[i].w, st[i], o[3]);
+      }
+      mrun = mnew;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vp[j] = vpn[j]; }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qv) {   // lane (g, qi): query qi, d = 16 g + 4 i + 0..3 <- o[0..3][i]
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      float* ro = out + (q0 + qi) * so + hh * HD + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(ro + 4 * i) = make_float4(o[0][i] * inv, o[1][i] * inv, o[2][i] * inv, o[3][i] * inv);
+      if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (mrun + log2f(l)) * kLn2 : 0.f;
+    }
+  }
+}
+
 // dQ (+ delta) of the one query tile: key tiles split over the waves as in the forward, partial dQ^T
 // summed through LDS in wave order.
 template <int NW>
@@ -2493,6 +2600,21 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? RQ_FEWQ_BWD_MINWG : 1) attn
   }
 }
 
+// Wave-uniform raw-buffer descriptor over `bytes` bytes from `base` (stride 0): stores past the range are
+// dropped by the hardware, so a tile's rows past the segment end need no branch around the store (a
+// divergent branch there made hipcc's waitcnt merge drain every load in flight at the loop head).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? bytes : 0x7fffffff));
+  float* p = reinterpret_cast<float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ void rsrc_store4(__amdgpu_buffer_rsrc_t r, int64_t off_floats, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(off_floats * 4), 0, 0);
+}
+
 // ------------------------------------- few-query fused backward, one wave per (sequence, head) unit
 // The round-6 form of attn_bwd_fewq_fused_kernel (the decoder's cross-attention: <= 16 future queries over
 // <= 128 context keys; its causal self-attention over <= 16 tokens). The workgroup form spread ONE unit's
@@ -2549,29 +2671,44 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
     }
     // the query tile: Q, dO in the A pattern (row c, d = 16 g + 0..15) and the V pattern (rows 4 g + i,
     // d = 4 c + 0..3); O (A pattern) only for delta
+    // rows past lq read row lq - 1 (no per-lane branch) and are zeroed by select; a unit without queries
+    // (wave-uniform) loads nothing
     const bool qv = c < lq;
-    const int64_t qrow = q0 + (qv ? c : 0);
-    float qf[HD / 4], dof[HD / 4];
-    load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), qv, qf);
-    load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), qv, dof);
+    const int64_t qrow = q0 + min(c, max(lq - 1, 0));
+    float qf[HD / 4], dof[HD / 4], of[HD / 4];
     float4 qvp[4], dvp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) qvp[i] = dvp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float lraw = 0.f;
     if (lq > 0) {
+      load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), true, qf);
+      load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), true, dof);
+      load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), true, of);
       frag_vpat(q + q0 * sq + hh * HD, sq, 0, lq, lane, qvp);
       frag_vpat(dout + q0 * sdo + hh * HD, sdo, 0, lq, lane, dvp);
-    }
-    float delta = 0.f, lse2 = 0.f;
-    if (lq > 0) {
-      float of[HD / 4];
-      load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), qv, of);
+      lraw = lse[(int64_t)hh * Tq + qrow];
+    } else {
 #pragma unroll
-      for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
-      delta += __shfl_xor(delta, 16, 64);
-      delta += __shfl_xor(delta, 32, 64);
-      if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
-      lse2 = qv ? lse[(int64_t)hh * Tq + qrow] * kLog2e : 0.f;
+      for (int d = 0; d < HD / 4; ++d) qf[d] = dof[d] = of[d] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qvp[i] = dvp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) {
+      qf[d] = qv ? qf[d] : 0.f;
+      dof[d] = qv ? dof[d] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // V pattern rows 4 g + i
+      const bool ok = 4 * g + i < lq;
+      qvp[i] = ok ? qvp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      dvp[i] = ok ? dvp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float delta = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
+    const float lse2 = qv ? lraw * kLog2e : 0.f;
     float dl[4], ls[4];   // per-lane values of the queries 4 g + i (held by lane 4 g + i)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2581,13 +2718,19 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
     f32x4 acc[4];   // dQ^T (d permuted) over the unit's key tiles, in tile order
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // this unit's dK / dV rows [0, lk) as store ranges (a row past lk: dropped, no branch)
+    const __amdgpu_buffer_rsrc_t rdk = uniform_rsrc(dk + k0 * sdk + hh * HD, (int64_t)lk * sdk * 4);
+    const __amdgpu_buffer_rsrc_t rdv = uniform_rsrc(dv + k0 * sdv + hh * HD, (int64_t)lk * sdv * 4);
     for (int t = 0; t < nkt; ++t) {
-      // next tile's K / V in flight (the last tile re-reads itself: cache hits, no branch)
+      // this tile's K in the V pattern first (the kp lines: cache hits), then the next tile's K / V in flight
+      // (the last tile re-reads itself: cache hits, no branch) — issued in this order so the kv wait before
+      // the dQ products leaves the prefetch in flight
       const int tn = t + 1 < nkt ? t + 1 : t;
       float4 kpn[4], vkn[4], kv[4];
+      frag_vpat(kb_, sk, t, lk, lane, kv);
       frag_kpat(kb_, sk, tn, lk, lane, kpn);
       frag_kpat(vb_, sv, tn, lk, lane, vkn);
-      frag_vpat(kb_, sk, t, lk, lane, kv);   // this tile's K in the V pattern (the kp lines: cache hits)
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the tile's MFMAs
       f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
@@ -2602,10 +2745,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
       }
       const int key = t * 16 + c;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i) {   // masks as selects (no short-circuit branches inside the tile loop)
         const int qr = 4 * g + i;
-        float p = exp2_fast(__builtin_fmaf(st[i], sl2, -ls[i]));
-        if (!(qr < lq && key < lk && (!causal || key <= qr))) p = 0.f;
+        const bool ok = (qr < lq) & (key < lk) & ((causal == 0) | (key <= qr));
+        const float p = ok ? exp2_fast(__builtin_fmaf(st[i], sl2, -ls[i])) : 0.f;
         st[i] = p;
         dp[i] = p * (dp[i] - dl[i]);   // dS
       }
@@ -2632,15 +2775,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
         acc[2] = mfma4(kv[i].z, dst[i], acc[2]);
         acc[3] = mfma4(kv[i].w, dst[i], acc[3]);
       }
-      if (key < lk) {
-        float* rk = dk + (k0 + key) * sdk + hh * HD + 16 * g;
-        float* rv = dv + (k0 + key) * sdv + hh * HD + 16 * g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          *reinterpret_cast<float4*>(rk + 4 * i) =
-              make_float4(dka[0][i] * scale, dka[1][i] * scale, dka[2][i] * scale, dka[3][i] * scale);
-          *reinterpret_cast<float4*>(rv + 4 * i) = make_float4(dva[0][i], dva[1][i], dva[2][i], dva[3][i]);
-        }
+      for (int i = 0; i < 4; ++i) {   // row key (dropped past lk by the descriptor range)
+        rsrc_store4(rdk, (int64_t)key * sdk + 16 * g + 4 * i,
+                    make_float4(dka[0][i] * scale, dka[1][i] * scale, dka[2][i] * scale, dka[3][i] * scale));
+        rsrc_store4(rdv, (int64_t)key * sdv + 16 * g + 4 * i, make_float4(dva[0][i], dva[1][i], dva[2][i], dva[3][i]));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vk[j] = vkn[j]; }
@@ -2905,7 +3044,7 @@ struct AttnPolicy {
   bool x3;   // RQ_ATTN_SPLIT_BF16: the long-range forwards multiply in split-bf16 (matmul precision 'high')
   bool lpt_short;   // RQ_ATTN_LPT_SHORT: longest-first sequence order for the short / few-query forms too
   bool order_given;   // RQ_ATTN_ORDER_GIVEN: ws[0, B) already holds the LPT order of cu_k (no order launch)
-  bool wg_units;      // RQ_ATTN_WG_UNITS: the round-5 one-pass short / few-query backwards (a workgroup per unit)
+  bool wg_units;      // RQ_ATTN_WG_UNITS: the round-5 few-query forward / one-pass backward (a workgroup per unit)
 };
 static AttnPolicy attn_policy(int flags) {
   return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
@@ -3023,6 +3162,12 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     if (order && short_lpt_plan(B, pol) && (fewq_plan(HD, max_q, max_k, pol) || dma_fwd_plan(HD, max_q, max_k, pol))) {
       if (!pol.order_given) hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, ck, (int)B, order);
       sord = order;
+    }
+    if (fewq_plan(HD, max_q, max_k, pol) && !pol.wg_units) {   // one wave per (sequence, head)
+      const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>((B * H + 3) / 4, 8192));
+      hipLaunchKernelGGL(attn_fwd_fewq_unit_kernel, dim3((unsigned)wgs), dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck,
+                         causal, scale, out, so, lse, Tq, sord, (int)B, (int)H);
+      return;
     }
     if (fewq_plan(HD, max_q, max_k, pol)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
