@@ -971,7 +971,8 @@ __global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pa
 #define RQ_X3W_EPI_LDS 1   // epilogue through LDS in whole rows (0: straight from the accumulators)
 #endif
 #ifndef RQ_X3W_DIAG
-#define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs, 3 = no epilogue (wrong results)
+#define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs, 3 = no epilogue, 4 = B re-read
+                           // from its first k step (cache-resident), 5 = A likewise (wrong results)
 #endif
 #ifndef RQ_X3W_PRIO
 #define RQ_X3W_PRIO 1      // s_setprio(1) around each MFMA cluster (keeps hipcc from moving it)
@@ -1050,14 +1051,14 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
   // issues the same DMA count in every phase and the vmcnt counts stay static.
   auto issue_a = [&](int h, int step, int slot) {
     if (RQ_X3W_DIAG == 1) return;   // diagnostic build: no operand loads (wrong results)
-    const int64_t o = (h == 0 ? oa0 : oa1) + (int64_t)(step < nk ? step : nk - 1) * da;
+    const int64_t o = (h == 0 ? oa0 : oa1) + (RQ_X3W_DIAG == 5 ? 0 : (int64_t)(step < nk ? step : nk - 1) * da);
     char* dst = wl + slot * kWStep + h * 2 * kWH;
     glds16(Ah + o, dst);
     glds16(Al + o, dst + kWH);
   };
   auto issue_b = [&](int g, int step) {
     if (RQ_X3W_DIAG == 1) return;
-    const int64_t o = (g == 0 ? ob0 : ob1) + (int64_t)(step < nk ? step : nk - 1) * db;
+    const int64_t o = (g == 0 ? ob0 : ob1) + (RQ_X3W_DIAG == 4 ? 0 : (int64_t)(step < nk ? step : nk - 1) * db);
     char* dst = wl + kWB0 + (step & 1) * kWStep + g * 2 * kWH;
     glds16(Bh + o, dst);
     glds16(Bl + o, dst + kWH);

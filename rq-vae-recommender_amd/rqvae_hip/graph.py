@@ -111,9 +111,10 @@ class GraphedSteps:
       where their hooks fire (in bucket order, overlapping the rest of the backward) together with
       the final wait / average (`in_graph_exchange`, the default there); `buckets.synchronize()` after
       the replay then only finalises. With gloo (rehearsals, CPU tests) the hooks are suspended in the
-      graph and the exchange runs after the replay. When capturing the collectives fails on a rank, that
-      rank falls back to the post-replay exchange at world 1 (or with `local_fallback`); at world > 1
-      it raises by default, so the placement stays one decision shared by every rank (`_deviate`).
+      graph and the exchange runs after the replay. The placement is one decision shared by every rank:
+      the job's first capture (the same step on every rank) settles it with one MIN all-reduce of the
+      ranks' capture outcomes; a later capture that cannot hold the collectives raises at world > 1
+      (falls back at world 1, or with `local_fallback`).
       Every rank runs exactly one exchange per step: the very first step is an eager probe (it also
       settles which parameters are unused on every rank), and a new key's warm-up passes do not
       communicate.
@@ -146,6 +147,7 @@ class GraphedSteps:
         self.static = None
         self.pool = None
         self._probed = False
+        self._settled = False   # the job's first capture (and with it the exchange placement) is done
         self.eager_steps = 0
 
     @staticmethod
@@ -245,20 +247,33 @@ class GraphedSteps:
                 "RQVAE_LOCAL_EXCHANGE_FALLBACK=1 to let this rank exchange after its replay, or build the "
                 "GraphedSteps with in_graph_exchange=False on every rank." % (self._rank(), why))
 
+    def _agree_all(self, ok: bool) -> bool:
+        """MIN over the ranks of this rank's outcome (one small eager all-reduce on the default group); the
+        local outcome when no process group is up."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self._device())
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     def _capture(self, key, batch):
         """Warm up and capture a new key's step. Whether a graph holds the exchange is decided ONCE for
-        the job (`in_graph`, the same on every rank: the backend's, or the caller's argument). At world 1
-        a capture of the collectives that fails (or cannot be made safe, below) falls back to a graph
-        without them and an exchange after the replay. At world > 1 that deviation raises unless the
-        local fallback is enabled (`_deviate`); with it, every rank still issues the same all-reduces in
-        bucket order once per step, in the graph or after it, so ranks that decide differently — or that
-        capture different keys in the same step (the decoder's keys come from each rank's own shard), or
-        replay while another rank captures or runs eagerly past `max_graphs` — issue matching sequences.
-        No collective depends on the key."""
+        the job, the same on every rank: at the job's FIRST capture — every rank's second call (the first
+        is the eager probe), so the same step everywhere whatever the keys — each rank tries to capture the
+        collectives and one MIN all-reduce of the outcomes settles it; if any rank failed, every rank
+        records its graphs without them and exchanges after the replay from then on. A later capture (a new
+        key) that cannot hold the collectives after the job agreed on in-graph exchange raises at world > 1
+        (`_deviate`) unless the local fallback is enabled; at world 1 it falls back to a graph without them.
+        With the local fallback, every rank still issues the same all-reduces in bucket order once per step,
+        in the graph or after it, so ranks that decide differently — or that capture different keys in the
+        same step (the decoder's keys come from each rank's own shard), or replay while another rank
+        captures or runs eagerly past `max_graphs` — issue matching sequences."""
         if self.prepare is not None:
             self.prepare(self.static, batch)
         self._warm()
         exchanged = self.in_graph
+        agree = exchanged and not self._settled and self._agreed()   # the job's first capture, world > 1
         # thread_local capture mode everywhere: other threads of the process keep making HIP calls while
         # the step is captured — the process group's watchdog polls the events of earlier (eager)
         # collectives, a trainer's feed thread pins host memory (the caching host allocator queries and
@@ -269,23 +284,41 @@ class GraphedSteps:
             idle = watchdog_retired(bound)
             if not idle:
                 exchanged = False
-                if idle is None:   # cannot be checked in this process: never capture the exchange
-                    self._deviate("flight recorder off: the watchdog's work list cannot be checked")
-                    self.in_graph = False
-                else:              # this key exchanges after its replay; later keys try again
-                    self._deviate(f"watchdog kept an eager collective past {bound} s")
+                why = ("flight recorder off: the watchdog's work list cannot be checked" if idle is None else
+                       f"watchdog kept an eager collective past {bound} s")
+                if agree:
+                    self.capture_error = why
+                else:
+                    self._deviate(why)
+                    if idle is None:   # cannot be checked in this process: never capture the exchange
+                        self.in_graph = False
         g, out, err = self._try_capture(exchanged)
         if err is not None:
             if not exchanged:
                 raise err if isinstance(err, BaseException) else RuntimeError(err)
             if self.capture:
                 torch.cuda.synchronize()
-            self._deviate(repr(err))
-            self.in_graph = False   # this rank exchanges after the replay from now on
+            if agree:
+                self.capture_error = repr(err)[:300]
+            else:
+                self._deviate(repr(err))
+                self.in_graph = False   # this rank exchanges after the replay from now on
             exchanged = False
             g, out, err2 = self._try_capture(False)
             if err2 is not None:
                 raise err2
+        if agree:
+            if not self._agree_all(exchanged):   # some rank could not: nobody holds the exchange in a graph
+                self.in_graph = False
+                self.capture_error = self.capture_error or "a peer rank could not capture the exchange"
+                if exchanged:
+                    exchanged = False
+                    if self.capture:
+                        torch.cuda.synchronize()
+                    g, out, err2 = self._try_capture(False)   # the graph with the collectives is dropped unreplayed
+                    if err2 is not None:
+                        raise err2
+        self._settled = True
         if g is not None and self.pool is None:
             self.pool = g.pool()
         self.graphs[key] = (g, out, exchanged)

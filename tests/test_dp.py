@@ -115,7 +115,7 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
             buckets = dp.GradBuckets([ps[len(ps) // 2:][::-1], ps[:len(ps) // 2][::-1]], bucket_bytes=bucket_bytes)
         elif mode == "empty":   # buckets in forward order: the last bucket's grads are ready first
             buckets = dp.GradBuckets([list(model.parameters())], bucket_bytes=bucket_bytes)
-        elif mode in ("graphed", "graphed_mixed", "tied"):
+        elif mode in ("graphed", "graphed_mixed", "graphed_agree", "tied"):
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes, flat_views=True)
         else:
             buckets = dp.GradBuckets(model.parameters(), bucket_bytes=bucket_bytes)
@@ -139,6 +139,16 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
             gs = GraphedSteps(lambda xb: _loss(model, xb) * dp.shard_weight(b - a, gb),
                               lambda xb: step[0] if r == 1 else 0, buckets, capture=False, in_graph_exchange=True,
                               max_graphs=1, local_fallback=True)
+            if r == 1:
+                orig = gs._try_capture
+                gs._try_capture = lambda in_graph: ((None, None, RuntimeError("simulated capture failure"))
+                                                    if in_graph else orig(in_graph))
+        elif mode == "graphed_agree":
+            # rank 1's FIRST capture of the exchange fails: the MIN all-reduce at the job's first capture
+            # moves every rank's exchange after the replay (no rank keeps collectives in a graph)
+            from rqvae_hip.graph import GraphedSteps
+            gs = GraphedSteps(lambda xb: _loss(model, xb) * dp.shard_weight(b - a, gb), lambda xb: 0, buckets,
+                              capture=False, in_graph_exchange=True)
             if r == 1:
                 orig = gs._try_capture
                 gs._try_capture = lambda in_graph: ((None, None, RuntimeError("simulated capture failure"))
@@ -181,6 +191,8 @@ def _worker(rank, world, port, gb, bucket_bytes, q, mode):
         params = {n: p.detach().numpy().copy() for n, p in model.named_parameters()}
         if mode == "graphed_mixed":
             assert (gs.in_graph, gs.eager_steps, len(gs.graphs)) == ((True, 1, 1) if r == 0 else (False, 2, 1))
+        if mode == "graphed_agree":
+            assert not gs.in_graph and [e[2] for e in gs.graphs.values()] == [False]
         q.put((r, (a, b), params, grads, len(buckets.buckets), mine))
     finally:
         if dist.is_initialized():
@@ -234,6 +246,7 @@ def _single_process(state0, gb, mode, world):
     (3, 2, 2048, "empty"),          # global batch < world: rank 2 has no sequences, several buckets
     (2, 64, 2048, "graphed"),       # GraphedSteps bodies with the in-graph exchange (run eagerly)
     (2, 64, 2048, "graphed_mixed"),  # ranks with different keys / capture outcomes / eager fallbacks
+    (2, 64, 2048, "graphed_agree"),  # one rank's first capture fails: every rank exchanges after the replay
     (2, 64, 1024, "tied"),          # one weight, two direct-gradient contributions per backward
 ])
 def test_bucketed_allreduce_matches_single_process(world, gb, bucket_bytes, mode):
@@ -347,31 +360,39 @@ def test_graphed_steps_copy_in_mixed_dtypes():
     assert ptrs == [t.data_ptr() for t in (static.a, static.b, static.mask, static.x, *static.nested)]
 
 
-@pytest.mark.parametrize("world,fallback", [(1, None), (2, None), (2, True)])
-def test_graphed_steps_capture_failure_policy(world, fallback, monkeypatch):
-    """A rank whose capture of the in-graph exchange fails: at world 1, or with the opt-in
-    local fallback, it records the graph without the collectives and exchanges after the replay; at
-    world > 1 by default it raises instead of silently replaying a different collective placement than
-    its peers (one agreed decision per job). Single process; the world size is what GraphedSteps sees."""
+@pytest.mark.parametrize("world,fallback,fail_at", [(1, None, 1), (2, None, 1), (2, None, 2), (2, True, 2)])
+def test_graphed_steps_capture_failure_policy(world, fallback, fail_at, monkeypatch):
+    """A rank whose capture of the in-graph exchange fails. The job's first capture (call 2 on
+    every rank) settles the placement for all ranks (a MIN all-reduce of the outcomes; single process here:
+    the local outcome), so failing there falls back everywhere. A failure at a later capture (a new key)
+    after the job agreed on in-graph exchange: world 1 or the opt-in local fallback record the graph without
+    the collectives and exchange after the replay; world > 1 by default raises instead of silently replaying
+    a different collective placement than its peers. Single process; the world size is what GraphedSteps sees."""
     from rqvae_hip.graph import GraphedSteps
     monkeypatch.delenv("RQVAE_LOCAL_EXCHANGE_FALLBACK", raising=False)
     torch.manual_seed(0)
     model = _Net()
     buckets = dp.GradBuckets(model.parameters(), flat_views=True)
-    gs = GraphedSteps(lambda xb: _loss(model, xb), lambda xb: 0, buckets, capture=False, in_graph_exchange=True,
+    step = [0]
+    gs = GraphedSteps(lambda xb: _loss(model, xb), lambda xb: step[0], buckets, capture=False, in_graph_exchange=True,
                       local_fallback=fallback)
     monkeypatch.setattr(GraphedSteps, "_world", staticmethod(lambda: world))
     orig = gs._try_capture
     gs._try_capture = lambda in_graph: ((None, None, RuntimeError("simulated capture failure"))
-                                        if in_graph else orig(in_graph))
+                                        if in_graph and len(gs.graphs) + 1 == fail_at else orig(in_graph))
     x = _data(16)[0]
     gs(x)                      # eager probe step
     buckets.synchronize()
-    if world > 1 and not fallback:
-        with pytest.raises(RuntimeError, match="cannot capture the gradient exchange"):
-            gs(x)
-        assert "simulated capture failure" in gs.capture_error
-        return
-    gs(x)
-    buckets.synchronize()
-    assert not gs.in_graph and "simulated capture failure" in gs.capture_error and len(gs.graphs) == 1
+    for n in range(1, 3):      # capture n (a new key each call)
+        step[0] += 1
+        if n == fail_at and world > 1 and not fallback and fail_at > 1:
+            with pytest.raises(RuntimeError, match="cannot capture the gradient exchange"):
+                gs(x)
+            assert "simulated capture failure" in gs.capture_error
+            return
+        gs(x)
+        buckets.synchronize()
+        if n < fail_at:
+            assert gs.in_graph and gs.capture_error is None
+    assert not gs.in_graph and "simulated capture failure" in gs.capture_error and len(gs.graphs) == 2
+    assert [e[2] for e in gs.graphs.values()] == [fail_at > 1, False]
