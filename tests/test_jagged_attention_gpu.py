@@ -255,8 +255,7 @@ def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal):
         for a, b, what in zip(res["unit"], res[other], ("dq", "dk", "dv")):
             assert torch.isfinite(a).all(), what
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5, msg=f"{what} vs {other}")
-    if max(lq) <= 16:   # few-query unit form: the workgroup form's per-tile products, so dK / dV bitwise
-        assert torch.equal(res["unit"][1], res["wg"][1]) and torch.equal(res["unit"][2], res["wg"][2])
+    # (not bitwise across forms: the unit forward's online softmax rounds out / lse differently, and delta follows)
     dq, dk, dv = res["unit"]
     assert torch.count_nonzero(dq[int(cq[-1]):]) == 0 and torch.count_nonzero(dk[int(ck[-1]):]) == 0
     assert torch.count_nonzero(dv[int(ck[-1]):]) == 0

@@ -16,6 +16,9 @@ import torch  # noqa: E402
 # (M, N, K, a_kcontig, b_kcontig): the RQ-VAE step's wide launches (forward / data grad / weight grad)
 SHAPES = [(65536, 768, 512, True, True), (65536, 512, 768, True, True), (65536, 512, 512, True, False),
           (768, 512, 65536, False, False), (11332, 1024, 512, True, True)]
+# the decoder's context-row launches on the 128-tile kernel: A fp32 (split while staged), B pre-split
+DEC_SHAPES = [(11332, 1536, 512, True, True), (11332, 512, 1536, True, False), (11332, 1024, 512, True, True),
+              (11332, 512, 1024, True, False)]
 
 
 def timed(fn, reps=10):
@@ -51,6 +54,13 @@ def main():
         kern, S = ops.gemm_x3_choice(M, N, K, True, True, akc, bkc, 0)
         print(json.dumps({"tag": tag, "M": M, "N": N, "K": K, "akc": akc, "bkc": bkc, "kernel": kern, "S": S,
                           "us": us, "tflops": round(2.0 * M * N * K / us / 1e6, 1)}), flush=True)
+    for M, N, K, akc, bkc in DEC_SHAPES:
+        a = torch.randn((M, K) if akc else (K, M), generator=gen, device=dev)
+        b = ops.split_bf16x3(torch.randn((N, K) if bkc else (K, N), generator=gen, device=dev) * 0.05)
+        us = timed(lambda: ops.gemm_x3(a, akc, b, bkc, M, N, K))
+        kern, S = ops.gemm_x3_choice(M, N, K, False, True, akc, bkc, 0)
+        print(json.dumps({"tag": tag, "M": M, "N": N, "K": K, "akc": akc, "bkc": bkc, "a": "fp32", "kernel": kern,
+                          "S": S, "us": us, "tflops": round(2.0 * M * N * K / us / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
