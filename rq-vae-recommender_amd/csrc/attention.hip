@@ -2250,10 +2250,16 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_fewq_unit_kernel(
     const int nkt = (kend + 15) >> 4;
     const float* kb_ = k + k0 * sk + hh * HD;
     const float* vb_ = v + k0 * sv + hh * HD;
-    float4 kp[4], vp[4];
+    // tiles t, t + 1, t + 2 in registers while t is multiplied; t + 3 issued at the top of iteration t (one
+    // tile's compute, ~0.6 us, is well below an HBM round trip, so one tile of lookahead left it exposed)
+    float4 kp[4], vp[4], kp1[4], vp1[4], kp2[4], vp2[4];
     if (nkt > 0) {
       frag_kpat(kb_, sk, 0, lk, lane, kp);
       frag_vpat(vb_, sv, 0, lk, lane, vp);
+      frag_kpat(kb_, sk, min(1, nkt - 1), lk, lane, kp1);
+      frag_vpat(vb_, sv, min(1, nkt - 1), lk, lane, vp1);
+      frag_kpat(kb_, sk, min(2, nkt - 1), lk, lane, kp2);
+      frag_vpat(vb_, sv, min(2, nkt - 1), lk, lane, vp2);
     }
     float qf[HD / 4];
     load_frag<HD>(q + (q0 + min(qi, lq - 1)) * sq + hh * HD + g * (HD / 4), true, qf);
@@ -2264,7 +2270,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_fewq_unit_kernel(
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < nkt; ++t) {
-      const int tn = t + 1 < nkt ? t + 1 : t;
+      const int tn = t + 3 < nkt ? t + 3 : nkt - 1;
       float4 kpn[4], vpn[4];
       frag_kpat(kb_, sk, tn, lk, lane, kpn);
       frag_vpat(vb_, sv, tn, lk, lane, vpn);
@@ -2310,7 +2316,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_fewq_unit_kernel(
       }
       mrun = mnew;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vp[j] = vpn[j]; }
+      for (int j = 0; j < 4; ++j) {
+        kp[j] = kp1[j]; vp[j] = vp1[j];
+        kp1[j] = kp2[j]; vp1[j] = vp2[j];
+        kp2[j] = kpn[j]; vp2[j] = vpn[j];
+      }
     }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
@@ -2650,10 +2660,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
       *reinterpret_cast<float4*>(dv + (rk + f / f4) * sdv + (f % f4) * 4) = z4;
     }
   }
-  // 0/1 permutation operand of the transpose: step s, lane (g, c) = [c == 4 g + s]
-  float pe[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) pe[s] = c == 4 * g + s ? 1.f : 0.f;
   const float sl2 = scale * kLog2e;
   const int nunits = B * H;
   for (int u = blockIdx.x * NWG + wave; u < nunits; u += gridDim.x * NWG) {
@@ -2664,10 +2670,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
     const float* kb_ = k + k0 * sk + hh * HD;
     const float* vb_ = v + k0 * sv + hh * HD;
     // the first key tile's K / V fragments go out before the query tile's loads (independent of them)
-    float4 kp[4], vk[4];
+    float4 kp[4], vk[4], kv[4];
     if (nkt > 0) {
       frag_kpat(kb_, sk, 0, lk, lane, kp);
       frag_kpat(vb_, sv, 0, lk, lane, vk);
+      frag_vpat(kb_, sk, 0, lk, lane, kv);
     }
     // the query tile: Q, dO in the A pattern (row c, d = 16 g + 0..15) and the V pattern (rows 4 g + i,
     // d = 4 c + 0..3); O (A pattern) only for delta
@@ -2722,14 +2729,14 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
     const __amdgpu_buffer_rsrc_t rdk = uniform_rsrc(dk + k0 * sdk + hh * HD, (int64_t)lk * sdk * 4);
     const __amdgpu_buffer_rsrc_t rdv = uniform_rsrc(dv + k0 * sdv + hh * HD, (int64_t)lk * sdv * 4);
     for (int t = 0; t < nkt; ++t) {
-      // this tile's K in the V pattern first (the kp lines: cache hits), then the next tile's K / V in flight
-      // (the last tile re-reads itself: cache hits, no branch) — issued in this order so the kv wait before
-      // the dQ products leaves the prefetch in flight
+      // every load of the next tile (K and V in the K pattern, K in the V pattern) goes out before this
+      // tile's dK / dV stores: vmcnt retires in issue order, so a load issued after the stores would wait for
+      // their write acknowledgements (the last tile re-reads itself: cache hits, no branch)
       const int tn = t + 1 < nkt ? t + 1 : t;
-      float4 kpn[4], vkn[4], kv[4];
-      frag_vpat(kb_, sk, t, lk, lane, kv);
+      float4 kpn[4], vkn[4], kvn[4];
       frag_kpat(kb_, sk, tn, lk, lane, kpn);
       frag_kpat(vb_, sv, tn, lk, lane, vkn);
+      frag_vpat(kb_, sk, tn, lk, lane, kvn);
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the tile's MFMAs
       f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2752,22 +2759,33 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
         st[i] = p;
         dp[i] = p * (dp[i] - dl[i]);   // dS
       }
-      f32x4 dka[4], dva[4], dst = f32x4{0.f, 0.f, 0.f, 0.f};
+      // dV^T += dO^T P (stored), then dK^T += Q^T dS (stored): one set of 16 accumulator registers at a time
+      // (k = the query index 4 g + i); row key, dropped past lk by the descriptor range
+      f32x4 da[4], dst = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) { dka[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+      for (int dt = 0; dt < 4; ++dt) da[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {   // dV^T += dO^T P, dK^T += Q^T dS (k = the query index 4 g + i)
-        dva[0] = mfma4(dvp[i].x, st[i], dva[0]);
-        dva[1] = mfma4(dvp[i].y, st[i], dva[1]);
-        dva[2] = mfma4(dvp[i].z, st[i], dva[2]);
-        dva[3] = mfma4(dvp[i].w, st[i], dva[3]);
-        dka[0] = mfma4(qvp[i].x, dp[i], dka[0]);
-        dka[1] = mfma4(qvp[i].y, dp[i], dka[1]);
-        dka[2] = mfma4(qvp[i].z, dp[i], dka[2]);
-        dka[3] = mfma4(qvp[i].w, dp[i], dka[3]);
+      for (int i = 0; i < 4; ++i) {
+        da[0] = mfma4(dvp[i].x, st[i], da[0]);
+        da[1] = mfma4(dvp[i].y, st[i], da[1]);
+        da[2] = mfma4(dvp[i].z, st[i], da[2]);
+        da[3] = mfma4(dvp[i].w, st[i], da[3]);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) dst = mfma4(dp[s], pe[s], dst);   // dS^T: rows = keys 4 g + i, lanes = queries
+      for (int s = 0; s < 4; ++s)   // dS^T (rows = keys 4 g + i, lanes = queries) against the 0/1 permutation
+        dst = mfma4(dp[s], c == 4 * g + s ? 1.f : 0.f, dst);   // operand [c == 4 g + s] (recomputed: registers)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        rsrc_store4(rdv, (int64_t)key * sdv + 16 * g + 4 * i, make_float4(da[0][i], da[1][i], da[2][i], da[3][i]));
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) da[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        da[0] = mfma4(qvp[i].x, dp[i], da[0]);
+        da[1] = mfma4(qvp[i].y, dp[i], da[1]);
+        da[2] = mfma4(qvp[i].z, dp[i], da[2]);
+        da[3] = mfma4(qvp[i].w, dp[i], da[3]);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {   // dQ^T += K^T dS^T (k = the key index 4 g + i of the tile)
         acc[0] = mfma4(kv[i].x, dst[i], acc[0]);
@@ -2776,13 +2794,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
         acc[3] = mfma4(kv[i].w, dst[i], acc[3]);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {   // row key (dropped past lk by the descriptor range)
+      for (int i = 0; i < 4; ++i)
         rsrc_store4(rdk, (int64_t)key * sdk + 16 * g + 4 * i,
-                    make_float4(dka[0][i] * scale, dka[1][i] * scale, dka[2][i] * scale, dka[3][i] * scale));
-        rsrc_store4(rdv, (int64_t)key * sdv + 16 * g + 4 * i, make_float4(dva[0][i], dva[1][i], dva[2][i], dva[3][i]));
-      }
+                    make_float4(da[0][i] * scale, da[1][i] * scale, da[2][i] * scale, da[3][i] * scale));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vk[j] = vkn[j]; }
+      for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vk[j] = vkn[j]; kv[j] = kvn[j]; }
     }
     if (qv) {   // lane (g, c): query c, d = 16 g + 4 i + 0..3 <- acc[0..3][i]
       float* rq = dq + (q0 + c) * sdq + hh * HD + 16 * g;

@@ -357,37 +357,6 @@ struct XStage {
     }
   }
 
-  // L2 prefetch of one stage (RQ_X3_PF): this thread loads one dword of one 64-B granule of the stage's
-  // operand tile (2 TR granules: fp32 — TR rows x 128 B or 32 k-rows x 4 TR B; split — two planes of TR rows x
-  // 64 B or 32 k-rows x 2 TR B), pulling the line into L2 ahead of the stage's own loads. Addresses stay
-  // inside the operand (rows clamped to R - 1, k to k_hi - 1). The dword lands in `sink` (kept live by the
-  // caller: a reused destination would be overwritten when the load returns).
-  __device__ __forceinline__ void prefetch(const void* __restrict__ Xv, const void* __restrict__ Xlv, int64_t ld, int r0,
-                                           int R, int64_t kb, int64_t k_hi, int tid, uint32_t& sink) const {
-    const int t = tid & (2 * TR - 1);
-    const void* p;
-    if constexpr (!SP) {
-      const float* X = static_cast<const float*>(Xv);
-      if constexpr (KC) {
-        const int64_t k = min(kb + 16 * (t & 1), k_hi - 1);
-        p = X + (int64_t)min(r0 + (t >> 1), R - 1) * ld + k;
-      } else {
-        constexpr int G = TR / 16;   // granules per k-row
-        p = X + min(kb + t / G, k_hi - 1) * ld + max(0, min(r0 + 16 * (t % G), R - 16));
-      }
-    } else {
-      const uint16_t* X = static_cast<const uint16_t*>(t >= TR ? Xlv : Xv);
-      const int u = t % TR;
-      if constexpr (KC) {
-        p = X + (int64_t)min(r0 + u, R - 1) * ld + min(kb, k_hi - 1);
-      } else {
-        constexpr int G = TR / 32;
-        p = X + min(kb + u / G, k_hi - 1) * ld + max(0, min(r0 + 32 * (u % G), R - 32));
-      }
-    }
-    asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(p) : "memory");
-  }
-
   __device__ __forceinline__ void store(char* hi_plane, char* lo_plane, int tid) const {
     if constexpr (!SP) {
       constexpr int NJ = KC ? NJ_FK : NJ_FM;
@@ -503,10 +472,6 @@ __device__ __forceinline__ bf16x8_t xfrag16(const char* plane, int rb, int lane)
 
 #ifndef RQ_X3S_DEPTH
 #define RQ_X3S_DEPTH 2   // stage sets in flight of the 64-tile form (A/B on MI355X: 2, 3, 4 within 3 %)
-#endif
-
-#ifndef RQ_X3_PF
-#define RQ_X3_PF 0       // L2 prefetch of stage st + kDepth + PF while stage st + kDepth is loaded (0 = off; A/B)
 #endif
 
 #ifndef RQ_X3_SETPRIO
@@ -759,7 +724,6 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
   // 64-tile stage is 4x less MFMA work, so that form keeps 4 stages in flight).
   constexpr int kDepth = TS == 64 ? RQ_X3S_DEPTH : RQ_X3_DEPTH;
   static_assert(kDepth >= 2 && kDepth <= 4, "stage sets");
-  uint32_t pf_sink = 0;   // RQ_X3_PF destination, live to the end
   XStage<AKC, ASP, TS, KF> sa0, sa1, sa2, sa3;
   XStage<BKC, BSP, TS, KF> sb0, sb1, sb2, sb3;
   sa0.load(A, Al, lda, m0, M, k_lo, k_lo, k_hi, tid);
@@ -782,11 +746,6 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
   {                                                                                                           \
     const int st_ = (ST), buf = st_ & 1;                                                                      \
     const bool on_ = (ON);                                                                                    \
-    if (RQ_X3_PF) {  /* older than the stage loads below: hipcc's counted waits stay valid */              \
-      const int64_t kp_ = k_lo + (int64_t)min(st_ + kDepth + RQ_X3_PF, nst - 1) * kXK;                        \
-      LA.prefetch(A, Al, lda, m0, M, kp_, k_hi, tid, pf_sink);                                                \
-      LB.prefetch(B, Bl, ldb, n0, N, kp_, k_hi, tid, pf_sink);                                                \
-    }                                                                                                         \
     {  /* unconditional (past the end: the last stage again, an L2 hit) so vmcnt counts stay static */       \
       const int64_t kb = k_lo + (int64_t)min(st_ + kDepth, nst - 1) * kXK;                                    \
       LA.load(A, Al, lda, m0, M, kb, k_lo, k_hi, tid);                                                        \
@@ -901,7 +860,6 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
 
   // Each lane stores C[m][n .. n + 3] quads: 16-B fp32 / 8-B bf16 stores (N % 4 == 0).
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
-  if (RQ_X3_PF && pf_sink == 0x7fc00001u && M < 0) C[0] = 0.f;   // keeps pf_sink live (never true: M > 0)
 #if RQ_X3_MFMA16
   // 16x16 C/D map of D = B A^T: column (lane & 15) = m, row 4 (lane >> 4) + j = n (j = register).
   constexpr int kPM = kP, kPN = kP, kG = 1;
@@ -1019,11 +977,7 @@ __global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pa
 #ifndef RQ_X3W_PRIO
 #define RQ_X3W_PRIO 1      // s_setprio(1) around each MFMA cluster (keeps hipcc from moving it)
 #endif
-#ifndef RQ_X3W_PF
-#define RQ_X3W_PF 0        // L2 prefetch distance in k steps (0 = off): at phase 0 of step t every lane loads one
-                           // dword of a distinct 64-B granule of A's and B's step t + PF (the plain loads pull the
-                           // lines into L2, so the LDS-DMA of that step later hits instead of missing to HBM)
-#endif
+
 constexpr int kWT2 = 256;          // output tile (m and n)
 constexpr int kWH = 8192;          // one half-plane: 128 rows x 32 k bf16
 constexpr int kWStep = 4 * kWH;    // one operand's k step: 2 halves x 2 planes
@@ -1065,11 +1019,7 @@ __device__ __forceinline__ bf16x8_t wfrag16(const char* plane, int rb, int lane)
 
 #define RQ_W_BAR() __builtin_amdgcn_s_barrier()
 #define RQ_W_VM6() asm volatile("s_waitcnt vmcnt(6)" ::: "memory")
-#if RQ_X3W_PF
-#define RQ_W_VM0() asm volatile("s_waitcnt vmcnt(8)" ::: "memory")   // phase 0: + this step's two prefetch loads
-#else
-#define RQ_W_VM0() RQ_W_VM6()
-#endif
+
 #define RQ_W_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
 template <bool AKC, bool BKC, int EPI, bool DROP>
@@ -1115,26 +1065,6 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
     glds16(Bh + o, dst);
     glds16(Bl + o, dst + kWH);
   };
-  // L2 prefetch of step `step` (RQ_X3W_PF): lane index p = 64 wave + lane over 512 granules of 64 B per operand
-  // (plane p >> 8; row image: row p & 255; column image: k-row (p >> 3) & 31, segment p & 7). The loaded
-  // dword lands in pf_sink, which stays live to the end (a destination the compiler reused before the load
-  // returned would be overwritten).
-  uint32_t pf_sink = 0;
-  const int pidx = wave * 64 + lane;
-  const uint16_t* const pfa = (pidx >> 8) ? Al : Ah;
-  const uint16_t* const pfb = (pidx >> 8) ? Bl : Bh;
-  const int64_t pfa0 = AKC ? k_lo + (int64_t)min(m0 + (pidx & 255), M - 1) * lda
-                           : (k_lo + ((pidx >> 3) & 31)) * lda + max(0, min(m0 + 32 * (pidx & 7), M - 32));
-  const int64_t pfb0 = BKC ? k_lo + (int64_t)min(n0 + (pidx & 255), N - 1) * ldb
-                           : (k_lo + ((pidx >> 3) & 31)) * ldb + max(0, min(n0 + 32 * (pidx & 7), N - 32));
-  auto prefetch = [&](int step) {
-    if (RQ_X3W_PF == 0 || RQ_X3W_DIAG == 1) return;
-    const int64_t st = step < nk ? step : nk - 1;
-    const uint16_t* a = pfa + pfa0 + st * da;
-    const uint16_t* b = pfb + pfb0 + st * db;
-    asm volatile("global_load_dword %0, %1, off" : "+v"(pf_sink) : "v"(a) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "+v"(pf_sink) : "v"(b) : "memory");
-  };
   auto aplane = [&](int slot, int h, int pl) -> const char* { return lds + slot * kWStep + (h * 2 + pl) * kWH; };
   auto bplane = [&](int par, int g, int pl) -> const char* {
     return lds + kWB0 + par * kWStep + (g * 2 + pl) * kWH;
@@ -1175,8 +1105,6 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 
   // prologue, in the steady state's issue order (A of steps 0 and 1, B of step 0); phase 0 of
   // step 0 needs A0 (0) and B0 (0): B1 (0), A0 (1), A1 (1) may stay in flight
-#pragma unroll
-  for (int p = 2; p < RQ_X3W_PF; ++p) prefetch(p);   // steps 2 .. PF - 1 (older than every DMA: counts unchanged)
   issue_a(0, 0, 0);
   issue_a(1, 0, 0);
   issue_b(0, 0);
@@ -1190,15 +1118,14 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
   for (int st = 0; st < nk; ++st) {
     const int par = st & 1, slot2 = slot == 0 ? 2 : slot - 1;
     // phase 0: quadrant (A0, B0)
-    prefetch(st + RQ_X3W_PF);
     RQ_W_READ_A(slot, 0)
     RQ_W_READ_B(par, 0, fb0h, fb0l)
     issue_b(0, st + 1);
-    if (g1) RQ_W_VM0();   // B1 (and A1) of this step, for phases 1 and 2
+    if (g1) RQ_W_VM6();   // B1 (and A1) of this step, for phases 1 and 2
     RQ_W_BAR();
     RQ_W_LGKM0();
     RQ_W_MMA(0, 0, fb0h, fb0l)
-    if (!g1) RQ_W_VM0();
+    if (!g1) RQ_W_VM6();
     RQ_W_BAR();
     // phase 1: (A0, B1)
     RQ_W_READ_B(par, 1, fb1h, fb1l)
@@ -1228,7 +1155,6 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 #undef RQ_W_MMA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!g1) RQ_W_BAR();   // balance group 1's extra barrier
-  if (RQ_X3W_PF && pf_sink == 0x7fc00001u && M < 0) C[0] = 0.f;   // keeps pf_sink live (never true: M > 0)
 
   float* Cs = C + (int64_t)s * M * N;   // split-K partial slab (S > 1: ldc == N)
   if (RQ_X3W_DIAG == 3) {   // diagnostic build: no epilogue (the accumulators must look used)
@@ -1295,7 +1221,6 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 }
 #undef RQ_W_BAR
 #undef RQ_W_VM6
-#undef RQ_W_VM0
 #undef RQ_W_LGKM0
 
 // Split-K slab reduction with the GEMM's epilogue: element j of the (M, N) output (ldc == N) is the
