@@ -2218,123 +2218,6 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_fewq_kernel(
   }
 }
 
-// Few-query forward, one wave per (sequence, head) unit (the round-6 form of attn_fwd_fewq_kernel, as
-// attn_bwd_fewq_unit_kernel for the backward): the wave walks the unit's key tiles in order with the next
-// tile's K / V fragments in flight, an online softmax over the tiles (running max and sum per query, the
-// partial O^T rescaled when the max grows), no LDS and no barrier; units in LPT order, waves striding over
-// them. S^T = K Q^T per tile (keys on the accumulator rows, query = lane & 15), O^T += V^T P^T (d permuted).
-__global__ void __launch_bounds__(256, 2) attn_fwd_fewq_unit_kernel(
-    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
-    int64_t sv, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k, int causal, float scale,
-    float* __restrict__ out, int64_t so, float* __restrict__ lse, int64_t Tq, const int* __restrict__ order, int B,
-    int H) {
-  constexpr int HD = 64, NWG = 4;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, qi = lane & 15;
-  {   // rows past the last sequence: zero out over every head
-    const int64_t f4 = (int64_t)H * (HD / 4), nth = (int64_t)gridDim.x * 256, me = (int64_t)blockIdx.x * 256 + tid;
-    const int64_t rq = cu_q[B];
-    for (int64_t f = me; f < (Tq - rq) * f4; f += nth)
-      *reinterpret_cast<float4*>(out + (rq + f / f4) * so + (f % f4) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  const float sl2 = scale * kLog2e;
-  const int nunits = B * H;
-  for (int u = blockIdx.x * NWG + wave; u < nunits; u += gridDim.x * NWG) {
-    const int b = seq_of(order, u / H), hh = u % H;
-    const int64_t q0 = cu_q[b], k0 = cu_k[b];
-    const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-    if (lq <= 0) continue;
-    const bool qv = qi < lq;
-    const int kend = causal ? min(lk, 16) : lk;
-    const int nkt = (kend + 15) >> 4;
-    const float* kb_ = k + k0 * sk + hh * HD;
-    const float* vb_ = v + k0 * sv + hh * HD;
-    // tiles t, t + 1, t + 2 in registers while t is multiplied; t + 3 issued at the top of iteration t (one
-    // tile's compute, ~0.6 us, is well below an HBM round trip, so one tile of lookahead left it exposed)
-    float4 kp[4], vp[4], kp1[4], vp1[4], kp2[4], vp2[4];
-    if (nkt > 0) {
-      frag_kpat(kb_, sk, 0, lk, lane, kp);
-      frag_vpat(vb_, sv, 0, lk, lane, vp);
-      frag_kpat(kb_, sk, min(1, nkt - 1), lk, lane, kp1);
-      frag_vpat(vb_, sv, min(1, nkt - 1), lk, lane, vp1);
-      frag_kpat(kb_, sk, min(2, nkt - 1), lk, lane, kp2);
-      frag_vpat(vb_, sv, min(2, nkt - 1), lk, lane, vp2);
-    }
-    float qf[HD / 4];
-    load_frag<HD>(q + (q0 + min(qi, lq - 1)) * sq + hh * HD + g * (HD / 4), true, qf);
-#pragma unroll
-    for (int d = 0; d < HD / 4; ++d) qf[d] = qv ? qf[d] : 0.f;
-    float mrun = -INFINITY, l = 0.f;   // running max (log2 units, scaled) and this lane's partial sum
-    f32x4 o[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nkt; ++t) {
-      const int tn = t + 3 < nkt ? t + 3 : nkt - 1;
-      float4 kpn[4], vpn[4];
-      frag_kpat(kb_, sk, tn, lk, lane, kpn);
-      frag_vpat(vb_, sv, tn, lk, lane, vpn);
-      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the tile's MFMAs
-      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        st = mfma4(kp[s4].x, qf[4 * s4], st);
-        st = mfma4(kp[s4].y, qf[4 * s4 + 1], st);
-        st = mfma4(kp[s4].z, qf[4 * s4 + 2], st);
-        st = mfma4(kp[s4].w, qf[4 * s4 + 3], st);
-      }
-      float mt = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {   // masks as selects
-        const int key = t * 16 + 4 * g + i;
-        const bool ok = (key < lk) & ((causal == 0) | (key <= qi));
-        st[i] = ok ? st[i] : -INFINITY;
-        mt = fmaxf(mt, st[i]);
-      }
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      // branch-free (a divergent branch here would make hipcc drain the prefetch at the loop head): every
-      // tile holds a valid key of every query (non-causal: keys < lk; causal: one tile, key 0), so mnew is
-      // finite; the selects only guard the all-masked case
-      const float mnew = fmaxf(mrun, mt * sl2);
-      const float msub = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = mrun == -INFINITY ? 0.f : exp2_fast(mrun - msub);
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = o[dt] * alpha;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        st[i] = exp2_fast(__builtin_fmaf(st[i], sl2, -msub));
-        l += st[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        o[0] = mfma4(vp[i].x, st[i], o[0]);
-        o[1] = mfma4(vp[i].y, st[i], o[1]);
-        o[2] = mfma4(vp[i].z, st[i], o[2]);
-        o[3] = mfma4(vp[i].w, st[i], o[3]);
-      }
-      mrun = mnew;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        kp[j] = kp1[j]; vp[j] = vp1[j];
-        kp1[j] = kp2[j]; vp1[j] = vp2[j];
-        kp2[j] = kpn[j]; vp2[j] = vpn[j];
-      }
-    }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    if (qv) {   // lane (g, qi): query qi, d = 16 g + 4 i + 0..3 <- o[0..3][i]
-      const float inv = l > 0.f ? 1.f / l : 0.f;
-      float* ro = out + (q0 + qi) * so + hh * HD + 16 * g;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(ro + 4 * i) = make_float4(o[0][i] * inv, o[1][i] * inv, o[2][i] * inv, o[3][i] * inv);
-      if (g == 0) lse[(int64_t)hh * Tq + q0 + qi] = l > 0.f ? (mrun + log2f(l)) * kLn2 : 0.f;
-    }
-  }
-}
-
 // dQ (+ delta) of the one query tile: key tiles split over the waves as in the forward, partial dQ^T
 // summed through LDS in wave order.
 template <int NW>
@@ -2610,206 +2493,6 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? RQ_FEWQ_BWD_MINWG : 1) attn
   }
 }
 
-// Wave-uniform raw-buffer descriptor over `bytes` bytes from `base` (stride 0): stores past the range are
-// dropped by the hardware, so a tile's rows past the segment end need no branch around the store (a
-// divergent branch there made hipcc's waitcnt merge drain every load in flight at the loop head).
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* base, int64_t bytes) {
-  const uint64_t a = (uint64_t)(uintptr_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? bytes : 0x7fffffff));
-  float* p = reinterpret_cast<float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
-  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, n, 0x00020000);
-}
-__device__ __forceinline__ void rsrc_store4(__amdgpu_buffer_rsrc_t r, int64_t off_floats, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(off_floats * 4), 0, 0);
-}
-
-// ------------------------------------- few-query fused backward, one wave per (sequence, head) unit
-// The round-6 form of attn_bwd_fewq_fused_kernel (the decoder's cross-attention: <= 16 future queries over
-// <= 128 context keys; its causal self-attention over <= 16 tokens). The workgroup form spread ONE unit's
-// <= 6 key tiles over 4 waves and merged their dQ partials through LDS: 2,048 workgroups in ~4 dependent
-// rounds of load -> compute -> LDS reduce -> store, bound by neither HBM nor MFMA (Amazon: 44 us a launch,
-// ~2.3 TB/s of its algorithmic K / V / dK / dV bytes). Here every wave owns whole units (unit u = rank
-// u / H of the LPT order, head u % H; waves stride over the units) and walks the unit's key tiles in order
-// with the NEXT tile's K / V fragments in flight while the current tile multiplies; dK / dV rows of a tile
-// are stored as soon as formed, dQ^T accumulates in registers over all the unit's tiles (ascending tile
-// order: deterministic, no LDS, no barrier) and is stored once. Per tile the products are the workgroup
-// form's (S and dP once in the dK / dV orientation, dV^T += dO^T P, dK^T += Q^T dS, the exact permutation
-// transpose of dS, dQ^T += K^T dS^T), so dK / dV are bitwise the workgroup form's; dQ sums the same terms
-// in tile order instead of (wave, tile) order.
-__global__ void __launch_bounds__(256, 2) attn_bwd_fewq_unit_kernel(
-    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
-    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
-    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
-    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
-    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out, const int* __restrict__ order,
-    int B, int H) {
-  constexpr int HD = 64, NWG = 4;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c = lane & 15;
-  {   // rows past the last sequence (a row-bucketed tail): zero dq / dk / dv over every head
-    const int64_t f4 = (int64_t)H * (HD / 4), nth = (int64_t)gridDim.x * 256, me = (int64_t)blockIdx.x * 256 + tid;
-    const int64_t rq = cu_q[B], rk = cu_k[B];
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t f = me; f < (Tq - rq) * f4; f += nth)
-      *reinterpret_cast<float4*>(dq + (rq + f / f4) * sdq + (f % f4) * 4) = z4;
-    for (int64_t f = me; f < (Tk - rk) * f4; f += nth) {
-      *reinterpret_cast<float4*>(dk + (rk + f / f4) * sdk + (f % f4) * 4) = z4;
-      *reinterpret_cast<float4*>(dv + (rk + f / f4) * sdv + (f % f4) * 4) = z4;
-    }
-  }
-  const float sl2 = scale * kLog2e;
-  const int nunits = B * H;
-  for (int u = blockIdx.x * NWG + wave; u < nunits; u += gridDim.x * NWG) {
-    const int b = seq_of(order, u / H), hh = u % H;
-    const int64_t q0 = cu_q[b], k0 = cu_k[b];
-    const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
-    const int nkt = (lk + 15) >> 4;   // every key tile gets its dK / dV rows written (zeros past the queries)
-    const float* kb_ = k + k0 * sk + hh * HD;
-    const float* vb_ = v + k0 * sv + hh * HD;
-    // the first key tile's K / V fragments go out before the query tile's loads (independent of them)
-    float4 kp[4], vk[4], kv[4];
-    if (nkt > 0) {
-      frag_kpat(kb_, sk, 0, lk, lane, kp);
-      frag_kpat(vb_, sv, 0, lk, lane, vk);
-      frag_vpat(kb_, sk, 0, lk, lane, kv);
-    }
-    // the query tile: Q, dO in the A pattern (row c, d = 16 g + 0..15) and the V pattern (rows 4 g + i,
-    // d = 4 c + 0..3); O (A pattern) only for delta
-    // rows past lq read row lq - 1 (no per-lane branch) and are zeroed by select; a unit without queries
-    // (wave-uniform) loads nothing
-    const bool qv = c < lq;
-    const int64_t qrow = q0 + min(c, max(lq - 1, 0));
-    float qf[HD / 4], dof[HD / 4], of[HD / 4];
-    float4 qvp[4], dvp[4];
-    float lraw = 0.f;
-    if (lq > 0) {
-      load_frag<HD>(q + qrow * sq + hh * HD + g * (HD / 4), true, qf);
-      load_frag<HD>(dout + qrow * sdo + hh * HD + g * (HD / 4), true, dof);
-      load_frag<HD>(out + qrow * so + hh * HD + g * (HD / 4), true, of);
-      frag_vpat(q + q0 * sq + hh * HD, sq, 0, lq, lane, qvp);
-      frag_vpat(dout + q0 * sdo + hh * HD, sdo, 0, lq, lane, dvp);
-      lraw = lse[(int64_t)hh * Tq + qrow];
-    } else {
-#pragma unroll
-      for (int d = 0; d < HD / 4; ++d) qf[d] = dof[d] = of[d] = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) qvp[i] = dvp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int d = 0; d < HD / 4; ++d) {
-      qf[d] = qv ? qf[d] : 0.f;
-      dof[d] = qv ? dof[d] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {   // V pattern rows 4 g + i
-      const bool ok = 4 * g + i < lq;
-      qvp[i] = ok ? qvp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      dvp[i] = ok ? dvp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    float delta = 0.f;
-#pragma unroll
-    for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
-    delta += __shfl_xor(delta, 16, 64);
-    delta += __shfl_xor(delta, 32, 64);
-    if (qv && g == 0) delta_out[(int64_t)hh * Tq + qrow] = delta;
-    const float lse2 = qv ? lraw * kLog2e : 0.f;
-    float dl[4], ls[4];   // per-lane values of the queries 4 g + i (held by lane 4 g + i)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dl[i] = __shfl(delta, 4 * g + i, 64);
-      ls[i] = __shfl(lse2, 4 * g + i, 64);
-    }
-    f32x4 acc[4];   // dQ^T (d permuted) over the unit's key tiles, in tile order
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // this unit's dK / dV rows [0, lk) as store ranges (a row past lk: dropped, no branch)
-    const __amdgpu_buffer_rsrc_t rdk = uniform_rsrc(dk + k0 * sdk + hh * HD, (int64_t)lk * sdk * 4);
-    const __amdgpu_buffer_rsrc_t rdv = uniform_rsrc(dv + k0 * sdv + hh * HD, (int64_t)lk * sdv * 4);
-    for (int t = 0; t < nkt; ++t) {
-      // every load of the next tile (K and V in the K pattern, K in the V pattern) goes out before this
-      // tile's dK / dV stores: vmcnt retires in issue order, so a load issued after the stores would wait for
-      // their write acknowledgements (the last tile re-reads itself: cache hits, no branch)
-      const int tn = t + 1 < nkt ? t + 1 : t;
-      float4 kpn[4], vkn[4], kvn[4];
-      frag_kpat(kb_, sk, tn, lk, lane, kpn);
-      frag_kpat(vb_, sv, tn, lk, lane, vkn);
-      frag_vpat(kb_, sk, tn, lk, lane, kvn);
-      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the tile's MFMAs
-      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        st = mfma4(qf[4 * s4], kp[s4].x, st);
-        dp = mfma4(dof[4 * s4], vk[s4].x, dp);
-        st = mfma4(qf[4 * s4 + 1], kp[s4].y, st);
-        dp = mfma4(dof[4 * s4 + 1], vk[s4].y, dp);
-        st = mfma4(qf[4 * s4 + 2], kp[s4].z, st);
-        dp = mfma4(dof[4 * s4 + 2], vk[s4].z, dp);
-        st = mfma4(qf[4 * s4 + 3], kp[s4].w, st);
-        dp = mfma4(dof[4 * s4 + 3], vk[s4].w, dp);
-      }
-      const int key = t * 16 + c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {   // masks as selects (no short-circuit branches inside the tile loop)
-        const int qr = 4 * g + i;
-        const bool ok = (qr < lq) & (key < lk) & ((causal == 0) | (key <= qr));
-        const float p = ok ? exp2_fast(__builtin_fmaf(st[i], sl2, -ls[i])) : 0.f;
-        st[i] = p;
-        dp[i] = p * (dp[i] - dl[i]);   // dS
-      }
-      // dV^T += dO^T P (stored), then dK^T += Q^T dS (stored): one set of 16 accumulator registers at a time
-      // (k = the query index 4 g + i); row key, dropped past lk by the descriptor range
-      f32x4 da[4], dst = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) da[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        da[0] = mfma4(dvp[i].x, st[i], da[0]);
-        da[1] = mfma4(dvp[i].y, st[i], da[1]);
-        da[2] = mfma4(dvp[i].z, st[i], da[2]);
-        da[3] = mfma4(dvp[i].w, st[i], da[3]);
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)   // dS^T (rows = keys 4 g + i, lanes = queries) against the 0/1 permutation
-        dst = mfma4(dp[s], c == 4 * g + s ? 1.f : 0.f, dst);   // operand [c == 4 g + s] (recomputed: registers)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        rsrc_store4(rdv, (int64_t)key * sdv + 16 * g + 4 * i, make_float4(da[0][i], da[1][i], da[2][i], da[3][i]));
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) da[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        da[0] = mfma4(qvp[i].x, dp[i], da[0]);
-        da[1] = mfma4(qvp[i].y, dp[i], da[1]);
-        da[2] = mfma4(qvp[i].z, dp[i], da[2]);
-        da[3] = mfma4(qvp[i].w, dp[i], da[3]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {   // dQ^T += K^T dS^T (k = the key index 4 g + i of the tile)
-        acc[0] = mfma4(kv[i].x, dst[i], acc[0]);
-        acc[1] = mfma4(kv[i].y, dst[i], acc[1]);
-        acc[2] = mfma4(kv[i].z, dst[i], acc[2]);
-        acc[3] = mfma4(kv[i].w, dst[i], acc[3]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        rsrc_store4(rdk, (int64_t)key * sdk + 16 * g + 4 * i,
-                    make_float4(da[0][i] * scale, da[1][i] * scale, da[2][i] * scale, da[3][i] * scale));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { kp[j] = kpn[j]; vk[j] = vkn[j]; kv[j] = kvn[j]; }
-    }
-    if (qv) {   // lane (g, c): query c, d = 16 g + 4 i + 0..3 <- acc[0..3][i]
-      float* rq = dq + (q0 + c) * sdq + hh * HD + 16 * g;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(rq + 4 * i) =
-            make_float4(acc[0][i] * scale, acc[1][i] * scale, acc[2][i] * scale, acc[3][i] * scale);
-    }
-  }
-}
-
 // ----------------------------------------------- fused backward over short query and key ranges
 // The one-pass form of the few-query kernel above for self-attention over <= R rows (the Amazon encoder's
 // contexts, n <= 81: R = 96): one workgroup per (sequence, head), Q and dO staged by LDS-DMA (swizzled
@@ -3060,13 +2743,11 @@ struct AttnPolicy {
   bool x3;   // RQ_ATTN_SPLIT_BF16: the long-range forwards multiply in split-bf16 (matmul precision 'high')
   bool lpt_short;   // RQ_ATTN_LPT_SHORT: longest-first sequence order for the short / few-query forms too
   bool order_given;   // RQ_ATTN_ORDER_GIVEN: ws[0, B) already holds the LPT order of cu_k (no order launch)
-  bool wg_units;      // RQ_ATTN_WG_UNITS: the round-5 few-query forward / one-pass backward (a workgroup per unit)
 };
 static AttnPolicy attn_policy(int flags) {
   return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
                     (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15, (flags & RQ_ATTN_SPLIT_BF16) != 0,
-                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0,
-                    (flags & RQ_ATTN_WG_UNITS) != 0};
+                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0};
 }
 // LPT order of the short / few-query forms (by key length: their work per workgroup grows with it)
 static bool short_lpt_plan(int64_t B, const AttnPolicy& pol) { return RQ_ATTN_LPT && pol.lpt_short && B >= 2 && B <= kOrderMax; }
@@ -3178,12 +2859,6 @@ static void launch_fwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
     if (order && short_lpt_plan(B, pol) && (fewq_plan(HD, max_q, max_k, pol) || dma_fwd_plan(HD, max_q, max_k, pol))) {
       if (!pol.order_given) hipLaunchKernelGGL(attn_order_kernel, dim3(1), dim3(1024), 0, st, ck, (int)B, order);
       sord = order;
-    }
-    if (fewq_plan(HD, max_q, max_k, pol) && !pol.wg_units) {   // one wave per (sequence, head)
-      const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>((B * H + 3) / 4, 8192));
-      hipLaunchKernelGGL(attn_fwd_fewq_unit_kernel, dim3((unsigned)wgs), dim3(256), 0, st, q, sq, k, sk, v, sv, cq, ck,
-                         causal, scale, out, so, lse, Tq, sord, (int)B, (int)H);
-      return;
     }
     if (fewq_plan(HD, max_q, max_k, pol)) {
       const dim3 g(1, (unsigned)H, (unsigned)B + 1);   // + tail slice
@@ -3300,13 +2975,6 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
         default: RQ_SHF(4, 128); break;
       }
 #undef RQ_SHF
-      return;
-    }
-    if (fewq_plan(HD, max_q, max_k, pol) && pol.fused && !pol.wg_units) {   // one wave per (sequence, head)
-      const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>((B * H + 3) / 4, 8192));
-      hipLaunchKernelGGL(attn_bwd_fewq_unit_kernel, dim3((unsigned)wgs), dim3(256), 0, st, q, sq, k, sk, v, sv, out, so,
-                         dout, sdo, lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, order, (int)B,
-                         (int)H);
       return;
     }
     if (fewq_plan(HD, max_q, max_k, pol) && pol.fused) {

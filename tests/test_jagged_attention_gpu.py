@@ -87,16 +87,13 @@ def _varlen_case(g, B, max_q, max_k, H, hd, same):
     (3, 200, 200, 6, 64, True, True),    # causal over several 64-key blocks (fused dQ partials, causal reduce)
     (4, 150, 260, 6, 64, False, False),  # long ragged q x k, lq != lk
 ])
-@pytest.mark.parametrize("fused", [True, False, "wg"])
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("dma", [True, False])
 def test_varlen_attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same, fused, dma):
-    """One-pass (fused: the short / few-query forms one wave per (sequence, head); "wg": their workgroup-per-
-    unit forms) and two-pass backwards, and the LDS-DMA short forms (key ranges <= 128, hd 64) on and off:
-    the per-call RQ_ATTN_* policy flags."""
+    """One-pass (fused) and two-pass backwards, and the LDS-DMA short forms (key ranges <= 128, hd 64) on
+    and off: the per-call RQ_ATTN_* policy flags."""
     from rqvae_hip import ops
-    if fused == "wg" and not dma:
-        pytest.skip("the workgroup forms are LDS-DMA / register forms selected with dma on")
-    flags = ({True: 0, False: ops.ATTN_TWO_PASS, "wg": ops.ATTN_WG_UNITS}[fused]) | (0 if dma else ops.ATTN_NO_DMA)
+    flags = (0 if fused else ops.ATTN_TWO_PASS) | (0 if dma else ops.ATTN_NO_DMA)
     with ops.attn_policy(flags):
         _attention_vs_oracle(device, B, max_q, max_k, H, hd, causal, same)
 
@@ -239,24 +236,20 @@ def test_varlen_attention_fewq_fused_vs_two_pass(device, lq, lk, causal):
     v0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
     do = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
     res = {}
-    # default (one wave per (sequence, head) unit), again (determinism), the workgroup-per-unit forms, two-pass
-    modes = {"unit": 0, "wg": ops.ATTN_WG_UNITS, "two": ops.ATTN_TWO_PASS}
-    for mode in ("unit", "unit", "wg", "two"):
-        with ops.attn_policy(modes[mode]):
+    for fused in (True, True, False):
+        with ops.attn_policy(0 if fused else ops.ATTN_TWO_PASS):
             qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
             o = ops.varlen_attention(qt, kt, vt, cq, ck, H, causal, max(lq), max(lk))
             o.backward(do)
         r = (qt.grad, kt.grad, vt.grad)
-        if mode in res:
-            for a, b in zip(res[mode], r):
+        if fused in res:
+            for a, b in zip(res[fused], r):
                 assert torch.equal(a, b)
-        res[mode] = r
-    for other in ("wg", "two"):
-        for a, b, what in zip(res["unit"], res[other], ("dq", "dk", "dv")):
-            assert torch.isfinite(a).all(), what
-            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5, msg=f"{what} vs {other}")
-    # (not bitwise across forms: the unit forward's online softmax rounds out / lse differently, and delta follows)
-    dq, dk, dv = res["unit"]
+        res[fused] = r
+    for a, b, what in zip(res[True], res[False], ("dq", "dk", "dv")):
+        assert torch.isfinite(a).all(), what
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5, msg=what)
+    dq, dk, dv = res[True]
     assert torch.count_nonzero(dq[int(cq[-1]):]) == 0 and torch.count_nonzero(dk[int(ck[-1]):]) == 0
     assert torch.count_nonzero(dv[int(ck[-1]):]) == 0
     for b in range(len(lq)):
