@@ -27,16 +27,22 @@ def enable(results_file: str = None, tune_new_shapes: bool = True, max_tuning_ms
     keep the default library heuristic."""
     if os.environ.get("RQVAE_TUNABLE_GEMM", "1") == "0":
         return ""
+    import tempfile
     import torch.cuda.tunable as tunable
     path = results_file or os.environ.get("RQVAE_TUNABLEOP_FILE", DEFAULT_FILE)
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-    tunable.set_filename(path, insert_device_ordinal=False)
+    # one writer per table: under a multi-process launch only rank 0 writes the shared table at exit; every
+    # other rank reads it and keeps what it tunes itself in a file of its own outside the tree (N processes
+    # rewriting one CSV at exit could leave it torn for the next run)
+    rank = int(os.environ.get("RANK", "0") or 0)
+    own = path if rank == 0 else os.path.join(tempfile.gettempdir(), f"rqvae_tunableop_rank{rank}.csv")
+    tunable.set_filename(own, insert_device_ordinal=False)
     tunable.set_max_tuning_duration(int(max_tuning_ms))
     tunable.tuning_enable(bool(tune_new_shapes))
     tunable.enable(True)
     if os.path.exists(path):
         tunable.read_file(path)
-    return path
+    return own
 
 
 def bucket_rows(n: int, bucket: int = ROW_BUCKET) -> int:
