@@ -2503,6 +2503,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? RQ_FEWQ_BWD_MINWG : 1) attn
 // summed in wave order (deterministic) by the whole workgroup. delta = rowsum(dO * O) and lse per query are
 // staged in LDS first. 5 products + the transpose per tile pair (the two-pass form: 7), Q / dO / K / V read
 // once.
+#ifndef RQ_ATTN_SHORT_PAIR
+#define RQ_ATTN_SHORT_PAIR 1   // 0: a wave's two key tiles one after the other (A/B: same bits)
+#endif
 template <int NW, int R>
 __global__ void __launch_bounds__(64 * NW, 2) attn_bwd_short_fused_kernel(
     const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
@@ -2590,10 +2593,94 @@ __global__ void __launch_bounds__(64 * NW, 2) attn_bwd_short_fused_kernel(
       dl[i] = dl_s[qt * 16 + 4 * g + i];
       ls[i] = lse_s[qt * 16 + 4 * g + i];
     }
+    // both key tiles of this wave live for this query tile (wave-uniform): their S / dP, dV / dK and dS^T chains
+    // interleaved, each Q / dO chunk read from LDS once for both — the same products in the same per-
+    // accumulator order as the tile-by-tile loop below (dQ^T: tile 0's terms, then tile 1's), so the same bits
+    const bool two = RQ_ATTN_SHORT_PAIR && TPW == 2 && wave + NW < nkt && (!causal || wave + NW <= qt);
+    if constexpr (TPW == 2) {
+      if (two) {
+        f32x4 st0 = f32x4{0.f, 0.f, 0.f, 0.f}, st1 = st0, dp0 = st0, dp1 = st0;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const float4 a = lds_chunk(Q_s, qt * 16 + c, 4 * g + s4);
+          const float4 e = lds_chunk(O_s, qt * 16 + c, 4 * g + s4);
+          st0 = mfma4(a.x, kp[0][s4].x, st0);
+          st1 = mfma4(a.x, kp[1][s4].x, st1);
+          dp0 = mfma4(e.x, vk[0][s4].x, dp0);
+          dp1 = mfma4(e.x, vk[1][s4].x, dp1);
+          st0 = mfma4(a.y, kp[0][s4].y, st0);
+          st1 = mfma4(a.y, kp[1][s4].y, st1);
+          dp0 = mfma4(e.y, vk[0][s4].y, dp0);
+          dp1 = mfma4(e.y, vk[1][s4].y, dp1);
+          st0 = mfma4(a.z, kp[0][s4].z, st0);
+          st1 = mfma4(a.z, kp[1][s4].z, st1);
+          dp0 = mfma4(e.z, vk[0][s4].z, dp0);
+          dp1 = mfma4(e.z, vk[1][s4].z, dp1);
+          st0 = mfma4(a.w, kp[0][s4].w, st0);
+          st1 = mfma4(a.w, kp[1][s4].w, st1);
+          dp0 = mfma4(e.w, vk[0][s4].w, dp0);
+          dp1 = mfma4(e.w, vk[1][s4].w, dp1);
+        }
+        const int key0 = wave * 16 + c, key1 = (wave + NW) * 16 + c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qr = qt * 16 + 4 * g + i;
+          float p0 = exp2_fast(__builtin_fmaf(st0[i], sl2, -ls[i]));
+          float p1 = exp2_fast(__builtin_fmaf(st1[i], sl2, -ls[i]));
+          if (!(qr < lq && key0 < lk && (!causal || key0 <= qr))) p0 = 0.f;
+          if (!(qr < lq && key1 < lk && (!causal || key1 <= qr))) p1 = 0.f;
+          st0[i] = p0;
+          st1[i] = p1;
+          dp0[i] = p0 * (dp0[i] - dl[i]);
+          dp1[i] = p1 * (dp1[i] - dl[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 oo = lds_chunk(O_s, qt * 16 + 4 * g + i, c);
+          const float4 qq = lds_chunk(Q_s, qt * 16 + 4 * g + i, c);
+          dva[0][0] = mfma4(oo.x, st0[i], dva[0][0]);
+          dva[1][0] = mfma4(oo.x, st1[i], dva[1][0]);
+          dva[0][1] = mfma4(oo.y, st0[i], dva[0][1]);
+          dva[1][1] = mfma4(oo.y, st1[i], dva[1][1]);
+          dva[0][2] = mfma4(oo.z, st0[i], dva[0][2]);
+          dva[1][2] = mfma4(oo.z, st1[i], dva[1][2]);
+          dva[0][3] = mfma4(oo.w, st0[i], dva[0][3]);
+          dva[1][3] = mfma4(oo.w, st1[i], dva[1][3]);
+          dka[0][0] = mfma4(qq.x, dp0[i], dka[0][0]);
+          dka[1][0] = mfma4(qq.x, dp1[i], dka[1][0]);
+          dka[0][1] = mfma4(qq.y, dp0[i], dka[0][1]);
+          dka[1][1] = mfma4(qq.y, dp1[i], dka[1][1]);
+          dka[0][2] = mfma4(qq.z, dp0[i], dka[0][2]);
+          dka[1][2] = mfma4(qq.z, dp1[i], dka[1][2]);
+          dka[0][3] = mfma4(qq.w, dp0[i], dka[0][3]);
+          dka[1][3] = mfma4(qq.w, dp1[i], dka[1][3]);
+        }
+        f32x4 dst0 = f32x4{0.f, 0.f, 0.f, 0.f}, dst1 = dst0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          dst0 = mfma4(dp0[s], pe[s], dst0);
+          dst1 = mfma4(dp1[s], pe[s], dst1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {   // tile 0's dQ^T terms first (the loop's order)
+          acc[0] = mfma4(kv[0][i].x, dst0[i], acc[0]);
+          acc[1] = mfma4(kv[0][i].y, dst0[i], acc[1]);
+          acc[2] = mfma4(kv[0][i].z, dst0[i], acc[2]);
+          acc[3] = mfma4(kv[0][i].w, dst0[i], acc[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[0] = mfma4(kv[1][i].x, dst1[i], acc[0]);
+          acc[1] = mfma4(kv[1][i].y, dst1[i], acc[1]);
+          acc[2] = mfma4(kv[1][i].z, dst1[i], acc[2]);
+          acc[3] = mfma4(kv[1][i].w, dst1[i], acc[3]);
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const int t = wave + j * NW;
-      if (t < nkt && (!causal || t <= qt)) {
+      if (!two && t < nkt && (!causal || t <= qt)) {
         f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {   // S = Q K^T, dP = dO V^T (queries on rows, keys on lanes)
