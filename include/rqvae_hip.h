@@ -403,6 +403,8 @@ int rq_dec_prologue_fwd(const int64_t* user_ids, const int64_t* sem_ids, const i
                                      Q K^T and P V in split-bf16 (3 bf16 MFMA products, fp32 accumulate and
                                      softmax) instead of exact fp32; so does the fused long-range backward (S, dP,
                                      dV, dK and dQ products; P, dS fp32) */
+#define RQ_ATTN_FEWQ_WG 16        /* few-query backward over 49..128 keys: one workgroup per (sequence, head) instead of
+                                     the persistent walk with the next unit staged by LDS-DMA (same bits) */
 #define RQ_ATTN_LPT_SHORT 32      /* the short / few-query forms (<= 128 keys) also dispatch their sequences longest-first
                                      (an order launch; the backward's scratch then holds B ints) */
 #define RQ_ATTN_ORDER_GIVEN 64    /* ws[0, B) (as int32) already holds the longest-first order of cu_k's segments (e.g. from

@@ -2493,6 +2493,267 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? RQ_FEWQ_BWD_MINWG : 1) attn
   }
 }
 
+// -------------------------------- few-query fused backward, persistent, next unit staged by LDS-DMA
+// attn_bwd_fewq_fused_kernel with the unit loop inside: a workgroup walks units u = blockIdx.x + i gridDim.x
+// (unit = LPT rank u / H, head u % H) and, while it multiplies unit u, its K / V rows (R staged rows), its
+// Q / dO / O rows (16) and lse are already on their way into LDS for unit u + gridDim.x by LDS-DMA. The
+// workgroup form paid one load round trip per unit with nothing to overlap it (2,048 workgroups in ~4
+// dependent rounds: 44 us for the Amazon cross-attention, 0.034 of fp32 peak). Per unit the fragments are
+// read from the images into the registers the workgroup form loads from global memory (K / V in the K
+// pattern, K in the V pattern, Q / dO in the A and V patterns, rows past a segment = its last row), so the
+// products, the wave-order dQ sum and every stored value are the workgroup form's bit for bit.
+// The images are refilled in two phases so that a wave holds one key tile's fragments at a time: phase A
+// (key rows < 64 = every wave's first tile, Q / dO / O, lse) right after the first tiles were read, phase B
+// (key rows >= 64, the second tiles) after the second tiles were read, at the dQ-reduction barrier.
+// vmcnt discipline (it retires in issue order): per unit every wave issues the same counts — 12 phase-A DMA
+// instructions, 8 dK / dV stores per tile slot (buffer stores whose descriptor range drops rows past the
+// segment, so no branch changes a count), 2 (R - 64) / 16 phase-B instructions, the dQ and delta stores — and
+// the next unit starts with s_waitcnt vmcnt(2) (R = 64: vmcnt(18)): its DMA landed, the stores issued after it
+// may still be in flight. Barriers are bare s_barrier (__syncthreads would wait vmcnt(0)).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const float* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? (bytes > 0 ? bytes : 0) : 0x7fffffff));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>((uintptr_t)(((uint64_t)hi << 32) | lo)), (short)0, n,
+                                           0x00020000);
+}
+__device__ __forceinline__ void rsrc_st4(__amdgpu_buffer_rsrc_t r, int64_t off_floats, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, (int)(off_floats * 4), 0, 0);
+}
+__device__ __forceinline__ void rsrc_st1(__amdgpu_buffer_rsrc_t r, int64_t off_floats, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)(off_floats * 4), 0, 0);
+}
+// rows [rlo, rhi) of a strided head slice into a swizzled image (rows >= n read row n - 1, clamped to the
+// buffer's last row T - 1); instruction j (4 rows) by wave j % NW: (rhi - rlo) / (4 NW) instructions per wave
+template <int NW>
+__device__ __forceinline__ void dma_img(const float* __restrict__ head0, int64_t stride, int64_t row0, int n, int64_t T,
+                                        int rlo, int rhi, char* img, int wave, int lane) {
+  for (int j = rlo / 4 + wave; j < rhi / 4; j += NW) {
+    const int r = 4 * j + (lane >> 4);
+    const int64_t rr = min(row0 + min(r, max(n, 1) - 1), T - 1);
+    const int c = (lane & 15) ^ swz16(r);
+    glds16f(head0 + rr * stride + 4 * c, img + j * 1024);
+  }
+}
+
+template <int R>
+__global__ void __launch_bounds__(256, R <= 96 ? 2 : 1) attn_bwd_fewq_stream_kernel(
+    const float* __restrict__ q, int64_t sq, const float* __restrict__ k, int64_t sk, const float* __restrict__ v,
+    int64_t sv, const float* __restrict__ out, int64_t so, const float* __restrict__ dout, int64_t sdo,
+    const float* __restrict__ lse, int64_t Tq, const int64_t* __restrict__ cu_q, const int64_t* __restrict__ cu_k,
+    int causal, float scale, float* __restrict__ dq, int64_t sdq, float* __restrict__ dk, int64_t sdk,
+    float* __restrict__ dv, int64_t sdv, int64_t Tk, float* __restrict__ delta_out, const int* __restrict__ order,
+    int B, int H) {
+  constexpr int HD = 64, NW = 4, TPW = 2, NKT = R / 16;
+  static_assert(R % 64 == 0 || R == 96, "staged key rows: whole 4-row DMA instructions on every wave");
+  __shared__ __attribute__((aligned(16))) char K_s[R * 256];
+  __shared__ __attribute__((aligned(16))) char V_s[R * 256];
+  __shared__ __attribute__((aligned(16))) char Q_s[16 * 256];
+  __shared__ __attribute__((aligned(16))) char D_s[16 * 256];
+  __shared__ __attribute__((aligned(16))) char O_s[16 * 256];
+  __shared__ __attribute__((aligned(16))) float L_s[64];
+  __shared__ __attribute__((aligned(16))) float part[NW][16][HD + kPartPad];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  {   // rows past the last sequence: zero dq / dk / dv over every head (before the first unit's wait)
+    const int64_t f4 = (int64_t)H * (HD / 4), nth = (int64_t)gridDim.x * 256, me = (int64_t)blockIdx.x * 256 + tid;
+    const int64_t rq = cu_q[B], rk = cu_k[B];
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t f = me; f < (Tq - rq) * f4; f += nth)
+      *reinterpret_cast<float4*>(dq + (rq + f / f4) * sdq + (f % f4) * 4) = z4;
+    for (int64_t f = me; f < (Tk - rk) * f4; f += nth) {
+      *reinterpret_cast<float4*>(dk + (rk + f / f4) * sdk + (f % f4) * 4) = z4;
+      *reinterpret_cast<float4*>(dv + (rk + f / f4) * sdv + (f % f4) * 4) = z4;
+    }
+  }
+  const int nunits = B * H;
+  // DMA of unit uu's rows into the images in two phases: A = key rows [0, 64) (the first tile of every
+  // wave), Q / dO / O, lse (12 instructions per wave); B = key rows [64, R) (the second tiles: 2 (R - 64) / 16
+  // per wave). The same counts for every unit.
+  auto stage_a = [&](int uu) {
+    const int bb = seq_of(order, uu / H), h2 = uu % H;
+    const int64_t qa = cu_q[bb], ka = cu_k[bb];
+    const int nq = (int)(cu_q[bb + 1] - qa), nk = (int)(cu_k[bb + 1] - ka);
+    dma_img<NW>(k + h2 * HD, sk, ka, nk, Tk, 0, 64, K_s, wave, lane);
+    dma_img<NW>(v + h2 * HD, sv, ka, nk, Tk, 0, 64, V_s, wave, lane);
+    dma_img<NW>(q + h2 * HD, sq, qa, nq, Tq, 0, 16, Q_s, wave, lane);
+    dma_img<NW>(dout + h2 * HD, sdo, qa, nq, Tq, 0, 16, D_s, wave, lane);
+    dma_img<NW>(out + h2 * HD, so, qa, nq, Tq, 0, 16, O_s, wave, lane);
+    const int64_t lr = min(qa + min(lane, max(nq, 1) - 1), Tq - 1);   // lse (H, Tq): 4 B per lane, lanes 16.. repeat
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(lse + (int64_t)h2 * Tq + lr),
+                                     (__attribute__((address_space(3))) void*)L_s, 4, 0, 0);
+  };
+  auto stage_b = [&](int uu) {
+    if constexpr (R > 64) {
+      const int bb = seq_of(order, uu / H), h2 = uu % H;
+      const int64_t ka = cu_k[bb];
+      const int nk = (int)(cu_k[bb + 1] - ka);
+      dma_img<NW>(k + h2 * HD, sk, ka, nk, Tk, 64, R, K_s, wave, lane);
+      dma_img<NW>(v + h2 * HD, sv, ka, nk, Tk, 64, R, V_s, wave, lane);
+    }
+  };
+  int u = blockIdx.x;
+  if (u < nunits) { stage_a(u); stage_b(u); }
+  const float sl2 = scale * kLog2e;
+  bool first = true;
+  for (; u < nunits; u += gridDim.x) {
+    // this unit's DMA landed; what may still fly: the last unit's stores issued after its phase-B DMA
+    // (R > 64: dQ, delta) or after its phase-A DMA (R = 64: 16 dK / dV pieces, dQ, delta)
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (R > 64) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    first = false;
+    __builtin_amdgcn_s_barrier();   // every wave's DMA landed: the images are complete
+    const int b = seq_of(order, u / H), hh = u % H;
+    const int64_t q0 = cu_q[b], k0 = cu_k[b];
+    const int lq = (int)(cu_q[b + 1] - q0), lk = (int)(cu_k[b + 1] - k0);
+    const int nkt = min((lk + 15) >> 4, NKT);
+    // fragments from the images (the workgroup form's global-load layouts): the first tile's now (rows < 64,
+    // phase A), the second tile's after the first tile is done (rows >= 64, phase B)
+    float4 kp[4], vk[4], kv[4];
+    auto read_tile = [&](int t) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        kp[s4] = lds_chunk(K_s, t * 16 + c, 4 * g + s4);
+        vk[s4] = lds_chunk(V_s, t * 16 + c, 4 * g + s4);
+        kv[s4] = lds_chunk(K_s, t * 16 + 4 * g + s4, c);
+      }
+    };
+    read_tile(min(wave, NKT - 1));
+    const bool qv = c < lq;
+    float qf[HD / 4], dof[HD / 4], of[HD / 4];
+    float4 qvp[4], dvp[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const float4 a = lds_chunk(Q_s, c, 4 * g + s4), d = lds_chunk(D_s, c, 4 * g + s4), o = lds_chunk(O_s, c, 4 * g + s4);
+      qf[4 * s4] = a.x; qf[4 * s4 + 1] = a.y; qf[4 * s4 + 2] = a.z; qf[4 * s4 + 3] = a.w;
+      dof[4 * s4] = d.x; dof[4 * s4 + 1] = d.y; dof[4 * s4 + 2] = d.z; dof[4 * s4 + 3] = d.w;
+      of[4 * s4] = o.x; of[4 * s4 + 1] = o.y; of[4 * s4 + 2] = o.z; of[4 * s4 + 3] = o.w;
+      qvp[s4] = lds_chunk(Q_s, 4 * g + s4, c);
+      dvp[s4] = lds_chunk(D_s, 4 * g + s4, c);
+    }
+    const float lraw = L_s[c];
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) {   // queries past lq: zero (the workgroup form's masked loads)
+      qf[d] = qv ? qf[d] : 0.f;
+      dof[d] = qv ? dof[d] : 0.f;
+      of[d] = qv ? of[d] : 0.f;
+    }
+    float delta = 0.f;   // before the barrier: O's fragment is dead after it
+#pragma unroll
+    for (int d = 0; d < HD / 4; ++d) delta += dof[d] * of[d];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave has its fragments: the images are free
+    asm volatile("" ::: "memory");
+    const int un = u + (int)gridDim.x < nunits ? u + (int)gridDim.x : u;   // the next unit (past the end: this one)
+    stage_a(un);   // rows < 64 and Q / dO / O / lse are free: every wave holds its first tile and query fragments
+    asm volatile("" ::: "memory");
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    const float lse2 = qv ? lraw * kLog2e : 0.f;
+    float dl[4], ls[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dl[i] = __shfl(delta, 4 * g + i, 64);
+      ls[i] = __shfl(lse2, 4 * g + i, 64);
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dK / dV of each tile stored right after it is formed (one accumulator set live; 8 stores per tile
+    // always — a tile past nkt stores its zero rows past lk, dropped by the descriptor range)
+    const __amdgpu_buffer_rsrc_t rk_ = wave_rsrc(dk + k0 * sdk + hh * HD, (int64_t)lk * sdk * 4);
+    const __amdgpu_buffer_rsrc_t rv_ = wave_rsrc(dv + k0 * sdv + hh * HD, (int64_t)lk * sdv * 4);
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int t = wave + j * NW;
+      if (j > 0) read_tile(min(t, NKT - 1));
+      f32x4 dka[1][4], dva[1][4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) { dka[0][dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dva[0][dt] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+      if (t < nkt) {
+        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          st = mfma4(qf[4 * s4], kp[s4].x, st);
+          dp = mfma4(dof[4 * s4], vk[s4].x, dp);
+          st = mfma4(qf[4 * s4 + 1], kp[s4].y, st);
+          dp = mfma4(dof[4 * s4 + 1], vk[s4].y, dp);
+          st = mfma4(qf[4 * s4 + 2], kp[s4].z, st);
+          dp = mfma4(dof[4 * s4 + 2], vk[s4].z, dp);
+          st = mfma4(qf[4 * s4 + 3], kp[s4].w, st);
+          dp = mfma4(dof[4 * s4 + 3], vk[s4].w, dp);
+        }
+        const int key = t * 16 + c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qr = 4 * g + i;
+          float p = exp2_fast(__builtin_fmaf(st[i], sl2, -ls[i]));
+          if (!(qr < lq && key < lk && (!causal || key <= qr))) p = 0.f;
+          st[i] = p;
+          dp[i] = p * (dp[i] - dl[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dva[0][0] = mfma4(dvp[i].x, st[i], dva[0][0]);
+          dva[0][1] = mfma4(dvp[i].y, st[i], dva[0][1]);
+          dva[0][2] = mfma4(dvp[i].z, st[i], dva[0][2]);
+          dva[0][3] = mfma4(dvp[i].w, st[i], dva[0][3]);
+          dka[0][0] = mfma4(qvp[i].x, dp[i], dka[0][0]);
+          dka[0][1] = mfma4(qvp[i].y, dp[i], dka[0][1]);
+          dka[0][2] = mfma4(qvp[i].z, dp[i], dka[0][2]);
+          dka[0][3] = mfma4(qvp[i].w, dp[i], dka[0][3]);
+        }
+        f32x4 dst = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) dst = mfma4(dp[s2], c == 4 * g + s2 ? 1.f : 0.f, dst);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[0] = mfma4(kv[i].x, dst[i], acc[0]);
+          acc[1] = mfma4(kv[i].y, dst[i], acc[1]);
+          acc[2] = mfma4(kv[i].z, dst[i], acc[2]);
+          acc[3] = mfma4(kv[i].w, dst[i], acc[3]);
+        }
+      }
+      const int key = t * 16 + c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        rsrc_st4(rk_, (int64_t)key * sdk + 16 * g + 4 * i,
+                 make_float4(dka[0][0][i] * scale, dka[0][1][i] * scale, dka[0][2][i] * scale, dka[0][3][i] * scale));
+        rsrc_st4(rv_, (int64_t)key * sdv + 16 * g + 4 * i, make_float4(dva[0][0][i], dva[0][1][i], dva[0][2][i], dva[0][3][i]));
+      }
+    }
+    // dQ: partials through LDS in wave order (the workgroup form's sum), one float4 per thread
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(&part[wave][c][16 * g + 4 * i]) = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave read its second tile: rows >= 64 are free
+    asm volatile("" ::: "memory");
+    stage_b(un);
+    asm volatile("" ::: "memory");
+    {
+      const int r = tid >> 4, cc = (tid & 15) * 4;
+      float4 s4 = *reinterpret_cast<const float4*>(&part[0][r][cc]);
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        const float4 a = *reinterpret_cast<const float4*>(&part[w][r][cc]);
+        s4.x += a.x; s4.y += a.y; s4.z += a.z; s4.w += a.w;
+      }
+      // stores (18 per wave): dQ row r (dropped past lq), dK / dV rows of both tiles (dropped past lk), delta
+      const __amdgpu_buffer_rsrc_t rq_ = wave_rsrc(dq + q0 * sdq + hh * HD, (int64_t)lq * sdq * 4);
+      rsrc_st4(rq_, (int64_t)r * sdq + cc, make_float4(s4.x * scale, s4.y * scale, s4.z * scale, s4.w * scale));
+    }
+    {
+      const __amdgpu_buffer_rsrc_t rd_ = wave_rsrc(delta_out + (int64_t)hh * Tq + q0, (int64_t)lq * 4);
+      rsrc_st1(rd_, c, delta);   // (every wave and lane group: the same value to the same row)
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the extra DMA of the last unit lands before the exit
+}
+
 // ----------------------------------------------- fused backward over short query and key ranges
 // The one-pass form of the few-query kernel above for self-attention over <= R rows (the Amazon encoder's
 // contexts, n <= 81: R = 96): one workgroup per (sequence, head), Q and dO staged by LDS-DMA (swizzled
@@ -2830,11 +3091,13 @@ struct AttnPolicy {
   bool x3;   // RQ_ATTN_SPLIT_BF16: the long-range forwards multiply in split-bf16 (matmul precision 'high')
   bool lpt_short;   // RQ_ATTN_LPT_SHORT: longest-first sequence order for the short / few-query forms too
   bool order_given;   // RQ_ATTN_ORDER_GIVEN: ws[0, B) already holds the LPT order of cu_k (no order launch)
+  bool fewq_stream;   // !RQ_ATTN_FEWQ_WG: the 4-wave few-query backward as the persistent LDS-DMA-staged walk
 };
 static AttnPolicy attn_policy(int flags) {
   return AttnPolicy{!(flags & RQ_ATTN_NO_DMA), !(flags & RQ_ATTN_TWO_PASS), !(flags & RQ_ATTN_NO_SPLIT),
                     (flags >> RQ_ATTN_QSPLIT_SHIFT) & 15, (flags & RQ_ATTN_SPLIT_BF16) != 0,
-                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0};
+                    (flags & RQ_ATTN_LPT_SHORT) != 0, (flags & RQ_ATTN_ORDER_GIVEN) != 0,
+                    !(flags & RQ_ATTN_FEWQ_WG)};
 }
 // LPT order of the short / few-query forms (by key length: their work per workgroup grows with it)
 static bool short_lpt_plan(int64_t B, const AttnPolicy& pol) { return RQ_ATTN_LPT && pol.lpt_short && B >= 2 && B <= kOrderMax; }
@@ -2877,6 +3140,19 @@ static bool fewq_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy
   return pol.dma && hd == 64 && max_q <= 16 && max_k <= 128;
 }
 static int fewq_waves(int64_t max_k) { return max_k <= 16 ? 1 : (max_k <= 32 ? 2 : 4); }
+#ifndef RQ_ATTN_FEWQ_STREAM
+#define RQ_ATTN_FEWQ_STREAM 1   // 0: the workgroup-per-unit few-query backward for 4-wave launches too (A/B)
+#endif
+static int attn_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
 // one-pass backward of the self-attention style short launches (attn_bwd_short_fused_kernel) and of the
 // few-query launches (attn_bwd_fewq_fused_kernel); RQ_ATTN_TWO_PASS keeps the two-pass dQ + dK/dV kernels
 static bool short_fused_plan(int64_t hd, int64_t max_q, int64_t max_k, const AttnPolicy& pol) {
@@ -3062,6 +3338,17 @@ static void launch_bwd(int64_t B, int64_t H, int64_t max_q, int64_t max_k, hipSt
         default: RQ_SHF(4, 128); break;
       }
 #undef RQ_SHF
+      return;
+    }
+    if (fewq_plan(HD, max_q, max_k, pol) && pol.fused && fewq_waves(max_k) == 4 && RQ_ATTN_FEWQ_STREAM && pol.fewq_stream && Tq > 0 &&
+        Tk > 0) {   // persistent workgroups, the next unit staged by LDS-DMA
+      const int64_t slots = (int64_t)attn_cus() * (max_k <= 96 ? 2 : 1);
+      const dim3 gs((unsigned)std::max<int64_t>(1, std::min<int64_t>(B * H, slots)));
+#define RQ_FQS(R_)                                                                                                 \
+  hipLaunchKernelGGL((attn_bwd_fewq_stream_kernel<R_>), gs, dim3(256), 0, st, q, sq, k, sk, v, sv, out, so, dout, sdo, \
+                     lse, Tq, cq, ck, causal, scale, dq, sdq, dk, sdk, dv, sdv, Tk, delta, order, (int)B, (int)H)
+      if (max_k <= 64) { RQ_FQS(64); } else if (max_k <= 96) { RQ_FQS(96); } else { RQ_FQS(128); }
+#undef RQ_FQS
       return;
     }
     if (fewq_plan(HD, max_q, max_k, pol) && pol.fused) {

@@ -1937,6 +1937,7 @@ class JaggedToPaddedValues(torch.autograd.Function):
 # Kernel policy of the attention calls (the `flags` argument, RQ_ATTN_* in include/rqvae_hip.h; 0 = the
 # measured-best forms): set only by kernel-vs-kernel tests and A/B probes through attn_policy().
 ATTN_NO_DMA, ATTN_TWO_PASS, ATTN_NO_SPLIT, ATTN_SPLIT_BF16, ATTN_LPT_SHORT, ATTN_ORDER_GIVEN = 1, 2, 4, 8, 32, 64
+ATTN_FEWQ_WG = 16
 _ATTN_POLICY = {"flags": 0}
 
 

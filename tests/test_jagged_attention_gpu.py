@@ -497,3 +497,49 @@ def test_varlen_attention_lpt_order_bitwise(device, lq, lk, causal):
     for mode in ("lpt", "given"):
         for a, b, what in zip(res[mode], res["default"], ("out", "dq", "dk", "dv")):
             assert torch.equal(a, b), (mode, what)
+
+
+@pytest.mark.parametrize("B,max_k,lpt", [
+    (96, 81, False),    # the Amazon cross-attention shape: 96 x 8 units > 512 slots (workgroups walk twice)
+    (96, 81, True),     # ... dispatched longest-first
+    (40, 64, False),    # 64 staged key rows (phase-A DMA only)
+    (70, 96, False),    # 96 rows
+    (40, 128, False),   # 128 staged key rows (one slot per CU)
+])
+def test_varlen_attention_fewq_stream_bitwise(device, B, max_k, lpt):
+    """The persistent few-query backward (attn_bwd_fewq_stream_kernel: each workgroup walks units, the next
+    unit's K / V / Q / dO / O / lse staged by LDS-DMA while this one multiplies) against the workgroup-per-unit
+    kernel (RQ_ATTN_FEWQ_WG): dQ, dK, dV bitwise, over ragged ranges with empty segments, rows past the last
+    segment and more units than resident workgroups."""
+    from rqvae_hip import ops
+    g = gi.rng(B * 131 + max_k)
+    H, hd = 8, 64
+    A_ = H * hd
+    lq = g.integers(0, 17, size=B)
+    lk = g.integers(0, max_k + 1, size=B)
+    lq[0], lk[0], lk[1], lk[2], lq[3] = 16, 1, max_k, 0, 0
+    cq = torch.tensor(np.concatenate([[0], np.cumsum(lq)]), device=device)
+    ck = torch.tensor(np.concatenate([[0], np.cumsum(lk)]), device=device)
+    Tq, Tk = int(cq[-1]) + 3, int(ck[-1]) + 5
+    q0 = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
+    k0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
+    v0 = torch.from_numpy(g.standard_normal((Tk, A_), dtype=np.float32)).to(device)
+    do = torch.from_numpy(g.standard_normal((Tq, A_), dtype=np.float32)).to(device)
+    res = {}
+    for mode in ("stream", "wg", "stream2"):
+        flags = (ops.ATTN_FEWQ_WG if mode == "wg" else 0) | (ops.ATTN_LPT_SHORT if lpt else 0)
+        with ops.attn_policy(flags):
+            qt, kt, vt = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
+            out = ops.varlen_attention(qt, kt, vt, cq, ck, H, False, 16, max_k)
+            out.backward(do)
+        res[mode] = (qt.grad, kt.grad, vt.grad)
+    for mode in ("wg", "stream2"):
+        for a, b, what in zip(res[mode], res["stream"], ("dq", "dk", "dv")):
+            assert torch.equal(a, b), (mode, what)
+    dq, dk, dv = res["stream"]
+    assert torch.isfinite(dq).all() and torch.isfinite(dk).all() and torch.isfinite(dv).all()
+    assert torch.count_nonzero(dq[int(cq[-1]):]) == 0 and torch.count_nonzero(dk[int(ck[-1]):]) == 0
+    assert torch.count_nonzero(dv[int(ck[-1]):]) == 0
+    for b in range(B):
+        if lq[b] == 0:
+            assert torch.count_nonzero(dk[int(ck[b]):int(ck[b + 1])]) == 0

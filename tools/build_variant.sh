@@ -9,6 +9,8 @@ C="$R/rq-vae-recommender_amd/csrc"
 make -C "$C" -j8 >/dev/null
 mkdir -p "$R/build_ab"
 obj="$R/build_ab/$name.$(basename "$src" .hip).o"
+# the Makefile's per-file flags (attention: MFMA accumulators in VGPRs)
+if [ "$(basename "$src")" = "attention.hip" ]; then flags="-mllvm -amdgpu-mfma-vgpr-form $flags"; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function $flags \
   -c "$C/$(basename "$src")" -o "$obj"
 objs=""
