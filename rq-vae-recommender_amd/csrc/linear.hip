@@ -535,21 +535,35 @@ __device__ __forceinline__ float sigmoid_fast(float z) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
 }
 
-// Epilogue of one lane quad C[m][n .. n + 3] = v (fp32 accumulator values); Cs = the split-K slab
-// (kEpiStore) or C itself.
+// What the epilogue of lane quad (m, n .. n + 3) reads besides the accumulators: Z (SiLU', residual add) or,
+// for an accumulating plain store, the current C quad; zeros otherwise. Loaded for a whole group of quads
+// before any of their stores (x3_epi4z): the output pointers may alias Z for the compiler, so a load written
+// after a store waits for that store and its own round trip, one quad at a time.
+template <int EPI>
+__device__ __forceinline__ float4 x3_epi_in(int m, int n, float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
+  if constexpr (EPI == kEpiSiluBwd || EPI == kEpiAdd) {
+    return *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
+  } else if constexpr (EPI == kEpiStore) {
+    if (ep.acc) return *reinterpret_cast<const float4*>(Cs + (int64_t)m * ldc + n);
+  }
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Epilogue of one lane quad C[m][n .. n + 3] = v (fp32 accumulator values) with its input quad z
+// (x3_epi_in); Cs = the split-K slab (kEpiStore) or C itself.
 template <int EPI, bool DROP>
-__device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, float* __restrict__ C,
-                                        float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
+__device__ __forceinline__ void x3_epi4z(const float4 v, const float4 z, int m, int n, int N, float* __restrict__ C,
+                                         float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
   if constexpr (EPI == kEpiStore) {
     float4* c = reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n);
     if (ep.acc) {   // fixed order c + v: bitwise the slab reduction's C[j] + P[0][j]
-      const float4 o = *c;
+      const float4 o = z;
       *c = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
     } else {
       *c = v;
     }
   } else if constexpr (EPI == kEpiAdd) {
-    const float4 r = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
+    const float4 r = z;
     if constexpr (DROP) {   // C = Z + Dropout(A B^T): dropout_add_fwd's mask (element m N + n) and arithmetic
       const uint64_t e = (uint64_t)m * N + n;
       float d[4];
@@ -573,7 +587,6 @@ __device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, flo
       o = make_float4(v.x * sigmoid_fast(v.x) * d[0], v.y * sigmoid_fast(v.y) * d[1], v.z * sigmoid_fast(v.z) * d[2],
                       v.w * sigmoid_fast(v.w) * d[3]);
     } else {   // silu'(z) g = g s (1 + z (1 - s)), g = Dropout(A B^T)
-      const float4 z = *reinterpret_cast<const float4*>(ep.Z + (int64_t)m * ldc + n);
       const float sx = sigmoid_fast(z.x), sy = sigmoid_fast(z.y), sz = sigmoid_fast(z.z), sw = sigmoid_fast(z.w);
       o = make_float4(v.x * d[0] * sx * (1.f + z.x * (1.f - sx)), v.y * d[1] * sy * (1.f + z.y * (1.f - sy)),
                       v.z * d[2] * sz * (1.f + z.z * (1.f - sz)), v.w * d[3] * sw * (1.f + z.w * (1.f - sw)));
@@ -584,6 +597,12 @@ __device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, flo
     *reinterpret_cast<uint2*>(ep.Hh + (int64_t)m * ep.ldh + n) = hi;
     *reinterpret_cast<uint2*>(ep.Hl + (int64_t)m * ep.ldh + n) = lo;
   }
+}
+
+template <int EPI, bool DROP>
+__device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, float* __restrict__ C,
+                                        float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
+  x3_epi4z<EPI, DROP>(v, x3_epi_in<EPI>(m, n, Cs, ldc, ep), m, n, N, C, Cs, ldc, ep);
 }
 
 __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo) {
@@ -868,27 +887,50 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
   // quad g holds n = 8 g + 4 (lane >> 5) + 0..3.
   constexpr int kPM = 2, kPN = 2, kG = 4;
 #endif
+  auto quad_m = [&](int p) {
+#if RQ_X3_MFMA16
+    return m0 + wm * kWTile + 16 * p + (lane & 15);
+#else
+    return m0 + wm * 64 + 32 * p + (lane & 31);
+#endif
+  };
+  auto quad_n = [&](int q, int g) {
+#if RQ_X3_MFMA16
+    return n0 + wn * kWTile + 16 * q + 4 * (lane >> 4);
+#else
+    return n0 + wn * 64 + 32 * q + 8 * g + 4 * (lane >> 5);
+#endif
+  };
+  // the Z quads (SiLU', residual add) for every quad first: one round trip, not one per quad
+  constexpr bool kZ = EPI == kEpiSiluBwd || EPI == kEpiAdd;
+  float4 zin[kPM][kPN][kG];
+#pragma unroll
+  for (int p = 0; p < kPM; ++p)
+#pragma unroll
+    for (int q = 0; q < kPN; ++q)
+#pragma unroll
+      for (int g = 0; g < kG; ++g) {
+        const int m = quad_m(p), n = quad_n(q, g);
+        zin[p][q][g] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kZ && m < M && n < N) zin[p][q][g] = x3_epi_in<EPI>(m, n, Cs, ldc, ep);
+      }
 #pragma unroll
   for (int p = 0; p < kPM; ++p) {
-#if RQ_X3_MFMA16
-    const int m = m0 + wm * kWTile + 16 * p + (lane & 15);
-#else
-    const int m = m0 + wm * 64 + 32 * p + (lane & 31);
-#endif
+    const int m = quad_m(p);
     if (m < M) {
 #pragma unroll
       for (int q = 0; q < kPN; ++q)
 #pragma unroll
         for (int g = 0; g < kG; ++g) {
+          const int n = quad_n(q, g);
 #if RQ_X3_MFMA16
-          const int n = n0 + wn * kWTile + 16 * q + 4 * (lane >> 4);
           const float4 v = make_float4(acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]);
 #else
-          const int n = n0 + wn * 64 + 32 * q + 8 * g + 4 * (lane >> 5);
           const float4 v = make_float4(acc[p][q][4 * g], acc[p][q][4 * g + 1], acc[p][q][4 * g + 2], acc[p][q][4 * g + 3]);
 #endif
           if (n >= N) continue;
-          x3_epi4<EPI, DROP>(v, m, n, N, C, Cs, ldc, ep);
+          if constexpr (kZ) x3_epi4z<EPI, DROP>(v, zin[p][q][g], m, n, N, C, Cs, ldc, ep);
+          else x3_epi4<EPI, DROP>(v, m, n, N, C, Cs, ldc, ep);
         }
     }
   }
@@ -1190,13 +1232,32 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
           const int c = 32 * g + 8 * wc + 4 * j + (lane >> 4);
           *reinterpret_cast<floatx4v*>(img + r * 256 + 4 * (c ^ (r & 15))) = acc[h][g][i][j];
         }
-    __syncthreads();
     const int n = n0 + 4 * lane;
+    if constexpr (EPI == kEpiSiluBwd || EPI == kEpiAdd) {
+      // the 16 rows' Z quads in flight together, in the registers this half's accumulators just left
+      // (x3_epi_in: one round trip instead of one per row)
+      float4 zin[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + 128 * h + wave * 16 + q;
+        zin[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < M && n < N) zin[q] = x3_epi_in<EPI>(m, n, Cs, ldc, ep);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int r = wave * 16 + q, m = m0 + 128 * h + r;
+        const floatx4v a = *reinterpret_cast<const floatx4v*>(img + r * 256 + 4 * (lane ^ (r & 15)));
+        if (m < M && n < N) x3_epi4z<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), zin[q], m, n, N, C, Cs, ldc, ep);
+      }
+    } else {   // store-only epilogues (the accumulating store's C read stays per row: unsplit wide calls only)
+      __syncthreads();
 #pragma unroll 4
-    for (int q = 0; q < 16; ++q) {
-      const int r = wave * 16 + q, m = m0 + 128 * h + r;
-      const floatx4v a = *reinterpret_cast<const floatx4v*>(img + r * 256 + 4 * (lane ^ (r & 15)));
-      if (m < M && n < N) x3_epi4<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), m, n, N, C, Cs, ldc, ep);
+      for (int q = 0; q < 16; ++q) {
+        const int r = wave * 16 + q, m = m0 + 128 * h + r;
+        const floatx4v a = *reinterpret_cast<const floatx4v*>(img + r * 256 + 4 * (lane ^ (r & 15)));
+        if (m < M && n < N) x3_epi4<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), m, n, N, C, Cs, ldc, ep);
+      }
     }
     __syncthreads();
   }
