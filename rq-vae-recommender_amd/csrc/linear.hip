@@ -901,8 +901,9 @@ __device__ __forceinline__ void x3_body_k(const X3Args& a, int bid, char* __rest
     return n0 + wn * 64 + 32 * q + 8 * g + 4 * (lane >> 5);
 #endif
   };
-  // the Z quads (SiLU', residual add) for every quad first: one round trip, not one per quad
-  constexpr bool kZ = EPI == kEpiSiluBwd || EPI == kEpiAdd;
+  // the SiLU' epilogue's Z quads for every quad first: one round trip, not one per quad (the residual add
+  // keeps its per-quad reads: preloaded it measured 2 us slower per decoder launch, profiles/r06/epi_z)
+  constexpr bool kZ = EPI == kEpiSiluBwd;
   float4 zin[kPM][kPN][kG];
 #pragma unroll
   for (int p = 0; p < kPM; ++p)
@@ -1233,7 +1234,7 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
           *reinterpret_cast<floatx4v*>(img + r * 256 + 4 * (c ^ (r & 15))) = acc[h][g][i][j];
         }
     const int n = n0 + 4 * lane;
-    if constexpr (EPI == kEpiSiluBwd || EPI == kEpiAdd) {
+    if constexpr (EPI == kEpiSiluBwd) {
       // the 16 rows' Z quads in flight together, in the registers this half's accumulators just left
       // (x3_epi_in: one round trip instead of one per row)
       float4 zin[16];
