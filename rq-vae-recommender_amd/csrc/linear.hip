@@ -1017,6 +1017,11 @@ __global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pa
 #define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs, 3 = no epilogue, 4 = B re-read
                            // from its first k step (cache-resident), 5 = A likewise (wrong results)
 #endif
+#ifndef RQ_X3W_BUFLDS
+#define RQ_X3W_BUFLDS 1    // operand DMA as buffer_load ... lds (SGPR descriptor rebased at the workgroup's first
+                           // row / k chunk + 32-bit byte offset): 1-2.5 % faster than global_load_lds with 64-bit
+                           // per-lane addresses (profiles/r06/gemm_diag); 0 = global_load_lds (A/B switch)
+#endif
 #ifndef RQ_X3W_PRIO
 #define RQ_X3W_PRIO 1      // s_setprio(1) around each MFMA cluster (keeps hipcc from moving it)
 #endif
@@ -1094,19 +1099,41 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
   // A half h of k step `step` into A slot `slot`; B half g of step `step` into B parity step & 1.
   // Steps past the end are clamped (the last step again, into a slot nobody reads), so every wave
   // issues the same DMA count in every phase and the vmcnt counts stay static.
+#if RQ_X3W_BUFLDS
+  // descriptors based at the workgroup's first A / B row (k-contiguous) or first k row (m/n-contiguous): every
+  // offset below is then < x3w_span() elements, which x3w_choose keeps under 2^30 (32-bit byte offsets)
+  const int64_t abase = AKC ? (int64_t)m0 * lda : k_lo * lda, bbase = BKC ? (int64_t)n0 * ldb : k_lo * ldb;
+  const __amdgpu_buffer_rsrc_t rah = __builtin_amdgcn_make_buffer_rsrc((void*)(Ah + abase), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ral = __builtin_amdgcn_make_buffer_rsrc((void*)(Al + abase), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbh = __builtin_amdgcn_make_buffer_rsrc((void*)(Bh + bbase), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbl = __builtin_amdgcn_make_buffer_rsrc((void*)(Bl + bbase), (short)0, 0x7fffffff, 0x00020000);
+  auto bdma = [](__amdgpu_buffer_rsrc_t r, int64_t rel, char* dst) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, (int)(rel * 2), 0, 0, 0);
+  };
+#endif
   auto issue_a = [&](int h, int step, int slot) {
     if (RQ_X3W_DIAG == 1) return;   // diagnostic build: no operand loads (wrong results)
     const int64_t o = (h == 0 ? oa0 : oa1) + (RQ_X3W_DIAG == 5 ? 0 : (int64_t)(step < nk ? step : nk - 1) * da);
     char* dst = wl + slot * kWStep + h * 2 * kWH;
+#if RQ_X3W_BUFLDS
+    bdma(rah, o - abase, dst);
+    bdma(ral, o - abase, dst + kWH);
+#else
     glds16(Ah + o, dst);
     glds16(Al + o, dst + kWH);
+#endif
   };
   auto issue_b = [&](int g, int step) {
     if (RQ_X3W_DIAG == 1) return;
     const int64_t o = (g == 0 ? ob0 : ob1) + (RQ_X3W_DIAG == 4 ? 0 : (int64_t)(step < nk ? step : nk - 1) * db);
     char* dst = wl + kWB0 + (step & 1) * kWStep + g * 2 * kWH;
+#if RQ_X3W_BUFLDS
+    bdma(rbh, o - bbase, dst);
+    bdma(rbl, o - bbase, dst + kWH);
+#else
     glds16(Bh + o, dst);
     glds16(Bl + o, dst + kWH);
+#endif
   };
   auto aplane = [&](int slot, int h, int pl) -> const char* { return lds + slot * kWStep + (h * 2 + pl) * kWH; };
   auto bplane = [&](int par, int g, int pl) -> const char* {
@@ -1587,6 +1614,12 @@ static bool x3w_plan(int64_t M, int64_t N, int64_t K, bool allow_split, X3Plan* 
   return (int64_t)p->tiles * p->S >= cus / 4;
 }
 
+// Elements one wide workgroup's operand DMA spans from its descriptor base (RQ_X3W_BUFLDS: 32-bit byte offsets):
+// 256 rows of a k-contiguous operand (+ K), or one k chunk of rows of an m/n-contiguous one (+ its rows).
+static int64_t x3w_span(int64_t R, int64_t K, int64_t ld, bool kc, int64_t chunk) {
+  return kc ? (int64_t)kWT2 * ld + K : (chunk + 32) * ld + R;
+}
+
 // The wide kernel runs when both operands are split planes, the (layout, epilogue) pair is
 // instantiated (every layout for the plain store; the fused MLP chain's layouts otherwise), the shape
 // plans (x3w_plan) and the time model prefers it — or wherever it can run under RQ_GEMM_FORCE_WIDE;
@@ -1721,7 +1754,9 @@ static int x3_prepare(const rq_gemm_desc& d, hipStream_t s, X3Call* c, bool dry 
   const int flags = d.flags;
   X3Plan pl = x3_plan(M, N, K, flags, true, epilogue);
   X3Plan pw;
-  const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, flags, &pw);
+  // (the span at the largest chunk, K: a forced split count below only shortens it)
+  const bool wide = x3w_choose(M, N, K, asp, bsp, a_kcontig, b_kcontig, epilogue, flags, &pw) &&
+                    x3w_span(M, K, lda, a_kcontig, K) < (1ll << 30) && x3w_span(N, K, ldb, b_kcontig, K) < (1ll << 30);
   if (wide) pl = pw;
   // a tuned plan: RQ_GEMM_SPLIT(S) forces the split-K count on the kernel the policy picked
   const int forced_s = (flags >> RQ_GEMM_SPLIT_SHIFT) & RQ_GEMM_SPLIT_MASK;
