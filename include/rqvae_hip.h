@@ -286,6 +286,16 @@ size_t rq_unique_workspace(int64_t B, int64_t L, int64_t K);
 int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, void* workspace,
                     size_t ws_bytes, void* stream);
 
+/* p_unique_ids itself (modules/rqvae.py:152-157: the count / B the train step logs, as torch's true_divide by
+ * the scalar B computes it, count * (1 / B) in fp32) -> *out_frac (device float), and the count -> *out_count
+ * (either may be NULL, not both); B >= 1. Two launches where K^L <= 2^24 at large B: a bit map of the keys
+ * (atomicOr) and one counting pass that also clears it — the workspace (>= rq_unique_fraction_workspace bytes)
+ * must then be ALL ZERO on entry and is left all zero (keep one per stream; zero it once). Else the hash table
+ * of rq_unique_count (self-initialising) and a division launch. */
+size_t rq_unique_fraction_workspace(int64_t B, int64_t L, int64_t K);
+int rq_unique_fraction(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, float* out_frac,
+                       void* workspace, size_t ws_bytes, void* stream);
+
 /* out[j] (+)= sum_{s < S} P[s * n + j] for j < n, in a fixed order (deterministic, no atomics):
  * the batch-sum gradient of a parameter broadcast over the batch — `pos + seq_emb` and
  * `bos_emb.repeat(B, 1, 1)` of EncoderDecoderRetrievalModel._predict (modules/model.py:91-95).

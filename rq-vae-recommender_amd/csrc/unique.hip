@@ -100,6 +100,70 @@ __global__ void __launch_bounds__(256) unique_map_count_kernel(const uint4* __re
     atomicAdd(count, (unsigned long long)(part[0] + part[1] + part[2] + part[3]) + (blockIdx.x == 0 ? *bad : 0ull));
 }
 
+// p_unique_ids in two launches with a workspace that stays zero between calls: a bit map of the K^L keys
+// (<= 2^24: 2 MiB) marked with atomicOr, then one pass that counts the set bits, clears the words it found set
+// and adds (1 << 40 | its count) to a packed counter with ONE atomic per workgroup — the workgroup that sees
+// every other one's increment in the returned value writes the count and count * inv_b (torch's true_divide by
+// a scalar multiplies by the host reciprocal), and clears the out-of-range counter. The map's memset, the
+// byte-map count and the division kernel of the rq_unique_count route are gone.
+__global__ void __launch_bounds__(256) unique_mark_bits_kernel(const int64_t* __restrict__ ids, int64_t B, int L, int64_t K,
+                                                                unsigned* __restrict__ bits,
+                                                                unsigned long long* __restrict__ bad,
+                                                                unsigned long long* __restrict__ packed) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r == 0) *packed = 0ull;   // the count kernel runs after this launch
+  bool out_of_range = false;
+  if (r < B) {
+    int64_t key = 0;
+    for (int l = L - 1; l >= 0; --l) {
+      const int64_t v = ids[r * L + l];
+      out_of_range |= v < 0 || v >= K;
+      key = key * K + v;
+    }
+    if (!out_of_range) atomicOr(bits + (key >> 5), 1u << (key & 31));
+  }
+  const unsigned long long n = __popcll(__ballot(out_of_range));
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
+}
+
+__global__ void __launch_bounds__(256) unique_count_clear_kernel(uint4* __restrict__ bits, int64_t n16,
+                                                                  unsigned long long* __restrict__ bad,
+                                                                  unsigned long long* __restrict__ packed,
+                                                                  int64_t* __restrict__ out_count,
+                                                                  float* __restrict__ out_frac, float inv_b) {
+  __shared__ unsigned int part[4];
+  unsigned int c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    const uint4 v = bits[i];
+    if (v.x | v.y | v.z | v.w) {
+      c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+      bits[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = (unsigned long long)(part[0] + part[1] + part[2] + part[3]);
+    const unsigned long long old = atomicAdd(packed, (1ull << 40) | t);
+    if ((old >> 40) == (unsigned long long)(gridDim.x - 1)) {   // the last workgroup
+      const unsigned long long total = (old & ((1ull << 40) - 1)) + t + *bad;
+      if (out_count) *out_count = (int64_t)total;
+      if (out_frac) *out_frac = (float)total * inv_b;
+      *bad = 0ull;
+      *packed = 0ull;   // every workgroup's increment is in: the workspace is all zero again
+    }
+  }
+}
+
+// The hash-table route's count -> count and count * inv_b.
+__global__ void unique_fraction_kernel(const unsigned long long* __restrict__ count, int64_t* __restrict__ out_count,
+                                       float* __restrict__ out_frac, float inv_b) {
+  const unsigned long long c = *count;
+  if (out_count) *out_count = (int64_t)c;
+  if (out_frac) *out_frac = (float)c * inv_b;
+}
+
 }  // namespace rqhip
 
 using namespace rqhip;
@@ -153,6 +217,50 @@ int rq_unique_count(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t
     hipLaunchKernelGGL(unique_insert_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, ids, B, (int)L, K,
                        (unsigned long long*)workspace, slots - 1, (unsigned long long*)out_count);
   RQ_LAUNCH_CHECK("rq_unique_count");
+  return 0;
+}
+
+// rq_unique_fraction: the bit-map route where K^L <= 2^24 and B * kMapRowsDiv >= K^L (the map + two 8-B
+// counters, ZERO on entry and left zero), else the hash table (+ its count word)
+static bool use_bit_map(int64_t B, double keys) { return use_byte_map(B, keys); }
+
+size_t rq_unique_fraction_workspace(int64_t B, int64_t L, int64_t K) {
+  double keys = 1;
+  for (int64_t l = 0; l < L; ++l) keys *= (double)K;
+  return use_bit_map(B, keys) ? (size_t)(((int64_t)keys + 127) / 128 * 16 + 16) : table_bytes(B) + 16;
+}
+
+int rq_unique_fraction(const int64_t* ids, int64_t B, int64_t L, int64_t K, int64_t* out_count, float* out_frac,
+                       void* workspace, size_t ws_bytes, void* stream) {
+  RQ_CHECK_ARG(ids && (out_count || out_frac) && workspace, "rq_unique_fraction: null pointer");
+  RQ_CHECK_ARG(B >= 1 && L >= 1 && K >= 1, "rq_unique_fraction: bad shape");
+  double bits = 0;
+  for (int64_t k = K - 1; k > 0; k >>= 1) bits += 1;
+  RQ_CHECK_ARG(bits * L <= 63, "rq_unique_fraction: K^L must fit 63 bits (K=%lld, L=%lld)", (long long)K, (long long)L);
+  RQ_CHECK_ARG(ws_bytes >= rq_unique_fraction_workspace(B, L, K), "rq_unique_fraction: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const float inv_b = 1.0f / (float)B;   // torch: true_divide(count, B) = count * (1 / B) in fp32
+  double keys = 1;
+  for (int64_t l = 0; l < L; ++l) keys *= (double)K;
+  if (use_bit_map(B, keys)) {
+    const int64_t nb = ((int64_t)keys + 127) / 128 * 16;   // bytes of the bit map (whole uint4 words)
+    unsigned long long* bad = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + nb);
+    hipLaunchKernelGGL(unique_mark_bits_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, ids, B, (int)L, K,
+                       (unsigned*)workspace, bad, bad + 1);
+    const int64_t n16 = nb / 16;
+    hipLaunchKernelGGL(unique_count_clear_kernel, dim3((unsigned)std::min<int64_t>(128, (n16 + 255) / 256)), dim3(256),
+                       0, s, (uint4*)workspace, n16, bad, bad + 1, out_count, out_frac, inv_b);
+    RQ_LAUNCH_CHECK("rq_unique_fraction");
+    return 0;
+  }
+  const int64_t slots = table_slots(B);
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + table_bytes(B));
+  hipLaunchKernelGGL(unique_table_init_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s,
+                     (unsigned long long*)workspace, slots, cnt);
+  hipLaunchKernelGGL(unique_insert_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, ids, B, (int)L, K,
+                     (unsigned long long*)workspace, slots - 1, cnt);
+  hipLaunchKernelGGL(unique_fraction_kernel, dim3(1), dim3(1), 0, s, cnt, out_count, out_frac, inv_b);
+  RQ_LAUNCH_CHECK("rq_unique_fraction");
   return 0;
 }
 

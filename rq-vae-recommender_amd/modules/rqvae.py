@@ -172,6 +172,6 @@ class RqVae(nn.Module):
         loss, recon_mean, rq_mean = hip_ops.loss_means(reconstruction, qloss)
         with torch.no_grad():
             embs_norm = emb_norms.T
-            p_unique_ids = torch.true_divide(hip_ops.unique_count(ids, self.codebook_size), ids.shape[0])
+            p_unique_ids = hip_ops.unique_fraction(ids, self.codebook_size)
         return RqVaeComputedLosses(loss=loss, reconstruction_loss=recon_mean, rqvae_loss=rq_mean,
                                    embs_norm=embs_norm, p_unique_ids=p_unique_ids)

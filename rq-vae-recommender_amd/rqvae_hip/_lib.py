@@ -61,6 +61,8 @@ _SIGS = {
     "rq_split_bf16x3_multi": ([_I, _P, _P, _P, _P, _P], _I),
     "rq_unique_workspace": ([_I64, _I64, _I64], _SZ),
     "rq_unique_count": ([_P, _I64, _I64, _I64, _P, _P, _SZ, _P], _I),
+    "rq_unique_fraction_workspace": ([_I64, _I64, _I64], _SZ),
+    "rq_unique_fraction": ([_P, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I),
     "rq_l2norm_recon_fwd": ([_P, _P, _I64, _I64, _P, _P, _P], _I),
     "rq_col_sum": ([_P, _I64, _I64, _P, _I, _P], _I),
     "rq_row_norms": ([_P, _I64, _I64, _P, _P], _I),

@@ -2,6 +2,7 @@
 
   rq_quantize(x, codebooks, mode, beta)      fused L-level residual quantization (fwd + VJP)
   unique_count(ids, K)                       #distinct semantic-ID tuples (device scalar)
+  unique_fraction(ids, K)                    p_unique_ids = that count / B (fp32 device scalar, 2 launches)
   padded_to_jagged_values(x, lengths, N)     jagged gather (+1-1 rounding) + offsets (fwd + VJP)
   varlen_attention(q, k, v, cu_q, cu_k, ...) jagged SDPA (fwd + deterministic VJP)
   gemm_bf16x3 / gemm_x3 / mlp_chain          fp32 matmuls at 'high' precision (split-bf16 MFMA)
@@ -1690,6 +1691,29 @@ def unique_count(ids: torch.Tensor, K: int) -> torch.Tensor:
     nbytes = _lib.load().rq_unique_workspace(B, L, int(K))
     ws = torch.empty((nbytes,), device=ids.device, dtype=torch.uint8)
     call("rq_unique_count", ptr(ids), B, L, int(K), ptr(out), ptr(ws), nbytes, stream_handle(ids.device))
+    return out
+
+
+_UNIQ_WS = {}   # (device, bytes) -> the zero-between-calls workspace of rq_unique_fraction
+
+
+def unique_fraction(ids: torch.Tensor, K: int) -> torch.Tensor:
+    """p_unique_ids = (number of distinct rows of ids (B, L)) / B as a device fp32 scalar, bitwise
+    torch.true_divide(unique_count(ids, K), B) (modules/rqvae.py:152-157): two launches, through a workspace kept
+    per device and size that rq_unique_fraction leaves zero (allocated zeroed on the first call, outside any
+    graph capture that follows)."""
+    require_gpu(ids, what="unique_fraction")
+    ids = ids.contiguous().to(torch.int64)
+    B, L = ids.shape
+    if B == 0:
+        return torch.full((), float("nan"), device=ids.device)
+    out = torch.empty((), device=ids.device, dtype=torch.float32)
+    nbytes = _lib.load().rq_unique_fraction_workspace(B, L, int(K))
+    key = (ids.device, nbytes)
+    ws = _UNIQ_WS.get(key)
+    if ws is None:
+        ws = _UNIQ_WS[key] = torch.zeros((nbytes,), device=ids.device, dtype=torch.uint8)
+    call("rq_unique_fraction", ptr(ids), B, L, int(K), None, ptr(out), ptr(ws), nbytes, stream_handle(ids.device))
     return out
 
 

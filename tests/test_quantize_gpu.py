@@ -299,3 +299,40 @@ def test_unique_count_graph_replay(device, B):
         graph.replay()
         torch.cuda.synchronize()
         assert int(out) == np.unique(ids, axis=0).shape[0], (rep, int(out))
+
+
+def test_unique_fraction(device):
+    """rq_unique_fraction (p_unique_ids of the train step) = torch.true_divide(unique_count, B) bitwise on the
+    bit-map route (K^L <= 2^24, large B: workspace zero on entry and left zero, checked) and the hash route,
+    with out-of-range ids, repeated calls on the same workspace and a hipGraph replay."""
+    from rqvae_hip import ops
+    g = gi.rng(17)
+    for B, L, K in [(65536, 3, 256), (32768, 3, 256), (4096, 3, 256), (5000, 3, 4), (1, 3, 256), (20000, 4, 2048),
+                    (65536, 3, 256)]:
+        for rep in range(2):
+            ids = g.integers(0, K if rep else max(2, K // 16), size=(B, L))
+            if B > 1000 and rep:
+                ids[::997, 1] = K + 3
+                ids[7::1001, 0] = -2
+            t = torch.from_numpy(ids).to(device)
+            got = ops.unique_fraction(t, K)
+            want = torch.true_divide(ops.unique_count(t, K), B)
+            assert got.dtype == torch.float32 and got.shape == ()
+            assert torch.equal(got, want), (B, L, K, rep, float(got), float(want))
+    from rqvae_hip import _lib
+    for (B, L, K) in [(65536, 3, 256), (32768, 3, 256)]:   # the bit-map route's workspaces
+        ws = ops._UNIQ_WS[(torch.device(device), _lib.load().rq_unique_fraction_workspace(B, L, K))]
+        assert int(torch.count_nonzero(ws)) == 0, "the bit-map workspace must be left zero"
+    B = 65536
+    static = torch.zeros((B, 3), dtype=torch.int64, device=device)
+    ops.unique_fraction(static, 256)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = ops.unique_fraction(static, 256)
+    for rep in range(3):
+        ids = g.integers(0, 256 if rep % 2 else 8, size=(B, 3))
+        static.copy_(torch.from_numpy(ids))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert float(out) == np.float32(np.unique(ids, axis=0).shape[0]) * np.float32(np.float32(1.0) / np.float32(B))
