@@ -332,6 +332,9 @@ int rq_l2norm_recon_bwd_fix(const float* pre, const float* x, const float* norms
  *                  deterministic pass (the loss and the two logged components). */
 int rq_row_norms(const float* x, int64_t rows, int64_t D, float* out, void* stream);
 int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out, void* stream);
+/* Its backward when only the total loss out[0] has a gradient g (device scalar): *out_scalar = g * (1 / B)
+ * (torch: g / B), and out_vec[0..B) = the same value (the per-row qloss gradient) — one launch. */
+int rq_loss_means_bwd(const float* g, int64_t B, float* out_scalar, float* out_vec, void* stream);
 
 /* Gumbel-softmax quantize, training (replaces modules/quantize.py:107-112,121,124-129 with
  * distributions/gumbel.py:14-18 for GUMBEL_SOFTMAX + L2): per row b, dist_k = |x|^2 + |c_k|^2 - 2 x.c_k,

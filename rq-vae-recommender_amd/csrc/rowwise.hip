@@ -11,6 +11,8 @@
 //        written fp32, or (rq_l2norm_recon_bwd_split) as the split-bf16 planes the next data-grad /
 //        weight-grad GEMMs of the 'high' path consume directly (same bytes as fp32).
 #include "common.h"
+
+#include <algorithm>
 #include <stdlib.h>
 
 namespace rqhip {
@@ -474,6 +476,17 @@ __global__ void __launch_bounds__(256) row_norm_kernel(const float* __restrict__
   if (ok && lane == 0) out[r] = sqrtf(s);
 }
 
+// Their backward when only the total has a gradient (the train step): s = g * (1 / B) — torch's true_divide of
+// a 0-dim tensor by the scalar B — once as a scalar (the reconstruction rows read it with stride 0) and as the
+// (B,) per-row qloss gradient the quantize backward reads, in one launch (was a scalar op + an expand copy).
+__global__ void __launch_bounds__(256) loss_means_bwd_kernel(const float* __restrict__ g, int64_t B, float inv_b,
+                                                             float* __restrict__ out_scalar, float* __restrict__ out_vec) {
+  const float v = g[0] * inv_b;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i0 == 0) *out_scalar = v;
+  for (int64_t i = i0; i < B; i += (int64_t)gridDim.x * 256) out_vec[i] = v;
+}
+
 // The three scalar losses of RqVae.forward (modules/rqvae.py:151-162) in one pass over (B,) vectors:
 // out = {mean(recon + qloss), mean(recon), mean(qloss)}; one 1024-thread workgroup, each thread a
 // strided slice, then a fixed-order tree in LDS (deterministic).
@@ -921,6 +934,16 @@ int rq_loss_means(const float* recon, const float* qloss, int64_t B, float* out,
   RQ_CHECK_ARG(((uintptr_t)recon | (uintptr_t)qloss) % 16 == 0, "rq_loss_means: inputs must be 16-byte aligned");
   hipLaunchKernelGGL(loss_means_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, recon, qloss, B, out);
   RQ_LAUNCH_CHECK("rq_loss_means");
+  return 0;
+}
+
+int rq_loss_means_bwd(const float* g, int64_t B, float* out_scalar, float* out_vec, void* stream) {
+  RQ_CHECK_ARG(B > 0 && g && out_scalar && out_vec, "rq_loss_means_bwd: bad arguments");
+  const float inv_b = 1.0f / (float)B;
+  const int64_t blocks = std::min<int64_t>(256, (B + 255) / 256);
+  hipLaunchKernelGGL(loss_means_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, g, B, inv_b,
+                     out_scalar, out_vec);
+  RQ_LAUNCH_CHECK("rq_loss_means_bwd");
   return 0;
 }
 

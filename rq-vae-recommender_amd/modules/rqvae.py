@@ -148,6 +148,13 @@ class RqVae(nn.Module):
                            quantize_loss=qloss)
 
     def forward(self, batch: SeqBatch, gumbel_t: float) -> RqVaeComputedLosses:
+        # every encoder / decoder GEMM weight split once for the step, in one launch (the fused chains take
+        # their planes from the scope; two chains split separately were two launches)
+        weights = [m.weight for mlp in (self.encoder.mlp, self.decoder.mlp) for m in mlp if isinstance(m, nn.Linear)]
+        with hip_ops.weight_split_scope(weights):
+            return self._forward(batch, gumbel_t)
+
+    def _forward(self, batch: SeqBatch, gumbel_t: float) -> RqVaeComputedLosses:
         x = batch.x
         # the level loop also returns embs_norm = |emb_l| (modules/rqvae.py:151 of the reference),
         # written from the fused kernel's level epilogue

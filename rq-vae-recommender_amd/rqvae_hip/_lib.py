@@ -67,6 +67,7 @@ _SIGS = {
     "rq_col_sum": ([_P, _I64, _I64, _P, _I, _P], _I),
     "rq_row_norms": ([_P, _I64, _I64, _P, _P], _I),
     "rq_loss_means": ([_P, _P, _I64, _P, _P], _I),
+    "rq_loss_means_bwd": ([_P, _I64, _P, _P, _P], _I),
     "rq_gumbel_softmax_fwd": ([_P, _I64, _I64, _P, _I64, _P, _F, _P, _P, _P, _P], _I),
     "rq_gumbel_softmax_bwd": ([_P, _P, _P, _P, _I64, _I64, _I64, _F, _P, _P, _P], _I),
     "rq_l2norm_recon_bwd": ([_P, _P, _P, _P, _I64, _I64, _P, _P], _I),

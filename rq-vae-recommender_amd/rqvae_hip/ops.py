@@ -1880,7 +1880,12 @@ class LossMeansFunction(torch.autograd.Function):
         gr, gq = tot(g0, g1), tot(g0, g2)
         if gr is None and gq is None:
             return None, None
-        if gr is gq:   # only the total loss has a gradient: one scale for both inputs
+        if gr is gq:   # only the total loss has a gradient: one scale for both inputs, one launch
+            if gr.is_cuda and gr.dtype == torch.float32 and gr.dim() == 0:
+                s = torch.empty((), device=gr.device, dtype=torch.float32)
+                vec = torch.empty((B,), device=gr.device, dtype=torch.float32)
+                call("rq_loss_means_bwd", ptr(gr.contiguous()), B, ptr(s), ptr(vec), stream_handle(gr.device))
+                return s.expand(B), vec   # bitwise (gr / B).expand(B), the qloss one materialised
             gr = gq = (gr / B).expand(B)
             return gr, gq
         return (None if gr is None else (gr / B).expand(B)), (None if gq is None else (gq / B).expand(B))

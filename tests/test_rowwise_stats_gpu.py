@@ -26,3 +26,25 @@ def test_loss_means(device, B):
         assert abs(float(got) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-7
     again = ops.loss_means(r, q)
     assert all(torch.equal(a, b) for a, b in zip((loss, rm, qm), again)), "fixed-order reduction"
+
+
+@pytest.mark.parametrize("B", [65536, 65537, 3, 1])
+def test_loss_means_backward(device, B):
+    """LossMeansFunction.backward when only the total loss has a gradient (rq_loss_means_bwd, one launch):
+    bitwise torch's (g / B).expand(B) for both inputs; with the logged means also differentiated, the torch
+    composite."""
+    from rqvae_hip import ops
+    gen = torch.Generator(device=device).manual_seed(B + 1)
+    for scale in (1.0, 0.37, 3.0):
+        r = torch.rand(B, device=device, generator=gen).requires_grad_(True)
+        q = torch.rand(B, device=device, generator=gen).requires_grad_(True)
+        loss, rm, qm = ops.loss_means(r, q)
+        g = torch.tensor(scale, device=device)
+        loss.backward(g)
+        want = (g / B).expand(B)
+        assert torch.equal(r.grad, want) and torch.equal(q.grad, want)
+        r.grad = q.grad = None
+        loss, rm, qm = ops.loss_means(r, q)
+        (loss * scale + rm).backward()
+        torch.testing.assert_close(r.grad, torch.full((B,), (scale + 1.0) / B, device=device), rtol=1e-6, atol=0)
+        torch.testing.assert_close(q.grad, torch.full((B,), scale / B, device=device), rtol=1e-6, atol=0)
