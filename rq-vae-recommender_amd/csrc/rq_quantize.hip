@@ -27,6 +27,7 @@
 // chained inside the launch so the residual never round-trips through a separate kernel.
 #include "common.h"
 
+#include <algorithm>
 #include <math.h>
 
 namespace rqhip {
@@ -600,6 +601,109 @@ __global__ void __launch_bounds__(256) rq_segsum_finalize_kernel(const int* __re
     grad_cb[((int64_t)l * K + k) * D + d] = s;
   }
 }
+
+// ---------------------------------------------------------------------------------------
+// Codebook gradient without the sort (rotation / STE at K D <= 16,384: the RQ-VAE's 256 x 64 levels), two
+// launches instead of six. Workgroup (c, l) owns rows [c R, (c + 1) R) of level l and sums their codeword
+// contributions 2 gl_b (e_k - x_b) into an LDS image acc[K][D]: wave w of 16 owns the codewords k with
+// 16 k / K == w and walks the chunk's rows in order (a ballot per 64 rows, matches taken lowest row first,
+// their residual and codeword rows loaded sixteen at a time), so every acc[k] is a row-ordered sum —
+// deterministic with no atomics. The
+// image goes to partial[l][c] (zeros where the chunk has no row of k); rq_cb_chunk_reduce sums the chunks in
+// c order (four interleaved partial sums, slab_sum_w4). Lane = VPL consecutive dims (D = 64 VPL).
+#ifndef RQ_CB_CHUNK
+#define RQ_CB_CHUNK 1   // 0: the sort + segmented-sum codebook gradient for every mode (A/B)
+#endif
+constexpr int kCbRows = 1024;   // rows per workgroup
+constexpr int kCbWaves = 16, kCbBatch = 16;
+constexpr int kCbList = 256;   // match-list entries per wave (a skewed chunk drains it more often)
+template <int VPL>
+__global__ void __launch_bounds__(64 * kCbWaves) rq_cb_chunk_kernel(const float* __restrict__ res, const float* __restrict__ cbs,
+                                                          const float* __restrict__ g_qloss,
+                                                          const int64_t* __restrict__ ids, int B, int K, int L,
+                                                          float* __restrict__ partial) {
+  constexpr int D = 64 * VPL, NB = kCbBatch / VPL;   // matches per batch (VGPRs: 16 waves per workgroup)
+  extern __shared__ __attribute__((aligned(16))) float acc[];   // [K][D], the chunk's ids, the waves' match lists
+  int* ids_s = reinterpret_cast<int*>(acc + (int64_t)K * D);
+  const int c = blockIdx.x, l = blockIdx.y, nchunk = gridDim.x, tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  unsigned short* list = reinterpret_cast<unsigned short*>(ids_s + kCbRows) + wave * kCbList;
+  const int r0 = c * kCbRows;
+  for (int i = tid; i < K * D / 4; i += 64 * kCbWaves) reinterpret_cast<float4*>(acc)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < kCbRows; i += 64 * kCbWaves) {
+    const int r = r0 + i;
+    const int64_t k = r < B ? ids[(int64_t)r * L + l] : -1;
+    ids_s[i] = (k >= 0 && k < K) ? (int)k : -1;
+  }
+  __syncthreads();
+  const int64_t BD = (int64_t)B * D;
+  const float* xl = res + (int64_t)l * BD;
+  const float* el = cbs + (int64_t)l * K * D;
+  // this wave's rows (ascending) in batches of NB: loads first, then the row-ordered accumulation
+  auto drain = [&](int n_list) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the list entries other lanes wrote
+    for (int i0 = 0; i0 < n_list; i0 += NB) {
+      int rr[NB], kc[NB];
+      float xv[NB][VPL], ev[NB][VPL], gg[NB];
+      // every load unconditional (entries past the list repeat its last one, not accumulated): a branch
+      // around a load makes the compiler wait for it at the merge, one round trip per match
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int row = list[min(i0 + u, n_list - 1)];
+        rr[u] = r0 + row;
+        kc[u] = ids_s[row];
+        gg[u] = 2.f * g_qloss[rr[u]];
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+          xv[u][j] = xl[(int64_t)rr[u] * D + lane * VPL + j];
+          ev[u][j] = el[(int64_t)kc[u] * D + lane * VPL + j];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (i0 + u < n_list) {
+          float* a = acc + (int64_t)kc[u] * D + lane * VPL;
+#pragma unroll
+          for (int j = 0; j < VPL; ++j) a[j] += gg[u] * (ev[u][j] - xv[u][j]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the list is rewritten after this
+  };
+  int n_list = 0;
+  for (int g0 = 0; g0 < kCbRows; g0 += 64) {
+    const int kk = ids_s[g0 + lane];
+    const bool mine = kk >= 0 && (kCbWaves * kk) / K == wave;
+    const unsigned long long m = __ballot(mine);
+    const int cnt = __popcll(m);
+    if (n_list + cnt > kCbList) {
+      drain(n_list);
+      n_list = 0;
+    }
+    const int before = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    if (mine) list[n_list + before] = (unsigned short)(g0 + lane);
+    n_list += cnt;
+  }
+  drain(n_list);
+  __syncthreads();
+  float4* dst = reinterpret_cast<float4*>(partial + ((int64_t)l * nchunk + c) * K * D);
+  for (int i = tid; i < K * D / 4; i += 64 * kCbWaves) dst[i] = reinterpret_cast<const float4*>(acc)[i];
+}
+
+// grad_cb[l][j] = sum over chunks c (in order) of partial[l][c][j], one float4 column per thread.
+__global__ void __launch_bounds__(256) rq_cb_chunk_reduce_kernel(const float* __restrict__ partial, int nchunk,
+                                                                 int64_t KD, float* __restrict__ grad_cb) {
+  const int l = blockIdx.y;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j >= KD) return;
+  const float4 r = slab_sum_w4(partial + (int64_t)l * nchunk * KD, nchunk, KD, j);
+  *reinterpret_cast<float4*>(grad_cb + (int64_t)l * KD + j) = r;
+}
+
+static bool cb_chunk_path(int64_t B, int64_t D, int64_t K, int mode, const float* g_qloss) {
+  return mode != kEval && g_qloss && (D == 64 || D == 128 || D == 256) && K * D <= 16384 && B >= 4 * kCbRows;
+}
+static int64_t cb_chunks(int64_t B) { return (B + kCbRows - 1) / kCbRows; }
 
 // ---------------------------------------------------------------------------------------
 // Register-resident forward for small D (D <= 64): items stay on the MFMA lane axis for the
@@ -1567,12 +1671,14 @@ static int quantize_fwd(const float* x, int64_t B, int64_t D, const float* codeb
 size_t rq_quantize_bwd_workspace(int64_t B, int64_t D, int64_t K, int64_t L) {
   const int64_t nblk = (B + kSortRows - 1) / kSortRows;
   size_t bytes = 0;
+  // the chunk path's partial images (every mode but eval; the sort path's buffers below cover the rest)
+  const size_t chunk_bytes = (size_t)(L * cb_chunks(B) * K * D) * sizeof(float) + 256;
   bytes += (size_t)(L * B * D) * sizeof(float);          // contrib
   bytes += (size_t)(L * K * nblk) * sizeof(int);         // hist / scanned positions
   bytes += (size_t)(L * (K + 1)) * sizeof(int);          // key offsets
   bytes += (size_t)(L * B) * sizeof(int);                // perm
   bytes += (size_t)(kSegSplit * L * K * D) * sizeof(float);   // heavy-segment partials
-  return bytes + 256;
+  return std::max(bytes + 256, chunk_bytes);
 }
 
 int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* codebooks, int64_t B, int64_t D, int64_t K,
@@ -1614,6 +1720,21 @@ int rq_quantize_bwd(const float* residuals, const int64_t* ids, const float* cod
     default: RQ_CHECK_ARG(false, "rq_quantize_bwd: unsupported D");
   }
   RQ_LAUNCH_CHECK("rq_bwd_rows");
+  if (RQ_CB_CHUNK && cb_chunk_path(B, D, K, mode, g_qloss)) {
+    float* partial = (float*)(((uintptr_t)workspace + 15) & ~(uintptr_t)15);
+    const int nchunk = (int)cb_chunks(B);
+    const size_t lds = (size_t)K * D * sizeof(float) + kCbRows * sizeof(int) + kCbWaves * kCbList * sizeof(unsigned short);
+    switch (D) {
+      case 64: hipLaunchKernelGGL(rq_cb_chunk_kernel<1>, dim3(nchunk, l), dim3(64 * kCbWaves), lds, s, residuals, codebooks, g_qloss, ids, b, k, l, partial); break;
+      case 128: hipLaunchKernelGGL(rq_cb_chunk_kernel<2>, dim3(nchunk, l), dim3(64 * kCbWaves), lds, s, residuals, codebooks, g_qloss, ids, b, k, l, partial); break;
+      default: hipLaunchKernelGGL(rq_cb_chunk_kernel<4>, dim3(nchunk, l), dim3(64 * kCbWaves), lds, s, residuals, codebooks, g_qloss, ids, b, k, l, partial); break;
+    }
+    const int64_t KD = K * D;
+    hipLaunchKernelGGL(rq_cb_chunk_reduce_kernel, dim3((unsigned)((KD / 4 + 255) / 256), l), dim3(256), 0, s, partial,
+                       nchunk, KD, grad_codebooks);
+    RQ_LAUNCH_CHECK("rq_codebook_grad");
+    return 0;
+  }
   hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk, l), dim3(256), k * sizeof(int), s, ids, b, l, k, nblk, hist);
   hipLaunchKernelGGL(sort_keyscan_kernel, dim3((k + 15) / 16, l), dim3(256), 0, s, hist, k, nblk, key_off);
   hipLaunchKernelGGL(sort_offsets_kernel, dim3(l), dim3(1024), 0, s, key_off, k, b);

@@ -336,3 +336,42 @@ def test_unique_fraction(device):
         graph.replay()
         torch.cuda.synchronize()
         assert float(out) == np.float32(np.unique(ids, axis=0).shape[0]) * np.float32(np.float32(1.0) / np.float32(B))
+
+
+@pytest.mark.parametrize("skew", ["uniform", "one_code", "half"])
+@pytest.mark.parametrize("mode", [3, 2])   # rotation trick, STE (MODE_ROTATION, MODE_STE)
+def test_codebook_grad_chunk_path(device, skew, mode):
+    """The rotation / STE codebook gradient at K D <= 16,384 and B >= 4,096 (rq_cb_chunk_kernel: per-chunk
+    row-ordered sums over per-wave match lists, chunks summed in order) against a float64 segment sum of the
+    per-row contributions 2 gl_b (e_k - res_l[b]), bitwise deterministic — with every row of a level on one
+    codeword (one wave's match list drained four times per chunk) and with half of them."""
+    from rqvae_hip import ops
+    B, D, K, L = 65536, 64, 256, 3
+    g = torch.Generator().manual_seed(11 + mode)
+    x = torch.randn(B, D, generator=g).to(device)
+    cbs = torch.randn(L, K, D, generator=g).to(device) * 0.1
+    if skew != "uniform":
+        far = cbs.clone()
+        far[0] += 50.0                    # level 0: every row nearest to codeword 7 ...
+        far[0, 7] = 0.0
+        if skew == "half":
+            far[0, 7 + 1:] -= 50.0        # ... or to 7 and the rest of the (near) codewords
+        cbs = far
+    gq = torch.rand(B, generator=g).to(device)
+    outs = []
+    for _ in range(2):
+        cb = cbs.clone().requires_grad_(True)
+        emb, res, ids, ql, es = ops.rq_quantize(x, cb, mode, 0.25)
+        (ql * gq).sum().backward()
+        outs.append((cb.grad.clone(), res.detach(), ids))
+    assert torch.equal(outs[0][0], outs[1][0]), "bitwise determinism"
+    grad, res, ids = outs[0]
+    if skew == "one_code":
+        assert int((ids[:, 0] == 7).sum()) == B
+    ref = torch.zeros(L, K, D, dtype=torch.float64, device=device)
+    for l in range(L):
+        contrib = 2.0 * gq.double()[:, None] * (cbs[l].double()[ids[:, l]] - res[l].double())
+        ref[l].index_add_(0, ids[:, l], contrib)
+    err = (grad.double() - ref).abs()
+    tol = 1e-4 * ref.abs().amax() + 1e-5
+    assert float(err.max()) <= float(tol), (float(err.max()), float(tol))
