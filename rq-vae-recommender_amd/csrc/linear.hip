@@ -535,6 +535,20 @@ __device__ __forceinline__ float sigmoid_fast(float z) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
 }
 
+// Epilogue stores; NT: non-temporal (the wide kernel's all-CU write bursts, A/B RQ_X3W_NT)
+typedef unsigned ux4_t __attribute__((ext_vector_type(4)));
+typedef unsigned ux2_t __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void epi_st16(void* p, float4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(__builtin_bit_cast(ux4_t, v), reinterpret_cast<ux4_t*>(p));
+  else *reinterpret_cast<float4*>(p) = v;
+}
+template <bool NT>
+__device__ __forceinline__ void epi_st8(void* p, uint2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(__builtin_bit_cast(ux2_t, v), reinterpret_cast<ux2_t*>(p));
+  else *reinterpret_cast<uint2*>(p) = v;
+}
+
 // What the epilogue of lane quad (m, n .. n + 3) reads besides the accumulators: Z (SiLU', residual add) or,
 // for an accumulating plain store, the current C quad; zeros otherwise. Loaded for a whole group of quads
 // before any of their stores (x3_epi4z): the output pointers may alias Z for the compiler, so a load written
@@ -551,16 +565,16 @@ __device__ __forceinline__ float4 x3_epi_in(int m, int n, float* __restrict__ Cs
 
 // Epilogue of one lane quad C[m][n .. n + 3] = v (fp32 accumulator values) with its input quad z
 // (x3_epi_in); Cs = the split-K slab (kEpiStore) or C itself.
-template <int EPI, bool DROP>
+template <int EPI, bool DROP, bool NT = false>
 __device__ __forceinline__ void x3_epi4z(const float4 v, const float4 z, int m, int n, int N, float* __restrict__ C,
                                          float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
   if constexpr (EPI == kEpiStore) {
     float4* c = reinterpret_cast<float4*>(Cs + (int64_t)m * ldc + n);
     if (ep.acc) {   // fixed order c + v: bitwise the slab reduction's C[j] + P[0][j]
       const float4 o = z;
-      *c = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+      epi_st16<NT>(c, make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w));
     } else {
-      *c = v;
+      epi_st16<NT>(c, v);
     }
   } else if constexpr (EPI == kEpiAdd) {
     const float4 r = z;
@@ -569,10 +583,9 @@ __device__ __forceinline__ void x3_epi4z(const float4 v, const float4 z, int m, 
       float d[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) d[j] = keep1(ep.seed, e + j, ep.thr) ? ep.scale : 0.f;
-      *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) =
-          make_float4(r.x + v.x * d[0], r.y + v.y * d[1], r.z + v.z * d[2], r.w + v.w * d[3]);
+      epi_st16<NT>(C + (int64_t)m * ldc + n, make_float4(r.x + v.x * d[0], r.y + v.y * d[1], r.z + v.z * d[2], r.w + v.w * d[3]));
     } else {
-      *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+      epi_st16<NT>(C + (int64_t)m * ldc + n, make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w));
     }
   } else {
     const uint64_t e = (uint64_t)m * N + n;
@@ -583,7 +596,7 @@ __device__ __forceinline__ void x3_epi4z(const float4 v, const float4 z, int m, 
     }
     float4 o;
     if constexpr (EPI == kEpiSiluFwd) {
-      *reinterpret_cast<float4*>(C + (int64_t)m * ldc + n) = v;
+      epi_st16<NT>(C + (int64_t)m * ldc + n, v);
       o = make_float4(v.x * sigmoid_fast(v.x) * d[0], v.y * sigmoid_fast(v.y) * d[1], v.z * sigmoid_fast(v.z) * d[2],
                       v.w * sigmoid_fast(v.w) * d[3]);
     } else {   // silu'(z) g = g s (1 + z (1 - s)), g = Dropout(A B^T)
@@ -594,15 +607,15 @@ __device__ __forceinline__ void x3_epi4z(const float4 v, const float4 z, int m, 
     uint2 hi, lo;
     split_bf16x2(o.x, o.y, hi.x, lo.x);
     split_bf16x2(o.z, o.w, hi.y, lo.y);
-    *reinterpret_cast<uint2*>(ep.Hh + (int64_t)m * ep.ldh + n) = hi;
-    *reinterpret_cast<uint2*>(ep.Hl + (int64_t)m * ep.ldh + n) = lo;
+    epi_st8<NT>(ep.Hh + (int64_t)m * ep.ldh + n, hi);
+    epi_st8<NT>(ep.Hl + (int64_t)m * ep.ldh + n, lo);
   }
 }
 
-template <int EPI, bool DROP>
+template <int EPI, bool DROP, bool NT = false>
 __device__ __forceinline__ void x3_epi4(const float4 v, int m, int n, int N, float* __restrict__ C,
                                         float* __restrict__ Cs, int64_t ldc, const X3Epilogue& ep) {
-  x3_epi4z<EPI, DROP>(v, x3_epi_in<EPI>(m, n, Cs, ldc, ep), m, n, N, C, Cs, ldc, ep);
+  x3_epi4z<EPI, DROP, NT>(v, x3_epi_in<EPI>(m, n, Cs, ldc, ep), m, n, N, C, Cs, ldc, ep);
 }
 
 __device__ __forceinline__ void split_store1(float v, uint16_t* hi, uint16_t* lo) {
@@ -1022,6 +1035,9 @@ __global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pa
                            // row / k chunk + 32-bit byte offset): 1-2.5 % faster than global_load_lds with 64-bit
                            // per-lane addresses (profiles/r06/gemm_diag); 0 = global_load_lds (A/B switch)
 #endif
+#ifndef RQ_X3W_NT
+#define RQ_X3W_NT 1        // the wide kernel's epilogue stores non-temporal (0: default policy; A/B)
+#endif
 #ifndef RQ_X3W_PRIO
 #define RQ_X3W_PRIO 1      // s_setprio(1) around each MFMA cluster (keeps hipcc from moving it)
 #endif
@@ -1276,7 +1292,8 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
       for (int q = 0; q < 16; ++q) {
         const int r = wave * 16 + q, m = m0 + 128 * h + r;
         const floatx4v a = *reinterpret_cast<const floatx4v*>(img + r * 256 + 4 * (lane ^ (r & 15)));
-        if (m < M && n < N) x3_epi4z<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), zin[q], m, n, N, C, Cs, ldc, ep);
+        if (m < M && n < N)
+          x3_epi4z<EPI, DROP, RQ_X3W_NT>(make_float4(a[0], a[1], a[2], a[3]), zin[q], m, n, N, C, Cs, ldc, ep);
       }
     } else {   // store-only epilogues (the accumulating store's C read stays per row: unsplit wide calls only)
       __syncthreads();
@@ -1284,7 +1301,7 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
       for (int q = 0; q < 16; ++q) {
         const int r = wave * 16 + q, m = m0 + 128 * h + r;
         const floatx4v a = *reinterpret_cast<const floatx4v*>(img + r * 256 + 4 * (lane ^ (r & 15)));
-        if (m < M && n < N) x3_epi4<EPI, DROP>(make_float4(a[0], a[1], a[2], a[3]), m, n, N, C, Cs, ldc, ep);
+        if (m < M && n < N) x3_epi4<EPI, DROP, RQ_X3W_NT>(make_float4(a[0], a[1], a[2], a[3]), m, n, N, C, Cs, ldc, ep);
       }
     }
     __syncthreads();
