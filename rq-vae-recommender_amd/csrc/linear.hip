@@ -1028,7 +1028,8 @@ __global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pa
 #endif
 #ifndef RQ_X3W_DIAG
 #define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs, 3 = no epilogue, 4 = B re-read
-                           // from its first k step (cache-resident), 5 = A likewise (wrong results)
+                           // from its first k step (cache-resident), 5 = A likewise, 6 = k-contiguous operands DMA whole
+                           // 128-B lines (8 rows per KiB, each line once per k-step pair) (wrong results)
 #endif
 #ifndef RQ_X3W_BUFLDS
 #define RQ_X3W_BUFLDS 1    // operand DMA as buffer_load ... lds (SGPR descriptor rebased at the workgroup's first
@@ -1060,6 +1061,10 @@ __device__ __forceinline__ int wrow_swz(int r) { return (r >> 2) & 2; }
 template <bool KC>
 __device__ __forceinline__ int64_t x3w_src(int64_t ld, int r0, int R, int wave, int lane) {
   if constexpr (KC) {   // row image: 16 rows x 4 chunks per 1 KiB; position c holds k-chunk c ^ swz
+    if (RQ_X3W_DIAG == 6) {   // diagnostic: 8 rows x one whole 128-B line per 1 KiB (wrong results)
+      const int row = 8 * wave + (lane >> 3);
+      return (int64_t)min(r0 + row, R - 1) * ld + 8 * (lane & 7);
+    }
     const int row = 16 * wave + (lane >> 2);
     const int kc = (lane & 3) ^ wrow_swz(row);
     return (int64_t)min(r0 + row, R - 1) * ld + 8 * kc;
@@ -1129,7 +1134,8 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
 #endif
   auto issue_a = [&](int h, int step, int slot) {
     if (RQ_X3W_DIAG == 1) return;   // diagnostic build: no operand loads (wrong results)
-    const int64_t o = (h == 0 ? oa0 : oa1) + (RQ_X3W_DIAG == 5 ? 0 : (int64_t)(step < nk ? step : nk - 1) * da);
+    const int sa = step < nk ? step : nk - 1;
+    const int64_t o = (h == 0 ? oa0 : oa1) + (RQ_X3W_DIAG == 5 ? 0 : (RQ_X3W_DIAG == 6 && AKC ? (int64_t)(sa & ~1) * da + (int64_t)(sa & 1) * 64 * lda : (int64_t)sa * da));
     char* dst = wl + slot * kWStep + h * 2 * kWH;
 #if RQ_X3W_BUFLDS
     bdma(rah, o - abase, dst);
@@ -1141,7 +1147,8 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
   };
   auto issue_b = [&](int g, int step) {
     if (RQ_X3W_DIAG == 1) return;
-    const int64_t o = (g == 0 ? ob0 : ob1) + (RQ_X3W_DIAG == 4 ? 0 : (int64_t)(step < nk ? step : nk - 1) * db);
+    const int sb = step < nk ? step : nk - 1;
+    const int64_t o = (g == 0 ? ob0 : ob1) + (RQ_X3W_DIAG == 4 ? 0 : (RQ_X3W_DIAG == 6 && BKC ? (int64_t)(sb & ~1) * db + (int64_t)(sb & 1) * 64 * ldb : (int64_t)sb * db));
     char* dst = wl + kWB0 + (step & 1) * kWStep + g * 2 * kWH;
 #if RQ_X3W_BUFLDS
     bdma(rbh, o - bbase, dst);
