@@ -496,9 +496,24 @@ __global__ void __launch_bounds__(1024) loss_means_kernel(const float* __restric
   __shared__ float red[3][1024];
   const int t = threadIdx.x;
   float a = 0.f, b = 0.f, c = 0.f;
-  // fixed order: thread t sums float4 groups t, t + 1024, ... (4 loads in flight), then the tail
+  // fixed order: thread t sums float4 groups t, t + 1024, ... (8 loads of each vector in flight: one
+  // round trip per 8 groups, the same additions in the same order as 4 or 1 at a time), then the tail
   const int64_t n4 = B / 4;
   int64_t i = t;
+  for (; i + 7 * 1024 < n4; i += 8 * 1024) {
+    float4 r[8], q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      r[u] = reinterpret_cast<const float4*>(recon)[i + u * 1024];
+      q[u] = reinterpret_cast<const float4*>(ql)[i + u * 1024];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a += (r[u].x + q[u].x) + (r[u].y + q[u].y) + (r[u].z + q[u].z) + (r[u].w + q[u].w);
+      b += r[u].x + r[u].y + r[u].z + r[u].w;
+      c += q[u].x + q[u].y + q[u].z + q[u].w;
+    }
+  }
   for (; i + 3 * 1024 < n4; i += 4 * 1024) {
     float4 r[4], q[4];
 #pragma unroll
@@ -527,13 +542,26 @@ __global__ void __launch_bounds__(1024) loss_means_kernel(const float* __restric
   }
   red[0][t] = a; red[1][t] = b; red[2][t] = c;
   __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
+  for (int o = 512; o >= 64; o >>= 1) {   // pairwise tree: the cross-wave levels through LDS
     if (t < o) {
       red[0][t] += red[0][t + o]; red[1][t] += red[1][t + o]; red[2][t] += red[2][t + o];
     }
     __syncthreads();
   }
-  if (t < 3) out[t] = red[t][0] / (float)B;
+  if (t < 64) {   // the last six levels inside wave 0 (lane t < o adds lane t + o: the same tree, no barriers)
+    float x0 = red[0][t], x1 = red[1][t], x2 = red[2][t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      x0 += __shfl_down(x0, o, 64);
+      x1 += __shfl_down(x1, o, 64);
+      x2 += __shfl_down(x2, o, 64);
+    }
+    if (t == 0) {
+      out[0] = x0 / (float)B;
+      out[1] = x1 / (float)B;
+      out[2] = x2 / (float)B;
+    }
+  }
 }
 
 // ------------------------------------------------------------- decoder output loss (cross-entropy)
