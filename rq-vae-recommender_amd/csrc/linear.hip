@@ -1029,7 +1029,8 @@ __global__ void __launch_bounds__(256, P1::kTS == 64 ? kXWG64 : kXWG) gemm_x3_pa
 #ifndef RQ_X3W_DIAG
 #define RQ_X3W_DIAG 0      // diagnostic builds only: 1 = no operand loads, 2 = no MFMAs, 3 = no epilogue, 4 = B re-read
                            // from its first k step (cache-resident), 5 = A likewise, 6 = k-contiguous operands DMA whole
-                           // 128-B lines (8 rows per KiB, each line once per k-step pair) (wrong results)
+                           // 128-B lines (8 rows per KiB, each line once per k-step pair), 7 = phases 1 / 2 skip
+                           // their fragment reads after the first k step (half the LDS reads) (wrong results)
 #endif
 #ifndef RQ_X3W_BUFLDS
 #define RQ_X3W_BUFLDS 1    // operand DMA as buffer_load ... lds (SGPR descriptor rebased at the workgroup's first
@@ -1221,14 +1222,14 @@ gemm_x3w_kernel(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al
     if (!g1) RQ_W_VM6();
     RQ_W_BAR();
     // phase 1: (A0, B1)
-    RQ_W_READ_B(par, 1, fb1h, fb1l)
+    if (RQ_X3W_DIAG != 7 || st == 0) RQ_W_READ_B(par, 1, fb1h, fb1l)
     issue_b(1, st + 1);
     RQ_W_BAR();
     RQ_W_LGKM0();
     RQ_W_MMA(0, 1, fb1h, fb1l)
     RQ_W_BAR();
     // phase 2: (A1, B1)
-    RQ_W_READ_A(slot, 1)
+    if (RQ_X3W_DIAG != 7 || st == 0) RQ_W_READ_A(slot, 1)
     issue_a(0, st + 2, slot2);
     RQ_W_BAR();
     RQ_W_LGKM0();
